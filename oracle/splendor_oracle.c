@@ -1,0 +1,698 @@
+/*
+ * splendor_oracle.c — scalar CPU restatement of the reference Splendor hot path.
+ *
+ * TEST INFRASTRUCTURE (parity checker + CPU baseline). See splendor_oracle.h for the
+ * usage rule and the list of reference functions restated. Pinned against the golden
+ * vectors in tests/golden (recorded from the reference itself by make_golden.py).
+ *
+ * Build: make -C oracle   (gcc -O2 -ffp-contract=off: strict IEEE order, no FMA, so
+ *        the float arithmetic matches the Python-recorded golden vectors bit-exactly)
+ */
+#include "splendor_oracle.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ game tables
+ * Card / noble data: SplendorLogic.py:320-473. Cards are [color][k] -> (cost[5], pts);
+ * the gain row is one-hot(color) + points (SplendorLogic.py:336-467).               */
+static const int8_t NOBLES[10][5] = {
+    {0,0,4,4,0},{0,0,0,4,4},{0,4,4,0,0},{4,0,0,0,4},{4,4,0,0,0},
+    {3,0,0,3,3},{3,3,3,0,0},{0,0,3,3,3},{0,3,3,3,0},{3,3,0,0,3}};
+/* deck colour order in the tables: blue, red, black, white, green (gain colours) */
+static const int8_t DECK_GAIN_COLOR[5] = {1, 3, 4, 0, 2};
+static const int8_t T1[5][8][6] = {
+ {{0,0,0,0,3,0},{1,0,0,0,2,0},{0,0,2,0,2,0},{1,0,2,2,0,0},{0,1,3,1,0,0},{1,0,1,1,1,0},{1,0,1,2,1,0},{0,0,0,4,0,1}},
+ {{3,0,0,0,0,0},{0,2,1,0,0,0},{2,0,0,2,0,0},{2,0,1,0,2,0},{1,0,0,1,3,0},{1,1,1,0,1,0},{2,1,1,0,1,0},{4,0,0,0,0,1}},
+ {{0,0,3,0,0,0},{0,0,2,1,0,0},{2,0,2,0,0,0},{2,2,0,1,0,0},{0,0,1,3,1,0},{1,1,1,1,0,0},{1,2,1,1,0,0},{0,4,0,0,0,1}},
+ {{0,3,0,0,0,0},{0,0,0,2,1,0},{0,2,0,0,2,0},{0,2,2,0,1,0},{3,1,0,0,1,0},{0,1,1,1,1,0},{0,1,2,1,1,0},{0,0,4,0,0,1}},
+ {{0,0,0,3,0,0},{2,1,0,0,0,0},{0,2,0,2,0,0},{0,1,0,2,2,0},{1,3,1,0,0,0},{1,1,0,1,1,0},{1,1,0,1,2,0},{0,0,0,0,4,1}}};
+static const int8_t T2[5][6][6] = {
+ {{0,2,2,3,0,1},{0,2,3,0,3,1},{0,5,0,0,0,2},{5,3,0,0,0,2},{2,0,0,1,4,2},{0,6,0,0,0,3}},
+ {{2,0,0,2,3,1},{0,3,0,2,3,1},{0,0,0,0,5,2},{3,0,0,0,5,2},{1,4,2,0,0,2},{0,0,0,6,0,3}},
+ {{3,2,2,0,0,1},{3,0,3,0,2,1},{5,0,0,0,0,2},{0,0,5,3,0,2},{0,1,4,2,0,2},{0,0,0,0,6,3}},
+ {{0,0,3,2,2,1},{2,3,0,3,0,1},{0,0,0,5,0,2},{0,0,0,5,3,2},{0,0,1,4,2,2},{6,0,0,0,0,3}},
+ {{2,3,0,0,2,1},{3,0,2,3,0,1},{0,0,5,0,0,2},{0,5,3,0,0,2},{4,2,0,0,1,2},{0,0,6,0,0,3}}};
+static const int8_t T3[5][4][6] = {
+ {{3,0,3,3,5,3},{7,0,0,0,0,4},{6,3,0,0,3,4},{7,3,0,0,0,5}},
+ {{3,5,3,0,3,3},{0,0,7,0,0,4},{0,3,6,3,0,4},{0,0,7,3,0,5}},
+ {{3,3,5,3,0,3},{0,0,0,7,0,4},{0,0,3,6,3,4},{0,0,0,7,3,5}},
+ {{0,3,3,5,3,3},{0,0,0,0,7,4},{3,0,0,3,6,4},{3,0,0,0,7,5}},
+ {{5,3,0,3,3,3},{0,7,0,0,0,4},{3,6,3,0,0,4},{0,7,3,0,0,5}}};
+static const int8_t DECK_LEN[3] = {8, 6, 4};
+
+static const int8_t *card_of(int tier, int color, int k) {
+    if (tier == 0) return T1[color][k];
+    if (tier == 1) return T2[color][k];
+    return T3[color][k];
+}
+
+/* gem combinations (SplendorLogic.py:250-280): itertools.combinations order */
+static int8_t DIFF3[25][5];     /* np_different_gems_up_to_3 */
+static int8_t SPEC3[40][5];     /* np_2specs_gems_up_to_3   */
+/* Board.give_ids (SplendorLogicNumba.py:100-166), used slices only */
+static const int8_t GIVE0[10][2] = {{3,4},{2,4},{2,3},{1,4},{1,3},{1,2},{0,4},{0,3},{0,2},{0,1}};
+static const int8_t GIVE1[10][3] = {{14,18,19},{13,17,19},{12,17,18},{11,16,19},{10,16,18},
+                                    {9,16,17},{8,15,19},{7,15,18},{6,15,17},{5,15,16}};
+static const int8_t GIVE2[10][6] = {{12,13,14,17,18,19},{10,11,14,16,18,19},{9,11,13,17,16,19},
+                                    {9,10,12,17,16,18},{7,8,14,15,19,18},{6,8,13,15,19,17},
+                                    {6,7,12,15,18,17},{5,8,11,15,19,16},{5,7,10,15,18,16},
+                                    {6,5,9,15,16,17}};
+static const int8_t GIVE3[5][10] = {{9,12,13,10,11,14,17,16,18,19},{6,7,8,12,13,14,15,17,18,19},
+                                    {5,7,8,10,11,14,15,16,18,19},{6,5,8,9,13,11,15,17,16,19},
+                                    {6,5,7,9,12,10,15,17,16,18}};
+static const int8_t GIVE4[10][3] = {{2,3,4},{1,3,4},{1,2,4},{1,2,3},{0,3,4},{0,2,4},{0,2,3},
+                                    {0,1,4},{0,1,3},{0,1,2}};
+static const int8_t GIVE5[5][4] = {{1,2,3,4},{0,2,3,4},{0,1,3,4},{0,1,2,4},{0,1,2,3}};
+static const int8_t GIVE_T1[20] = {1,2,3,4, 0,2,3,4, 0,1,3,4, 0,1,2,4, 0,1,2,3};
+/* give_ids3 (SplendorLogicNumba.py:169-210): (take3 id, give id, give id) */
+static const int8_t GIVE_IDS3[40][3] = {
+ {0,3,18},{0,18,4},{0,3,19},{0,19,4},{1,2,17},{1,17,4},{1,2,19},{1,19,4},{2,2,17},{2,17,3},
+ {2,2,18},{2,18,3},{3,1,16},{3,16,4},{3,1,19},{3,19,4},{4,1,16},{4,16,3},{4,1,18},{4,18,3},
+ {5,1,16},{5,16,2},{5,1,17},{5,17,2},{6,0,15},{6,15,4},{6,0,19},{6,19,4},{7,0,15},{7,15,3},
+ {7,0,18},{7,18,3},{8,0,15},{8,15,2},{8,0,17},{8,17,2},{9,0,15},{9,15,1},{9,0,16},{9,16,1}};
+
+/* give option g in [0,20): 0..14 = DIFF3[0..14] (up-to-2 different), 15..19 = 2 of one */
+static void give_vec(int g, int8_t v[5]) {
+    memset(v, 0, 5);
+    if (g < 15) memcpy(v, DIFF3[g], 5); else v[g - 15] = 2;
+}
+static void take_vec(int t, int8_t v[5]) {  /* t in [0,30): 25 different + 5 identical */
+    memset(v, 0, 5);
+    if (t < 25) memcpy(v, DIFF3[t], 5); else v[t - 25] = 2;
+}
+
+static int tables_ready = 0;
+static void build_tables(void) {
+    if (tables_ready) return;
+    int k = 0;
+    for (int c = 0; c < 5; c++) { memset(DIFF3[k], 0, 5); DIFF3[k][c] = 1; k++; }
+    for (int a = 0; a < 5; a++) for (int b = a + 1; b < 5; b++) {
+        memset(DIFF3[k], 0, 5); DIFF3[k][a] = DIFF3[k][b] = 1; k++; }
+    for (int a = 0; a < 5; a++) for (int b = a + 1; b < 5; b++) for (int c = b + 1; c < 5; c++) {
+        memset(DIFF3[k], 0, 5); DIFF3[k][a] = DIFF3[k][b] = DIFF3[k][c] = 1; k++; }
+    for (int i = 0; i < 40; i++) {
+        int8_t g1[5], g2[5];
+        give_vec(GIVE_IDS3[i][1], g1); give_vec(GIVE_IDS3[i][2], g2);
+        for (int c = 0; c < 5; c++) SPEC3[i][c] = (int8_t)(g1[c] + g2[c]);
+    }
+    tables_ready = 1;
+}
+
+/* ------------------------------------------------------------------ layout */
+typedef struct { int n, nn, bank, tiers, decks, nobles, gems, pnobles, cards, rsv, rows; } lay_t;
+static lay_t lay(int n) {
+    lay_t L; L.n = n; L.nn = n + 1;
+    L.bank = 0; L.tiers = 1; L.decks = 25; L.nobles = 31; L.gems = 32 + n;
+    L.pnobles = 32 + 2 * n; L.cards = 32 + 3 * n + n * n; L.rsv = 32 + 4 * n + n * n;
+    L.rows = 32 + 10 * n + n * n;
+    return L;
+}
+#define RW(s, r) ((s) + 7 * (r))
+
+int or_rows(int n) { return 32 + 10 * n + n * n; }
+int or_get_round(const int8_t *s) { return (uint8_t)s[6]; }
+
+int or_get_score(int n, const int8_t *s, int p) {
+    lay_t L = lay(n);
+    int sc = RW(s, L.cards + p)[6];
+    for (int i = 0; i < 3; i++) sc += RW(s, L.pnobles + 3 * p + i)[6];  /* hard-coded 3 :219 */
+    return sc;
+}
+
+static int sum7(const int8_t *r) { int t = 0; for (int c = 0; c < 7; c++) t += r[c]; return t; }
+static int sum5(const int8_t *r) { int t = 0; for (int c = 0; c < 5; c++) t += r[c]; return t; }
+
+/* ------------------------------------------------------------------ chance */
+/* my_random_choice: searchsorted(cumsum(prob), U, side='right') (:39-41) */
+static int rand_choice(const double *prob, int len, double u) {
+    double c = 0.0;
+    for (int i = 0; i < len; i++) { c += prob[i]; if (c > u) return i; }
+    return len;
+}
+
+typedef struct { const double *u; int used; } chance_t;
+static double draw(chance_t *ch) { return ch->u[ch->used++]; }
+
+/* _get_deck_card (:400-420). Returns 0 if the deck is empty. */
+static int deck_card(lay_t L, int8_t *s, int tier, chance_t *ch, int8_t out[14]) {
+    int8_t *cnt = RW(s, L.decks + 2 * tier), *bits = RW(s, L.decks + 2 * tier + 1);
+    int tot = sum5(cnt);
+    if (tot == 0) return 0;
+    double p[8];
+    for (int c = 0; c < 5; c++) p[c] = (double)cnt[c] / (double)tot;
+    int color = rand_choice(p, 5, draw(ch));
+    if (color > 4) color = 4;                     /* unreachable (prob ~1e-16) */
+    uint8_t b = (uint8_t)bits[color];
+    int nb = 0; int on[8];
+    for (int k = 0; k < 8; k++) { on[k] = (b >> (7 - k)) & 1; nb += on[k]; }
+    for (int k = 0; k < 8; k++) p[k] = (double)on[k] / (double)nb;
+    int idx = rand_choice(p, 8, draw(ch));
+    if (idx > 7) idx = 7;
+    b &= (uint8_t)~(1u << (7 - idx));
+    bits[color] = (int8_t)b;                      /* packbits + int8 wrap (:44-46) */
+    cnt[color] -= 1;
+    const int8_t *cd = card_of(tier, color, idx);
+    memset(out, 0, 14);
+    memcpy(out, cd, 5);
+    out[7 + DECK_GAIN_COLOR[color]] = 1;
+    out[7 + 6] = cd[5];
+    return 1;
+}
+
+void or_card(int tier, int color, int k, int8_t *out) {
+    const int8_t *cd = card_of(tier, color, k);
+    memset(out, 0, 14); memcpy(out, cd, 5);
+    out[7 + DECK_GAIN_COLOR[color]] = 1; out[13] = cd[5];
+}
+
+static void fill_new_card(lay_t L, int8_t *s, int tier, int idx, int det, chance_t *ch) {
+    int8_t *slot = RW(s, L.tiers + 8 * tier + 2 * idx);
+    memset(slot, 0, 14);
+    if (!det) { int8_t c[14]; if (deck_card(L, s, tier, ch, c)) memcpy(slot, c, 14); }
+}
+
+void or_init(int n, int8_t *s, const double *u, int *used) {
+    build_tables();
+    lay_t L = lay(n);
+    chance_t ch = {u, 0};
+    memset(s, 0, (size_t)7 * L.rows);
+    int g = n == 2 ? 4 : (n == 3 ? 5 : 7);
+    for (int c = 0; c < 5; c++) s[c] = (int8_t)g;
+    s[5] = 5;
+    for (int t = 0; t < 3; t++) {
+        uint8_t bits = (uint8_t)(0xFFu << (8 - DECK_LEN[t]));
+        for (int c = 0; c < 5; c++) {
+            RW(s, L.decks + 2 * t)[c] = DECK_LEN[t];
+            RW(s, L.decks + 2 * t + 1)[c] = (int8_t)bits;   /* 255/252/240 -> -1/-4/-16 */
+        }
+    }
+    for (int t = 0; t < 3; t++)
+        for (int i = 0; i < 4; i++) fill_new_card(L, s, t, i, 0, &ch);
+    int perm[10]; for (int i = 0; i < 10; i++) perm[i] = i;
+    for (int i = 0; i < L.nn; i++) {       /* injected noble draw (make_golden.py) */
+        int j = i + (int)floor(draw(&ch) * (10 - i));
+        int t = perm[i]; perm[i] = perm[j]; perm[j] = t;
+    }
+    for (int i = 0; i < L.nn; i++) {
+        int8_t *r = RW(s, L.nobles + i);
+        memcpy(r, NOBLES[perm[i]], 5); r[5] = 0; r[6] = 3;
+    }
+    if (used) *used = ch.used;
+}
+
+/* ------------------------------------------------------------------ valid moves */
+void or_valid_moves(int n, const int8_t *s, int p, uint8_t *res) {
+    build_tables();
+    lay_t L = lay(n);
+    const int8_t *bank = RW(s, 0), *gems = RW(s, L.gems + p), *cards = RW(s, L.cards + p);
+    int T = sum7(gems), gold = gems[5];
+    memset(res, 0, OR_ACTIONS);
+    /* _valid_buy :476-501 */
+    for (int i = 0; i < 12; i++) {
+        const int8_t *cost = RW(s, L.tiers + 2 * i);
+        int miss = 0;
+        for (int c = 0; c < 5; c++) { int d = cost[c] - gems[c] - cards[c]; if (d > 0) miss += d; }
+        res[i] = (miss <= gold) && sum5(cost) != 0;
+    }
+    /* _valid_reserve :508-515 (no-limit flags kept for the exchange block) */
+    uint8_t rsv[15];
+    int slot_free = sum5(RW(s, L.rsv + 6 * p + 5)) == 0;
+    for (int i = 0; i < 15; i++) {
+        const int8_t *r = i < 12 ? RW(s, L.tiers + 2 * i) : RW(s, L.decks + 2 * (i - 12));
+        rsv[i] = (sum5(r) != 0) && slot_free;
+    }
+    int limited = (T == 10 && bank[5] > 0);
+    for (int i = 0; i < 15; i++) res[12 + i] = limited ? 0 : rsv[i];
+    /* _valid_buy_reserve :538-552 */
+    for (int i = 0; i < 3; i++) {
+        const int8_t *cost = RW(s, L.rsv + 6 * p + 2 * i);
+        int miss = 0;
+        for (int c = 0; c < 5; c++) { int d = cost[c] - gems[c] - cards[c]; if (d > 0) miss += d; }
+        res[27 + i] = (miss <= gold) && sum5(cost) != 0;
+    }
+    /* _valid_get_gems / _identical :562-583 */
+    uint8_t get[30];
+    int nspec = 0;
+    for (int c = 0; c < 5; c++) nspec += bank[c] != 0;
+    for (int i = 0; i < 25; i++) {
+        int ok = 1, k = 0;
+        for (int c = 0; c < 5; c++) { ok &= (bank[c] - DIFF3[i][c]) >= 0; k += DIFF3[i][c]; }
+        get[i] = (uint8_t)ok;
+        int lim = ok && (T + k <= 10);
+        if (i < 5 && T != 9 && nspec != 1) lim = 0;
+        if (i >= 5 && i < 15 && T != 8 && nspec != 2) lim = 0;
+        res[30 + i] = (uint8_t)lim;
+    }
+    for (int c = 0; c < 5; c++) {
+        get[25 + c] = bank[c] >= 4;
+        res[55 + c] = get[25 + c] && (T + 2 <= 10);
+    }
+    /* give flags :595-613 */
+    uint8_t giv[20], giv3[40];
+    for (int g = 0; g < 20; g++) {
+        int8_t v[5]; give_vec(g, v); int ok = 1;
+        for (int c = 0; c < 5; c++) ok &= (gems[c] - v[c]) >= 0;
+        giv[g] = (uint8_t)ok;
+    }
+    for (int k = 0; k < 40; k++) {
+        int ok = 1;
+        for (int c = 0; c < 5; c++) ok &= (gems[c] - SPEC3[k][c]) >= 0;
+        giv3[k] = (uint8_t)ok;
+    }
+    /* _valid_exchange :615-680 */
+    uint8_t *ex = res + 60;
+    const uint8_t *dif2 = get + 5, *dif3 = get + 15, *same2 = get + 25;
+    if (T == 8) {
+        for (int k = 0; k < 20; k++) ex[k] = dif3[k / 2] && giv[GIVE0[k / 2][k % 2]];
+    } else if (T == 9) {
+        for (int k = 0; k < 30; k++) ex[20 + k] = dif3[k / 3] && giv[GIVE1[k / 3][k % 3]];
+        for (int k = 0; k < 30; k++) ex[160 + k] = dif2[k / 3] && giv[GIVE4[k / 3][k % 3]];
+        for (int k = 0; k < 20; k++) ex[190 + k] = same2[k / 4] && giv[GIVE5[k / 4][k % 4]];
+    } else if (T >= 10) {
+        for (int k = 0; k < 60; k++) ex[50 + k] = dif2[k / 6] && giv[GIVE2[k / 6][k % 6]];
+        for (int k = 0; k < 50; k++) ex[110 + k] = same2[k / 10] && giv[GIVE3[k / 10][k % 10]];
+        for (int k = 0; k < 20; k++) ex[210 + k] = get[k / 4] && giv[GIVE_T1[k]];
+        for (int k = 0; k < 40; k++) ex[305 + k] = dif3[k / 4] && giv3[k];
+        if (bank[5] > 0)
+            for (int k = 0; k < 75; k++) ex[230 + k] = rsv[k / 5] && giv[k % 5];
+    }
+    /* select-noble 405..407 never valid (WIP stub :682); pass iff nothing else */
+    int any = 0;
+    for (int a = 0; a < 408; a++) any |= res[a];
+    res[408] = !any;
+}
+
+/* ------------------------------------------------------------------ make move */
+static void give_nobles(lay_t L, int8_t *s, int p) {      /* :763-768 */
+    for (int i = 0; i < L.nn; i++) {
+        int8_t *nob = RW(s, L.nobles + i);
+        const int8_t *cards = RW(s, L.cards + p);
+        if (sum5(nob) > 0) {
+            int ok = 1;
+            for (int c = 0; c < 5; c++) ok &= cards[c] >= nob[c];
+            if (ok) { memcpy(RW(s, L.pnobles + L.nn * p + i), nob, 7); memset(nob, 0, 7); }
+        }
+    }
+}
+
+static void buy_card(lay_t L, int8_t *s, const int8_t *cost, const int8_t *gain, int p) {
+    int8_t *bank = RW(s, 0), *gems = RW(s, L.gems + p), *cards = RW(s, L.cards + p);
+    int miss = 0;
+    for (int c = 0; c < 5; c++) { int d = cost[c] - gems[c] - cards[c]; if (d > 0) miss += d; }
+    for (int c = 0; c < 5; c++) {
+        int need = cost[c] - cards[c]; if (need < 0) need = 0;
+        int paid = need < gems[c] ? need : gems[c];
+        gems[c] = (int8_t)(gems[c] - paid);
+        bank[c] = (int8_t)(bank[c] + paid);
+    }
+    gems[5] = (int8_t)(gems[5] - miss);
+    bank[5] = (int8_t)(bank[5] + miss);
+    int8_t g[7]; memcpy(g, gain, 7);           /* gain may alias a row we write below */
+    for (int c = 0; c < 7; c++) cards[c] = (int8_t)(cards[c] + g[c]);
+    give_nobles(L, s, p);
+}
+
+static void move_gems(lay_t L, int8_t *s, const int8_t v[5], int p, int sign) {
+    int8_t *bank = RW(s, 0), *gems = RW(s, L.gems + p);
+    for (int c = 0; c < 5; c++) {
+        bank[c] = (int8_t)(bank[c] - sign * v[c]);
+        gems[c] = (int8_t)(gems[c] + sign * v[c]);
+    }
+}
+static void get_gems(lay_t L, int8_t *s, int t, int p) { int8_t v[5]; take_vec(t, v); move_gems(L, s, v, p, +1); }
+static void give_gems(lay_t L, int8_t *s, int g, int p) { int8_t v[5]; give_vec(g, v); move_gems(L, s, v, p, -1); }
+
+static void reserve(lay_t L, int8_t *s, int i, int p, int det, chance_t *ch) {   /* :517-536 */
+    int slot = -1;
+    for (int k = 0; k < 3; k++)
+        if (sum5(RW(s, L.rsv + 6 * p + 2 * k)) == 0) { slot = L.rsv + 6 * p + 2 * k; break; }
+    if (i < 12) {
+        int tier = i / 4, idx = i % 4;
+        if (slot >= 0) memcpy(RW(s, slot), RW(s, L.tiers + 8 * tier + 2 * idx), 14);
+        fill_new_card(L, s, tier, idx, det, ch);
+    } else if (!det) {
+        int8_t c[14];
+        if (deck_card(L, s, i - 12, ch, c) && slot >= 0) memcpy(RW(s, slot), c, 14);
+    }
+    if (s[5] > 0) { RW(s, L.gems + p)[5] += 1; s[5] -= 1; }
+}
+
+static void give_and_get(lay_t L, int8_t *s, int i, int p) {     /* :697-756 */
+    if (i < 20)       { get_gems(L, s, i / 2 + 15, p); give_gems(L, s, GIVE0[i / 2][i % 2], p); }
+    else if (i < 50)  { i -= 20;  get_gems(L, s, i / 3 + 15, p); give_gems(L, s, GIVE1[i / 3][i % 3], p); }
+    else if (i < 110) { i -= 50;  get_gems(L, s, i / 6 + 5, p);  give_gems(L, s, GIVE2[i / 6][i % 6], p); }
+    else if (i < 160) { i -= 110; get_gems(L, s, i / 10 + 25, p); give_gems(L, s, GIVE3[i / 10][i % 10], p); }
+    else if (i < 190) { i -= 160; get_gems(L, s, i / 3 + 5, p);  give_gems(L, s, GIVE4[i / 3][i % 3], p); }
+    else if (i < 210) { i -= 190; get_gems(L, s, i / 4 + 25, p); give_gems(L, s, GIVE5[i / 4][i % 4], p); }
+    else if (i < 230) { i -= 210; get_gems(L, s, i / 4, p);      give_gems(L, s, GIVE_T1[i], p); }
+    else {
+        i -= 305;
+        get_gems(L, s, GIVE_IDS3[i][0] + 15, p);
+        give_gems(L, s, GIVE_IDS3[i][1], p);
+        give_gems(L, s, GIVE_IDS3[i][2], p);
+    }
+}
+
+int or_make_move(int n, int8_t *s, int a, int p, int det, const double *u, int *used) {
+    build_tables();
+    lay_t L = lay(n);
+    chance_t ch = {u, 0};
+    if (a < 12) {
+        buy_card(L, s, RW(s, L.tiers + 2 * a), RW(s, L.tiers + 2 * a + 1), p);
+        fill_new_card(L, s, a / 4, a % 4, det, &ch);
+    } else if (a < 27) {
+        reserve(L, s, a - 12, p, det, &ch);
+    } else if (a < 30) {
+        int i = a - 27, st = L.rsv + 6 * p + 2 * i;
+        buy_card(L, s, RW(s, st), RW(s, st + 1), p);
+        if (i < 2) memmove(RW(s, st), RW(s, st + 2), (size_t)7 * (6 * p + 4 + L.rsv - st));
+        memset(RW(s, L.rsv + 6 * p + 4), 0, 14);
+    } else if (a < 60) {
+        get_gems(L, s, a - 30, p);
+    } else if (a < 290) {
+        give_and_get(L, s, a - 60, p);
+    } else if (a < 365) {
+        int i = a - 290;
+        reserve(L, s, i / 5, p, det, &ch);
+        give_gems(L, s, i % 5, p);
+    } else if (a < 405) {
+        give_and_get(L, s, a - 60, p);
+    } /* 405..408: no-op (undefined at HEAD, see make_golden.py P5) */
+    s[6] = (int8_t)(s[6] + 1);
+    if (used) *used = ch.used;
+    return (p + 1) % n;
+}
+
+/* ------------------------------------------------------------------ end / swap */
+void or_check_end(int n, const int8_t *s, float *out) {
+    lay_t L = lay(n);
+    for (int i = 0; i < n; i++) out[i] = 0.f;
+    int r = (uint8_t)s[6];
+    if (r % n != 0) return;
+    int sc[4], mx = -1000;
+    for (int p = 0; p < n; p++) { sc[p] = (int8_t)or_get_score(n, s, p); if (sc[p] > mx) mx = sc[p]; }
+    if (!(mx >= 15 || r >= 62 * n)) return;
+    int nmax = 0;
+    for (int p = 0; p < n; p++) nmax += sc[p] == mx;
+    if (nmax == 1) { for (int p = 0; p < n; p++) out[p] = sc[p] == mx ? 1.f : -1.f; return; }
+    int8_t masked[4], mn = 127;
+    for (int p = 0; p < n; p++) {
+        masked[p] = (int8_t)sum5(RW(s, L.cards + p));
+        if (sc[p] < mx) masked[p] = (int8_t)-25;  /* int8(999) (:313) */
+        if (masked[p] < mn) mn = masked[p];
+    }
+    int cnt = 0;
+    for (int p = 0; p < n; p++) cnt += masked[p] == mn;
+    for (int p = 0; p < n; p++) out[p] = masked[p] == mn ? (cnt > 1 ? 0.01f : 1.f) : -1.f;
+}
+
+static void roll_rows(int8_t *blk, int rows, int shift) {
+    int8_t tmp[7 * 40];
+    memcpy(tmp, blk, (size_t)7 * rows);
+    for (int i = 0; i < rows; i++) memcpy(blk + 7 * i, tmp + 7 * ((i + shift) % rows), 7);
+}
+
+void or_swap_players(int n, int8_t *s, int k) {
+    lay_t L = lay(n);
+    roll_rows(RW(s, L.gems), n, k);
+    roll_rows(RW(s, L.pnobles), n * (n + 1), 3 * k);  /* hard-coded 3 (:345) */
+    roll_rows(RW(s, L.cards), n, k);
+    roll_rows(RW(s, L.rsv), 6 * n, 6 * k);
+}
+
+int or_tree_step(int n, const int8_t *parent, int a, int8_t *child) {
+    memcpy(child, parent, (size_t)7 * or_rows(n));
+    int nxt = or_make_move(n, child, a, 0, 1, NULL, NULL);
+    if (nxt != 0) or_swap_players(n, child, nxt);
+    return nxt;
+}
+
+/* ------------------------------------------------------------------ symmetries */
+static const int8_t CARD_SYM[3][4] = {{1,3,0,2},{2,0,3,1},{3,2,1,0}};   /* SplendorLogic.py:283 */
+static const int8_t RSV_SYM[4][2][3] = {{{-1,-1,-1},{-1,-1,-1}},{{-1,-1,-1},{-1,-1,-1}},
+                                        {{1,0,2},{-1,-1,-1}},{{1,2,0},{2,0,1}}};
+
+int or_symmetries(int n, const int8_t *s, const float *pi, const uint8_t *va,
+                  int8_t *os, float *op, uint8_t *ov) {
+    lay_t L = lay(n);
+    int S = 7 * L.rows, cnt = 0;
+#define EMIT_BASE() do { memcpy(os + (size_t)cnt * S, s, S); memcpy(op + cnt * 409, pi, 409 * 4); \
+                         memcpy(ov + cnt * 409, va, 409); } while (0)
+    EMIT_BASE(); cnt++;
+    for (int t = 0; t < 3; t++) for (int q = 0; q < 3; q++) {
+        EMIT_BASE();
+        int8_t *st = os + (size_t)cnt * S;
+        for (int i = 0; i < 4; i++) {
+            int src = CARD_SYM[q][i];
+            memcpy(RW(st, L.tiers + 8 * t + 2 * i), RW(s, L.tiers + 8 * t + 2 * src), 14);
+            op[cnt * 409 + 4 * t + i] = pi[4 * t + src];
+            op[cnt * 409 + 12 + 4 * t + i] = pi[12 + 4 * t + src];
+            ov[cnt * 409 + 4 * t + i] = va[4 * t + src];
+            ov[cnt * 409 + 12 + 4 * t + i] = va[12 + 4 * t + src];
+        }
+        cnt++;
+    }
+    for (int p = 0; p < n; p++) {
+        int nb = 3;
+        for (int c = 0; c < 3; c++) if (sum5(RW(s, L.rsv + 6 * p + 2 * c)) == 0) { nb = c; break; }
+        for (int q = 0; q < 2; q++) {
+            const int8_t *perm = RSV_SYM[nb][q];
+            if (perm[0] < 0) continue;
+            EMIT_BASE();
+            int8_t *st = os + (size_t)cnt * S;
+            for (int i = 0; i < 3; i++)
+                memcpy(RW(st, L.rsv + 6 * p + 2 * i), RW(s, L.rsv + 6 * p + 2 * perm[i]), 14);
+            if (p == 0)
+                for (int i = 0; i < 3; i++) {
+                    op[cnt * 409 + 27 + i] = pi[27 + perm[i]];
+                    ov[cnt * 409 + 27 + i] = va[27 + perm[i]];
+                }
+            cnt++;
+        }
+    }
+#undef EMIT_BASE
+    return cnt;
+}
+
+/* ------------------------------------------------------------------ Philox */
+void or_philox4x32(uint32_t k0, uint32_t k1, const uint32_t in[4], uint32_t out[4]) {
+    uint32_t c0 = in[0], c1 = in[1], c2 = in[2], c3 = in[3];
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+double or_uniform(uint64_t seed, uint32_t board, uint32_t stream, uint32_t d) {
+    uint32_t ctr[4] = {d, board, stream, 0x53504C44u /* 'SPLD' */}, o[4];
+    or_philox4x32((uint32_t)seed, (uint32_t)(seed >> 32), ctr, o);
+    return ((double)(o[0] >> 5) * 67108864.0 + (double)(o[1] >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+/* ------------------------------------------------------------------ fake NN */
+uint64_t or_state_hash(const int8_t *st, int bytes) {
+    uint64_t h = 0xCBF29CE484222325ull;
+    for (int i = 0; i < bytes; i++) { h ^= (uint8_t)st[i]; h *= 0x100000001B3ull; }
+    return h;
+}
+static uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+void or_fake_predict(int n, const int8_t *st, const uint8_t *va, float *pi, float *v) {
+    uint64_t h = or_state_hash(st, 7 * or_rows(n));
+    for (int a = 0; a < 409; a++)
+        pi[a] = va[a] ? (float)((double)(1 + (splitmix64(h + (uint64_t)a) >> 40)) * 0x1p-24) : 0.f;
+    for (int i = 0; i < n; i++)
+        v[i] = (float)((double)(splitmix64(h ^ (0xA5A5ull + (uint64_t)i)) >> 40) * 0x1p-23 - 1.0);
+}
+
+static float pw_sum(const float *a, int len) {   /* numpy pairwise_sum, float32 */
+    if (len < 8) { float r = 0.f; for (int i = 0; i < len; i++) r += a[i]; return r; }
+    if (len <= 128) {
+        float r[8]; int i;
+        for (int j = 0; j < 8; j++) r[j] = a[j];
+        for (i = 8; i < len - (len % 8); i += 8) for (int j = 0; j < 8; j++) r[j] += a[i + j];
+        float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < len; i++) res += a[i];
+        return res;
+    }
+    int n2 = len / 2; n2 -= n2 % 8;
+    return pw_sum(a, n2) + pw_sum(a + n2, len - n2);
+}
+float or_np_sum_f32(const float *x, int len) { return pw_sum(x, len); }
+
+/* ------------------------------------------------------------------ MCTS */
+#define NAN_Q (-42.0)
+typedef struct {
+    int8_t *key;              /* state bytes */
+    int terminal, has_ps;
+    float es[4];
+    uint8_t vs[409];
+    float ps[409];
+    long long ns;
+    double qsa[409];
+    long long nsa[409];
+    double qs;
+} node_t;
+
+struct or_mcts {
+    int n, S, sims, forced;
+    double cpuct, fpu;
+    node_t **slots; int cap, count;
+    int step;
+};
+
+or_mcts *or_mcts_new(int n, int sims, double cpuct, double fpu, int forced) {
+    build_tables();
+    or_mcts *m = (or_mcts *)calloc(1, sizeof(or_mcts));
+    m->n = n; m->S = 7 * or_rows(n); m->sims = sims; m->cpuct = cpuct; m->fpu = fpu;
+    m->forced = forced; m->cap = 1 << 12;
+    m->slots = (node_t **)calloc((size_t)m->cap, sizeof(node_t *));
+    return m;
+}
+void or_mcts_free(or_mcts *m) {
+    for (int i = 0; i < m->cap; i++) if (m->slots[i]) { free(m->slots[i]->key); free(m->slots[i]); }
+    free(m->slots); free(m);
+}
+static node_t **lookup(or_mcts *m, const int8_t *st) {
+    uint64_t h = or_state_hash(st, m->S);
+    int i = (int)(h & (uint64_t)(m->cap - 1));
+    while (m->slots[i] && memcmp(m->slots[i]->key, st, (size_t)m->S) != 0) i = (i + 1) & (m->cap - 1);
+    return &m->slots[i];
+}
+static node_t *insert(or_mcts *m, const int8_t *st) {
+    if (2 * (m->count + 1) > m->cap) {
+        node_t **old = m->slots; int oc = m->cap;
+        m->cap *= 2; m->slots = (node_t **)calloc((size_t)m->cap, sizeof(node_t *));
+        for (int i = 0; i < oc; i++) if (old[i]) *lookup(m, old[i]->key) = old[i];
+        free(old);
+    }
+    node_t **slot = lookup(m, st);
+    node_t *nd = (node_t *)calloc(1, sizeof(node_t));
+    nd->key = (int8_t *)malloc((size_t)m->S); memcpy(nd->key, st, (size_t)m->S);
+    *slot = nd; m->count++;
+    return nd;
+}
+
+/* pick_highest_UCB (MCTS.py:199-219), float64 as Numba types it */
+static int pick_ucb(or_mcts *m, node_t *nd, int forced) {
+    double best = -INFINITY; int ba = -1;
+    double fpu_init = m->fpu > 0 ? nd->qs - m->fpu : m->fpu;
+    for (int a = 0; a < 409; a++) {
+        if (!nd->vs[a]) continue;
+        double P = (double)nd->ps[a];
+        if (forced && (double)nd->nsa[a] < (double)(long long)sqrt(0.5 * P * (double)m->step)) return a;
+        double u;
+        if (nd->qsa[a] != NAN_Q) u = nd->qsa[a] + m->cpuct * P * sqrt((double)nd->ns) / (double)(1 + nd->nsa[a]);
+        else u = fpu_init + m->cpuct * P * sqrt((double)nd->ns + 1e-8);
+        if (u > best) { best = u; ba = a; }
+    }
+    return ba;
+}
+
+static void search(or_mcts *m, const int8_t *st, int forced, float *vout) {
+    int n = m->n;
+    node_t *nd = *lookup(m, st);
+    if (!nd) {
+        float es[4]; or_check_end(n, st, es);
+        int any = 0; for (int i = 0; i < n; i++) any |= es[i] != 0.f;
+        nd = insert(m, st);
+        memcpy(nd->es, es, sizeof es);
+        if (any) { nd->terminal = 1; memcpy(vout, es, sizeof(float) * n); return; }
+    } else if (nd->terminal) { memcpy(vout, nd->es, sizeof(float) * n); return; }
+    if (!nd->has_ps) {
+        or_valid_moves(n, st, 0, nd->vs);
+        float v[4];
+        or_fake_predict(n, st, nd->vs, nd->ps, v);
+        float sum = pw_sum(nd->ps, 409);        /* normalise (MCTS.py:239-242) */
+        for (int a = 0; a < 409; a++) nd->ps[a] = nd->ps[a] / sum;
+        nd->has_ps = 1; nd->ns = 0; nd->qs = (double)v[0];
+        for (int a = 0; a < 409; a++) { nd->qsa[a] = NAN_Q; nd->nsa[a] = 0; }
+        memcpy(vout, v, sizeof(float) * n);
+        return;
+    }
+    int a = pick_ucb(m, nd, forced);
+    int8_t *child = (int8_t *)malloc((size_t)m->S);
+    int nxt = or_tree_step(n, st, a, child);
+    float vc[4];
+    search(m, child, 0, vc);
+    free(child);
+    nd = *lookup(m, st);                       /* table may have been rehashed */
+    for (int i = 0; i < n; i++) vout[i] = vc[((i - nxt) % n + n) % n];   /* np.roll */
+    double v0 = (double)vout[0];
+    nd->qsa[a] = ((double)nd->nsa[a] * nd->qsa[a] + v0) / (double)(nd->nsa[a] + 1);
+    nd->qs = ((double)(nd->ns + 1) * nd->qs + v0) / (double)(nd->ns + 2);
+    nd->nsa[a] += 1; nd->ns += 1;
+}
+
+int or_mcts_search(or_mcts *m, const int8_t *root, int64_t *counts, double *qsa,
+                   double *probs, double *q) {
+    float v[4];
+    for (m->step = 0; m->step < m->sims; m->step++) search(m, root, m->forced, v);
+    node_t *nd = *lookup(m, root);
+    long long c[409], best = 0;
+    for (int a = 0; a < 409; a++) { c[a] = nd->nsa[a]; if (c[a] > best) best = c[a]; }
+    if (m->forced) {                                  /* MCTS.py:69-74 */
+        for (int a = 0; a < 409; a++) {
+            if (c[a] != best) c[a] -= (long long)sqrt(0.5 * (double)nd->ps[a] * (double)m->sims);
+            if (c[a] <= 1) c[a] = 0;
+        }
+    }
+    long long tot = 0;
+    for (int a = 0; a < 409; a++) tot += c[a];
+    for (int a = 0; a < 409; a++) {
+        counts[a] = nd->nsa[a]; qsa[a] = nd->qsa[a];
+        probs[a] = (double)c[a] / (double)tot;
+    }
+    q[0] = nd->qs;
+    for (int i = 1; i < m->n; i++) q[i] = -nd->qs / (double)(m->n - 1);
+    return m->count;
+}
+
+/* ------------------------------------------------------------------ CPU baseline loop */
+long long or_random_rollouts(int n, int B, int steps, uint64_t seed, int threads) {
+    (void)threads;
+    int S = 7 * or_rows(n);
+    int8_t *st = (int8_t *)malloc((size_t)B * S), canon[7 * 88];
+    int *pl = (int *)calloc((size_t)B, sizeof(int));
+    uint8_t mask[409];
+    double u[40];
+    long long done = 0;
+    for (int b = 0; b < B; b++) {
+        for (int d = 0; d < 40; d++) u[d] = or_uniform(seed, (uint32_t)b, 0xFFFFFFFFu, (uint32_t)d);
+        or_init(n, st + (size_t)b * S, u, NULL);
+    }
+    for (int t = 0; t < steps; t++) {
+        for (int b = 0; b < B; b++) {
+            int8_t *s = st + (size_t)b * S;
+            memcpy(canon, s, (size_t)S);
+            if (pl[b]) or_swap_players(n, canon, pl[b]);
+            or_valid_moves(n, canon, 0, mask);
+            int cnt = 0; for (int a = 0; a < 409; a++) cnt += mask[a];
+            int k = (int)(or_uniform(seed, (uint32_t)b, (uint32_t)t, 0) * cnt), a = 0;
+            for (a = 0; a < 409; a++) if (mask[a] && k-- == 0) break;
+            u[0] = or_uniform(seed, (uint32_t)b, (uint32_t)t, 1);
+            u[1] = or_uniform(seed, (uint32_t)b, (uint32_t)t, 2);
+            pl[b] = or_make_move(n, s, a, pl[b], 0, u, NULL);
+            float e[4]; or_check_end(n, s, e);
+            int any = 0; for (int i = 0; i < n; i++) any |= e[i] != 0.f;
+            if (any) {
+                for (int d = 0; d < 29; d++) u[d] = or_uniform(seed, (uint32_t)b, (uint32_t)t, 3u + (uint32_t)d);
+                or_init(n, s, u, NULL);
+                pl[b] = 0;
+            }
+            done++;
+        }
+    }
+    free(st); free(pl);
+    return done;
+}

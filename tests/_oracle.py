@@ -1,0 +1,170 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so). Test infrastructure only."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(ORACLE_DIR, "splendor_oracle.c")
+        if (not os.path.exists(LIB_PATH)) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        L = C.CDLL(LIB_PATH)
+        p8, pu8, pf, pd, pi = (C.POINTER(C.c_int8), C.POINTER(C.c_uint8), C.POINTER(C.c_float),
+                               C.POINTER(C.c_double), C.POINTER(C.c_int))
+        L.or_rows.argtypes = [C.c_int]
+        L.or_init.argtypes = [C.c_int, p8, pd, pi]
+        L.or_valid_moves.argtypes = [C.c_int, p8, C.c_int, pu8]
+        L.or_make_move.argtypes = [C.c_int, p8, C.c_int, C.c_int, C.c_int, pd, pi]
+        L.or_make_move.restype = C.c_int
+        L.or_check_end.argtypes = [C.c_int, p8, pf]
+        L.or_swap_players.argtypes = [C.c_int, p8, C.c_int]
+        L.or_get_score.argtypes = [C.c_int, p8, C.c_int]
+        L.or_get_round.argtypes = [p8]
+        L.or_card.argtypes = [C.c_int, C.c_int, C.c_int, p8]
+        L.or_tree_step.argtypes = [C.c_int, p8, C.c_int, p8]
+        L.or_symmetries.argtypes = [C.c_int, p8, pf, pu8, p8, pf, pu8]
+        L.or_uniform.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.or_uniform.restype = C.c_double
+        L.or_state_hash.argtypes = [p8, C.c_int]
+        L.or_state_hash.restype = C.c_uint64
+        L.or_fake_predict.argtypes = [C.c_int, p8, pu8, pf, pf]
+        L.or_np_sum_f32.argtypes = [pf, C.c_int]
+        L.or_np_sum_f32.restype = C.c_float
+        L.or_mcts_new.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, C.c_int]
+        L.or_mcts_new.restype = C.c_void_p
+        L.or_mcts_free.argtypes = [C.c_void_p]
+        L.or_mcts_search.argtypes = [C.c_void_p, p8, C.POINTER(C.c_int64), pd, pd, pd]
+        L.or_random_rollouts.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int]
+        L.or_random_rollouts.restype = C.c_longlong
+        L.or_philox4x32.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def rows(n):
+    return lib().or_rows(n)
+
+
+def init(n, uniforms):
+    st = np.zeros((rows(n), 7), np.int8)
+    u = np.ascontiguousarray(uniforms, np.float64)
+    used = C.c_int(0)
+    lib().or_init(n, _p(st, C.c_int8), _p(u, C.c_double), C.byref(used))
+    return st, used.value
+
+
+def valid_moves(n, state, player):
+    st = np.ascontiguousarray(state, np.int8)
+    m = np.zeros(409, np.uint8)
+    lib().or_valid_moves(n, _p(st, C.c_int8), player, _p(m, C.c_uint8))
+    return m
+
+
+def make_move(n, state, action, player, deterministic, uniforms=()):
+    st = np.array(state, np.int8, copy=True)
+    u = np.ascontiguousarray(np.concatenate([np.asarray(uniforms, np.float64), np.zeros(4)]))
+    used = C.c_int(0)
+    nxt = lib().or_make_move(n, _p(st, C.c_int8), int(action), int(player), int(deterministic),
+                             _p(u, C.c_double), C.byref(used))
+    return st, nxt, used.value
+
+
+def check_end(n, state):
+    st = np.ascontiguousarray(state, np.int8)
+    out = np.zeros(n, np.float32)
+    lib().or_check_end(n, _p(st, C.c_int8), _p(out, C.c_float))
+    return out
+
+
+def swap_players(n, state, k):
+    st = np.array(state, np.int8, copy=True)
+    lib().or_swap_players(n, _p(st, C.c_int8), int(k))
+    return st
+
+
+def score(n, state, p):
+    st = np.ascontiguousarray(state, np.int8)
+    return lib().or_get_score(n, _p(st, C.c_int8), p)
+
+
+def tree_step(n, state, action):
+    st = np.ascontiguousarray(state, np.int8)
+    out = np.zeros_like(st)
+    nxt = lib().or_tree_step(n, _p(st, C.c_int8), int(action), _p(out, C.c_int8))
+    return out, nxt
+
+
+def card(tier, color, k):
+    out = np.zeros((2, 7), np.int8)
+    lib().or_card(tier, color, k, _p(out, C.c_int8))
+    return out
+
+
+def symmetries(n, state, pi, valids):
+    st = np.ascontiguousarray(state, np.int8)
+    pi = np.ascontiguousarray(pi, np.float32)
+    va = np.ascontiguousarray(valids, np.uint8)
+    mx = 1 + 9 + 2 * n
+    os_ = np.zeros((mx,) + st.shape, np.int8)
+    op = np.zeros((mx, 409), np.float32)
+    ov = np.zeros((mx, 409), np.uint8)
+    k = lib().or_symmetries(n, _p(st, C.c_int8), _p(pi, C.c_float), _p(va, C.c_uint8),
+                            _p(os_, C.c_int8), _p(op, C.c_float), _p(ov, C.c_uint8))
+    return os_[:k], op[:k], ov[:k]
+
+
+def uniform(seed, board, stream, draw):
+    return lib().or_uniform(seed, board, stream, draw)
+
+
+def fake_predict(n, state, valids):
+    st = np.ascontiguousarray(state, np.int8)
+    va = np.ascontiguousarray(valids, np.uint8)
+    pi = np.zeros(409, np.float32)
+    v = np.zeros(n, np.float32)
+    lib().or_fake_predict(n, _p(st, C.c_int8), _p(va, C.c_uint8), _p(pi, C.c_float), _p(v, C.c_float))
+    return pi, v
+
+
+def np_sum_f32(x):
+    x = np.ascontiguousarray(x, np.float32)
+    return np.float32(lib().or_np_sum_f32(_p(x, C.c_float), len(x)))
+
+
+class Mcts:
+    def __init__(self, n, sims, cpuct, fpu, forced):
+        self.n = n
+        self.h = lib().or_mcts_new(n, sims, cpuct, fpu, int(forced))
+
+    def search(self, root):
+        st = np.ascontiguousarray(root, np.int8)
+        counts = np.zeros(409, np.int64)
+        qsa = np.zeros(409, np.float64)
+        probs = np.zeros(409, np.float64)
+        q = np.zeros(self.n, np.float64)
+        nodes = lib().or_mcts_search(self.h, _p(st, C.c_int8), _p(counts, C.c_int64),
+                                     _p(qsa, C.c_double), _p(probs, C.c_double), _p(q, C.c_double))
+        return counts, qsa, probs, q, nodes
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_mcts_free(self.h)
+            self.h = None
+
+
+def random_rollouts(n, B, steps, seed, threads=1):
+    return lib().or_random_rollouts(n, B, steps, seed, threads)
