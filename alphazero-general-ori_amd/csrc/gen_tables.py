@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Emits splendor_tables.h: the device constant tables of the Splendor engine.
+
+Card / noble data are the game's published component lists (reference data tables at
+SplendorLogic.py:320-473). Gem-combination tables follow SplendorLogic.py:250-280
+(itertools.combinations order). The 409-entry action descriptor table encodes
+SplendorLogicNumba.valid_moves (:251-265) as "flag0 AND flag1 AND condition", so a wave
+evaluates 64 actions per instruction stream with no divergence.
+
+Run:  python gen_tables.py > splendor_tables.h
+"""
+import itertools
+
+NOBLES = [(0, 0, 4, 4, 0), (0, 0, 0, 4, 4), (0, 4, 4, 0, 0), (4, 0, 0, 0, 4), (4, 4, 0, 0, 0),
+          (3, 0, 0, 3, 3), (3, 3, 3, 0, 0), (0, 0, 3, 3, 3), (0, 3, 3, 3, 0), (3, 3, 0, 0, 3)]
+# deck column c holds cards whose gain colour is GAIN[c]
+GAIN = (1, 3, 4, 0, 2)
+# (cost white, blue, green, red, black, points) per [deck column][card]
+TIER1 = [
+    [(0,0,0,0,3,0),(1,0,0,0,2,0),(0,0,2,0,2,0),(1,0,2,2,0,0),(0,1,3,1,0,0),(1,0,1,1,1,0),(1,0,1,2,1,0),(0,0,0,4,0,1)],
+    [(3,0,0,0,0,0),(0,2,1,0,0,0),(2,0,0,2,0,0),(2,0,1,0,2,0),(1,0,0,1,3,0),(1,1,1,0,1,0),(2,1,1,0,1,0),(4,0,0,0,0,1)],
+    [(0,0,3,0,0,0),(0,0,2,1,0,0),(2,0,2,0,0,0),(2,2,0,1,0,0),(0,0,1,3,1,0),(1,1,1,1,0,0),(1,2,1,1,0,0),(0,4,0,0,0,1)],
+    [(0,3,0,0,0,0),(0,0,0,2,1,0),(0,2,0,0,2,0),(0,2,2,0,1,0),(3,1,0,0,1,0),(0,1,1,1,1,0),(0,1,2,1,1,0),(0,0,4,0,0,1)],
+    [(0,0,0,3,0,0),(2,1,0,0,0,0),(0,2,0,2,0,0),(0,1,0,2,2,0),(1,3,1,0,0,0),(1,1,0,1,1,0),(1,1,0,1,2,0),(0,0,0,0,4,1)]]
+TIER2 = [
+    [(0,2,2,3,0,1),(0,2,3,0,3,1),(0,5,0,0,0,2),(5,3,0,0,0,2),(2,0,0,1,4,2),(0,6,0,0,0,3)],
+    [(2,0,0,2,3,1),(0,3,0,2,3,1),(0,0,0,0,5,2),(3,0,0,0,5,2),(1,4,2,0,0,2),(0,0,0,6,0,3)],
+    [(3,2,2,0,0,1),(3,0,3,0,2,1),(5,0,0,0,0,2),(0,0,5,3,0,2),(0,1,4,2,0,2),(0,0,0,0,6,3)],
+    [(0,0,3,2,2,1),(2,3,0,3,0,1),(0,0,0,5,0,2),(0,0,0,5,3,2),(0,0,1,4,2,2),(6,0,0,0,0,3)],
+    [(2,3,0,0,2,1),(3,0,2,3,0,1),(0,0,5,0,0,2),(0,5,3,0,0,2),(4,2,0,0,1,2),(0,0,6,0,0,3)]]
+TIER3 = [
+    [(3,0,3,3,5,3),(7,0,0,0,0,4),(6,3,0,0,3,4),(7,3,0,0,0,5)],
+    [(3,5,3,0,3,3),(0,0,7,0,0,4),(0,3,6,3,0,4),(0,0,7,3,0,5)],
+    [(3,3,5,3,0,3),(0,0,0,7,0,4),(0,0,3,6,3,4),(0,0,0,7,3,5)],
+    [(0,3,3,5,3,3),(0,0,0,0,7,4),(3,0,0,3,6,4),(3,0,0,0,7,5)],
+    [(5,3,0,3,3,3),(0,7,0,0,0,4),(3,6,3,0,0,4),(0,7,3,0,0,5)]]
+
+# exchange give tables (Board.give_ids slices actually read, SplendorLogicNumba.py:100-166)
+GIVE0 = [[3,4],[2,4],[2,3],[1,4],[1,3],[1,2],[0,4],[0,3],[0,2],[0,1]]
+GIVE1 = [[14,18,19],[13,17,19],[12,17,18],[11,16,19],[10,16,18],[9,16,17],[8,15,19],[7,15,18],[6,15,17],[5,15,16]]
+GIVE2 = [[12,13,14,17,18,19],[10,11,14,16,18,19],[9,11,13,17,16,19],[9,10,12,17,16,18],[7,8,14,15,19,18],
+         [6,8,13,15,19,17],[6,7,12,15,18,17],[5,8,11,15,19,16],[5,7,10,15,18,16],[6,5,9,15,16,17]]
+GIVE3 = [[9,12,13,10,11,14,17,16,18,19],[6,7,8,12,13,14,15,17,18,19],[5,7,8,10,11,14,15,16,18,19],
+         [6,5,8,9,13,11,15,17,16,19],[6,5,7,9,12,10,15,17,16,18]]
+GIVE4 = [[2,3,4],[1,3,4],[1,2,4],[1,2,3],[0,3,4],[0,2,4],[0,2,3],[0,1,4],[0,1,3],[0,1,2]]
+GIVE5 = [[1,2,3,4],[0,2,3,4],[0,1,3,4],[0,1,2,4],[0,1,2,3]]
+GIVE_T1 = [1,2,3,4, 0,2,3,4, 0,1,3,4, 0,1,2,4, 0,1,2,3]
+GIVE_IDS3 = [(0,3,18),(0,18,4),(0,3,19),(0,19,4),(1,2,17),(1,17,4),(1,2,19),(1,19,4),(2,2,17),(2,17,3),
+             (2,2,18),(2,18,3),(3,1,16),(3,16,4),(3,1,19),(3,19,4),(4,1,16),(4,16,3),(4,1,18),(4,18,3),
+             (5,1,16),(5,16,2),(5,1,17),(5,17,2),(6,0,15),(6,15,4),(6,0,19),(6,19,4),(7,0,15),(7,15,3),
+             (7,0,18),(7,18,3),(8,0,15),(8,15,2),(8,0,17),(8,17,2),(9,0,15),(9,15,1),(9,0,16),(9,16,1)]
+
+
+def combos():
+    out = []
+    for k in (1, 2, 3):
+        for c in itertools.combinations(range(5), k):
+            out.append(tuple(1 if i in c else 0 for i in range(5)))
+    return out
+
+
+DIFF = combos()                      # 25 (first 15 = up to 2 different)
+TAKE = DIFF + [tuple(2 if i == c else 0 for i in range(5)) for c in range(5)]  # 30
+GIVE = DIFF[:15] + [tuple(2 if i == c else 0 for i in range(5)) for c in range(5)]  # 20
+SPEC3 = [tuple(GIVE[a][c] + GIVE[b][c] for c in range(5)) for (_, a, b) in GIVE_IDS3]
+
+# condition codes (must match splendor_device.h)
+C_ALWAYS, C_RSV_LIMIT, C_TAKE1, C_TAKE2D, C_TAKE3, C_TAKE2S, C_EX8, C_EX9, C_EX10, C_EX10G, C_NEVER = range(11)
+
+
+def desc(i0, i1, cond):
+    d = cond << 16
+    if i0 is not None:
+        d |= (1 << 6) | i0
+    if i1 is not None:
+        d |= (1 << 14) | (i1 << 8)
+    return d
+
+
+def action_table():
+    t = []
+    for a in range(12):
+        t.append(desc(a, None, C_ALWAYS))
+    for a in range(12, 27):
+        t.append(desc(a, None, C_RSV_LIMIT))
+    for a in range(27, 30):
+        t.append(desc(a, None, C_ALWAYS))
+    for a in range(30, 35):
+        t.append(desc(a, None, C_TAKE1))
+    for a in range(35, 45):
+        t.append(desc(a, None, C_TAKE2D))
+    for a in range(45, 55):
+        t.append(desc(a, None, C_TAKE3))
+    for a in range(55, 60):
+        t.append(desc(a, None, C_TAKE2S))
+    t += [desc(45 + k // 2, GIVE0[k // 2][k % 2], C_EX8) for k in range(20)]          # 60-79
+    t += [desc(45 + k // 3, GIVE1[k // 3][k % 3], C_EX9) for k in range(30)]          # 80-109
+    t += [desc(35 + k // 6, GIVE2[k // 6][k % 6], C_EX10) for k in range(60)]         # 110-169
+    t += [desc(55 + k // 10, GIVE3[k // 10][k % 10], C_EX10) for k in range(50)]      # 170-219
+    t += [desc(35 + k // 3, GIVE4[k // 3][k % 3], C_EX9) for k in range(30)]          # 220-249
+    t += [desc(55 + k // 4, GIVE5[k // 4][k % 4], C_EX9) for k in range(20)]          # 250-269
+    t += [desc(30 + k // 4, GIVE_T1[k], C_EX10) for k in range(20)]                   # 270-289
+    t += [desc(12 + k // 5, k % 5, C_EX10G) for k in range(75)]                       # 290-364
+    t += [desc(45 + k // 4, 20 + k, C_EX10) for k in range(40)]                       # 365-404
+    t += [desc(None, None, C_NEVER)] * 4                                              # 405-408
+    assert len(t) == 409
+    return t
+
+
+# move decode for _give_and_get_gems / _reserve_and_give (SplendorLogicNumba.py:697-761):
+# for exchange action a in [60,405): (take id in TAKE, give id 1 in GIVE, give id 2 or 255,
+# reserve index or 255)
+def exchange_table():
+    t = []
+    for a in range(60, 405):
+        i = a - 60
+        if a >= 290 and a < 365:
+            j = a - 290
+            t.append((255, j % 5, 255, j // 5))
+        elif i < 20:
+            t.append((i // 2 + 15, GIVE0[i // 2][i % 2], 255, 255))
+        elif i < 50:
+            k = i - 20; t.append((k // 3 + 15, GIVE1[k // 3][k % 3], 255, 255))
+        elif i < 110:
+            k = i - 50; t.append((k // 6 + 5, GIVE2[k // 6][k % 6], 255, 255))
+        elif i < 160:
+            k = i - 110; t.append((k // 10 + 25, GIVE3[k // 10][k % 10], 255, 255))
+        elif i < 190:
+            k = i - 160; t.append((k // 3 + 5, GIVE4[k // 3][k % 3], 255, 255))
+        elif i < 210:
+            k = i - 190; t.append((k // 4 + 25, GIVE5[k // 4][k % 4], 255, 255))
+        elif i < 230:
+            k = i - 210; t.append((k // 4, GIVE_T1[k], 255, 255))
+        else:
+            k = i - 305; tk, g1, g2 = GIVE_IDS3[k]; t.append((tk + 15, g1, g2, 255))
+    return t
+
+
+def arr(name, ctype, rows, fmt=str):
+    body = ",\n  ".join("{" + ",".join(fmt(x) for x in r) + "}" if isinstance(r, (list, tuple)) else fmt(r)
+                        for r in rows)
+    return f"{name} = {{\n  {body}}};\n"
+
+
+def main():
+    out = ["// GENERATED by gen_tables.py — do not edit by hand.",
+           "#pragma once", "#include <stdint.h>", ""]
+    cards = []
+    for tier, tab in enumerate((TIER1, TIER2, TIER3)):
+        for col in range(5):
+            for k in range(8):
+                if k < len(tab[col]):
+                    cost = tab[col][k][:5]
+                    pts = tab[col][k][5]
+                    cards.append(list(cost) + [GAIN[col], pts, 0])
+                else:
+                    cards.append([0] * 8)
+    out.append("// [tier*40 + deckcol*8 + k] -> cost[5], gain colour, points, pad")
+    out.append(arr("static __constant__ int8_t K_CARDS[120][8]", None, cards))
+    out.append(arr("static __constant__ int8_t K_NOBLES[10][8]", None, [list(n) + [0, 3, 0] for n in NOBLES]))
+    out.append(arr("static __constant__ int8_t K_TAKE[30][8]", None, [list(v) + [sum(v), 0, 0] for v in TAKE]))
+    out.append(arr("static __constant__ int8_t K_GIVE[20][8]", None, [list(v) + [sum(v), 0, 0] for v in GIVE]))
+    out.append(arr("static __constant__ int8_t K_SPEC3[40][8]", None, [list(v) + [0, 0, 0] for v in SPEC3]))
+    out.append("// action descriptor: bits0-5 flag0 idx, bit6 use flag0, bits8-13 flag1 idx, bit14 use flag1,")
+    out.append("// bits16-19 condition code")
+    out.append(arr("static __constant__ uint32_t K_ACTION_DESC[409]", None, action_table(), lambda x: f"0x{x:06x}u"))
+    out.append("// exchange actions 60..404: take id, give id, give id (255 none), reserve index (255 none)")
+    out.append(arr("static __constant__ uint8_t K_EXCHANGE[345][4]", None, exchange_table()))
+    print("\n".join(out))
+
+
+if __name__ == "__main__":
+    main()

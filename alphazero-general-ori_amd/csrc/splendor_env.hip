@@ -1,0 +1,335 @@
+// splendor_env.hip — batched Splendor environment kernels for gfx950 + the C ABI
+// declared in include/splendor_amd.h.
+//
+// Mapping: one 64-lane wave per board, 4 boards per 256-thread workgroup; each wave stages
+// its board in its own LDS slot (Lay<N>::SPAD bytes), so boards never share LDS and no
+// workgroup barrier is needed (waves exit independently). Device logic: splendor_device.h.
+#include <hip/hip_runtime.h>
+
+#include <new>
+
+#include "../../include/splendor_amd.h"
+#include "splendor_device.h"
+
+using namespace spl;
+
+struct spl_ctx {
+    int n;
+    int token_limit;
+};
+
+namespace {
+
+constexpr int WAVES = 4;            // boards per workgroup
+constexpr int THREADS = 64 * WAVES;
+
+__device__ __forceinline__ uint64_t pick_word(const uint64_t w[7], int j) {
+    uint64_t v = w[0];
+#pragma unroll
+    for (int k = 1; k < 7; k++) v = j == k ? w[k] : v;
+    return v;
+}
+
+template <int N>
+__device__ __forceinline__ void store_board(int8_t *dst, const int8_t *lds) {
+    wave_copy_board<N>(dst, lds);
+}
+
+// ---------------------------------------------------------------- kernels
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_init(int B, int8_t *__restrict__ state,
+                                                  int8_t *__restrict__ player,
+                                                  const double *__restrict__ u, int ustride,
+                                                  uint64_t seed, uint32_t stream, uint32_t bbase) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
+    if (b >= B) return;
+    int8_t *s = lds[w];
+    Chance ch{u ? u + (size_t)b * ustride : nullptr, seed, bbase + (uint32_t)b, stream, 0};
+    init_game<N>(s, ch);
+    store_board<N>(state + (size_t)b * Lx::S, s);
+    if (player && lane_id() == 0) player[b] = 0;
+}
+
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_valid(int B, const int8_t *__restrict__ state,
+                                                   const int8_t *__restrict__ player, int lim,
+                                                   uint64_t *__restrict__ mask) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
+    if (b >= B) return;
+    int8_t *s = lds[w];
+    wave_copy_board<N>(s, state + (size_t)b * Lx::S);
+    const int p = player ? player[b] : 0;
+    uint64_t m[7];
+    wave_valid_moves<N>(s, p, lim, m);
+    const int l = lane_id();
+    if (l < 7) mask[(size_t)b * 7 + l] = pick_word(m, l);
+}
+
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_step(int B, int8_t *__restrict__ state,
+                                                  const int8_t *__restrict__ player,
+                                                  const int16_t *__restrict__ action,
+                                                  int8_t *__restrict__ next_player, int det,
+                                                  const double *__restrict__ u, int ustride,
+                                                  uint64_t seed, uint32_t stream, uint32_t bbase,
+                                                  int32_t *err) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
+    if (b >= B) return;
+    const int a = action[b];
+    const int p = player ? player[b] : 0;
+    if (a < 0 || a >= SPL_ACTIONS) {
+        if (err && lane_id() == 0) atomicOr(err, SPL_ERR_BAD_ACTION);
+        if (next_player && lane_id() == 0) next_player[b] = (int8_t)p;
+        return;
+    }
+    int8_t *s = lds[w];
+    int8_t *g = state + (size_t)b * Lx::S;
+    wave_copy_board<N>(s, g);
+    Chance ch{u ? u + (size_t)b * ustride : nullptr, seed, bbase + (uint32_t)b, stream, 0};
+    const int nxt = make_move<N>(s, a, p, det != 0, ch);
+    __builtin_amdgcn_wave_barrier();
+    store_board<N>(g, s);
+    if (next_player && lane_id() == 0) next_player[b] = (int8_t)nxt;
+}
+
+// end / score / round read ~20 bytes per board: one lane per board straight from HBM
+template <int N>
+__global__ __launch_bounds__(256) void k_ended(int B, const int8_t *__restrict__ state,
+                                               float *__restrict__ out) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    float e[N];
+    check_end<N>(state + (size_t)b * Lay<N>::S, e);
+#pragma unroll
+    for (int i = 0; i < N; i++) out[(size_t)b * N + i] = e[i];
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_score_round(int B, const int8_t *__restrict__ state,
+                                                     int32_t *__restrict__ score,
+                                                     int32_t *__restrict__ round) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    const int8_t *s = state + (size_t)b * Lay<N>::S;
+    if (score)
+#pragma unroll
+        for (int p = 0; p < N; p++) score[(size_t)b * N + p] = get_score<N>(s, p);
+    if (round) round[b] = (uint8_t)s[6];
+}
+
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_canonical(int B, const int8_t *__restrict__ state,
+                                                       const int8_t *__restrict__ player,
+                                                       int8_t *out) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
+    if (b >= B) return;
+    int8_t *s = lds[w];
+    wave_copy_board<N>(s, state + (size_t)b * Lx::S);
+    const int p = player ? player[b] : 0;
+    if (p) wave_roll_players<N>(s, s, p);
+    store_board<N>(out + (size_t)b * Lx::S, s);
+}
+
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__restrict__ parent,
+                                                       const int16_t *__restrict__ action,
+                                                       int8_t *__restrict__ child, int32_t *err) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
+    if (b >= B) return;
+    int8_t *s = lds[w];
+    wave_copy_board<N>(s, parent + (size_t)b * Lx::S);
+    const int a = action[b];
+    if (a < 0 || a >= SPL_ACTIONS) {
+        if (err && lane_id() == 0) atomicOr(err, SPL_ERR_BAD_ACTION);
+    } else {
+        Chance ch{nullptr, 0, 0, 0, 0};
+        const int nxt = make_move<N>(s, a, 0, true, ch);
+        __builtin_amdgcn_wave_barrier();
+        if (nxt) wave_roll_players<N>(s, s, nxt);
+    }
+    store_board<N>(child + (size_t)b * Lx::S, s);
+}
+
+// Fused random-policy self-play step (see splendor_amd.h spl_rollout_step)
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_rollout(int B, int8_t *__restrict__ state,
+                                                     int8_t *__restrict__ player, int lim,
+                                                     uint64_t *__restrict__ mask_out,
+                                                     int16_t *__restrict__ action_out,
+                                                     float *__restrict__ ended_out,
+                                                     int32_t *__restrict__ games_done,
+                                                     uint64_t seed, uint32_t step, uint32_t bbase) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][2][Lx::SPAD];
+    const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
+    if (b >= B) return;
+    const int l = lane_id();
+    int8_t *s = lds[w][0], *c = lds[w][1];
+    int8_t *g = state + (size_t)b * Lx::S;
+    wave_copy_board<N>(s, g);
+    const int p = player[b];
+    wave_roll_players<N>(c, s, p);                       // getCanonicalForm
+    uint64_t m[7];
+    wave_valid_moves<N>(c, 0, lim, m);                   // getValidMoves(canonical, 0)
+    if (l < 7) mask_out[(size_t)b * 7 + l] = pick_word(m, l);
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < 7; j++) cnt += __popcll(m[j]);
+    const uint32_t gb = bbase + (uint32_t)b;
+    const int k = (int)(philox_u01(seed, gb, step, 0) * (double)cnt);
+    const int a = select_bit(m, k);
+    Chance ch{nullptr, seed, gb, step, 1};
+    int nxt = make_move<N>(s, a, p, false, ch);          // getNextState (chance)
+    __builtin_amdgcn_wave_barrier();
+    float e[N];
+    check_end<N>(s, e);                                  // getGameEnded
+    bool ended = false;
+#pragma unroll
+    for (int i = 0; i < N; i++) ended |= e[i] != 0.f;
+    if (l < N) ended_out[(size_t)b * N + l] = e[l < N ? l : 0];
+    if (l == 0) action_out[b] = (int16_t)a;
+    if (ended) {                                         // auto-reset finished games
+        Chance ch2{nullptr, seed, gb, step, 3};
+        init_game<N>(s, ch2);
+        nxt = 0;
+        if (games_done && l == 0) games_done[b] += 1;
+    }
+    store_board<N>(g, s);
+    if (l == 0) player[b] = (int8_t)nxt;
+}
+
+// ---------------------------------------------------------------- launch helpers
+inline int check_launch() { return hipGetLastError() == hipSuccess ? 0 : SPL_EDEVICE; }
+inline dim3 wave_grid(int B) { return dim3((unsigned)((B + WAVES - 1) / WAVES)); }
+inline dim3 lane_grid(int B) { return dim3((unsigned)((B + 255) / 256)); }
+inline bool ok_ctx(const spl_ctx *c) { return c && c->n >= 2 && c->n <= 4; }
+
+#define SPL_DISPATCH(n, CALL)            \
+    switch (n) {                         \
+        case 2: { constexpr int N = 2; CALL; break; } \
+        case 3: { constexpr int N = 3; CALL; break; } \
+        default: { constexpr int N = 4; CALL; break; } \
+    }
+
+}  // namespace
+
+// ---------------------------------------------------------------- C ABI
+extern "C" {
+
+int spl_abi_version(void) { return SPL_ABI_VERSION; }
+
+int spl_ctx_create(int n, int token_limit, spl_ctx **out) {
+    if (!out || n < 2 || n > 4 || token_limit < 3 || token_limit > 100) return SPL_EINVAL;
+    spl_ctx *c = new (std::nothrow) spl_ctx;
+    if (!c) return SPL_EINVAL;
+    c->n = n;
+    c->token_limit = token_limit;
+    *out = c;
+    return 0;
+}
+
+int spl_ctx_destroy(spl_ctx *ctx) {
+    delete ctx;
+    return 0;
+}
+
+int spl_state_rows(const spl_ctx *c) { return ok_ctx(c) ? 32 + 10 * c->n + c->n * c->n : SPL_EINVAL; }
+int spl_state_bytes(const spl_ctx *c) { return ok_ctx(c) ? 7 * spl_state_rows(c) : SPL_EINVAL; }
+
+int spl_init(const spl_ctx *c, int B, int8_t *state, int8_t *player_out, const double *u,
+             int u_stride, uint64_t seed, uint32_t stream, uint32_t board_base, void *hs) {
+    if (!ok_ctx(c) || B < 0 || (B && !state) || (u && u_stride < 29)) return SPL_EINVAL;
+    if (!B) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_init<N>, wave_grid(B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, B, state, player_out, u, u_stride,
+                                          seed, stream, board_base));
+    return check_launch();
+}
+
+int spl_valid_moves(const spl_ctx *c, int B, const int8_t *state, const int8_t *player,
+                    uint64_t *mask, void *hs) {
+    if (!ok_ctx(c) || B < 0 || (B && (!state || !mask))) return SPL_EINVAL;
+    if (!B) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_valid<N>, wave_grid(B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, B, state, player, c->token_limit, mask));
+    return check_launch();
+}
+
+int spl_step(const spl_ctx *c, int B, int8_t *state, const int8_t *player, const int16_t *action,
+             int8_t *next_player, int det, const double *u, int u_stride, uint64_t seed,
+             uint32_t stream, uint32_t board_base, int32_t *err, void *hs) {
+    if (!ok_ctx(c) || B < 0 || (B && (!state || !action)) || (u && u_stride < 2)) return SPL_EINVAL;
+    if (!B) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_step<N>, wave_grid(B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, B, state, player, action, next_player,
+                                          det, u, u_stride, seed, stream, board_base, err));
+    return check_launch();
+}
+
+int spl_game_ended(const spl_ctx *c, int B, const int8_t *state, float *out, void *hs) {
+    if (!ok_ctx(c) || B < 0 || (B && (!state || !out))) return SPL_EINVAL;
+    if (!B) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_ended<N>, lane_grid(B), dim3(256), 0,
+                                          (hipStream_t)hs, B, state, out));
+    return check_launch();
+}
+
+int spl_canonical(const spl_ctx *c, int B, const int8_t *state, const int8_t *player,
+                  int8_t *out, void *hs) {
+    if (!ok_ctx(c) || B < 0 || (B && (!state || !out))) return SPL_EINVAL;
+    if (!B) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_canonical<N>, wave_grid(B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, B, state, player, out));
+    return check_launch();
+}
+
+int spl_score(const spl_ctx *c, int B, const int8_t *state, int32_t *out, void *hs) {
+    if (!ok_ctx(c) || B < 0 || (B && (!state || !out))) return SPL_EINVAL;
+    if (!B) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_score_round<N>, lane_grid(B), dim3(256), 0,
+                                          (hipStream_t)hs, B, state, out, (int32_t *)nullptr));
+    return check_launch();
+}
+
+int spl_round(const spl_ctx *c, int B, const int8_t *state, int32_t *out, void *hs) {
+    if (!ok_ctx(c) || B < 0 || (B && (!state || !out))) return SPL_EINVAL;
+    if (!B) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_score_round<N>, lane_grid(B), dim3(256), 0,
+                                          (hipStream_t)hs, B, state, (int32_t *)nullptr, out));
+    return check_launch();
+}
+
+int spl_tree_step(const spl_ctx *c, int B, const int8_t *parent, const int16_t *action,
+                  int8_t *child, int32_t *err, void *hs) {
+    if (!ok_ctx(c) || B < 0 || (B && (!parent || !action || !child))) return SPL_EINVAL;
+    if (!B) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_tree_step<N>, wave_grid(B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, B, parent, action, child, err));
+    return check_launch();
+}
+
+int spl_rollout_step(const spl_ctx *c, int B, int8_t *state, int8_t *player, uint64_t *mask_out,
+                     int16_t *action_out, float *ended_out, int32_t *games_done, uint64_t seed,
+                     uint32_t step, uint32_t board_base, void *hs) {
+    if (!ok_ctx(c) || B < 0 ||
+        (B && (!state || !player || !mask_out || !action_out || !ended_out)))
+        return SPL_EINVAL;
+    if (!B) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_rollout<N>, wave_grid(B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, B, state, player, c->token_limit,
+                                          mask_out, action_out, ended_out, games_done, seed,
+                                          step, board_base));
+    return check_launch();
+}
+
+}  // extern "C"

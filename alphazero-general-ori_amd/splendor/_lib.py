@@ -1,0 +1,78 @@
+"""Loader for libsplendor_amd.so (the HIP/gfx950 engine, C ABI in include/splendor_amd.h).
+
+There is NO CPU fallback: if the shared library is missing or cannot be loaded, every
+entry point raises NativeEngineMissing. Build it with `python __graft_entry__.py build`
+(or `make -C alphazero-general-ori_amd`).
+"""
+import ctypes as C
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "libsplendor_amd.so")
+
+ABI_VERSION = 1
+EINVAL, EDEVICE = -1, -2
+
+
+class NativeEngineMissing(RuntimeError):
+    pass
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+_lib = None
+
+_vp, _i8p, _i16p, _i32p, _u64p, _fp, _dp = (C.c_void_p,) * 7
+_SIGS = {
+    "spl_abi_version": ([], C.c_int),
+    "spl_ctx_create": ([C.c_int, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "spl_ctx_destroy": ([C.c_void_p], C.c_int),
+    "spl_state_rows": ([C.c_void_p], C.c_int),
+    "spl_state_bytes": ([C.c_void_p], C.c_int),
+    "spl_init": ([C.c_void_p, C.c_int, _vp, _vp, _vp, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
+                  _vp], C.c_int),
+    "spl_valid_moves": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_step": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, C.c_int, _vp, C.c_int, C.c_uint64,
+                  C.c_uint32, C.c_uint32, _vp, _vp], C.c_int),
+    "spl_game_ended": ([C.c_void_p, C.c_int, _vp, _vp, _vp], C.c_int),
+    "spl_canonical": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_score": ([C.c_void_p, C.c_int, _vp, _vp, _vp], C.c_int),
+    "spl_round": ([C.c_void_p, C.c_int, _vp, _vp, _vp], C.c_int),
+    "spl_tree_step": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_rollout_step": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.c_uint32,
+                          C.c_uint32, _vp], C.c_int),
+}
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def lib():
+    """Load the engine once; raise loudly if it is not there."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeEngineMissing(
+            f"{LIB_PATH} not found: the HIP engine must be built (no CPU fallback exists)")
+    try:
+        L = C.CDLL(LIB_PATH)
+    except OSError as e:
+        raise NativeEngineMissing(f"cannot load {LIB_PATH}: {e}") from e
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    if L.spl_abi_version() != ABI_VERSION:
+        raise NativeEngineMissing(f"ABI mismatch: library {L.spl_abi_version()} != {ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        kind = {EINVAL: "invalid argument", EDEVICE: "HIP device error"}.get(rc, f"rc={rc}")
+        raise EngineError(f"{what}: {kind}")

@@ -1,0 +1,161 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X Splendor self-play hot path (BASELINE.json).
+
+Default workload = BASELINE config 2: 2-player Splendor, 32,768 concurrent boards per GPU,
+random-policy self-play, one fused HIP launch per step over every board (canonical form ->
+409-action legality mask -> action -> chance transition -> end check -> auto-reset).
+A "rollout" here is one board-step of that loop (BASELINE.md units). Data are synthetic:
+boards start from Philox-seeded deals (seed 0x5EED, board id) and reset on game end.
+
+Contract: `python bench.py --gpus N --steps K --warmup W`; for N>1 launched by
+torch.distributed.run, one rank per GPU; boards are sharded by board id (board_base =
+rank * B), no data-path collective; rank 0 prints ONE JSON line.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "alphazero-general-ori_amd"))
+
+import torch  # noqa: E402
+
+METRIC = "self-play rollouts/sec (32k boards, 2p Splendor) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+
+
+def bytes_per_board_step(n):
+    """Algorithmic HBM bytes of one fused rollout step for one board:
+    state read + write (2S), player read + write (2), packed mask (56), action (2), ended (4n)."""
+    S = 7 * (32 + 10 * n + n * n)
+    return 2 * S + 2 + 56 + 2 + 4 * n
+
+
+def cpu_baseline(n, seed, target_s=10.0):
+    """Time the oracle (scalar C port of the reference rules, oracle/) on one host core on
+    a bounded sample of the same workload (same boards, same Philox draws)."""
+    path = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not os.path.exists(path):
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    L = ctypes.CDLL(path)
+    L.or_random_rollouts.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int]
+    L.or_random_rollouts.restype = ctypes.c_longlong
+    B = 32768
+    t = time.perf_counter()
+    L.or_random_rollouts(n, B, 4, seed, 1)
+    probe = time.perf_counter() - t
+    steps = max(4, int(target_s / max(probe / 4, 1e-6)))
+    t = time.perf_counter()
+    done = L.or_random_rollouts(n, B, steps, seed, 1)
+    dt = time.perf_counter() - t
+    return {"value": done / dt, "unit": "rollouts/s", "cores": 1, "kind": "port",
+            "sample": f"{B} boards x {steps} steps (incl. initial deal) on 1 host core, "
+                      f"{dt:.1f} s, oracle/splendor_oracle.c or_random_rollouts"}
+
+
+def load_traffic(path, B):
+    """Measured HBM bytes per launch from a committed rocprofv3 --pmc summary, if any."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    if d.get("boards") != B:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--boards", type=int, default=32768, help="boards per GPU")
+    ap.add_argument("--players", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_rollout_step.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.gpus == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.players, args.seed)
+
+    from splendor.env import RolloutBatch, SplendorEngine
+    eng = SplendorEngine(args.players, device=dev)
+    B = args.boards
+    rb = RolloutBatch(eng, B, seed=args.seed, board_base=rank * B)
+    for _ in range(args.warmup):
+        rb.step()
+    torch.cuda.synchronize(dev)
+
+    K = args.steps
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(K):
+        starts[k].record()
+        rb.step()
+        ends[k].record()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / K
+    games = int(rb.games.sum().item())
+
+    if rank == 0:
+        per = bytes_per_board_step(args.players)
+        achieved = per * B / (kernel_ms * 1e-3) / 1e9
+        traffic = load_traffic(args.traffic_json, B)
+        out = {
+            "metric": METRIC,
+            "value": world * B * K / elapsed,
+            "unit": "rollouts/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int8",
+            "data": "synthetic (Philox-seeded deals, uniform-random legal actions)",
+            "config": {"workload": "config2: env-step-only random-policy self-play, fused "
+                                   "canonical+mask+action+chance step+end check+auto-reset",
+                       "players": args.players, "boards_per_gpu": B, "global_boards": world * B,
+                       "parallelism": f"dp{world} (board shards, no data-path collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_rollout<2>", "kernel_avg_us": kernel_ms * 1e3,
+                         "bytes_per_board_step": per},
+            "cpu_baseline": cpu,
+            "games_completed": games,
+        }
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -658,9 +658,13 @@ int or_mcts_search(or_mcts *m, const int8_t *root, int64_t *counts, double *qsa,
     return m->count;
 }
 
-/* ------------------------------------------------------------------ CPU baseline loop */
-long long or_random_rollouts(int n, int B, int steps, uint64_t seed, int threads) {
-    (void)threads;
+/* ------------------------------------------------------------------ rollout loop */
+/* The fused random-policy env step of spl_rollout_step (include/splendor_amd.h), run
+ * for B boards x steps. Outputs are optional (NULL = skip). Returns board-steps done. */
+long long or_rollout_run(int n, int B, int steps, uint64_t seed, uint32_t board_base,
+                         int8_t *state_out, int8_t *player_out, int16_t *actions,
+                         float *ended, int32_t *games, uint64_t *mask_fold) {
+    build_tables();
     int S = 7 * or_rows(n);
     int8_t *st = (int8_t *)malloc((size_t)B * S), canon[7 * 88];
     int *pl = (int *)calloc((size_t)B, sizeof(int));
@@ -668,31 +672,51 @@ long long or_random_rollouts(int n, int B, int steps, uint64_t seed, int threads
     double u[40];
     long long done = 0;
     for (int b = 0; b < B; b++) {
-        for (int d = 0; d < 40; d++) u[d] = or_uniform(seed, (uint32_t)b, 0xFFFFFFFFu, (uint32_t)d);
+        uint32_t gb = board_base + (uint32_t)b;
+        for (int d = 0; d < 29; d++) u[d] = or_uniform(seed, gb, 0xFFFFFFFFu, (uint32_t)d);
         or_init(n, st + (size_t)b * S, u, NULL);
+        if (games) games[b] = 0;
+        if (mask_fold) mask_fold[b] = 0;
     }
     for (int t = 0; t < steps; t++) {
         for (int b = 0; b < B; b++) {
+            uint32_t gb = board_base + (uint32_t)b;
             int8_t *s = st + (size_t)b * S;
             memcpy(canon, s, (size_t)S);
             if (pl[b]) or_swap_players(n, canon, pl[b]);
             or_valid_moves(n, canon, 0, mask);
-            int cnt = 0; for (int a = 0; a < 409; a++) cnt += mask[a];
-            int k = (int)(or_uniform(seed, (uint32_t)b, (uint32_t)t, 0) * cnt), a = 0;
+            int cnt = 0;
+            uint64_t w[7] = {0};
+            for (int a = 0; a < 409; a++) { cnt += mask[a]; if (mask[a]) w[a >> 6] |= 1ull << (a & 63); }
+            if (mask_fold) for (int j = 0; j < 7; j++) mask_fold[b] ^= (w[j] * (2 * (uint64_t)j + 1)) ^ ((uint64_t)t << 40);
+            int k = (int)(or_uniform(seed, gb, (uint32_t)t, 0) * (double)cnt), a;
             for (a = 0; a < 409; a++) if (mask[a] && k-- == 0) break;
-            u[0] = or_uniform(seed, (uint32_t)b, (uint32_t)t, 1);
-            u[1] = or_uniform(seed, (uint32_t)b, (uint32_t)t, 2);
+            if (a == 409) a = 408;
+            u[0] = or_uniform(seed, gb, (uint32_t)t, 1);
+            u[1] = or_uniform(seed, gb, (uint32_t)t, 2);
             pl[b] = or_make_move(n, s, a, pl[b], 0, u, NULL);
-            float e[4]; or_check_end(n, s, e);
-            int any = 0; for (int i = 0; i < n; i++) any |= e[i] != 0.f;
+            float e[4];
+            or_check_end(n, s, e);
+            int any = 0;
+            for (int i = 0; i < n; i++) any |= e[i] != 0.f;
+            if (actions) actions[(size_t)t * B + b] = (int16_t)a;
+            if (ended) for (int i = 0; i < n; i++) ended[((size_t)t * B + b) * n + i] = e[i];
             if (any) {
-                for (int d = 0; d < 29; d++) u[d] = or_uniform(seed, (uint32_t)b, (uint32_t)t, 3u + (uint32_t)d);
+                for (int d = 0; d < 29; d++) u[d] = or_uniform(seed, gb, (uint32_t)t, 3u + (uint32_t)d);
                 or_init(n, s, u, NULL);
                 pl[b] = 0;
+                if (games) games[b] += 1;
             }
             done++;
         }
     }
+    if (state_out) memcpy(state_out, st, (size_t)B * S);
+    if (player_out) for (int b = 0; b < B; b++) player_out[b] = (int8_t)pl[b];
     free(st); free(pl);
     return done;
+}
+
+long long or_random_rollouts(int n, int B, int steps, uint64_t seed, int threads) {
+    (void)threads;
+    return or_rollout_run(n, B, steps, seed, 0, NULL, NULL, NULL, NULL, NULL, NULL);
 }

@@ -71,6 +71,10 @@ int or_mcts_search(or_mcts *m, const int8_t *root, int64_t *counts, double *qsa,
  * mask -> uniform valid action -> chance step -> end check -> reset on end.
  * Returns total board-steps executed. threads<=0 => 1. */
 long long or_random_rollouts(int n, int B, int steps, uint64_t seed, int threads);
+/* same loop with traces (spl_rollout_step semantics, include/splendor_amd.h); NULL skips */
+long long or_rollout_run(int n, int B, int steps, uint64_t seed, uint32_t board_base,
+                         int8_t *state_out, int8_t *player_out, int16_t *actions,
+                         float *ended, int32_t *games, uint64_t *mask_fold);
 
 #ifdef __cplusplus
 }

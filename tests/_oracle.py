@@ -46,6 +46,9 @@ def lib():
         L.or_mcts_search.argtypes = [C.c_void_p, p8, C.POINTER(C.c_int64), pd, pd, pd]
         L.or_random_rollouts.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int]
         L.or_random_rollouts.restype = C.c_longlong
+        L.or_rollout_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint32, p8, p8,
+                                     C.POINTER(C.c_int16), pf, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
+        L.or_rollout_run.restype = C.c_longlong
         L.or_philox4x32.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
@@ -168,3 +171,18 @@ class Mcts:
 
 def random_rollouts(n, B, steps, seed, threads=1):
     return lib().or_random_rollouts(n, B, steps, seed, threads)
+
+
+def rollout_run(n, B, steps, seed, board_base=0):
+    """Oracle of spl_rollout_step: returns dict of final state/player and traces."""
+    S = 7 * rows(n)
+    st = np.zeros((B, rows(n), 7), np.int8)
+    pl = np.zeros(B, np.int8)
+    act = np.zeros((steps, B), np.int16)
+    end = np.zeros((steps, B, n), np.float32)
+    games = np.zeros(B, np.int32)
+    fold = np.zeros(B, np.uint64)
+    lib().or_rollout_run(n, B, steps, seed, board_base, _p(st, C.c_int8), _p(pl, C.c_int8),
+                         _p(act, C.c_int16), _p(end, C.c_float), _p(games, C.c_int32),
+                         _p(fold, C.c_uint64))
+    return {"state": st, "player": pl, "action": act, "ended": end, "games": games, "mask_fold": fold}

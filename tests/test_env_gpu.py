@@ -1,0 +1,169 @@
+"""GPU parity of the HIP env kernels (libsplendor_amd.so via the C ABI) against the CPU
+oracle and the reference golden vectors. Bit-exact everywhere (integer/byte work)."""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import _oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NS = (2, 3, 4)
+
+
+def load(name):
+    with np.load(os.path.join(GOLD, name)) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="module")
+def engines():
+    from splendor.env import SplendorEngine
+    return {n: SplendorEngine(n) for n in NS}
+
+
+def dev(x, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def host_mask(words):
+    from splendor.env import unpack_mask
+    return unpack_mask(words).cpu().numpy().astype(np.uint8)
+
+
+@pytest.mark.parametrize("n", NS)
+def test_valid_moves_matches_reference(engines, n):
+    e, d = engines[n], load(f"env_{n}p.npz")
+    m = host_mask(e.valid_moves(dev(d["canon"])))
+    np.testing.assert_array_equal(m, d["mask_canon"])
+    m2 = host_mask(e.valid_moves(dev(d["state"]), dev(d["player"], torch.int8)))
+    np.testing.assert_array_equal(m2, d["mask_player"])
+
+
+@pytest.mark.parametrize("n", NS)
+def test_canonical_matches_reference(engines, n):
+    e, d = engines[n], load(f"env_{n}p.npz")
+    out = e.canonical(dev(d["state"]), dev(d["player"], torch.int8)).cpu().numpy()
+    np.testing.assert_array_equal(out, d["canon"])
+
+
+@pytest.mark.parametrize("n", NS)
+def test_game_ended_matches_reference(engines, n):
+    e, d, k = engines[n], load(f"env_{n}p.npz"), load(f"end_{n}p.npz")
+    np.testing.assert_array_equal(e.game_ended(dev(d["next_state"])).cpu().numpy(), d["next_ended"])
+    np.testing.assert_array_equal(e.game_ended(dev(d["state"])).cpu().numpy(), d["ended"])
+    np.testing.assert_array_equal(e.game_ended(dev(k["state"])).cpu().numpy(), k["ended"])
+    sc = e.score(dev(d["state"])).cpu().numpy()
+    np.testing.assert_array_equal(sc, d["scores"])
+    np.testing.assert_array_equal(e.round(dev(d["state"])).cpu().numpy(), d["round"])
+
+
+@pytest.mark.parametrize("n", NS)
+def test_chance_step_matches_reference(engines, n):
+    e, d = engines[n], load(f"env_{n}p.npz")
+    B = len(d["state"])
+    u = np.zeros((B, 4), np.float64)
+    for i in range(B):
+        off, ln = int(d["u_off"][i]), int(d["u_len"][i])
+        u[i, :ln] = d["uniforms"][off:off + ln]
+    st = dev(d["state"])
+    nxt = torch.empty(B, dtype=torch.int8, device="cuda")
+    e.step(st, dev(d["action"], torch.int16), dev(d["player"], torch.int8), nxt, deterministic=False,
+           uniforms=dev(u))
+    np.testing.assert_array_equal(st.cpu().numpy(), d["next_state"])
+    np.testing.assert_array_equal(nxt.cpu().numpy(), d["next_player"])
+
+
+@pytest.mark.parametrize("n", NS)
+def test_tree_step_matches_reference(engines, n):
+    e, d = engines[n], load(f"env_{n}p.npz")
+    parents = d["canon"][d["det_src"]]
+    child = e.tree_step(dev(parents), dev(d["det_action"], torch.int16)).cpu().numpy()
+    np.testing.assert_array_equal(child, d["det_next_state"])
+    # deterministic spl_step + canonical == tree_step
+    st = dev(parents)
+    nxt = torch.empty(len(parents), dtype=torch.int8, device="cuda")
+    e.step(st, dev(d["det_action"], torch.int16), None, nxt, deterministic=True)
+    np.testing.assert_array_equal(nxt.cpu().numpy(), d["det_next_player"])
+    np.testing.assert_array_equal(e.canonical(st, nxt).cpu().numpy(), d["det_next_state"])
+
+
+@pytest.mark.parametrize("n", NS)
+def test_init_matches_reference(engines, n):
+    e, d = engines[n], load(f"env_{n}p.npz")
+    G = len(d["init_state"])
+    u = np.zeros((G, 32), np.float64)
+    u[:, :d["init_uniforms"].shape[1]] = d["init_uniforms"]
+    st = e.new_state(G)
+    e.init(st, uniforms=dev(u))
+    np.testing.assert_array_equal(st.cpu().numpy(), d["init_state"])
+
+
+@pytest.mark.parametrize("n", NS)
+def test_fused_rollout_matches_oracle(engines, n):
+    from splendor.env import RolloutBatch
+    B, T, seed = 1024, 96, 0x5EED + n
+    ref = O.rollout_run(n, B, T, seed)
+    rb = RolloutBatch(engines[n], B, seed=seed)
+    for t in range(T):
+        rb.step()
+        np.testing.assert_array_equal(rb.action.cpu().numpy(), ref["action"][t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(rb.ended.cpu().numpy(), ref["ended"][t])
+    np.testing.assert_array_equal(rb.state.cpu().numpy(), ref["state"])
+    np.testing.assert_array_equal(rb.player.cpu().numpy(), ref["player"])
+    np.testing.assert_array_equal(rb.games.cpu().numpy(), ref["games"])
+
+
+def _invariants(n, st, gems_in_play):
+    R = 32 + 10 * n + n * n
+    gems = 32 + n
+    cards = 32 + 3 * n + n * n
+    rsv = 32 + 4 * n + n * n
+    st = st.astype(np.int64)
+    tot = st[:, 0, :6] + st[:, gems:gems + n, :6].sum(1)
+    assert (tot[:, :5] == gems_in_play).all() and (tot[:, 5] == 5).all()
+    visible = (st[:, 1:25:2, :5].sum(2) != 0).sum(1)
+    deck = st[:, 25:31:2, :5].sum((1, 2))
+    reserved = (st[:, rsv:rsv + 6 * n:2, :5].sum(2) != 0).sum(1)
+    bought = st[:, cards:cards + n, :5].sum((1, 2))
+    assert (visible + deck + reserved + bought == 90).all()
+    assert st.shape[1] == R
+
+
+@pytest.mark.parametrize("n", (2, 4))
+def test_full_size_rollout_invariants(engines, n):
+    """BASELINE config 2 size: 32768 boards; size-independent properties every step."""
+    from splendor.env import RolloutBatch, unpack_mask
+    B = 32768 if n == 2 else 16384
+    rb = RolloutBatch(engines[n], B, seed=0x5EED)
+    gip = {2: 4, 3: 5, 4: 7}[n]
+    prev_round = engines[n].round(rb.state)
+    for t in range(150):
+        rb.step()
+        m = unpack_mask(rb.mask)
+        legal = m[torch.arange(B, device="cuda"), rb.action.long()]
+        assert bool(legal.all()), f"illegal action chosen at t={t}"
+        r = engines[n].round(rb.state)
+        ended = (rb.ended != 0).any(1)
+        assert bool(((r == prev_round + 1) | ended).all())
+        prev_round = r
+        if t % 25 == 0:
+            _invariants(n, rb.state.cpu().numpy(), gip)
+    assert int(rb.games.sum()) > 0
+
+
+def test_bad_action_sets_error(engines):
+    e, d = engines[2], load("env_2p.npz")
+    st = dev(d["state"][:4])
+    before = st.clone()
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    e.step(st, dev(np.array([500, -1, 3000, 409], np.int16)), None, None, deterministic=True, err=err)
+    assert int(err.item()) == 1
+    assert torch.equal(st, before)
