@@ -58,7 +58,12 @@ def cpu_baseline(n, seed, target_s=10.0):
 
 
 def load_traffic(path, B):
-    """Measured HBM bytes per launch from a committed rocprofv3 --pmc summary, if any."""
+    """Measured HBM bytes per launch from the newest committed rocprofv3 --pmc summary
+    (profiles/rNN_rollout_pmc.json, corrected as DESIGN.md §6 describes), if any."""
+    if not path:
+        import glob
+        found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_rollout_pmc.json")))
+        path = found[-1] if found else None
     if not path or not os.path.exists(path):
         return None
     with open(path) as f:
@@ -77,7 +82,7 @@ def main():
     ap.add_argument("--players", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_rollout_step.json"))
+    ap.add_argument("--traffic-json", default=None)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -104,16 +109,18 @@ def main():
     torch.cuda.synchronize(dev)
 
     K = args.steps
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    # HIP events on the stream the kernel is launched on (torch's current stream): one
+    # pair around the K back-to-back launches -> average launch duration (incl. the
+    # ~1-2 us inter-launch gap; rocprofv3 --stats gives the pure kernel time)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(K):
-        starts[k].record()
+    ev0.record()
+    for _ in range(K):
         rb.step()
-        ends[k].record()
+    ev1.record()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if dist:
@@ -121,7 +128,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / K
+    kernel_ms = ev0.elapsed_time(ev1) / K
     games = int(rb.games.sum().item())
 
     if rank == 0:
