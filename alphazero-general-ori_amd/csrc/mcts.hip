@@ -1,0 +1,719 @@
+// mcts.hip — device-resident batched MCTS kernels + C ABI (include/splendor_amd.h §MCTS).
+// One wave per tree; every tree advances by exactly one simulation per select/backup pair,
+// so each tree's sequence of simulations is the reference's sequential search (MCTS.py).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <new>
+
+#include "../../include/splendor_amd.h"
+#include "mcts_device.h"
+
+using namespace spl;
+
+struct spl_ctx {  // must match splendor_env.hip
+    int n;
+    int token_limit;
+};
+
+struct spl_mcts {
+    int n, B, S, token_limit;
+    SearchCfg cfg;
+    Pools P;
+    void *arena;
+};
+
+namespace {
+
+constexpr int WAVES = 4;
+constexpr int THREADS = 64 * WAVES;
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const int l = lane_id();
+    return l ? (~0ull >> (64 - l)) : 0ull;
+}
+
+// ------------------------------------------------------------ edge selection
+// pick_highest_UCB (MCTS.py:199-219) over the CSR edges of `node`; forced playouts
+// return the first edge (action order) with N < int(sqrt(0.5 * P * step)).
+__device__ __forceinline__ int pick_edge(const Pools &P, const SearchCfg &C, int t, int node,
+                                         bool forced, int step) {
+    const int l = lane_id();
+    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
+    const int eb = P.neb[nb + node], ec = P.nec[nb + node], ns = P.nns[nb + node];
+    const double qs = P.nqs[nb + node];
+    const float *ep = P.ep + e0 + eb;
+    const int32_t *en = P.en + e0 + eb;
+    const double *eq = P.eq + e0 + eb;
+    if (forced) {
+        for (int base = 0; base < ec; base += 64) {
+            const int i = base + l;
+            bool f = false;
+            if (i < ec) f = (long long)en[i] < (long long)sqrt(0.5 * (double)ep[i] * (double)step);
+            const uint64_t b = __ballot(f);
+            if (b) return base + __ffsll((unsigned long long)b) - 1;
+        }
+    }
+    const double fpu_init = C.fpu > 0 ? qs - C.fpu : C.fpu;
+    const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
+    double bu = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int base = 0; base < ec; base += 64) {
+        const int i = base + l;
+        if (i < ec) {
+            const double p = (double)ep[i], q = eq[i];
+            double u;
+            if (q != Q_UNSET) u = q + C.cpuct * p * sq / (double)(1 + en[i]);
+            else u = fpu_init + C.cpuct * p * sq_eps;
+            if (u > bu) { bu = u; bi = i; }
+        }
+    }
+    wave_argmax(bu, bi);
+    return bi;
+}
+
+// ------------------------------------------------------------ Dirichlet root noise
+// applyDirNoise (MCTS.py:180-186) after softmax(Ps, T0) (:245-250), then normalise.
+// Gamma(alpha) by Marsaglia-Tsang with the alpha<1 boost, driven by Philox; the reference
+// uses numpy's Generator.dirichlet (unseeded), so parity here is distributional.
+__device__ __forceinline__ double gamma_sample(double alpha, uint64_t seed, uint32_t board,
+                                               uint32_t stream, uint32_t &ctr) {
+    const double a = alpha < 1.0 ? alpha + 1.0 : alpha;
+    const double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
+    double g = 0.0;
+    for (int it = 0; it < 64; it++) {
+        const double u1 = philox_u01(seed, board, stream, ctr++);
+        const double u2 = philox_u01(seed, board, stream, ctr++);
+        const double z = sqrt(-2.0 * log(fmax(u1, 1e-300))) * cos(6.283185307179586 * u2);
+        double v = 1.0 + c * z;
+        if (v <= 0.0) continue;
+        v = v * v * v;
+        const double u = philox_u01(seed, board, stream, ctr++);
+        if (log(fmax(u, 1e-300)) < 0.5 * z * z + d - d * v + d * log(v)) { g = d * v; break; }
+    }
+    if (alpha < 1.0) g *= pow(philox_u01(seed, board, stream, ctr++), 1.0 / alpha);
+    return g;
+}
+
+// P (float32, ec edges of the root) <- normalise(0.75*softmax(P,T0) + 0.25*Dir(alpha))
+__device__ __forceinline__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int eb,
+                                                 int ec, uint32_t stream) {
+    const int l = lane_id();
+    float *ep = P.ep + (size_t)t * P.ecap + eb;
+    const uint32_t gb = C.board_base + (uint32_t)t;
+    const bool tmp = C.dir_temp != 1.0;
+    double sp[3], g[3], ssum = 0.0, gsum = 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {   // <= 192 legal actions (observed max 133)
+        const int i = l + 64 * j;
+        sp[j] = 0.0; g[j] = 0.0;
+        if (i < ec) {
+            sp[j] = tmp ? pow((double)ep[i], 1.0 / C.dir_temp) : (double)ep[i];
+            uint32_t ctr = (uint32_t)i * 256u;
+            g[j] = gamma_sample(C.dir_alpha, C.seed, gb, stream, ctr);
+        }
+        ssum += sp[j];
+        gsum += g[j];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        ssum += __shfl_xor(ssum, o, 64);
+        gsum += __shfl_xor(gsum, o, 64);
+    }
+    float pn[3], nsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const int i = l + 64 * j;
+        pn[j] = 0.f;
+        if (i < ec) {
+            const float smx = tmp ? (float)(sp[j] / ssum) : (float)sp[j];
+            pn[j] = (float)(0.75 * (double)smx + 0.25 * (g[j] / gsum));
+        }
+        nsum += pn[j];
+    }
+    for (int o = 32; o > 0; o >>= 1) nsum += __shfl_xor(nsum, o, 64);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const int i = l + 64 * j;
+        if (i < ec) ep[i] = pn[j] / nsum;
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+}
+
+// ------------------------------------------------------------ garbage collection
+// Keep the root and every node whose round counter exceeds the root's: rounds strictly
+// increase along every move (SplendorLogicNumba.py:287), so no other node is reachable from
+// this root or any later one — an exact subset of the reference's table (which only
+// evicts rounds < R-5, MCTS.py:80-85). Compacts nodes + CSR edges in place, remaps child
+// links, rebuilds the hash table. Wave-collective; returns the root's new index.
+__device__ int compact_tree(const Pools &P, int t, int root, int root_round) {
+    const int l = lane_id();
+    TreeHdr *H = P.hdr + t;
+    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
+    const int nc = H->node_count;
+    int32_t *remap = P.remap + nb;
+    int kept = 0;
+    for (int base = 0; base < nc; base += 64) {
+        const int i = base + l;
+        const bool keep = i < nc && (i == root || P.nround[nb + i] > root_round);
+        const uint64_t b = __ballot(keep);
+        if (i < nc) remap[i] = keep ? kept + __popcll(b & lanemask_lt()) : -1;
+        kept += __popcll(b);
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    int edges = 0;
+    for (int base = 0; base < nc; base += 64) {
+        const int i = base + l;
+        const bool valid = i < nc;
+        const int ni = valid ? remap[i] : -1;
+        uint64_t k0 = 0, k1 = 0;
+        int oeb = 0, ec = 0, ns = 0, rd = 0;
+        double qs = 0;
+        int8_t term = 0;
+        float es[4] = {0, 0, 0, 0};
+        if (ni >= 0) {
+            k0 = P.nkey0[nb + i]; k1 = P.nkey1[nb + i];
+            oeb = P.neb[nb + i]; ec = P.nec[nb + i]; ns = P.nns[nb + i]; rd = P.nround[nb + i];
+            qs = P.nqs[nb + i]; term = P.nterm[nb + i];
+#pragma unroll
+            for (int j = 0; j < 4; j++) es[j] = P.nes[(nb + i) * 4 + j];
+        }
+        // exclusive scan of kept edge counts -> new edge base
+        int x = ni >= 0 ? ec : 0, incl = x;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            int y = __shfl_up(incl, o, 64);
+            if (l >= o) incl += y;
+        }
+        const int neb = edges + incl - x;
+        const int total = __shfl(incl, 63, 64);
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        if (ni >= 0) {
+            P.nkey0[nb + ni] = k0; P.nkey1[nb + ni] = k1;
+            P.neb[nb + ni] = neb; P.nec[nb + ni] = ec; P.nns[nb + ni] = ns; P.nround[nb + ni] = rd;
+            P.nqs[nb + ni] = qs; P.nterm[nb + ni] = term;
+#pragma unroll
+            for (int j = 0; j < 4; j++) P.nes[(nb + ni) * 4 + j] = es[j];
+        }
+        // move each kept node's edge block down (increasing order: never overlaps unread data)
+        for (int j = 0; j < 64; j++) {
+            const int jn = __shfl(ni, j, 64);
+            if (jn < 0) continue;
+            const int jo = __shfl(oeb, j, 64), jd = __shfl(neb, j, 64), jc = __shfl(ec, j, 64);
+            for (int base2 = 0; base2 < jc; base2 += 64) {
+                const int q = base2 + l;
+                const bool in = q < jc;
+                int16_t a = 0; float p = 0; int32_t cnt = 0, ch = -1; double qq = 0;
+                if (in) {
+                    a = P.ea[e0 + jo + q]; p = P.ep[e0 + jo + q]; cnt = P.en[e0 + jo + q];
+                    qq = P.eq[e0 + jo + q]; ch = P.echild[e0 + jo + q];
+                }
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+                if (in) {
+                    P.ea[e0 + jd + q] = a; P.ep[e0 + jd + q] = p; P.en[e0 + jd + q] = cnt;
+                    P.eq[e0 + jd + q] = qq; P.echild[e0 + jd + q] = ch >= 0 ? remap[ch] : -1;
+                }
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        edges += total;
+    }
+    // rebuild the transposition table
+    int32_t *hs = P.hslot + (size_t)t * P.hcap;
+    for (int i = l; i < P.hcap; i += 64) hs[i] = -1;
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    for (int i = l; i < kept; i += 64) {
+        const uint64_t k0 = P.nkey0[nb + i];
+        uint32_t h = (uint32_t)(k0 ^ (k0 >> 32)) & (uint32_t)(P.hcap - 1);
+        while (atomicCAS(&hs[h], -1, i) != -1) h = (h + 1) & (uint32_t)(P.hcap - 1);
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    const int nroot = root >= 0 ? remap[root] : -1;
+    if (l == 0) { H->node_count = kept; H->edge_count = edges; }
+    __builtin_amdgcn_wave_barrier();
+    return nroot;
+}
+
+// ------------------------------------------------------------ search start
+// Re-root every tree at the given canonical board (MCTS.getActionProb entry, :45-56):
+// look the root up in the persistent table (keep != 0) or start empty; draw the
+// full/fast search decision; arm root noise.
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int B,
+                                                       const int8_t *__restrict__ roots, int keep,
+                                                       int force_full) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    if (t >= B) return;
+    const int l = lane_id();
+    int8_t *s = lds[w];
+    for (int i = Lx::S + l; i < Lx::SPAD; i += 64) s[i] = 0;
+    wave_copy_board<N>(s, roots + (size_t)t * Lx::S);
+    wave_copy_board<N>(P.root_state + (size_t)t * Lx::S, s);
+    TreeHdr *H = P.hdr + t;
+    int root = -1;
+    if (keep && H->node_count > 0) {
+        uint64_t k0, k1;
+        wave_fingerprint<N>(s, k0, k1);
+        root = hash_lookup(P, t, k0, k1);
+        root = compact_tree(P, t, root, (uint8_t)s[6]);
+    } else {
+        int32_t *hs = P.hslot + (size_t)t * P.hcap;
+        for (int i = l; i < P.hcap; i += 64) hs[i] = -1;
+        if (l == 0) { H->node_count = 0; H->edge_count = 0; }
+    }
+    const int mv = H->move_no;
+    const bool full = force_full || philox_u01(C.seed, C.board_base + t, ST_FULL | (uint32_t)mv, 0) < C.prob_full;
+    __builtin_amdgcn_wave_barrier();
+    if (l == 0) {
+        H->root = root;
+        H->sims_done = 0;
+        H->full = full;
+        H->budget = full ? C.num_sims : C.num_sims / C.ratio_full;
+        H->forced = full && C.forced_playouts;
+        H->noise_pending = full && C.dirichlet;
+        H->leaf_kind = LEAF_NONE;
+        H->overflow = 0;
+        H->move_no = mv + 1;
+    }
+}
+
+// ------------------------------------------------------------ select
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B, int lim,
+                                                    int8_t *__restrict__ leaf_state,
+                                                    uint64_t *__restrict__ leaf_mask,
+                                                    uint8_t *__restrict__ leaf_valid) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    if (t >= B) return;
+    const int l = lane_id();
+    TreeHdr *H = P.hdr + t;
+    const int sims = H->sims_done;
+    if (sims >= H->budget || H->overflow) {
+        if (l == 0) { leaf_valid[t] = 0; H->leaf_kind = LEAF_NONE; }
+        return;
+    }
+    int8_t *s = lds[w];
+    for (int i = Lx::S + l; i < Lx::SPAD; i += 64) s[i] = 0;
+    wave_copy_board<N>(s, P.root_state + (size_t)t * Lx::S);
+    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
+    int32_t *path = P.path + (size_t)t * P.pcap * 2;
+    int node = H->root, depth = 0, kind = LEAF_NN;
+    uint64_t k0 = 0, k1 = 0;
+    float val[4] = {0, 0, 0, 0};
+    if (node < 0) {
+        wave_fingerprint<N>(s, k0, k1);                  // the root itself is the leaf
+    } else {
+        if (sims == 0 && H->noise_pending)
+            apply_root_noise(P, C, t, P.neb[nb + node], P.nec[nb + node], ST_DIR | (uint32_t)H->move_no);
+        const bool forced = H->forced;
+        for (;;) {
+            if (depth >= P.pcap) { kind = LEAF_NONE; if (l == 0) H->overflow = 2; break; }
+            const int e = pick_edge(P, C, t, node, forced && depth == 0, sims);
+            const int ge = P.neb[nb + node] + e;
+            if (l == 0) { path[2 * depth] = node; path[2 * depth + 1] = ge; }
+            depth++;
+            const int a = P.ea[e0 + ge];
+            int child = P.echild[e0 + ge];
+            Chance ch{nullptr, 0, 0, 0, 0};
+            const int nxt = make_move<N>(s, a, 0, true, ch);   // MCTS.py:227-235
+            __builtin_amdgcn_wave_barrier();
+            if (nxt) wave_roll_players<N>(s, s, nxt);
+            if (child < 0) {
+                wave_fingerprint<N>(s, k0, k1);
+                child = hash_lookup(P, t, k0, k1);
+                if (child >= 0 && l == 0) P.echild[e0 + ge] = child;
+            }
+            if (child >= 0) {
+                if (P.nterm[nb + child]) {
+                    kind = LEAF_TERMINAL;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) val[i] = P.nes[(nb + child) * 4 + i];
+                    break;
+                }
+                node = child;
+                continue;
+            }
+            float es[N];
+            check_end<N>(s, es);                             // MCTS.py:125
+            bool any = false;
+#pragma unroll
+            for (int i = 0; i < N; i++) any |= es[i] != 0.f;
+            if (any) {
+                const int id = H->node_count;
+                if (id >= P.ncap) { kind = LEAF_NONE; if (l == 0) H->overflow = 1; break; }
+                __builtin_amdgcn_wave_barrier();
+                if (l == 0) {
+                    P.nkey0[nb + id] = k0; P.nkey1[nb + id] = k1; P.neb[nb + id] = 0;
+                    P.nec[nb + id] = 0; P.nns[nb + id] = 0; P.nqs[nb + id] = 0;
+                    P.nround[nb + id] = (uint8_t)s[6]; P.nterm[nb + id] = 1;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) P.nes[(nb + id) * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
+                    hash_insert(P, t, k0, id);
+                    P.echild[e0 + ge] = id;
+                    H->node_count = id + 1;
+                }
+                kind = LEAF_TERMINAL;
+#pragma unroll
+                for (int i = 0; i < N; i++) val[i] = es[i];
+                break;
+            }
+            break;                                           // new NN leaf
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (kind == LEAF_NN) {
+        wave_copy_board<N>(leaf_state + (size_t)t * Lx::S, s);
+        uint64_t m[7];
+        wave_valid_moves<N>(s, 0, lim, m);                   // MCTS.py:136
+        uint64_t mv = m[0];
+#pragma unroll
+        for (int k = 1; k < 7; k++) mv = l == k ? m[k] : mv;
+        if (l < 7) leaf_mask[(size_t)t * 7 + l] = mv;
+    }
+    if (l == 0) {
+        H->depth = depth;
+        H->leaf_kind = kind;
+        H->leaf_k0 = k0; H->leaf_k1 = k1;
+        H->leaf_round = (uint8_t)s[6];
+#pragma unroll
+        for (int i = 0; i < 4; i++) H->leaf_v[i] = val[i];
+        leaf_valid[t] = kind == LEAF_NN;
+    }
+}
+
+// ------------------------------------------------------------ expand + backup
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_backup(Pools P, SearchCfg C, int B,
+                                                    const uint64_t *__restrict__ leaf_mask,
+                                                    const float *__restrict__ pi,
+                                                    const float *__restrict__ v) {
+    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    if (t >= B) return;
+    const int l = lane_id();
+    TreeHdr *H = P.hdr + t;
+    const int kind = H->leaf_kind;
+    if (kind == LEAF_NONE) return;
+    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
+    const int depth = H->depth;
+    const int32_t *path = P.path + (size_t)t * P.pcap * 2;
+    float val[4];
+    if (kind == LEAF_NN) {
+        const uint64_t *m = leaf_mask + (size_t)t * 7;
+        int ec = 0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) ec += __popcll(m[k]);
+        const int id = H->node_count, eb = H->edge_count;
+        if (id >= P.ncap || eb + ec > P.ecap) {
+            if (l == 0) { H->overflow = 1; H->leaf_kind = LEAF_NONE; }
+            return;
+        }
+        const float *pr = pi + (size_t)t * SPL_ACTIONS;
+        float sum = l == 0 ? np_sum409(pr) : 0.f;           // normalise (MCTS.py:144)
+        sum = __shfl(sum, 0, 64);
+        int run = 0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const uint64_t wd = m[k];
+            if ((wd >> l) & 1) {
+                const int r = eb + run + __popcll(wd & lanemask_lt());
+                const int a = 64 * k + l;
+                P.ea[e0 + r] = (int16_t)a;
+                P.ep[e0 + r] = pr[a] / sum;
+                P.en[e0 + r] = 0;
+                P.eq[e0 + r] = Q_UNSET;
+                P.echild[e0 + r] = -1;
+            }
+            run += __popcll(wd);
+        }
+#pragma unroll
+        for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
+        __builtin_amdgcn_wave_barrier();
+        if (l == 0) {
+            P.nkey0[nb + id] = H->leaf_k0; P.nkey1[nb + id] = H->leaf_k1;
+            P.neb[nb + id] = eb; P.nec[nb + id] = ec; P.nns[nb + id] = 0;
+            P.nqs[nb + id] = (double)val[0]; P.nround[nb + id] = H->leaf_round; P.nterm[nb + id] = 0;
+            hash_insert(P, t, H->leaf_k0, id);
+            if (depth == 0) H->root = id;
+            else P.echild[e0 + path[2 * (depth - 1) + 1]] = id;
+            H->node_count = id + 1;
+            H->edge_count = eb + ec;
+        }
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        if (depth == 0 && H->sims_done == 0 && H->noise_pending)   // noise on a new root
+            apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no);
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
+    }
+    if (l == 0) {
+        for (int d = depth - 1; d >= 0; d--) {               // MCTS.py:169-176
+            float r[N];
+#pragma unroll
+            for (int i = 0; i < N; i++) r[i] = val[(i + N - 1) % N];
+#pragma unroll
+            for (int i = 0; i < N; i++) val[i] = r[i];
+            const int node = path[2 * d], ge = path[2 * d + 1];
+            const int cnt = P.en[e0 + ge];
+            const double v0 = (double)val[0];
+            P.eq[e0 + ge] = ((double)cnt * P.eq[e0 + ge] + v0) / (double)(cnt + 1);
+            const int ns = P.nns[nb + node];
+            P.nqs[nb + node] = ((double)(ns + 1) * P.nqs[nb + node] + v0) / (double)(ns + 2);
+            P.en[e0 + ge] = cnt + 1;
+            P.nns[nb + node] = ns + 1;
+        }
+        H->sims_done += 1;
+        H->noise_pending = 0;
+        H->leaf_kind = LEAF_NONE;
+    }
+}
+
+// ------------------------------------------------------------ results
+// getActionProb tail (MCTS.py:61-97) for temp = 1: root visit counts (with policy-target
+// pruning when forced playouts were on), probs, q.
+__global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, int B, int n,
+                                                        int64_t *counts, double *qsa, double *probs,
+                                                        double *q) {
+    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    if (t >= B) return;
+    const int l = lane_id();
+    TreeHdr *H = P.hdr + t;
+    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
+    const int root = H->root;
+    for (int a = l; a < SPL_ACTIONS; a += 64) {
+        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = 0;
+        if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = Q_UNSET;
+        if (probs) probs[(size_t)t * SPL_ACTIONS + a] = 0.0;
+    }
+    if (root < 0) return;
+    __threadfence_block();
+    const int eb = P.neb[nb + root], ec = P.nec[nb + root];
+    int best = 0;
+    for (int i = l; i < ec; i += 64) best = max(best, P.en[e0 + eb + i]);
+    for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
+    const int sims = H->budget;
+    long long tot = 0;
+    for (int i = l; i < ec; i += 64) {
+        const int a = P.ea[e0 + eb + i];
+        long long c = P.en[e0 + eb + i];
+        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = c;
+        if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = P.eq[e0 + eb + i];
+        if (H->forced) {
+            if (c != best) c -= (long long)sqrt(0.5 * (double)P.ep[e0 + eb + i] * (double)sims);
+            if (c <= 1) c = 0;
+        }
+        tot += c;
+    }
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    for (int i = l; i < ec; i += 64) {
+        const int a = P.ea[e0 + eb + i];
+        long long c = P.en[e0 + eb + i];
+        if (H->forced) {
+            if (c != best) c -= (long long)sqrt(0.5 * (double)P.ep[e0 + eb + i] * (double)sims);
+            if (c <= 1) c = 0;
+        }
+        if (probs) probs[(size_t)t * SPL_ACTIONS + a] = (double)c / (double)tot;
+    }
+    if (q && l == 0) {
+        const double q0 = P.nqs[nb + root];
+        q[(size_t)t * n] = q0;
+        for (int i = 1; i < n; i++) q[(size_t)t * n + i] = -q0 / (double)(n - 1);
+    }
+}
+
+// ------------------------------------------------------------ network I/O
+// leaf int8 [B,R,7] + packed mask -> float32 board and bool mask (predict, :160-161)
+__global__ __launch_bounds__(256) void k_nn_input(int B, int S, const int8_t *__restrict__ st,
+                                                  const uint64_t *__restrict__ mask,
+                                                  float *__restrict__ x, uint8_t *__restrict__ valid) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t nx = (size_t)B * S, nv = (size_t)B * SPL_ACTIONS;
+    if (i < nx) x[i] = (float)st[i];
+    if (valid && i < nv) {
+        const size_t b = i / SPL_ACTIONS, a = i % SPL_ACTIONS;
+        valid[i] = (uint8_t)((mask[b * 7 + a / 64] >> (a % 64)) & 1);
+    }
+}
+
+// deterministic hash network (oracle or_fake_predict; used for search-parity tests and
+// tree-only throughput runs)
+template <int N>
+__global__ __launch_bounds__(256) void k_hash_eval(int B, const int8_t *__restrict__ st,
+                                                   const uint64_t *__restrict__ mask,
+                                                   float *__restrict__ pi, float *__restrict__ v) {
+    const int t = blockIdx.x;
+    if (t >= B) return;
+    const int8_t *s = st + (size_t)t * Lay<N>::S;
+    __shared__ uint64_t hsh;
+    if (threadIdx.x == 0) {
+        uint64_t h = 0xCBF29CE484222325ull;
+        for (int i = 0; i < Lay<N>::S; i++) { h ^= (uint8_t)s[i]; h *= 0x100000001B3ull; }
+        hsh = h;
+    }
+    __syncthreads();
+    const uint64_t h = hsh;
+    for (int a = threadIdx.x; a < SPL_ACTIONS; a += 256) {
+        const bool ok = (mask[(size_t)t * 7 + a / 64] >> (a % 64)) & 1;
+        pi[(size_t)t * SPL_ACTIONS + a] =
+            ok ? (float)((double)(1 + (mix64(h + (uint64_t)a) >> 40)) * 0x1p-24) : 0.f;
+    }
+    if (threadIdx.x < N)
+        v[(size_t)t * N + threadIdx.x] =
+            (float)((double)(mix64(h ^ (0xA5A5ull + threadIdx.x)) >> 40) * 0x1p-23 - 1.0);
+}
+
+inline int check_launch() { return hipGetLastError() == hipSuccess ? 0 : SPL_EDEVICE; }
+inline dim3 wave_grid(int B) { return dim3((unsigned)((B + WAVES - 1) / WAVES)); }
+
+#define SPL_DISPATCH(n, CALL)                          \
+    switch (n) {                                       \
+        case 2: { constexpr int N = 2; CALL; break; }  \
+        case 3: { constexpr int N = 3; CALL; break; }  \
+        default: { constexpr int N = 4; CALL; break; } \
+    }
+
+template <class T>
+T *carve(char *&p, size_t count) {
+    T *r = reinterpret_cast<T *>(p);
+    size_t bytes = (count * sizeof(T) + 255) & ~size_t(255);
+    p += bytes;
+    return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_mcts **out) {
+    if (!ctx || ctx->n < 2 || ctx->n > 4 || B <= 0 || !cfg || !out) return SPL_EINVAL;
+    if (cfg->num_sims <= 0 || cfg->ratio_full <= 0 || cfg->node_cap <= 0 || cfg->edge_cap <= 0)
+        return SPL_EINVAL;
+    spl_mcts *m = new (std::nothrow) spl_mcts;
+    if (!m) return SPL_EINVAL;
+    m->n = ctx->n; m->B = B; m->S = 7 * (32 + 10 * ctx->n + ctx->n * ctx->n);
+    m->token_limit = ctx->token_limit;
+    SearchCfg &C = m->cfg;
+    C.cpuct = cfg->cpuct; C.fpu = cfg->fpu; C.dir_alpha = cfg->dirichlet_alpha;
+    C.dir_temp = cfg->dirichlet_temp > 0 ? cfg->dirichlet_temp : 1.0;
+    C.prob_full = cfg->prob_full; C.num_sims = cfg->num_sims; C.ratio_full = cfg->ratio_full;
+    C.forced_playouts = cfg->forced_playouts; C.dirichlet = cfg->dirichlet_alpha > 0;
+    C.temp_threshold = cfg->temp_threshold; C.seed = cfg->seed; C.board_base = cfg->board_base;
+    Pools &P = m->P;
+    P.ncap = cfg->node_cap; P.ecap = cfg->edge_cap;
+    int h = 1;
+    while (h < 2 * P.ncap) h <<= 1;
+    P.hcap = h;
+    P.pcap = cfg->num_sims + 64 > 256 ? cfg->num_sims + 64 : 256;
+    const size_t nn = (size_t)B * P.ncap, ne = (size_t)B * P.ecap;
+    size_t bytes = 0;
+    auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
+    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn); acc(4 * nn);
+    acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(2 * ne); acc(4 * ne); acc(4 * ne);
+    acc(4 * ne); acc(8 * ne); acc(4 * (size_t)B * P.hcap); acc(8 * (size_t)B * P.pcap);
+    acc(4 * nn); acc((size_t)B * m->S);
+    void *arena = nullptr;
+    if (hipMalloc(&arena, bytes) != hipSuccess) { delete m; return SPL_EDEVICE; }
+    if (hipMemset(arena, 0, bytes) != hipSuccess) { (void)hipFree(arena); delete m; return SPL_EDEVICE; }
+    m->arena = arena;
+    char *p = (char *)arena;
+    P.hdr = carve<TreeHdr>(p, B);
+    P.nkey0 = carve<uint64_t>(p, nn); P.nkey1 = carve<uint64_t>(p, nn);
+    P.neb = carve<int32_t>(p, nn); P.nec = carve<int32_t>(p, nn); P.nns = carve<int32_t>(p, nn);
+    P.nround = carve<int32_t>(p, nn); P.nqs = carve<double>(p, nn); P.nterm = carve<int8_t>(p, nn);
+    P.nes = carve<float>(p, 4 * nn);
+    P.ea = carve<int16_t>(p, ne); P.ep = carve<float>(p, ne); P.en = carve<int32_t>(p, ne);
+    P.echild = carve<int32_t>(p, ne); P.eq = carve<double>(p, ne);
+    P.hslot = carve<int32_t>(p, (size_t)B * P.hcap);
+    P.path = carve<int32_t>(p, 2 * (size_t)B * P.pcap);
+    P.remap = carve<int32_t>(p, nn);
+    P.root_state = carve<int8_t>(p, (size_t)B * m->S);
+    if (hipMemset(P.hslot, 0xFF, 4 * (size_t)B * P.hcap) != hipSuccess) {
+        (void)hipFree(arena); delete m; return SPL_EDEVICE;
+    }
+    *out = m;
+    return 0;
+}
+
+int spl_mcts_destroy(spl_mcts *m) {
+    if (!m) return 0;
+    (void)hipFree(m->arena);
+    delete m;
+    return 0;
+}
+
+long long spl_mcts_device_bytes(const spl_mcts *m) {
+    if (!m) return SPL_EINVAL;
+    const size_t nn = (size_t)m->B * m->P.ncap, ne = (size_t)m->B * m->P.ecap;
+    return (long long)(nn * 53 + ne * 22 + (size_t)m->B * (4 * m->P.hcap + 8 * m->P.pcap + m->S + sizeof(TreeHdr)));
+}
+
+int spl_mcts_set_roots(spl_mcts *m, const int8_t *roots, int keep_tree, int force_full, void *hs) {
+    if (!m || !roots) return SPL_EINVAL;
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_set_roots<N>, wave_grid(m->B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, m->P, m->cfg, m->B, roots, keep_tree,
+                                          force_full));
+    return check_launch();
+}
+
+int spl_mcts_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
+                    void *hs) {
+    if (!m || !leaf_state || !leaf_mask || !leaf_valid) return SPL_EINVAL;
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select<N>, wave_grid(m->B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
+                                          leaf_state, leaf_mask, leaf_valid));
+    return check_launch();
+}
+
+int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v,
+                    void *hs) {
+    if (!m || !leaf_mask || !pi || !v) return SPL_EINVAL;
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_backup<N>, wave_grid(m->B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, m->P, m->cfg, m->B, leaf_mask, pi, v));
+    return check_launch();
+}
+
+int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs, double *q,
+                        void *hs) {
+    if (!m) return SPL_EINVAL;
+    hipLaunchKernelGGL(k_root_stats, wave_grid(m->B), dim3(THREADS), 0, (hipStream_t)hs, m->P,
+                       m->cfg, m->B, m->n, counts, qsa, probs, q);
+    return check_launch();
+}
+
+int spl_mcts_headers(spl_mcts *m, int32_t *out, void *hs) {
+    if (!m || !out) return SPL_EINVAL;
+    return hipMemcpyAsync(out, m->P.hdr, sizeof(TreeHdr) * m->B, hipMemcpyDeviceToDevice,
+                          (hipStream_t)hs) == hipSuccess ? 0 : SPL_EDEVICE;
+}
+
+int spl_nn_input(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask, float *x,
+                 uint8_t *valid, void *hs) {
+    if (!ctx || B < 0 || (B && (!state || !x || (valid && !mask)))) return SPL_EINVAL;
+    if (!B) return 0;
+    const int S = 7 * (32 + 10 * ctx->n + ctx->n * ctx->n);
+    const size_t tot = (size_t)B * (S > SPL_ACTIONS ? S : SPL_ACTIONS);
+    hipLaunchKernelGGL(k_nn_input, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)hs, B, S, state, mask, x, valid);
+    return check_launch();
+}
+
+int spl_hash_eval(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask, float *pi,
+                  float *v, void *hs) {
+    if (!ctx || B < 0 || (B && (!state || !mask || !pi || !v))) return SPL_EINVAL;
+    if (!B) return 0;
+    SPL_DISPATCH(ctx->n, hipLaunchKernelGGL(k_hash_eval<N>, dim3((unsigned)B), dim3(256), 0,
+                                            (hipStream_t)hs, B, state, mask, pi, v));
+    return check_launch();
+}
+
+}  // extern "C"

@@ -43,7 +43,26 @@ _SIGS = {
     "spl_tree_step": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_rollout_step": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.c_uint32,
                           C.c_uint32, _vp], C.c_int),
+    "spl_mcts_create": ([C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)], C.c_int),
+    "spl_mcts_destroy": ([C.c_void_p], C.c_int),
+    "spl_mcts_device_bytes": ([C.c_void_p], C.c_longlong),
+    "spl_mcts_set_roots": ([C.c_void_p, _vp, C.c_int, C.c_int, _vp], C.c_int),
+    "spl_mcts_select": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_mcts_backup": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_mcts_root_stats": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_mcts_headers": ([C.c_void_p, _vp, _vp], C.c_int),
+    "spl_nn_input": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_hash_eval": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
 }
+
+
+class MctsConfig(C.Structure):
+    """spl_mcts_config (include/splendor_amd.h)"""
+    _fields_ = [("num_sims", C.c_int), ("ratio_full", C.c_int), ("prob_full", C.c_double),
+                ("cpuct", C.c_double), ("fpu", C.c_double), ("forced_playouts", C.c_int),
+                ("dirichlet_alpha", C.c_double), ("dirichlet_temp", C.c_double),
+                ("temp_threshold", C.c_int), ("node_cap", C.c_int), ("edge_cap", C.c_int),
+                ("seed", C.c_uint64), ("board_base", C.c_uint32)]
 
 
 def exported_symbols():

@@ -1,0 +1,150 @@
+"""Batched device-resident MCTS (host side of csrc/mcts.hip).
+
+`BatchedMCTS` holds B persistent search trees in HBM (one per board/game) and exposes the
+reference's search API in batched form:
+
+    reference (MCTS.py)                              here
+    MCTS(game, nnet, args, dirichlet_noise)          BatchedMCTS(engine, B, args, evaluator)
+    getActionProb(canonicalBoard, temp=1, full)      get_action_prob(canonical_boards, full)
+    reset_all_search_trees()                         reset()
+
+`evaluator(leaf_state int8[B,R,7], leaf_mask int64[B,7], leaf_valid uint8[B]) -> (pi
+float32[B,409], v float32[B,n])` is the batched `nnet.predict` (GenericNNetWrapper.py:141):
+`HashEvaluator` (deterministic, parity tests) or `splendor.nnet.NetEvaluator`
+(SplendorNNet under PyTorch-ROCm).
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .env import ACTIONS, MASK_WORDS, _ptr
+
+# TreeHdr (csrc/mcts_device.h), 112 bytes
+HDR_DTYPE = np.dtype([
+    ("node_count", "<i4"), ("edge_count", "<i4"), ("root", "<i4"), ("sims_done", "<i4"),
+    ("budget", "<i4"), ("full", "<i4"), ("noise_pending", "<i4"), ("depth", "<i4"),
+    ("leaf_kind", "<i4"), ("player", "<i4"), ("episode_step", "<i4"), ("move_no", "<i4"),
+    ("game_no", "<i4"), ("overflow", "<i4"), ("n_examples", "<i4"), ("leaf_round", "<i4"),
+    ("leaf_k0", "<u8"), ("leaf_k1", "<u8"), ("leaf_v", "<f4", (4,)),
+    ("games_done", "<i4"), ("forced", "<i4"), ("pad0", "<i4"), ("pad1", "<i4")])
+assert HDR_DTYPE.itemsize == 112
+
+DEFAULT_ARGS = dict(numMCTSSims=100, cpuct=1.0, fpu=0.0, prob_fullMCTS=1.0, ratio_fullMCTS=5,
+                    forced_playouts=False, dirichletAlpha=0.0, temperature=[1.25, 0.8],
+                    tempThreshold=10)
+
+
+def _arg(args, k):
+    if args is None:
+        return DEFAULT_ARGS[k]
+    try:
+        return args[k]
+    except (KeyError, TypeError):
+        return getattr(args, k, DEFAULT_ARGS[k])
+
+
+class HashEvaluator:
+    """Deterministic stand-in network (spl_hash_eval); identical to the oracle's."""
+
+    def __init__(self, engine):
+        self.e = engine
+
+    def __call__(self, leaf_state, leaf_mask, leaf_valid):
+        B = leaf_state.shape[0]
+        pi = torch.empty((B, ACTIONS), dtype=torch.float32, device=self.e.device)
+        v = torch.empty((B, self.e.n), dtype=torch.float32, device=self.e.device)
+        _lib.check(self.e.L.spl_hash_eval(self.e.ctx, B, _ptr(leaf_state), _ptr(leaf_mask), _ptr(pi),
+                                          _ptr(v), self.e._s()), "spl_hash_eval")
+        return pi, v
+
+
+class BatchedMCTS:
+    def __init__(self, engine, B, args=None, evaluator=None, dirichlet_noise=False, seed=0x5EED,
+                 board_base=0, node_cap=None, edge_cap=None):
+        self.e = engine
+        self.L = engine.L
+        self.B = B
+        self.args = args
+        sims = int(_arg(args, "numMCTSSims"))
+        cfg = _lib.MctsConfig()
+        cfg.num_sims = sims
+        cfg.ratio_full = int(_arg(args, "ratio_fullMCTS"))
+        cfg.prob_full = float(_arg(args, "prob_fullMCTS"))
+        cfg.cpuct = float(_arg(args, "cpuct"))
+        cfg.fpu = float(_arg(args, "fpu"))
+        cfg.forced_playouts = int(bool(_arg(args, "forced_playouts")))
+        cfg.dirichlet_alpha = float(_arg(args, "dirichletAlpha")) if dirichlet_noise else 0.0
+        cfg.dirichlet_temp = float(_arg(args, "temperature")[0])
+        cfg.temp_threshold = int(_arg(args, "tempThreshold"))
+        # capacity: a search adds <= sims nodes; keep room for retained subtrees
+        cfg.node_cap = int(node_cap or max(4 * sims + 64, 256))
+        cfg.edge_cap = int(edge_cap or 32 * cfg.node_cap)
+        cfg.seed = seed
+        cfg.board_base = board_base
+        self.cfg = cfg
+        h = C.c_void_p()
+        _lib.check(self.L.spl_mcts_create(engine.ctx, B, C.byref(cfg), C.byref(h)), "spl_mcts_create")
+        self.h = h
+        dev = engine.device
+        self.leaf_state = engine.new_state(B)
+        self.leaf_mask = torch.zeros((B, MASK_WORDS), dtype=torch.int64, device=dev)
+        self.leaf_valid = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.evaluator = evaluator or HashEvaluator(engine)
+        self._hdr = torch.empty((B, HDR_DTYPE.itemsize // 4), dtype=torch.int32, device=dev)
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None:
+            self.L.spl_mcts_destroy(self.h)
+            self.h = None
+
+    @property
+    def device_bytes(self):
+        return int(self.L.spl_mcts_device_bytes(self.h))
+
+    # ---------------------------------------------------------------- primitives
+    def set_roots(self, roots, keep_tree=True, force_full=True):
+        _lib.check(self.L.spl_mcts_set_roots(self.h, _ptr(roots), int(keep_tree), int(force_full),
+                                             self.e._s()), "spl_mcts_set_roots")
+
+    def simulate(self):
+        """One simulation on every tree with budget left: select -> evaluate -> backup."""
+        s = self.e._s()
+        _lib.check(self.L.spl_mcts_select(self.h, _ptr(self.leaf_state), _ptr(self.leaf_mask),
+                                          _ptr(self.leaf_valid), s), "spl_mcts_select")
+        pi, v = self.evaluator(self.leaf_state, self.leaf_mask, self.leaf_valid)
+        _lib.check(self.L.spl_mcts_backup(self.h, _ptr(self.leaf_mask), _ptr(pi), _ptr(v), s),
+                   "spl_mcts_backup")
+
+    def headers(self):
+        _lib.check(self.L.spl_mcts_headers(self.h, _ptr(self._hdr), self.e._s()), "spl_mcts_headers")
+        return self._hdr.cpu().numpy().view(HDR_DTYPE).reshape(self.B)
+
+    def root_stats(self):
+        B, dev = self.B, self.e.device
+        counts = torch.empty((B, ACTIONS), dtype=torch.int64, device=dev)
+        qsa = torch.empty((B, ACTIONS), dtype=torch.float64, device=dev)
+        probs = torch.empty((B, ACTIONS), dtype=torch.float64, device=dev)
+        q = torch.empty((B, self.e.n), dtype=torch.float64, device=dev)
+        _lib.check(self.L.spl_mcts_root_stats(self.h, _ptr(counts), _ptr(qsa), _ptr(probs), _ptr(q),
+                                              self.e._s()), "spl_mcts_root_stats")
+        return counts, qsa, probs, q
+
+    # ---------------------------------------------------------------- reference API
+    def get_action_prob(self, canonical_boards, force_full_search=True, keep_tree=True):
+        """Batched MCTS.getActionProb(temp=1) (MCTS.py:45-97): returns (probs f64 [B,409],
+        q f64 [B,n], is_full_search bool [B], counts i64 [B,409])."""
+        self.set_roots(canonical_boards, keep_tree=keep_tree, force_full=force_full_search)
+        hdr = self.headers()
+        for _ in range(int(hdr["budget"].max())):
+            self.simulate()
+        hdr = self.headers()
+        if hdr["overflow"].any():
+            raise _lib.EngineError(f"tree capacity exceeded on {int((hdr['overflow'] != 0).sum())} trees")
+        counts, _, probs, q = self.root_stats()
+        return probs, q, torch.from_numpy(hdr["full"] != 0), counts
+
+    def reset(self):
+        """reset_all_search_trees (MCTS.py:188-192): next set_roots starts empty trees."""
+        self._reset_pending = True

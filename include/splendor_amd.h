@@ -100,6 +100,65 @@ int spl_rollout_step(const spl_ctx *ctx, int B, int8_t *state, int8_t *player,
                      int32_t *games_done, uint64_t seed, uint32_t step, uint32_t board_base,
                      void *hip_stream);
 
+
+/* ===================================================================== MCTS
+ * Device-resident batched PUCT search (MCTS.py), one tree per board/game, B trees.
+ * The reference's MCTS(game, nnet, args).getActionProb(canonicalBoard, temp=1,
+ * force_full_search) (MCTS.py:45-97) maps to:
+ *     spl_mcts_set_roots(roots)                 -- re-root (tree persists when keep_tree)
+ *     repeat until every tree spent its budget:
+ *         spl_mcts_select(leaf_state, leaf_mask, leaf_valid)   -- MCTS.search descent
+ *         <network on leaf_state/leaf_mask -> pi[B][409], v[B][n]> (nnet.predict, :138)
+ *         spl_mcts_backup(leaf_mask, pi, v)     -- expansion + backup (:134-176)
+ *     spl_mcts_root_stats(counts, qsa, probs, q) -- :61-97 (temp = 1)
+ * Every tree runs exactly one simulation per select/backup pair, so each tree's search
+ * is the reference's sequential search. Trees own device memory allocated at create. */
+typedef struct spl_mcts spl_mcts;
+typedef struct {
+    int num_sims;            /* numMCTSSims (main.py:110) */
+    int ratio_full;          /* ratio_fullMCTS: fast search = num_sims / ratio_full */
+    double prob_full;        /* prob_fullMCTS: P(full search) (MCTS.py:54) */
+    double cpuct;            /* cpuct */
+    double fpu;              /* fpu (>0: parent-relative; <=0: absolute) (MCTS.py:203) */
+    int forced_playouts;     /* forced playouts + policy-target pruning (MCTS.py:56,69-74) */
+    double dirichlet_alpha;  /* > 0 enables root noise at step 0 of full searches */
+    double dirichlet_temp;   /* temperature[0]: softmax before noise (MCTS.py:142) */
+    int temp_threshold;      /* tempThreshold (Coach.py:82-83), self-play only */
+    int node_cap;            /* nodes per tree */
+    int edge_cap;            /* CSR edges per tree */
+    uint64_t seed;           /* Philox key for search/self-play randomness */
+    uint32_t board_base;     /* global id of tree 0 (multi-GPU sharding) */
+} spl_mcts_config;
+
+int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_mcts **out);
+int spl_mcts_destroy(spl_mcts *m);
+long long spl_mcts_device_bytes(const spl_mcts *m);
+/* roots: B canonical boards (device). keep_tree: look the root up in the persistent
+ * transposition table and keep its subtree (exact GC of unreachable nodes). */
+int spl_mcts_set_roots(spl_mcts *m, const int8_t *roots, int keep_tree, int force_full,
+                       void *hip_stream);
+/* leaf_state: B x S int8, leaf_mask: B x 7 u64, leaf_valid: B u8 (1 = needs the network) */
+int spl_mcts_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
+                    void *hip_stream);
+/* pi: B x 409 f32 (policy over all actions, as predict returns), v: B x n f32 */
+int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v,
+                    void *hip_stream);
+/* counts B x 409 i64, qsa B x 409 f64 (-42 = unvisited), probs B x 409 f64, q B x n f64;
+ * any may be NULL */
+int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs, double *q,
+                        void *hip_stream);
+/* copies the B per-tree headers (112 bytes each, layout in splendor/mcts.py) to `out` */
+int spl_mcts_headers(spl_mcts *m, int32_t *out, void *hip_stream);
+
+/* predict input conversion (GenericNNetWrapper.py:160-161): int8 boards -> f32, packed
+ * mask -> bool bytes (valid may be NULL) */
+int spl_nn_input(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask,
+                 float *x, uint8_t *valid, void *hip_stream);
+/* deterministic hash-prior network (see oracle or_fake_predict): parity tests and
+ * tree-only throughput runs */
+int spl_hash_eval(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask,
+                  float *pi, float *v, void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

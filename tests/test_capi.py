@@ -14,7 +14,7 @@ LIB = os.path.join(ROOT, "alphazero-general-ori_amd", "libsplendor_amd.so")
 
 def declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*int\s+(spl_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|long long)\s+(spl_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_header_declares_entry_points():
@@ -62,3 +62,20 @@ def test_missing_engine_fails_loudly(monkeypatch):
     monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libsplendor_amd.so")
     with pytest.raises(_lib.NativeEngineMissing):
         _lib.lib()
+
+
+def test_mcts_config_struct_layout(tmp_path):
+    """ctypes MctsConfig must match the C layout of spl_mcts_config."""
+    import subprocess
+    from splendor import _lib
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "splendor_amd.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu\\n", sizeof(spl_mcts_config),'
+                   'offsetof(spl_mcts_config, seed), offsetof(spl_mcts_config, node_cap),'
+                   'offsetof(spl_mcts_config, dirichlet_temp));return 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    size, off_seed, off_cap, off_temp = map(int, subprocess.check_output([str(exe)]).split())
+    M = _lib.MctsConfig
+    assert ctypes.sizeof(M) == size
+    assert M.seed.offset == off_seed and M.node_cap.offset == off_cap and M.dirichlet_temp.offset == off_temp
