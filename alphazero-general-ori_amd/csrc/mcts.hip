@@ -241,23 +241,16 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round) {
 }
 
 // ------------------------------------------------------------ search start
-// Re-root every tree at the given canonical board (MCTS.getActionProb entry, :45-56):
-// look the root up in the persistent table (keep != 0) or start empty; draw the
-// full/fast search decision; arm root noise.
+// Re-root tree t at the canonical board staged in LDS `s` (MCTS.getActionProb entry,
+// :45-56): look the root up in the persistent table (keep) and collect garbage, or start
+// empty; draw the full/fast search decision (ST_FULL) and arm root noise. Wave-collective.
 template <int N>
-__global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int B,
-                                                       const int8_t *__restrict__ roots, int keep,
-                                                       int force_full) {
+__device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const int8_t *s, bool keep,
+                             bool force_full) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
-    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
-    if (t >= B) return;
     const int l = lane_id();
-    int8_t *s = lds[w];
-    for (int i = Lx::S + l; i < Lx::SPAD; i += 64) s[i] = 0;
-    wave_copy_board<N>(s, roots + (size_t)t * Lx::S);
-    wave_copy_board<N>(P.root_state + (size_t)t * Lx::S, s);
     TreeHdr *H = P.hdr + t;
+    wave_copy_board<N>(P.root_state + (size_t)t * Lx::S, s);
     int root = -1;
     if (keep && H->node_count > 0) {
         uint64_t k0, k1;
@@ -271,6 +264,7 @@ __global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int
     }
     const int mv = H->move_no;
     const bool full = force_full || philox_u01(C.seed, C.board_base + t, ST_FULL | (uint32_t)mv, 0) < C.prob_full;
+    __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     if (l == 0) {
         H->root = root;
@@ -283,6 +277,218 @@ __global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int
         H->overflow = 0;
         H->move_no = mv + 1;
     }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int B,
+                                                       const int8_t *__restrict__ roots, int keep,
+                                                       int force_full) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    if (t >= B) return;
+    int8_t *s = lds[w];
+    for (int i = Lx::S + lane_id(); i < Lx::SPAD; i += 64) s[i] = 0;
+    wave_copy_board<N>(s, roots + (size_t)t * Lx::S);
+    begin_search<N>(P, C, t, s, keep != 0, force_full != 0);
+}
+
+// ------------------------------------------------------------ self-play
+// New game on tree t: Board.init_game with ST_DEAL draws, player 0, fresh tree.
+template <int N>
+__device__ void deal_game(const Pools &P, const SearchCfg &C, int t, int8_t *b) {
+    TreeHdr *H = P.hdr + t;
+    const int g = H->game_no;
+    Chance ch{nullptr, C.seed, C.board_base + (uint32_t)t, ST_DEAL | (uint32_t)g, 0};
+    init_game<N>(b, ch);
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    if (lane_id() == 0) {
+        H->game_no = g + 1;
+        H->player = 0;
+        H->episode_step = 0;
+        H->n_examples = 0;
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_reset_games(Pools P, SearchCfg C, int B) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    if (t >= B) return;
+    int8_t *b = lds[w];
+    for (int i = Lx::S + lane_id(); i < Lx::SPAD; i += 64) b[i] = 0;
+    deal_game<N>(P, C, t, b);
+    wave_copy_board<N>(P.board + (size_t)t * Lx::S, b);
+    begin_search<N>(P, C, t, b, false, false);
+}
+
+// policy-target pruning of MCTS.py:69-74 applied to one root edge
+__device__ __forceinline__ long long pruned_count(long long c, int best, bool forced, float p, int sims) {
+    if (forced) {
+        if (c != best) c -= (long long)sqrt(0.5 * (double)p * (double)sims);
+        if (c <= 1) c = 0;
+    }
+    return c;
+}
+
+// One Coach.executeEpisode iteration (Coach.py:72-100) for every tree whose search is done.
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B, int lim) {
+    using Lx = Lay<N>;
+    __shared__ __align__(16) int8_t lds[WAVES][2][Lx::SPAD];
+    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    if (t >= B) return;
+    const int l = lane_id();
+    TreeHdr *H = P.hdr + t;
+    if (H->sims_done < H->budget || H->overflow || H->root < 0) return;
+    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
+    const uint32_t gb = C.board_base + (uint32_t)t;
+    const int root = H->root, eb = P.neb[nb + root], ec = P.nec[nb + root];
+    const bool forced = H->forced;
+    const int sims = H->budget, cm = H->move_no;
+    const int16_t *ea = P.ea + e0 + eb;
+    const int32_t *en = P.en + e0 + eb;
+    const float *ep = P.ep + e0 + eb;
+    int best = 0;
+    for (int i = l; i < ec; i += 64) best = max(best, en[i]);
+    for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
+    long long tot = 0;
+    for (int i = l; i < ec; i += 64) tot += pruned_count(en[i], best, forced, ep[i], sims);
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    const int step = H->episode_step + 1;
+    const int player = H->player;
+    int8_t *s = lds[w][0], *b = lds[w][1];
+    for (int i = Lx::S + l; i < Lx::SPAD; i += 64) { s[i] = 0; b[i] = 0; }
+    // training example (Coach.py:76-80): canonical board, player, pi, valids, q
+    int nex = H->n_examples;
+    if (H->full && nex < P.excap) {
+        const size_t x = (size_t)t * P.excap + nex;
+        wave_copy_board<N>(s, P.root_state + (size_t)t * Lx::S);
+        wave_copy_board<N>(P.ex_state + x * Lx::S, s);
+        float *pi = P.ex_pi + x * SPL_ACTIONS;
+        for (int a = l; a < SPL_ACTIONS; a += 64) pi[a] = 0.f;
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        for (int i = l; i < ec; i += 64)   // getSymmetries stores pi as float32 (SplendorGame.py:59-61)
+            pi[ea[i]] = (float)((double)pruned_count(en[i], best, forced, ep[i], sims) / (double)tot);
+        uint64_t m[7];
+        wave_valid_moves<N>(s, 0, lim, m);
+        uint64_t mv = m[0];
+#pragma unroll
+        for (int k = 1; k < 7; k++) mv = l == k ? m[k] : mv;
+        if (l < 7) P.ex_valid[x * 7 + l] = mv;
+        if (l == 0) {
+            const double q0 = P.nqs[nb + root];
+            P.ex_player[x] = player;
+            for (int i = 0; i < 4; i++)
+                P.ex_q[x * 4 + i] = i == 0 ? (float)q0 : (i < N ? (float)(-q0 / (double)(N - 1)) : 0.f);
+        }
+        nex++;
+    }
+    // action = random_pick(pi, T) (Coach.py:30-33, 82-83): numpy legacy choice with p
+    int action = 408;
+    if (l == 0) {
+        const double T = C.temp_threshold > 0 ? (step < C.temp_threshold ? 2.0 : 0.2) : 1.0;
+        double sum = 0.0;
+        for (int i = 0; i < ec; i++)
+            sum += temp_pow((double)pruned_count(en[i], best, forced, ep[i], sims) / (double)tot, T);
+        double last = 0.0;
+        for (int i = 0; i < ec; i++)
+            last += temp_pow((double)pruned_count(en[i], best, forced, ep[i], sims) / (double)tot, T) / sum;
+        const double u = philox_u01(C.seed, gb, ST_PICK | (uint32_t)cm, 0);
+        double cdf = 0.0;
+        action = ea[ec - 1];
+        for (int i = 0; i < ec; i++) {
+            cdf += temp_pow((double)pruned_count(en[i], best, forced, ep[i], sims) / (double)tot, T) / sum;
+            if (cdf / last > u) { action = ea[i]; break; }
+        }
+    }
+    action = __shfl(action, 0, 64);
+    // getNextState with chance (Coach.py:86), getGameEnded (:88)
+    wave_copy_board<N>(b, P.board + (size_t)t * Lx::S);
+    Chance ch{nullptr, C.seed, gb, ST_MOVE | (uint32_t)cm, 0};
+    int nxt = make_move<N>(b, action, player, false, ch);
+    __builtin_amdgcn_wave_barrier();
+    float r[N];
+    check_end<N>(b, r);
+    bool ended = false;
+#pragma unroll
+    for (int i = 0; i < N; i++) ended |= r[i] != 0.f;
+    if (l == 0) { H->n_examples = nex; H->pad0 += 1; }      // pad0 = moves played
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    if (ended) {                                            // Coach.py:89-98
+        int f[N];
+#pragma unroll
+        for (int i = 0; i < N; i++) f[i] = get_score<N>(b, i);
+        for (int j = 0; j < nex; j++) {
+            const size_t x = (size_t)t * P.excap + j;
+            int slot = 0;
+            if (l == 0) slot = atomicAdd(&P.counters[0], 1);
+            slot = __shfl(slot, 0, 64);
+            if (slot >= P.out_cap) {
+                if (l == 0) atomicAdd(&P.counters[1], 1);
+                continue;
+            }
+            const int px = P.ex_player[x];
+            wave_copy_board<N>(P.out_state + (size_t)slot * Lx::S, P.ex_state + x * Lx::S);
+            for (int a = l; a < SPL_ACTIONS; a += 64)
+                P.out_pi[(size_t)slot * SPL_ACTIONS + a] = P.ex_pi[x * SPL_ACTIONS + a];
+            if (l < 7) P.out_valid[(size_t)slot * 7 + l] = P.ex_valid[x * 7 + l];
+            if (l < 4) {
+                const int src = (l + px) % N;
+                P.out_winner[(size_t)slot * 4 + l] = l < N ? r[src < N ? src : 0] : 0.f;
+                P.out_scdiff[(size_t)slot * 4 + l] = l < N ? f[src < N ? src : 0] - f[px < N ? px : 0] : 0;
+                P.out_q[(size_t)slot * 4 + l] = P.ex_q[x * 4 + l];
+                const int meta[4] = {(int)gb, H->game_no - 1, j, px};
+                P.out_meta[(size_t)slot * 4 + l] = meta[l];
+            }
+        }
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        if (l == 0) H->games_done += 1;
+        deal_game<N>(P, C, t, b);                               // next episode
+        nxt = 0;
+    } else if (l == 0) {
+        H->player = nxt;
+        H->episode_step = step;
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    wave_copy_board<N>(P.board + (size_t)t * Lx::S, b);
+    wave_roll_players<N>(s, b, nxt);                            // getCanonicalForm (:73)
+    begin_search<N>(P, C, t, s, !ended, false);
+}
+
+__global__ void k_drain_copy(Pools P, int S, int max, int8_t *st, float *pi, uint64_t *valid,
+                             float *winner, int32_t *scdiff, float *q, int n) {
+    const int k = min(P.counters[0], min(max, P.out_cap));
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)k * SPL_ACTIONS;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const size_t e = i / SPL_ACTIONS, j = i % SPL_ACTIONS;
+        if (pi) pi[i] = P.out_pi[i];
+        if (st && j < (size_t)S) st[e * S + j] = P.out_state[e * S + j];
+        if (j < 7 && valid) valid[e * 7 + j] = P.out_valid[e * 7 + j];
+        if (j < (size_t)n) {
+            if (winner) winner[e * n + j] = P.out_winner[e * 4 + j];
+            if (scdiff) scdiff[e * n + j] = P.out_scdiff[e * 4 + j];
+            if (q) q[e * n + j] = P.out_q[e * 4 + j];
+        }
+    }
+}
+
+__global__ void k_drain_reset(Pools P, int max, int32_t *n_out) {
+    const int c = P.counters[0];
+    const int k = min(c, min(max, P.out_cap));
+    if (n_out) *n_out = k;
+    P.counters[1] += c - k;
+    P.counters[0] = 0;
 }
 
 // ------------------------------------------------------------ select
@@ -608,6 +814,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     C.prob_full = cfg->prob_full; C.num_sims = cfg->num_sims; C.ratio_full = cfg->ratio_full;
     C.forced_playouts = cfg->forced_playouts; C.dirichlet = cfg->dirichlet_alpha > 0;
     C.temp_threshold = cfg->temp_threshold; C.seed = cfg->seed; C.board_base = cfg->board_base;
+    C.selfplay = cfg->selfplay;
     Pools &P = m->P;
     P.ncap = cfg->node_cap; P.ecap = cfg->edge_cap;
     int h = 1;
@@ -621,6 +828,11 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(2 * ne); acc(4 * ne); acc(4 * ne);
     acc(4 * ne); acc(8 * ne); acc(4 * (size_t)B * P.hcap); acc(8 * (size_t)B * P.pcap);
     acc(4 * nn); acc((size_t)B * m->S);
+    const int excap = cfg->selfplay ? 62 * ctx->n + 2 : 0;
+    const size_t nx = (size_t)B * excap, no = cfg->selfplay ? (size_t)(cfg->out_cap > 0 ? cfg->out_cap : 4 * B) : 0;
+    acc((size_t)B * m->S); acc(nx * m->S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
+    acc(no * m->S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
+    acc(16 * no); acc(64);
     void *arena = nullptr;
     if (hipMalloc(&arena, bytes) != hipSuccess) { delete m; return SPL_EDEVICE; }
     if (hipMemset(arena, 0, bytes) != hipSuccess) { (void)hipFree(arena); delete m; return SPL_EDEVICE; }
@@ -637,6 +849,15 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.path = carve<int32_t>(p, 2 * (size_t)B * P.pcap);
     P.remap = carve<int32_t>(p, nn);
     P.root_state = carve<int8_t>(p, (size_t)B * m->S);
+    P.excap = excap; P.out_cap = (int)no;
+    P.board = carve<int8_t>(p, (size_t)B * m->S);
+    P.ex_state = carve<int8_t>(p, nx * m->S); P.ex_pi = carve<float>(p, nx * SPL_ACTIONS);
+    P.ex_q = carve<float>(p, 4 * nx); P.ex_valid = carve<uint64_t>(p, 7 * nx);
+    P.ex_player = carve<int32_t>(p, nx);
+    P.out_state = carve<int8_t>(p, no * m->S); P.out_pi = carve<float>(p, no * SPL_ACTIONS);
+    P.out_winner = carve<float>(p, 4 * no); P.out_q = carve<float>(p, 4 * no);
+    P.out_valid = carve<uint64_t>(p, 7 * no); P.out_scdiff = carve<int32_t>(p, 4 * no);
+    P.out_meta = carve<int32_t>(p, 4 * no); P.counters = carve<int32_t>(p, 16);
     if (hipMemset(P.hslot, 0xFF, 4 * (size_t)B * P.hcap) != hipSuccess) {
         (void)hipFree(arena); delete m; return SPL_EDEVICE;
     }
@@ -687,6 +908,33 @@ int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs
     if (!m) return SPL_EINVAL;
     hipLaunchKernelGGL(k_root_stats, wave_grid(m->B), dim3(THREADS), 0, (hipStream_t)hs, m->P,
                        m->cfg, m->B, m->n, counts, qsa, probs, q);
+    return check_launch();
+}
+
+int spl_mcts_reset_games(spl_mcts *m, void *hs) {
+    if (!m || !m->cfg.selfplay) return SPL_EINVAL;
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_reset_games<N>, wave_grid(m->B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, m->P, m->cfg, m->B));
+    return check_launch();
+}
+
+int spl_mcts_commit(spl_mcts *m, void *hs) {
+    if (!m || !m->cfg.selfplay) return SPL_EINVAL;
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_commit<N>, wave_grid(m->B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit));
+    return check_launch();
+}
+
+int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *valid, float *winner,
+                            int32_t *scdiff, float *q, int max, int32_t *n_out, void *hs) {
+    if (!m || !m->cfg.selfplay || max < 0) return SPL_EINVAL;
+    const size_t work = (size_t)(max < m->P.out_cap ? max : m->P.out_cap) * SPL_ACTIONS;
+    if (work) {
+        const unsigned grid = (unsigned)((work + 255) / 256 > 4096 ? 4096 : (work + 255) / 256);
+        hipLaunchKernelGGL(k_drain_copy, dim3(grid), dim3(256), 0, (hipStream_t)hs, m->P, m->S, max,
+                           state, pi, valid, winner, scdiff, q, m->n);
+    }
+    hipLaunchKernelGGL(k_drain_reset, dim3(1), dim3(1), 0, (hipStream_t)hs, m->P, max, n_out);
     return check_launch();
 }
 

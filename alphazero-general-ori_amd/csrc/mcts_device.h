@@ -45,12 +45,24 @@ struct Pools {
     int32_t *path;                       // pcap x 2 (node, edge)
     int32_t *remap;                      // ncap scratch for compaction
     int8_t *root_state;                  // B x S (canonical root)
+    // self-play (Coach.executeEpisode) state
+    int excap, out_cap;                  // staged examples per tree, finished-example queue
+    int8_t *board;                       // B x S real (non-canonical) boards
+    int8_t *ex_state;                    // B x excap x S
+    float *ex_pi, *ex_q;                 // B x excap x 409, B x excap x 4
+    uint64_t *ex_valid;                  // B x excap x 7
+    int32_t *ex_player;                  // B x excap
+    int8_t *out_state;                   // out_cap x S
+    float *out_pi, *out_winner, *out_q;  // out_cap x 409 / 4 / 4
+    uint64_t *out_valid;                 // out_cap x 7
+    int32_t *out_scdiff, *out_meta;      // out_cap x 4, out_cap x 4 (board id, game, index, player)
+    int32_t *counters;                   // [0] queued examples [1] dropped
 };
 
 struct SearchCfg {
     double cpuct, fpu, dir_alpha, dir_temp, prob_full;
     int num_sims, ratio_full, forced_playouts, dirichlet;
-    int temp_threshold;
+    int temp_threshold, selfplay;
     uint64_t seed;
     uint32_t board_base;
 };
@@ -137,6 +149,22 @@ __device__ __forceinline__ float pw_block(const float *a, int len) {
 // pairwise(409) = ((pw[0,96) + pw[96,200)) + (pw[200,304) + pw[304,409)))
 __device__ __forceinline__ float np_sum409(const float *a) {
     return (pw_block(a, 96) + pw_block(a + 96, 104)) + (pw_block(a + 200, 104) + pw_block(a + 304, 105));
+}
+
+// x ** (1/T) of applyTemperatureAndNormalize (Coach.py:25) with an exactly specified
+// evaluation shared with the oracle: sqrt for 1/T = 0.5, left-to-right products for small
+// integer 1/T (T = 0.2 -> x^5), pow otherwise.
+__host__ __device__ inline double temp_pow(double x, double T) {
+    if (T == 1.0) return x;
+    const double e = 1.0 / T;
+    if (e == 0.5) return sqrt(x);
+    const int k = (int)e;
+    if ((double)k == e && k >= 1 && k <= 8) {
+        double r = x;
+        for (int j = 1; j < k; j++) r = r * x;
+        return r;
+    }
+    return pow(x, e);
 }
 
 }  // namespace spl

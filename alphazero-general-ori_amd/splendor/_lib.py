@@ -51,6 +51,9 @@ _SIGS = {
     "spl_mcts_backup": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_root_stats": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_headers": ([C.c_void_p, _vp, _vp], C.c_int),
+    "spl_mcts_reset_games": ([C.c_void_p, _vp], C.c_int),
+    "spl_mcts_commit": ([C.c_void_p, _vp], C.c_int),
+    "spl_mcts_drain_examples": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int, _vp, _vp], C.c_int),
     "spl_nn_input": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_hash_eval": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
 }
@@ -62,7 +65,8 @@ class MctsConfig(C.Structure):
                 ("cpuct", C.c_double), ("fpu", C.c_double), ("forced_playouts", C.c_int),
                 ("dirichlet_alpha", C.c_double), ("dirichlet_temp", C.c_double),
                 ("temp_threshold", C.c_int), ("node_cap", C.c_int), ("edge_cap", C.c_int),
-                ("seed", C.c_uint64), ("board_base", C.c_uint32)]
+                ("seed", C.c_uint64), ("board_base", C.c_uint32), ("selfplay", C.c_int),
+                ("out_cap", C.c_int)]
 
 
 def exported_symbols():

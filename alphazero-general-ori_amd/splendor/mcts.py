@@ -62,7 +62,7 @@ class HashEvaluator:
 
 class BatchedMCTS:
     def __init__(self, engine, B, args=None, evaluator=None, dirichlet_noise=False, seed=0x5EED,
-                 board_base=0, node_cap=None, edge_cap=None):
+                 board_base=0, node_cap=None, edge_cap=None, selfplay=False):
         self.e = engine
         self.L = engine.L
         self.B = B
@@ -83,6 +83,8 @@ class BatchedMCTS:
         cfg.edge_cap = int(edge_cap or 32 * cfg.node_cap)
         cfg.seed = seed
         cfg.board_base = board_base
+        cfg.selfplay = int(bool(selfplay))
+        cfg.out_cap = int(getattr(self, "_selfplay_out_cap", 0))
         self.cfg = cfg
         h = C.c_void_p()
         _lib.check(self.L.spl_mcts_create(engine.ctx, B, C.byref(cfg), C.byref(h)), "spl_mcts_create")
@@ -135,6 +137,8 @@ class BatchedMCTS:
     def get_action_prob(self, canonical_boards, force_full_search=True, keep_tree=True):
         """Batched MCTS.getActionProb(temp=1) (MCTS.py:45-97): returns (probs f64 [B,409],
         q f64 [B,n], is_full_search bool [B], counts i64 [B,409])."""
+        keep_tree = keep_tree and not getattr(self, "_reset_pending", False)
+        self._reset_pending = False
         self.set_roots(canonical_boards, keep_tree=keep_tree, force_full=force_full_search)
         hdr = self.headers()
         for _ in range(int(hdr["budget"].max())):

@@ -1,0 +1,210 @@
+"""SplendorNNet under PyTorch-ROCm: the leaf evaluator of the batched search.
+
+The architecture is the reference's SplendorNNet (SplendorNNet.py:56-159: dense layers over
+the 7 columns of the (R,7) board with partial max/avg global pooling, policy/value/score-diff
+heads). Parameter names follow the reference's state_dict keys so checkpoints saved as plain
+state_dicts load with torch.load(weights_only=True).
+
+Inference path (`LeafEvaluator`): eval-mode BatchNorms are folded into per-channel affine
+terms once, the score-diff head (training-only) is skipped, and the whole
+"int8 leaves -> pi, v" computation is captured in a HIP graph at a fixed batch.
+Returns exp(masked log_softmax(pi)) and tanh(v) like GenericNNetWrapper.predict (:141-168).
+"""
+import ctypes as C
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from .env import ACTIONS, _ptr
+
+
+def _lin(i, o):
+    m = nn.Linear(i, o)
+    nn.init.kaiming_uniform_(m.weight)
+    nn.init.zeros_(m.bias)
+    return m
+
+
+class _PoolDense(nn.Module):
+    """First `groups*items` features pooled (max, avg) per group; the rest -> Linear(+BN) ->
+    ReLU (reference DenseAndPartialGPool, SplendorNNet.py:6-28)."""
+
+    def __init__(self, width, groups, items, bn_channels):
+        super().__init__()
+        self.groups, self.items = groups, items
+        self.dense_part = nn.Sequential(_lin(width - groups * items, width - 2 * groups),
+                                        nn.BatchNorm1d(bn_channels))
+
+    def forward(self, x):
+        g = self.groups * self.items
+        head = x[..., :g].unflatten(-1, (self.groups, self.items))
+        return torch.cat([head.amax(-1), head.mean(-1), F.relu(self.dense_part(x[..., g:]))], -1)
+
+
+def _col_pool(x, length=64, chans=5):
+    """Reference FlattenAndPartialGPool(64, 5) (SplendorNNet.py:31-53): over the first 64
+    features pool the first 5 channels (max, avg), flatten the rest -> [B, 1, 704]."""
+    a, rest = x[..., :length], x[..., length:]
+    pooled = a[:, :chans]
+    return torch.cat([pooled.amax(1), pooled.mean(1), a[:, chans:].flatten(1), rest.flatten(1)], 1).unsqueeze(1)
+
+
+class SplendorNNet(nn.Module):
+    def __init__(self, n_players=2, action_size=ACTIONS, max_score_diff=15):
+        super().__init__()
+        self.n = n_players
+        self.rows = 32 + 10 * n_players + n_players * n_players
+        self.action_size = action_size
+        self.scdiff = 2 * max_score_diff + 1
+        relu = nn.ReLU
+        self.dense2d_1 = nn.Sequential(_lin(self.rows, 128), nn.BatchNorm1d(7), relu(), _lin(128, 128), relu())
+        self.partialgpool_1 = _PoolDense(128, 4, 8, 7)
+        self.dense2d_3 = nn.Sequential(_lin(128, 128), relu())
+        self.dense1d_4 = nn.Sequential(_lin(64 * 4 + 64 * 7, 128), relu())
+        self.partialgpool_4 = _PoolDense(128, 4, 4, 1)
+        self.dense1d_5 = nn.Sequential(_lin(128, 128), nn.BatchNorm1d(1), relu(), _lin(128, 128), relu())
+        self.partialgpool_5 = _PoolDense(128, 4, 4, 1)
+        self.output_layers_PI = nn.Sequential(_lin(128, 128), _lin(128, action_size))
+        self.output_layers_V = nn.Sequential(_lin(128, 128), _lin(128, n_players))
+        self.output_layers_SDIFF = nn.Sequential(_lin(128, 128), _lin(128, n_players * self.scdiff))
+        self.register_buffer("lowvalue", torch.FloatTensor([-1e8]))
+
+    def trunk(self, board):
+        x = board.transpose(-1, -2).reshape(-1, 7, self.rows)
+        x = self.partialgpool_1(self.dense2d_1(x))
+        x = _col_pool(self.dense2d_3(x))
+        x = self.partialgpool_4(self.dense1d_4(x))
+        return self.partialgpool_5(self.dense1d_5(x))
+
+    def forward(self, board, valid):
+        """Reference signature: (log_pi, tanh(v), log_softmax(scdiff))."""
+        x = self.trunk(board)
+        pi = torch.where(valid, self.output_layers_PI(x).squeeze(1), self.lowvalue)
+        v = self.output_layers_V(x).squeeze(1)
+        sd = self.output_layers_SDIFF(x).squeeze(1).view(-1, self.n, self.scdiff).transpose(1, 2)
+        return F.log_softmax(pi, 1), torch.tanh(v), F.log_softmax(sd, 1)
+
+
+def _bn_affine(bn):
+    s = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+    return s, bn.bias - bn.running_mean * s
+
+
+class FoldedNet(nn.Module):
+    """Eval-mode inference form of SplendorNNet: BNs folded, no score-diff head."""
+
+    def __init__(self, net):
+        super().__init__()
+        net = net.eval()
+        self.rows = net.rows
+        with torch.no_grad():
+            l1, bn1, l2 = net.dense2d_1[0], net.dense2d_1[1], net.dense2d_1[3]
+            s, t = _bn_affine(bn1)                      # per channel (7)
+            self.w1, self.b1 = l1.weight.clone(), l1.bias.clone()
+            self.s1, self.t1 = s.view(7, 1).clone(), t.view(7, 1).clone()
+            self.w2, self.b2 = l2.weight.clone(), l2.bias.clone()
+            pd = net.partialgpool_1.dense_part
+            s, t = _bn_affine(pd[1])
+            self.wp1, self.bp1 = pd[0].weight.clone(), pd[0].bias.clone()
+            self.sp1, self.tp1 = s.view(7, 1).clone(), t.view(7, 1).clone()
+            self.w3, self.b3 = net.dense2d_3[0].weight.clone(), net.dense2d_3[0].bias.clone()
+            self.w4, self.b4 = net.dense1d_4[0].weight.clone(), net.dense1d_4[0].bias.clone()
+
+            def fold1(lin, bn):                         # BN over 1 channel -> scalar affine
+                s, t = _bn_affine(bn)
+                return (lin.weight * s).clone(), (lin.bias * s + t).clone()
+            self.wp4, self.bp4 = fold1(net.partialgpool_4.dense_part[0], net.partialgpool_4.dense_part[1])
+            self.w5a, self.b5a = fold1(net.dense1d_5[0], net.dense1d_5[1])
+            self.w5b, self.b5b = net.dense1d_5[3].weight.clone(), net.dense1d_5[3].bias.clone()
+            self.wp5, self.bp5 = fold1(net.partialgpool_5.dense_part[0], net.partialgpool_5.dense_part[1])
+            h = net.output_layers_PI
+            self.wpi1, self.bpi1, self.wpi2, self.bpi2 = (h[0].weight.clone(), h[0].bias.clone(),
+                                                          h[1].weight.clone(), h[1].bias.clone())
+            h = net.output_layers_V
+            self.wv1, self.bv1, self.wv2, self.bv2 = (h[0].weight.clone(), h[0].bias.clone(),
+                                                      h[1].weight.clone(), h[1].bias.clone())
+        for k, v in list(vars(self).items()):
+            if isinstance(v, torch.Tensor):
+                delattr(self, k)
+                self.register_buffer(k, v.detach().contiguous())
+
+    @staticmethod
+    def _pool(x, groups, items, dense):
+        g = groups * items
+        head = x[..., :g].unflatten(-1, (groups, items))
+        return torch.cat([head.amax(-1), head.mean(-1), dense], -1)
+
+    def forward(self, board, valid):
+        x = board.transpose(-1, -2)                                        # [B, 7, R]
+        x = F.relu(F.linear(x, self.w1, self.b1) * self.s1 + self.t1)
+        x = F.relu(F.linear(x, self.w2, self.b2))
+        d = F.relu(F.linear(x[..., 32:], self.wp1, self.bp1) * self.sp1 + self.tp1)
+        x = self._pool(x, 4, 8, d)
+        x = F.relu(F.linear(x, self.w3, self.b3))
+        x = _col_pool(x)
+        x = F.relu(F.linear(x, self.w4, self.b4))
+        x = self._pool(x, 4, 4, F.relu(F.linear(x[..., 16:], self.wp4, self.bp4)))
+        x = F.relu(F.linear(x, self.w5a, self.b5a))
+        x = F.relu(F.linear(x, self.w5b, self.b5b))
+        x = self._pool(x, 4, 4, F.relu(F.linear(x[..., 16:], self.wp5, self.bp5))).squeeze(1)
+        pi = F.linear(F.linear(x, self.wpi1, self.bpi1), self.wpi2, self.bpi2)
+        pi = torch.softmax(pi.masked_fill(~valid, -1e8), 1)
+        v = torch.tanh(F.linear(F.linear(x, self.wv1, self.bv1), self.wv2, self.bv2))
+        return pi, v
+
+
+def random_net(n_players=2, seed=0, device="cuda"):
+    """Seeded random-init SplendorNNet (no pretrained weights load safely)."""
+    g = torch.random.fork_rng(devices=[])
+    with g:
+        torch.manual_seed(seed)
+        net = SplendorNNet(n_players)
+    return net.to(device).eval()
+
+
+class LeafEvaluator:
+    """Batched nnet.predict for the search (GenericNNetWrapper.predict, :141-168): int8 leaf
+    boards + packed masks -> (pi f32 [B,409], v f32 [B,n]); optional HIP-graph capture."""
+
+    def __init__(self, engine, net, B, use_graph=True):
+        self.e = engine
+        self.B = B
+        self.net = FoldedNet(net).to(engine.device).eval()
+        dev = engine.device
+        self.x = torch.zeros((B, engine.rows, 7), dtype=torch.float32, device=dev)
+        self.valid = torch.zeros((B, ACTIONS), dtype=torch.bool, device=dev)
+        self.use_graph = use_graph
+        self.graph = None
+        self.pi = self.v = None
+        self._state_ptr = self._mask_ptr = None
+
+    def _convert(self, leaf_state, leaf_mask):
+        _lib.check(self.e.L.spl_nn_input(self.e.ctx, self.B, _ptr(leaf_state), _ptr(leaf_mask),
+                                         _ptr(self.x), C.c_void_p(self.valid.data_ptr()), self.e._s()),
+                   "spl_nn_input")
+
+    @torch.no_grad()
+    def _run(self, leaf_state, leaf_mask):
+        self._convert(leaf_state, leaf_mask)
+        return self.net(self.x, self.valid)
+
+    @torch.no_grad()
+    def __call__(self, leaf_state, leaf_mask, leaf_valid=None):
+        if not self.use_graph:
+            return self._run(leaf_state, leaf_mask)
+        key = (leaf_state.data_ptr(), leaf_mask.data_ptr())
+        if self.graph is None or key != (self._state_ptr, self._mask_ptr):
+            s = torch.cuda.Stream(self.e.device)
+            s.wait_stream(torch.cuda.current_stream(self.e.device))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self._run(leaf_state, leaf_mask)
+            torch.cuda.current_stream(self.e.device).wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.pi, self.v = self._run(leaf_state, leaf_mask)
+            self._state_ptr, self._mask_ptr = key
+        self.graph.replay()
+        return self.pi, self.v

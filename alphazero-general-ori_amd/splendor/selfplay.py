@@ -1,0 +1,98 @@
+"""Batched self-play: Coach.executeEpisode (Coach.py:50-100) for B concurrent games.
+
+Every iteration runs one MCTS simulation on every game's tree (select -> leaf network ->
+backup) and then `spl_mcts_commit`, which plays the move of every game whose search budget
+is spent (policy, example, temperature sampling, chance step, end of game, re-root). Games
+restart automatically, so all B trees stay busy; moves commit asynchronously per game
+(full/fast search budgets differ, MCTS.py:54-55). The whole iteration is a fixed sequence
+of stream-ordered launches, captured once into a HIP graph and replayed.
+
+Finished examples are (board, pi, winner, scdiff, valids, surprise) as assembled at
+Coach.py:91-98, drained as device tensors (`drain()`), optionally gathered across ranks
+(`gather_examples`, RCCL all-gather) and expanded with `symmetries`.
+"""
+import ctypes as C
+
+import torch
+
+from . import _lib
+from .env import ACTIONS, MASK_WORDS, _ptr
+from .mcts import BatchedMCTS
+
+
+class SelfPlay(BatchedMCTS):
+    def __init__(self, engine, B, args=None, evaluator=None, dirichlet_noise=True, seed=0x5EED,
+                 board_base=0, out_cap=None, node_cap=None, edge_cap=None):
+        self._selfplay_out_cap = int(out_cap or 8 * B)
+        super().__init__(engine, B, args, evaluator, dirichlet_noise=dirichlet_noise, seed=seed,
+                         board_base=board_base, node_cap=node_cap, edge_cap=edge_cap, selfplay=True)
+        self.graph = None
+
+    def reset(self):
+        _lib.check(self.L.spl_mcts_reset_games(self.h, self.e._s()), "spl_mcts_reset_games")
+
+    def _iteration(self):
+        self.simulate()
+        _lib.check(self.L.spl_mcts_commit(self.h, self.e._s()), "spl_mcts_commit")
+
+    def step(self, use_graph=False):
+        if not use_graph:
+            self._iteration()
+            return
+        if self.graph is None:
+            if hasattr(self.evaluator, "use_graph"):
+                self.evaluator.use_graph = False     # the whole iteration is one graph
+            self._iteration()                        # eager iteration: warms libraries
+            torch.cuda.synchronize(self.e.device)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):       # capture only; nothing executes
+                self._iteration()
+            return
+        self.graph.replay()
+
+    def drain(self):
+        """Move finished examples out of the device queue: dict of device tensors."""
+        E, n, dev = self._selfplay_out_cap, self.e.n, self.e.device
+        out = {
+            "board": torch.empty((E, self.e.rows, 7), dtype=torch.int8, device=dev),
+            "pi": torch.empty((E, ACTIONS), dtype=torch.float32, device=dev),
+            "valids": torch.empty((E, MASK_WORDS), dtype=torch.int64, device=dev),
+            "winner": torch.empty((E, n), dtype=torch.float32, device=dev),
+            "scdiff": torch.empty((E, n), dtype=torch.int32, device=dev),
+            "surprise": torch.empty((E, n), dtype=torch.float32, device=dev),
+        }
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(self.L.spl_mcts_drain_examples(
+            self.h, _ptr(out["board"]), _ptr(out["pi"]), _ptr(out["valids"]), _ptr(out["winner"]),
+            _ptr(out["scdiff"]), _ptr(out["surprise"]), E, _ptr(cnt), self.e._s()), "drain")
+        k = int(cnt.item())
+        return {key: v[:k] for key, v in out.items()}
+
+    def stats(self):
+        h = self.headers()
+        return {"games_done": int(h["games_done"].sum()), "moves": int(h["pad0"].sum()),
+                "overflow": int((h["overflow"] != 0).sum()),
+                "nodes_max": int(h["node_count"].max()), "edges_max": int(h["edge_count"].max())}
+
+
+def gather_examples(examples, group=None):
+    """Episode-end exchange across ranks (torch.distributed all_gather; RCCL on ROCm):
+    sizes first, then records padded to the largest shard."""
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return examples
+    world = dist.get_world_size(group)
+    any_t = next(iter(examples.values()))
+    k = torch.tensor([any_t.shape[0]], dtype=torch.int64, device=any_t.device)
+    sizes = [torch.zeros_like(k) for _ in range(world)]
+    dist.all_gather(sizes, k, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    mx = max(sizes)
+    out = {}
+    for key, t in examples.items():
+        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[:t.shape[0]] = t
+        parts = [torch.zeros_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        out[key] = torch.cat([p[:s] for p, s in zip(parts, sizes)])
+    return out

@@ -128,6 +128,8 @@ typedef struct {
     int edge_cap;            /* CSR edges per tree */
     uint64_t seed;           /* Philox key for search/self-play randomness */
     uint32_t board_base;     /* global id of tree 0 (multi-GPU sharding) */
+    int selfplay;            /* 1: trees play games (spl_mcts_reset_games / spl_mcts_commit) */
+    int out_cap;             /* self-play: finished-example queue capacity (examples) */
 } spl_mcts_config;
 
 int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_mcts **out);
@@ -147,6 +149,23 @@ int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, con
  * any may be NULL */
 int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs, double *q,
                         void *hip_stream);
+/* ---- self-play (Coach.executeEpisode, Coach.py:50-100), selfplay=1 only ----
+ * reset_games: deal B new games (Board.init_game via Philox) and start their searches.
+ * commit: for every tree whose search budget is spent, play the move on device:
+ *   pi = root visit counts (pruned if forced playouts), record (board, player, pi, valids,
+ *   q) if it was a full search, sample the action with temperature 2 before tempThreshold
+ *   moves and 0.2 after (Coach.py:19-33, 82-83), getNextState with chance, getGameEnded;
+ *   on game end write every example of the game with winner = roll(r, -player) and
+ *   score difference (Coach.py:89-98) to the example queue and deal a new game; re-root
+ *   the tree at the next canonical board (exact GC) and draw the next search type. */
+int spl_mcts_reset_games(spl_mcts *m, void *hip_stream);
+int spl_mcts_commit(spl_mcts *m, void *hip_stream);
+/* copy up to `max` finished examples to caller buffers (state E x S i8, pi E x 409 f32,
+ * valid E x 7 u64, winner E x n f32, scdiff E x n i32, q E x n f32), write the count to
+ * *n_out (device int32) and empty the queue (examples beyond `max` are dropped). */
+int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *valid,
+                            float *winner, int32_t *scdiff, float *q, int max,
+                            int32_t *n_out, void *hip_stream);
 /* copies the B per-tree headers (112 bytes each, layout in splendor/mcts.py) to `out` */
 int spl_mcts_headers(spl_mcts *m, int32_t *out, void *hip_stream);
 

@@ -658,6 +658,153 @@ int or_mcts_search(or_mcts *m, const int8_t *root, int64_t *counts, double *qsa,
     return m->count;
 }
 
+/* ------------------------------------------------------------------ self-play loop */
+/* Coach.executeEpisode (Coach.py:50-100) driven exactly like the device (spl_mcts_commit):
+ * one MCTS simulation per iteration per game; when a search's budget is spent the move is
+ * committed. Random decisions use Philox streams shared with the device:
+ *   full/fast search ST_FULL|move, action pick ST_PICK|move, chance ST_MOVE|move,
+ *   deals ST_DEAL|game. Dirichlet noise off (the device's is distributional only). */
+#define ST_FULL (1u << 24)
+#define ST_PICK (3u << 24)
+#define ST_MOVE (4u << 24)
+#define ST_DEAL (5u << 24)
+
+static double temp_pow(double x, double T) {       /* mcts_device.h temp_pow */
+    if (T == 1.0) return x;
+    double e = 1.0 / T;
+    if (e == 0.5) return sqrt(x);
+    int k = (int)e;
+    if ((double)k == e && k >= 1 && k <= 8) { double r = x; for (int j = 1; j < k; j++) r = r * x; return r; }
+    return pow(x, e);
+}
+
+static long long pruned(long long c, long long best, int forced, float p, int sims) {
+    if (forced) {
+        if (c != best) c -= (long long)sqrt(0.5 * (double)p * (double)sims);
+        if (c <= 1) c = 0;
+    }
+    return c;
+}
+
+typedef struct {
+    int8_t st[7 * 88]; int player; float q[4];
+    float pi[409]; uint8_t va[409];
+} or_ex_t;
+
+int or_selfplay_run(int n, int B, int iters, uint64_t seed, uint32_t board_base, int num_sims,
+                    int ratio_full, double prob_full, double cpuct, double fpu, int forced_po,
+                    int temp_threshold, int8_t *board_out, int32_t *hdr_out, int max_ex,
+                    int8_t *ex_state, float *ex_pi, uint64_t *ex_valid, float *ex_winner,
+                    int32_t *ex_scdiff, float *ex_q, int32_t *ex_meta) {
+    build_tables();
+    int S = 7 * or_rows(n), n_out = 0;
+    or_ex_t *stage = (or_ex_t *)malloc(sizeof(or_ex_t) * (62 * n + 2));
+    for (int t = 0; t < B; t++) {
+        uint32_t gb = board_base + (uint32_t)t;
+        int8_t board[7 * 88], canon[7 * 88];
+        double u[40];
+        int player = 0, step = 0, move_no = 0, game_no = 0, games_done = 0, moves = 0, nex = 0;
+        for (int d = 0; d < 29; d++) u[d] = or_uniform(seed, gb, ST_DEAL | (uint32_t)game_no, (uint32_t)d);
+        or_init(n, board, u, NULL);
+        game_no++;
+        or_mcts *m = or_mcts_new(n, num_sims, cpuct, fpu, forced_po);
+        int full = 0, budget = 0, forced = 0, sims_done = 0;
+#define BEGIN_SEARCH() do {                                                            \
+            memcpy(canon, board, (size_t)S);                                           \
+            if (player) or_swap_players(n, canon, player);                             \
+            full = or_uniform(seed, gb, ST_FULL | (uint32_t)move_no, 0) < prob_full;   \
+            move_no++;                                                                 \
+            budget = full ? num_sims : num_sims / ratio_full;                          \
+            forced = full && forced_po; sims_done = 0;                                 \
+        } while (0)
+        BEGIN_SEARCH();
+        for (int it = 0; it < iters; it++) {
+            float v[4];
+            m->step = sims_done;
+            search(m, canon, forced, v);
+            sims_done++;
+            if (sims_done < budget) continue;
+            /* commit */
+            node_t *nd = *lookup(m, canon);
+            long long best = 0, tot = 0, c[409];
+            for (int a = 0; a < 409; a++) if (nd->vs[a] && nd->nsa[a] > best) best = nd->nsa[a];
+            for (int a = 0; a < 409; a++) { c[a] = nd->vs[a] ? pruned(nd->nsa[a], best, forced, nd->ps[a], budget) : 0; tot += c[a]; }
+            step++;
+            if (full && nex < 62 * n + 2) {
+                or_ex_t *x = &stage[nex++];
+                memcpy(x->st, canon, (size_t)S);
+                x->player = player;
+                for (int a = 0; a < 409; a++) x->pi[a] = (float)((double)c[a] / (double)tot);
+                or_valid_moves(n, canon, 0, x->va);
+                x->q[0] = (float)nd->qs;
+                for (int i = 1; i < 4; i++) x->q[i] = i < n ? (float)(-nd->qs / (double)(n - 1)) : 0.f;
+            }
+            double T = temp_threshold > 0 ? (step < temp_threshold ? 2.0 : 0.2) : 1.0;
+            double sum = 0.0, last = 0.0, cdf = 0.0;
+            for (int a = 0; a < 409; a++) if (c[a] || nd->vs[a]) sum += temp_pow((double)c[a] / (double)tot, T);
+            for (int a = 0; a < 409; a++) if (c[a] || nd->vs[a]) last += temp_pow((double)c[a] / (double)tot, T) / sum;
+            double uu = or_uniform(seed, gb, ST_PICK | (uint32_t)move_no, 0);
+            int action = 408;
+            for (int a = 408; a >= 0; a--) if (nd->vs[a]) { action = a; break; }
+            for (int a = 0; a < 409; a++) {
+                if (!(c[a] || nd->vs[a])) continue;
+                cdf += temp_pow((double)c[a] / (double)tot, T) / sum;
+                if (cdf / last > uu) { action = a; break; }
+            }
+            u[0] = or_uniform(seed, gb, ST_MOVE | (uint32_t)move_no, 0);
+            u[1] = or_uniform(seed, gb, ST_MOVE | (uint32_t)move_no, 1);
+            int nxt = or_make_move(n, board, action, player, 0, u, NULL);
+            moves++;
+            float r[4];
+            or_check_end(n, board, r);
+            int any = 0;
+            for (int i = 0; i < n; i++) any |= r[i] != 0.f;
+            if (any) {
+                int f[4];
+                for (int i = 0; i < n; i++) f[i] = or_get_score(n, board, i);
+                for (int j = 0; j < nex; j++) {
+                    if (n_out < max_ex) {
+                        or_ex_t *x = &stage[j];
+                        int px = x->player;
+                        memcpy(ex_state + (size_t)n_out * S, x->st, (size_t)S);
+                        memcpy(ex_pi + (size_t)n_out * 409, x->pi, 409 * 4);
+                        uint64_t w[7] = {0};
+                        for (int a = 0; a < 409; a++) if (x->va[a]) w[a >> 6] |= 1ull << (a & 63);
+                        memcpy(ex_valid + (size_t)n_out * 7, w, sizeof w);
+                        for (int i = 0; i < n; i++) {
+                            ex_winner[(size_t)n_out * n + i] = r[(i + px) % n];
+                            ex_scdiff[(size_t)n_out * n + i] = f[(i + px) % n] - f[px];
+                            ex_q[(size_t)n_out * n + i] = x->q[i];
+                        }
+                        int32_t meta[4] = {(int32_t)gb, game_no - 1, j, px};
+                        memcpy(ex_meta + (size_t)n_out * 4, meta, sizeof meta);
+                    }
+                    n_out++;
+                }
+                games_done++;
+                for (int d = 0; d < 29; d++) u[d] = or_uniform(seed, gb, ST_DEAL | (uint32_t)game_no, (uint32_t)d);
+                or_init(n, board, u, NULL);
+                game_no++;
+                player = 0; step = 0; nex = 0;
+                or_mcts_free(m);                          /* MCTS.reset_all_search_trees */
+                m = or_mcts_new(n, num_sims, cpuct, fpu, forced_po);
+            } else {
+                player = nxt;
+            }
+            BEGIN_SEARCH();
+        }
+#undef BEGIN_SEARCH
+        if (board_out) memcpy(board_out + (size_t)t * S, board, (size_t)S);
+        if (hdr_out) {
+            int32_t h[8] = {player, step, move_no, game_no, games_done, moves, sims_done, budget};
+            memcpy(hdr_out + (size_t)t * 8, h, sizeof h);
+        }
+        or_mcts_free(m);
+    }
+    free(stage);
+    return n_out;
+}
+
 /* ------------------------------------------------------------------ rollout loop */
 /* The fused random-policy env step of spl_rollout_step (include/splendor_amd.h), run
  * for B boards x steps. Outputs are optional (NULL = skip). Returns board-steps done. */

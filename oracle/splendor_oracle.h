@@ -67,6 +67,16 @@ void     or_mcts_free(or_mcts *m);
 int or_mcts_search(or_mcts *m, const int8_t *root, int64_t *counts, double *qsa,
                    double *probs, double *q);
 
+/* Coach.executeEpisode self-play with the hash network, one simulation per iteration per
+ * game (device spl_mcts_commit semantics). Returns the number of finished examples
+ * (written up to max_ex). hdr_out: B x 8 (player, episode_step, move_no, game_no,
+ * games_done, moves, sims_done, budget). */
+int or_selfplay_run(int n, int B, int iters, uint64_t seed, uint32_t board_base, int num_sims,
+                    int ratio_full, double prob_full, double cpuct, double fpu, int forced_po,
+                    int temp_threshold, int8_t *board_out, int32_t *hdr_out, int max_ex,
+                    int8_t *ex_state, float *ex_pi, uint64_t *ex_valid, float *ex_winner,
+                    int32_t *ex_scdiff, float *ex_q, int32_t *ex_meta);
+
 /* random-policy rollout loop used as the CPU baseline: B boards, steps steps each,
  * mask -> uniform valid action -> chance step -> end check -> reset on end.
  * Returns total board-steps executed. threads<=0 => 1. */

@@ -49,6 +49,11 @@ def lib():
         L.or_rollout_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint32, p8, p8,
                                      C.POINTER(C.c_int16), pf, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
         L.or_rollout_run.restype = C.c_longlong
+        L.or_selfplay_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint32, C.c_int, C.c_int,
+                                      C.c_double, C.c_double, C.c_double, C.c_int, C.c_int, p8,
+                                      C.POINTER(C.c_int32), C.c_int, p8, pf, C.POINTER(C.c_uint64), pf,
+                                      C.POINTER(C.c_int32), pf, C.POINTER(C.c_int32)]
+        L.or_selfplay_run.restype = C.c_int
         L.or_philox4x32.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
@@ -186,3 +191,25 @@ def rollout_run(n, B, steps, seed, board_base=0):
                          _p(act, C.c_int16), _p(end, C.c_float), _p(games, C.c_int32),
                          _p(fold, C.c_uint64))
     return {"state": st, "player": pl, "action": act, "ended": end, "games": games, "mask_fold": fold}
+
+
+def selfplay_run(n, B, iters, seed, num_sims, ratio_full, prob_full, cpuct, fpu, forced, temp_threshold,
+                 board_base=0, max_ex=20000):
+    """Oracle of the device self-play loop (spl_mcts_commit semantics)."""
+    R = rows(n)
+    board = np.zeros((B, R, 7), np.int8)
+    hdr = np.zeros((B, 8), np.int32)
+    st = np.zeros((max_ex, R, 7), np.int8)
+    pi = np.zeros((max_ex, 409), np.float32)
+    va = np.zeros((max_ex, 7), np.uint64)
+    win = np.zeros((max_ex, n), np.float32)
+    sd = np.zeros((max_ex, n), np.int32)
+    q = np.zeros((max_ex, n), np.float32)
+    meta = np.zeros((max_ex, 4), np.int32)
+    k = lib().or_selfplay_run(n, B, iters, seed, board_base, num_sims, ratio_full, prob_full, cpuct, fpu,
+                              int(forced), temp_threshold, _p(board, C.c_int8), _p(hdr, C.c_int32), max_ex,
+                              _p(st, C.c_int8), _p(pi, C.c_float), _p(va, C.c_uint64), _p(win, C.c_float),
+                              _p(sd, C.c_int32), _p(q, C.c_float), _p(meta, C.c_int32))
+    k = min(k, max_ex)
+    return {"board": board, "hdr": hdr, "ex_board": st[:k], "pi": pi[:k], "valids": va[:k],
+            "winner": win[:k], "scdiff": sd[:k], "surprise": q[:k], "meta": meta[:k]}

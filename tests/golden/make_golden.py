@@ -447,6 +447,54 @@ def fake_nn_vectors(numba_logic, n_players, states):
             "v": np.array(vs)}
 
 
+def deterministic_weights(state_dict):
+    """Assign every tensor of a SplendorNNet state_dict a closed-form value pattern (by
+    sorted key order) so an independent re-implementation can load identical weights."""
+    import torch
+    out = {}
+    for k, name in enumerate(sorted(state_dict)):
+        t = state_dict[name]
+        if not t.is_floating_point():
+            out[name] = t.clone()
+            continue
+        i = torch.arange(t.numel(), dtype=torch.float64)
+        u = torch.remainder(i * 0.6180339887498949 + 0.1234 * (k + 1), 1.0)
+        if name.endswith("running_var"):
+            v = 0.5 + u
+        elif name.endswith("lowvalue"):
+            v = torch.full_like(u, -1e8)
+        else:
+            v = (u - 0.5) * (0.3 if name.endswith("weight") else 0.1)
+        out[name] = v.to(t.dtype).view_as(t)
+    return out
+
+
+def nnet_fixture(n_players, boards):
+    import torch
+    _exec_module("splendor.SplendorNNet", f"{REF}/SplendorNNet.py")
+    mod = sys.modules["splendor.SplendorNNet"]
+
+    class _G:
+        num_players = n_players
+        def getBoardSize(self):
+            return (32 + 10 * n_players + n_players * n_players, 7)
+        def getActionSize(self):
+            return 409
+        def getMaxScoreDiff(self):
+            return 15
+    net = mod.SplendorNNet(_G(), {"nn_version": 1, "dropout": 0.3}, use_token_exchange=True)
+    sd = deterministic_weights(net.state_dict())
+    net.load_state_dict(sd)
+    net.eval()
+    b = torch.from_numpy(boards.astype(np.float32))
+    valid = torch.from_numpy(np.stack([(np.arange(409) % (3 + i)) != 0 for i in range(len(boards))]))
+    with torch.no_grad():
+        lp, v, sdf = net(b, valid)
+    return {"boards": boards, "valid": valid.numpy(), "log_pi": lp.numpy(), "v": v.numpy(),
+            "sdiff": sdf.numpy(), "keys": np.array(sorted(sd)),
+            "n_params": np.array(sum(p.numel() for p in net.parameters()))}
+
+
 def main():
     logic, numba_logic, game_mod, mcts_mod = load_reference()
     _patch_np_random()
@@ -466,6 +514,10 @@ def main():
               f"{len(env['uniforms'])} uniforms, masks mean {env['mask_canon'].sum(1).mean():.1f}")
         fnn = fake_nn_vectors(numba_logic, n, env["canon"][::7][:40])
         np.savez_compressed(os.path.join(OUT, f"fakenn_{n}p.npz"), **fnn)
+        if n in (2, 4):
+            nf = nnet_fixture(n, env["canon"][::37][:12])
+            np.savez_compressed(os.path.join(OUT, f"nnet_{n}p.npz"), **nf)
+            print(f"nnet {n}p: params {int(nf['n_params'])}")
     cases = [(25, 1.0, 0.0, False), (100, 2.5, 0.3, False), (100, 2.5, 0.3, True),
              (25, 1.5, -0.2, False)]
     for n in (2, 4):

@@ -70,12 +70,13 @@ def test_mcts_config_struct_layout(tmp_path):
     from splendor import _lib
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "splendor_amd.h"\n'
-                   'int main(void){printf("%zu %zu %zu %zu\\n", sizeof(spl_mcts_config),'
+                   'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(spl_mcts_config),'
                    'offsetof(spl_mcts_config, seed), offsetof(spl_mcts_config, node_cap),'
-                   'offsetof(spl_mcts_config, dirichlet_temp));return 0;}\n')
+                   'offsetof(spl_mcts_config, dirichlet_temp), offsetof(spl_mcts_config, out_cap));return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
-    size, off_seed, off_cap, off_temp = map(int, subprocess.check_output([str(exe)]).split())
+    size, off_seed, off_cap, off_temp, off_out = map(int, subprocess.check_output([str(exe)]).split())
     M = _lib.MctsConfig
     assert ctypes.sizeof(M) == size
     assert M.seed.offset == off_seed and M.node_cap.offset == off_cap and M.dirichlet_temp.offset == off_temp
+    assert M.out_cap.offset == off_out

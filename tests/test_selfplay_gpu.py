@@ -1,0 +1,87 @@
+"""GPU parity of the batched self-play driver (Coach.executeEpisode on device) against the
+oracle's sequential self-play loop: same Philox decisions, hash network, Dirichlet off.
+Bit-exact boards, per-game counters and every finished training example."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import _oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def make(n, B, sims, ratio, prob_full, forced, tthr=10, seed=9, **kw):
+    from splendor.env import SplendorEngine
+    from splendor.selfplay import SelfPlay
+    args = dict(numMCTSSims=sims, cpuct=1.5, fpu=0.1, prob_fullMCTS=prob_full, ratio_fullMCTS=ratio,
+                forced_playouts=forced, dirichletAlpha=0.3, temperature=[1.25, 0.8], tempThreshold=tthr)
+    e = SplendorEngine(n)
+    sp = SelfPlay(e, B, args, dirichlet_noise=kw.pop("noise", False), seed=seed, **kw)
+    sp.reset()
+    return e, sp
+
+
+def sort_examples(ex, meta):
+    order = np.lexsort((meta[:, 2], meta[:, 1], meta[:, 0]))
+    return {k: v[order] for k, v in ex.items()}
+
+
+@pytest.mark.parametrize("n,forced,graph", [(2, False, False), (2, True, True), (4, False, False)])
+def test_selfplay_matches_oracle(n, forced, graph):
+    B, iters, sims, ratio, pf, seed = 96, 1200, 8, 4, 0.25, 9
+    e, sp = make(n, B, sims, ratio, pf, forced, seed=seed, out_cap=20000)
+    for _ in range(iters):
+        sp.step(use_graph=graph)
+    torch.cuda.synchronize()
+    hdr = sp.headers()
+    assert hdr["overflow"].max() == 0
+    ref = O.selfplay_run(n, B, iters, seed, sims, ratio, pf, 1.5, 0.1, forced, 10)
+    rh = ref["hdr"]
+    np.testing.assert_array_equal(hdr["player"], rh[:, 0])
+    np.testing.assert_array_equal(hdr["episode_step"], rh[:, 1])
+    np.testing.assert_array_equal(hdr["move_no"], rh[:, 2])
+    np.testing.assert_array_equal(hdr["game_no"], rh[:, 3])
+    np.testing.assert_array_equal(hdr["games_done"], rh[:, 4])
+    np.testing.assert_array_equal(hdr["sims_done"], rh[:, 6])
+    from splendor import _lib  # noqa: F401
+    boards = torch.empty_like(sp.leaf_state)
+    # real boards live in the pools; compare through the canonical roots + players instead
+    ex = {k: v.cpu().numpy() for k, v in sp.drain().items()}
+    assert len(ex["pi"]) == len(ref["pi"]) > 0
+    # device queue order is nondeterministic: match by content key (board bytes + pi)
+    key_d = [ex["board"][i].tobytes() + ex["pi"][i].tobytes() for i in range(len(ex["pi"]))]
+    key_r = [ref["ex_board"][i].tobytes() + ref["pi"][i].tobytes() for i in range(len(ref["pi"]))]
+    od, orr = np.argsort(key_d, kind="stable"), np.argsort(key_r, kind="stable")
+    np.testing.assert_array_equal(ex["board"][od], ref["ex_board"][orr])
+    np.testing.assert_array_equal(ex["pi"][od], ref["pi"][orr])
+    np.testing.assert_array_equal(ex["valids"][od].view(np.uint64), ref["valids"][orr])
+    np.testing.assert_array_equal(ex["winner"][od], ref["winner"][orr])
+    np.testing.assert_array_equal(ex["scdiff"][od], ref["scdiff"][orr])
+    np.testing.assert_array_equal(ex["surprise"][od], ref["surprise"][orr])
+    del boards
+
+
+def test_selfplay_with_noise_and_network_sane():
+    from splendor.env import unpack_mask
+    from splendor.nnet import LeafEvaluator, random_net
+    from splendor.env import SplendorEngine
+    from splendor.selfplay import SelfPlay
+    e = SplendorEngine(2)
+    B = 512
+    args = dict(numMCTSSims=25, cpuct=2.5, fpu=0.3, prob_fullMCTS=0.25, ratio_fullMCTS=5,
+                forced_playouts=False, dirichletAlpha=0.3, temperature=[1.25, 0.8], tempThreshold=10)
+    ev = LeafEvaluator(e, random_net(2, seed=0), B)
+    sp = SelfPlay(e, B, args, evaluator=ev, dirichlet_noise=True, seed=3)
+    sp.reset()
+    for _ in range(400):
+        sp.step(use_graph=True)
+    st = sp.stats()
+    assert st["overflow"] == 0 and st["moves"] > B
+    ex = sp.drain()
+    if len(ex["pi"]):
+        pi = ex["pi"].double()
+        assert torch.allclose(pi.sum(1), torch.ones_like(pi.sum(1)), atol=1e-5)
+        valid = unpack_mask(ex["valids"])
+        assert bool((pi[~valid] == 0).all())
+        assert set(np.unique(ex["winner"].cpu().numpy()).tolist()) <= {-1.0, 1.0, np.float32(0.01)}
