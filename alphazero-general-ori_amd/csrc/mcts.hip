@@ -358,9 +358,18 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     int best = 0;
     for (int i = l; i < ec; i += 64) best = max(best, en[i]);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
+    // policy counts: pruned (MCTS.py:69-74); where the reference would divide 0/0
+    // (Coach.py:83 raises) fall back to raw counts, then to uniform
+    int mode = forced ? 0 : 1;
     long long tot = 0;
-    for (int i = l; i < ec; i += 64) tot += pruned_count(en[i], best, forced, ep[i], sims);
-    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    for (; mode < 3; mode++) {
+        tot = 0;
+        for (int i = l; i < ec; i += 64)
+            tot += mode == 0 ? pruned_count(en[i], best, true, ep[i], sims) : (mode == 1 ? en[i] : 1);
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        if (tot > 0) break;
+    }
+#define POLICY_COUNT(i) (mode == 0 ? pruned_count(en[i], best, true, ep[i], sims) : (mode == 1 ? (long long)en[i] : 1ll))
     const int step = H->episode_step + 1;
     const int player = H->player;
     int8_t *s = lds[w][0], *b = lds[w][1];
@@ -376,7 +385,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         for (int i = l; i < ec; i += 64)   // getSymmetries stores pi as float32 (SplendorGame.py:59-61)
-            pi[ea[i]] = (float)((double)pruned_count(en[i], best, forced, ep[i], sims) / (double)tot);
+            pi[ea[i]] = (float)((double)POLICY_COUNT(i) / (double)tot);
         uint64_t m[7];
         wave_valid_moves<N>(s, 0, lim, m);
         uint64_t mv = m[0];
@@ -397,19 +406,20 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         const double T = C.temp_threshold > 0 ? (step < C.temp_threshold ? 2.0 : 0.2) : 1.0;
         double sum = 0.0;
         for (int i = 0; i < ec; i++)
-            sum += temp_pow((double)pruned_count(en[i], best, forced, ep[i], sims) / (double)tot, T);
+            sum += temp_pow((double)POLICY_COUNT(i) / (double)tot, T);
         double last = 0.0;
         for (int i = 0; i < ec; i++)
-            last += temp_pow((double)pruned_count(en[i], best, forced, ep[i], sims) / (double)tot, T) / sum;
+            last += temp_pow((double)POLICY_COUNT(i) / (double)tot, T) / sum;
         const double u = philox_u01(C.seed, gb, ST_PICK | (uint32_t)cm, 0);
         double cdf = 0.0;
         action = ea[ec - 1];
         for (int i = 0; i < ec; i++) {
-            cdf += temp_pow((double)pruned_count(en[i], best, forced, ep[i], sims) / (double)tot, T) / sum;
+            cdf += temp_pow((double)POLICY_COUNT(i) / (double)tot, T) / sum;
             if (cdf / last > u) { action = ea[i]; break; }
         }
     }
     action = __shfl(action, 0, 64);
+#undef POLICY_COUNT
     // getNextState with chance (Coach.py:86), getGameEnded (:88)
     wave_copy_board<N>(b, P.board + (size_t)t * Lx::S);
     Chance ch{nullptr, C.seed, gb, ST_MOVE | (uint32_t)cm, 0};
@@ -467,14 +477,16 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
 }
 
 __global__ void k_drain_copy(Pools P, int S, int max, int8_t *st, float *pi, uint64_t *valid,
-                             float *winner, int32_t *scdiff, float *q, int n) {
+                             float *winner, int32_t *scdiff, float *q, int32_t *meta, int n) {
     const int k = min(P.counters[0], min(max, P.out_cap));
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)k * SPL_ACTIONS;
+    const size_t W = S > SPL_ACTIONS ? (size_t)S : (size_t)SPL_ACTIONS;   // per-example span
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)k * W;
          i += (size_t)gridDim.x * blockDim.x) {
-        const size_t e = i / SPL_ACTIONS, j = i % SPL_ACTIONS;
-        if (pi) pi[i] = P.out_pi[i];
+        const size_t e = i / W, j = i % W;
+        if (pi && j < SPL_ACTIONS) pi[e * SPL_ACTIONS + j] = P.out_pi[e * SPL_ACTIONS + j];
         if (st && j < (size_t)S) st[e * S + j] = P.out_state[e * S + j];
         if (j < 7 && valid) valid[e * 7 + j] = P.out_valid[e * 7 + j];
+        if (j < 4 && meta) meta[e * 4 + j] = P.out_meta[e * 4 + j];
         if (j < (size_t)n) {
             if (winner) winner[e * n + j] = P.out_winner[e * 4 + j];
             if (scdiff) scdiff[e * n + j] = P.out_scdiff[e * 4 + j];
@@ -926,13 +938,15 @@ int spl_mcts_commit(spl_mcts *m, void *hs) {
 }
 
 int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *valid, float *winner,
-                            int32_t *scdiff, float *q, int max, int32_t *n_out, void *hs) {
+                            int32_t *scdiff, float *q, int32_t *meta, int max, int32_t *n_out,
+                            void *hs) {
     if (!m || !m->cfg.selfplay || max < 0) return SPL_EINVAL;
-    const size_t work = (size_t)(max < m->P.out_cap ? max : m->P.out_cap) * SPL_ACTIONS;
+    const size_t work = (size_t)(max < m->P.out_cap ? max : m->P.out_cap) *
+                        (size_t)(m->S > SPL_ACTIONS ? m->S : SPL_ACTIONS);
     if (work) {
         const unsigned grid = (unsigned)((work + 255) / 256 > 4096 ? 4096 : (work + 255) / 256);
         hipLaunchKernelGGL(k_drain_copy, dim3(grid), dim3(256), 0, (hipStream_t)hs, m->P, m->S, max,
-                           state, pi, valid, winner, scdiff, q, m->n);
+                           state, pi, valid, winner, scdiff, q, meta, m->n);
     }
     hipLaunchKernelGGL(k_drain_reset, dim3(1), dim3(1), 0, (hipStream_t)hs, m->P, max, n_out);
     return check_launch();

@@ -60,11 +60,13 @@ class SelfPlay(BatchedMCTS):
             "winner": torch.empty((E, n), dtype=torch.float32, device=dev),
             "scdiff": torch.empty((E, n), dtype=torch.int32, device=dev),
             "surprise": torch.empty((E, n), dtype=torch.float32, device=dev),
+            "meta": torch.empty((E, 4), dtype=torch.int32, device=dev),
         }
         cnt = torch.zeros(1, dtype=torch.int32, device=dev)
         _lib.check(self.L.spl_mcts_drain_examples(
             self.h, _ptr(out["board"]), _ptr(out["pi"]), _ptr(out["valids"]), _ptr(out["winner"]),
-            _ptr(out["scdiff"]), _ptr(out["surprise"]), E, _ptr(cnt), self.e._s()), "drain")
+            _ptr(out["scdiff"]), _ptr(out["surprise"]), _ptr(out["meta"]), E, _ptr(cnt), self.e._s()),
+            "drain")
         k = int(cnt.item())
         return {key: v[:k] for key, v in out.items()}
 

@@ -161,10 +161,12 @@ int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs
 int spl_mcts_reset_games(spl_mcts *m, void *hip_stream);
 int spl_mcts_commit(spl_mcts *m, void *hip_stream);
 /* copy up to `max` finished examples to caller buffers (state E x S i8, pi E x 409 f32,
- * valid E x 7 u64, winner E x n f32, scdiff E x n i32, q E x n f32), write the count to
- * *n_out (device int32) and empty the queue (examples beyond `max` are dropped). */
+ * valid E x 7 u64, winner E x n f32, scdiff E x n i32, q E x n f32, meta E x 4 i32 =
+ * (global board id, game number, example index in game, player)), write the count to
+ * *n_out (device int32) and empty the queue (examples beyond `max` are dropped). Any
+ * output pointer may be NULL. */
 int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *valid,
-                            float *winner, int32_t *scdiff, float *q, int max,
+                            float *winner, int32_t *scdiff, float *q, int32_t *meta, int max,
                             int32_t *n_out, void *hip_stream);
 /* copies the B per-tree headers (112 bytes each, layout in splendor/mcts.py) to `out` */
 int spl_mcts_headers(spl_mcts *m, int32_t *out, void *hip_stream);

@@ -728,7 +728,15 @@ int or_selfplay_run(int n, int B, int iters, uint64_t seed, uint32_t board_base,
             node_t *nd = *lookup(m, canon);
             long long best = 0, tot = 0, c[409];
             for (int a = 0; a < 409; a++) if (nd->vs[a] && nd->nsa[a] > best) best = nd->nsa[a];
-            for (int a = 0; a < 409; a++) { c[a] = nd->vs[a] ? pruned(nd->nsa[a], best, forced, nd->ps[a], budget) : 0; tot += c[a]; }
+            for (int mode = forced ? 0 : 1; mode < 3; mode++) {   /* 0/0 fallback */
+                tot = 0;
+                for (int a = 0; a < 409; a++) {
+                    c[a] = !nd->vs[a] ? 0 : mode == 0 ? pruned(nd->nsa[a], best, 1, nd->ps[a], budget)
+                                                      : mode == 1 ? nd->nsa[a] : 1;
+                    tot += c[a];
+                }
+                if (tot > 0) break;
+            }
             step++;
             if (full && nex < 62 * n + 2) {
                 or_ex_t *x = &stage[nex++];
