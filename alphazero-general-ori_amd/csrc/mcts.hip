@@ -610,11 +610,35 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
 }
 
 // ------------------------------------------------------------ expand + backup
+// numpy pairwise float32 sum of the 409 staged priors (np_sum409 order), 32 lanes:
+// lane = 8*block + j accumulates r_j of block `block`; blocks [0,96) [96,200) [200,304)
+// [304,409); combine ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) (+ tail), then (b0+b1)+(b2+b3).
+__device__ __forceinline__ float wave_np_sum409(const float *a) {
+    const int l = lane_id();
+    const int blk = (l >> 3) & 3, j = l & 7;
+    const int off = blk == 0 ? 0 : (blk == 1 ? 96 : (blk == 2 ? 200 : 304));
+    const int len = blk == 0 ? 96 : (blk == 3 ? 105 : 104);
+    float r = a[off + j];
+    for (int i = 8; i < len - (len % 8); i += 8) r += a[off + i + j];
+    float r1 = __shfl_xor(r, 1, 64);
+    float p01 = (j & 1) ? r1 + r : r + r1;            // pair sums (r0+r1) etc. on even lanes
+    float p23 = __shfl_xor(p01, 2, 64);
+    float q = (j & 2) ? p23 + p01 : p01 + p23;        // ((r0+r1)+(r2+r3)) on lane 0 of quad
+    float q2 = __shfl_xor(q, 4, 64);
+    float res = (j & 4) ? q2 + q : q + q2;            // lane j==0 holds the block result
+    float blockv = __shfl(res, 8 * blk, 64);
+    if (blk == 3) blockv = blockv + a[off + 104];     // 105 = 13*8 + 1 trailing element
+    const float b0 = __shfl(blockv, 0, 64), b1 = __shfl(blockv, 8, 64);
+    const float b2 = __shfl(blockv, 16, 64), b3 = __shfl(blockv, 24, 64);
+    return (b0 + b1) + (b2 + b3);
+}
+
 template <int N>
 __global__ __launch_bounds__(THREADS) void k_backup(Pools P, SearchCfg C, int B,
                                                     const uint64_t *__restrict__ leaf_mask,
                                                     const float *__restrict__ pi,
                                                     const float *__restrict__ v) {
+    __shared__ __align__(16) float lpi[WAVES][416];
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
@@ -624,7 +648,7 @@ __global__ __launch_bounds__(THREADS) void k_backup(Pools P, SearchCfg C, int B,
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const int depth = H->depth;
     const int32_t *path = P.path + (size_t)t * P.pcap * 2;
-    float val[4];
+    float val[4] = {0, 0, 0, 0};
     if (kind == LEAF_NN) {
         const uint64_t *m = leaf_mask + (size_t)t * 7;
         int ec = 0;
@@ -635,9 +659,11 @@ __global__ __launch_bounds__(THREADS) void k_backup(Pools P, SearchCfg C, int B,
             if (l == 0) { H->overflow = 1; H->leaf_kind = LEAF_NONE; }
             return;
         }
-        const float *pr = pi + (size_t)t * SPL_ACTIONS;
-        float sum = l == 0 ? np_sum409(pr) : 0.f;           // normalise (MCTS.py:144)
-        sum = __shfl(sum, 0, 64);
+        float *pr = lpi[w];
+        const float *g = pi + (size_t)t * SPL_ACTIONS;
+        for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = g[a];      // coalesced stage
+        __builtin_amdgcn_wave_barrier();
+        const float sum = wave_np_sum409(pr);                        // normalise (MCTS.py:144)
         int run = 0;
 #pragma unroll
         for (int k = 0; k < 7; k++) {
@@ -655,6 +681,7 @@ __global__ __launch_bounds__(THREADS) void k_backup(Pools P, SearchCfg C, int B,
         }
 #pragma unroll
         for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
+        __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         if (l == 0) {
             P.nkey0[nb + id] = H->leaf_k0; P.nkey1[nb + id] = H->leaf_k1;
@@ -674,22 +701,21 @@ __global__ __launch_bounds__(THREADS) void k_backup(Pools P, SearchCfg C, int B,
 #pragma unroll
         for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
     }
+    // backup (MCTS.py:169-176): level d sees the leaf value rolled (depth - d) times; the
+    // levels touch distinct nodes/edges (rounds strictly increase along a path), so one
+    // lane per level applies exactly the sequential update.
+    for (int d = l; d < depth; d += 64) {
+        const int rot = (depth - d) % N;
+        const double v0 = (double)val[(N - rot) % N];
+        const int node = path[2 * d], ge = path[2 * d + 1];
+        const int cnt = P.en[e0 + ge];
+        P.eq[e0 + ge] = ((double)cnt * P.eq[e0 + ge] + v0) / (double)(cnt + 1);
+        const int ns = P.nns[nb + node];
+        P.nqs[nb + node] = ((double)(ns + 1) * P.nqs[nb + node] + v0) / (double)(ns + 2);
+        P.en[e0 + ge] = cnt + 1;
+        P.nns[nb + node] = ns + 1;
+    }
     if (l == 0) {
-        for (int d = depth - 1; d >= 0; d--) {               // MCTS.py:169-176
-            float r[N];
-#pragma unroll
-            for (int i = 0; i < N; i++) r[i] = val[(i + N - 1) % N];
-#pragma unroll
-            for (int i = 0; i < N; i++) val[i] = r[i];
-            const int node = path[2 * d], ge = path[2 * d + 1];
-            const int cnt = P.en[e0 + ge];
-            const double v0 = (double)val[0];
-            P.eq[e0 + ge] = ((double)cnt * P.eq[e0 + ge] + v0) / (double)(cnt + 1);
-            const int ns = P.nns[nb + node];
-            P.nqs[nb + node] = ((double)(ns + 1) * P.nqs[nb + node] + v0) / (double)(ns + 2);
-            P.en[e0 + ge] = cnt + 1;
-            P.nns[nb + node] = ns + 1;
-        }
         H->sims_done += 1;
         H->noise_pending = 0;
         H->leaf_kind = LEAF_NONE;
@@ -750,13 +776,18 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
 }
 
 // ------------------------------------------------------------ network I/O
-// leaf int8 [B,R,7] + packed mask -> float32 board and bool mask (predict, :160-161)
-__global__ __launch_bounds__(256) void k_nn_input(int B, int S, const int8_t *__restrict__ st,
+// leaf int8 [B,R,7] + packed mask -> float32 board and bool mask (predict, :160-161).
+// The board is written TRANSPOSED, [B,7,R] (the layout SplendorNNet.forward builds at
+// SplendorNNet.py:129), so the first layer is a plain row-major GEMM.
+__global__ __launch_bounds__(256) void k_nn_input(int B, int R, const int8_t *__restrict__ st,
                                                   const uint64_t *__restrict__ mask,
                                                   float *__restrict__ x, uint8_t *__restrict__ valid) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    const size_t nx = (size_t)B * S, nv = (size_t)B * SPL_ACTIONS;
-    if (i < nx) x[i] = (float)st[i];
+    const size_t S = (size_t)7 * R, nx = (size_t)B * S, nv = (size_t)B * SPL_ACTIONS;
+    if (i < nx) {                       // i indexes x[b][c][r]
+        const size_t b = i / S, rem = i % S, c = rem / R, r = rem % R;
+        x[i] = (float)st[b * S + r * 7 + c];
+    }
     if (valid && i < nv) {
         const size_t b = i / SPL_ACTIONS, a = i % SPL_ACTIONS;
         valid[i] = (uint8_t)((mask[b * 7 + a / 64] >> (a % 64)) & 1);
@@ -962,10 +993,10 @@ int spl_nn_input(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t 
                  uint8_t *valid, void *hs) {
     if (!ctx || B < 0 || (B && (!state || !x || (valid && !mask)))) return SPL_EINVAL;
     if (!B) return 0;
-    const int S = 7 * (32 + 10 * ctx->n + ctx->n * ctx->n);
+    const int R = 32 + 10 * ctx->n + ctx->n * ctx->n, S = 7 * R;
     const size_t tot = (size_t)B * (S > SPL_ACTIONS ? S : SPL_ACTIONS);
     hipLaunchKernelGGL(k_nn_input, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)hs, B, S, state, mask, x, valid);
+                       (hipStream_t)hs, B, R, state, mask, x, valid);
     return check_launch();
 }
 

@@ -136,8 +136,9 @@ class FoldedNet(nn.Module):
         head = x[..., :g].unflatten(-1, (groups, items))
         return torch.cat([head.amax(-1), head.mean(-1), dense], -1)
 
-    def forward(self, board, valid):
-        x = board.transpose(-1, -2)                                        # [B, 7, R]
+    def forward(self, board, valid, transposed=False):
+        """board [B,R,7] (or [B,7,R] when transposed=True, as spl_nn_input writes it)."""
+        x = board if transposed else board.transpose(-1, -2)              # [B, 7, R]
         x = F.relu(F.linear(x, self.w1, self.b1) * self.s1 + self.t1)
         x = F.relu(F.linear(x, self.w2, self.b2))
         d = F.relu(F.linear(x[..., 32:], self.wp1, self.bp1) * self.sp1 + self.tp1)
@@ -173,7 +174,7 @@ class LeafEvaluator:
         self.B = B
         self.net = FoldedNet(net).to(engine.device).eval()
         dev = engine.device
-        self.x = torch.zeros((B, engine.rows, 7), dtype=torch.float32, device=dev)
+        self.x = torch.zeros((B, 7, engine.rows), dtype=torch.float32, device=dev)   # transposed
         self.valid = torch.zeros((B, ACTIONS), dtype=torch.bool, device=dev)
         self.use_graph = use_graph
         self.graph = None
@@ -188,7 +189,7 @@ class LeafEvaluator:
     @torch.no_grad()
     def _run(self, leaf_state, leaf_mask):
         self._convert(leaf_state, leaf_mask)
-        return self.net(self.x, self.valid)
+        return self.net(self.x, self.valid, transposed=True)
 
     @torch.no_grad()
     def __call__(self, leaf_state, leaf_mask, leaf_valid=None):

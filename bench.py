@@ -57,6 +57,62 @@ def cpu_baseline(n, seed, target_s=10.0):
                       f"{dt:.1f} s, oracle/splendor_oracle.c or_random_rollouts"}
 
 
+# saved args of the reference's only checkpoint, genbu.pt, = BASELINE config 3
+GENBU_ARGS = dict(numMCTSSims=100, cpuct=2.5, fpu=0.3, prob_fullMCTS=0.25, ratio_fullMCTS=5,
+                  forced_playouts=False, dirichletAlpha=0.3, temperature=[1.25, 0.8], tempThreshold=10)
+
+
+def nn_flops_per_eval(n):
+    """SplendorNNet inference FLOPs per leaf (2 x MACs; score-diff head skipped)."""
+    R = 32 + 10 * n + n * n
+    macs = 7 * (R * 128 + 128 * 128) + 7 * 96 * 120 + 7 * 128 * 128 + 704 * 128 + 112 * 120 \
+        + 2 * 128 * 128 + 112 * 120 + 128 * 128 + 128 * 409 + 128 * 128 + 128 * n
+    return 2 * macs
+
+
+def run_selfplay(args, rank, world, dev, dist):
+    """BASELINE config 3 (config 4 per GPU at N>1): B concurrent self-play games, one MCTS
+    simulation per game per iteration, leaves evaluated by SplendorNNet (fp32, random
+    init: the reference's genbu.pt cannot be loaded safely), moves committed on device."""
+    from splendor.env import SplendorEngine
+    from splendor.nnet import LeafEvaluator, random_net
+    from splendor.selfplay import SelfPlay, gather_examples
+    B = args.boards
+    eng = SplendorEngine(args.players, device=dev)
+    sargs = dict(GENBU_ARGS, numMCTSSims=args.sims)
+    ev = LeafEvaluator(eng, random_net(args.players, seed=0, device=dev), B, use_graph=False)
+    sp = SelfPlay(eng, B, sargs, evaluator=ev, dirichlet_noise=True, seed=args.seed, board_base=rank * B)
+    sp.reset()
+    for _ in range(args.warmup):
+        sp.step(use_graph=True)
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        sp.step(use_graph=True)
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    st = sp.stats()
+    # episode-end exchange of finished examples (RCCL all-gather), timed separately
+    tg = time.perf_counter()
+    ex = gather_examples(sp.drain()) if dist else sp.drain()
+    torch.cuda.synchronize(dev)
+    gather_s = time.perf_counter() - tg
+    if dist:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return {"elapsed": elapsed, "iter_ms": ev0.elapsed_time(ev1) / args.steps, "stats": st,
+            "examples": int(next(iter(ex.values())).shape[0]), "gather_s": gather_s,
+            "device_bytes": sp.device_bytes}
+
+
 def load_traffic(path, B):
     """Measured HBM bytes per launch from the newest committed rocprofv3 --pmc summary
     (profiles/rNN_rollout_pmc.json, corrected as DESIGN.md §6 describes), if any."""
@@ -83,6 +139,11 @@ def main():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None)
+    ap.add_argument("--workload", choices=("env", "selfplay"), default="env")
+    ap.add_argument("--sims", type=int, default=100, help="selfplay: numMCTSSims")
+    ap.add_argument("--no-selfplay", action="store_true",
+                    help="env workload: skip the secondary config-3 self-play measurement")
+    ap.add_argument("--selfplay-steps", type=int, default=100)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -95,6 +156,31 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+
+    if args.workload == "selfplay":
+        r = run_selfplay(args, rank, world, dev, dist)
+        if rank == 0:
+            B, K = args.boards, args.steps
+            flops = nn_flops_per_eval(args.players) * B / (r["iter_ms"] * 1e-3) / 1e12
+            print(json.dumps({
+                "metric": METRIC, "value": world * B * K / r["elapsed"], "unit": "rollouts/s",
+                "n_gpus": world, "steps": K, "warmup": args.warmup,
+                "ms_per_step": r["elapsed"] / K * 1e3, "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "fp32 (network) / int8 (boards) / f64 (tree stats)",
+                "data": "synthetic (Philox-seeded deals), random-init SplendorNNet",
+                "config": {"workload": f"config3: batched self-play, numMCTSSims={args.sims}, genbu args, "
+                                       "SplendorNNet leaf eval, device move commit",
+                           "players": args.players, "games_per_gpu": B, "global_games": world * B,
+                           "parallelism": f"dp{world} (game shards; RCCL all-gather of examples)"},
+                "roofline": {"bound": "mfma", "achieved": flops, "peak": 157.3, "unit": "TFLOP/s",
+                             "frac": flops / 157.3, "traffic": None,
+                             "note": "network FLOPs per iteration / iteration time (fp32 MFMA peak)"},
+                "selfplay": {**r["stats"], "examples": r["examples"], "allgather_s": r["gather_s"],
+                             "tree_device_bytes": r["device_bytes"], "iter_ms": r["iter_ms"]},
+                "cpu_baseline": None}))
+        if dist:
+            dist.destroy_process_group()
+        return
 
     cpu = None
     if rank == 0 and world == 1 and args.gpus == 1 and not args.no_cpu_baseline:
@@ -131,6 +217,22 @@ def main():
     kernel_ms = ev0.elapsed_time(ev1) / K
     games = int(rb.games.sum().item())
 
+    secondary = None
+    if not args.no_selfplay:
+        del rb
+        torch.cuda.empty_cache()
+        sp_args = argparse.Namespace(**vars(args))
+        sp_args.steps, sp_args.warmup = args.selfplay_steps, 20
+        r = run_selfplay(sp_args, rank, world, dev, dist)
+        flops = nn_flops_per_eval(args.players) * B / (r["iter_ms"] * 1e-3) / 1e12
+        secondary = {"workload": f"config3: batched self-play, numMCTSSims={args.sims}, genbu args, "
+                                 "SplendorNNet fp32 leaf eval (random init), device move commit",
+                     "value": world * B * sp_args.steps / r["elapsed"], "unit": "rollouts/s (MCTS simulations)",
+                     "ms_per_iteration": r["elapsed"] / sp_args.steps * 1e3, "steps": sp_args.steps,
+                     "network_tflops": flops, "network_frac_fp32_peak": flops / 157.3,
+                     **r["stats"], "examples_drained": r["examples"], "allgather_s": r["gather_s"],
+                     "tree_device_bytes": r["device_bytes"]}
+
     if rank == 0:
         per = bytes_per_board_step(args.players)
         achieved = per * B / (kernel_ms * 1e-3) / 1e9
@@ -158,6 +260,7 @@ def main():
                          "bytes_per_board_step": per},
             "cpu_baseline": cpu,
             "games_completed": games,
+            "config3_selfplay": secondary,
         }
         print(json.dumps(out))
     if dist:

@@ -171,8 +171,9 @@ int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *val
 /* copies the B per-tree headers (112 bytes each, layout in splendor/mcts.py) to `out` */
 int spl_mcts_headers(spl_mcts *m, int32_t *out, void *hip_stream);
 
-/* predict input conversion (GenericNNetWrapper.py:160-161): int8 boards -> f32, packed
- * mask -> bool bytes (valid may be NULL) */
+/* predict input conversion (GenericNNetWrapper.py:160-161): int8 boards [B][R][7] -> f32
+ * written transposed as x[B][7][R] (SplendorNNet.py:129 layout), packed mask -> bool bytes
+ * (valid may be NULL) */
 int spl_nn_input(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask,
                  float *x, uint8_t *valid, void *hip_stream);
 /* deterministic hash-prior network (see oracle or_fake_predict): parity tests and
