@@ -727,7 +727,7 @@ __global__ __launch_bounds__(THREADS) void k_backup(Pools P, SearchCfg C, int B,
 // pruning when forced playouts were on), probs, q.
 __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, int B, int n,
                                                         int64_t *counts, double *qsa, double *probs,
-                                                        double *q) {
+                                                        double *q, int64_t *adjusted) {
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
@@ -736,36 +736,32 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
     const int root = H->root;
     for (int a = l; a < SPL_ACTIONS; a += 64) {
         if (counts) counts[(size_t)t * SPL_ACTIONS + a] = 0;
+        if (adjusted) adjusted[(size_t)t * SPL_ACTIONS + a] = 0;
         if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = Q_UNSET;
         if (probs) probs[(size_t)t * SPL_ACTIONS + a] = 0.0;
     }
     if (root < 0) return;
     __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
     const int eb = P.neb[nb + root], ec = P.nec[nb + root];
     int best = 0;
     for (int i = l; i < ec; i += 64) best = max(best, P.en[e0 + eb + i]);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
     const int sims = H->budget;
+    const bool forced = H->forced;
     long long tot = 0;
     for (int i = l; i < ec; i += 64) {
         const int a = P.ea[e0 + eb + i];
-        long long c = P.en[e0 + eb + i];
-        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = c;
+        const long long c = pruned_count(P.en[e0 + eb + i], best, forced, P.ep[e0 + eb + i], sims);
+        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = P.en[e0 + eb + i];
+        if (adjusted) adjusted[(size_t)t * SPL_ACTIONS + a] = c;
         if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = P.eq[e0 + eb + i];
-        if (H->forced) {
-            if (c != best) c -= (long long)sqrt(0.5 * (double)P.ep[e0 + eb + i] * (double)sims);
-            if (c <= 1) c = 0;
-        }
         tot += c;
     }
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
     for (int i = l; i < ec; i += 64) {
         const int a = P.ea[e0 + eb + i];
-        long long c = P.en[e0 + eb + i];
-        if (H->forced) {
-            if (c != best) c -= (long long)sqrt(0.5 * (double)P.ep[e0 + eb + i] * (double)sims);
-            if (c <= 1) c = 0;
-        }
+        const long long c = pruned_count(P.en[e0 + eb + i], best, forced, P.ep[e0 + eb + i], sims);
         if (probs) probs[(size_t)t * SPL_ACTIONS + a] = (double)c / (double)tot;
     }
     if (q && l == 0) {
@@ -775,7 +771,6 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
     }
 }
 
-// ------------------------------------------------------------ network I/O
 // leaf int8 [B,R,7] + packed mask -> float32 board and bool mask (predict, :160-161).
 // The board is written TRANSPOSED, [B,7,R] (the layout SplendorNNet.forward builds at
 // SplendorNNet.py:129), so the first layer is a plain row-major GEMM.
@@ -947,10 +942,10 @@ int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, con
 }
 
 int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs, double *q,
-                        void *hs) {
+                        int64_t *adjusted, void *hs) {
     if (!m) return SPL_EINVAL;
     hipLaunchKernelGGL(k_root_stats, wave_grid(m->B), dim3(THREADS), 0, (hipStream_t)hs, m->P,
-                       m->cfg, m->B, m->n, counts, qsa, probs, q);
+                       m->cfg, m->B, m->n, counts, qsa, probs, q, adjusted);
     return check_launch();
 }
 

@@ -208,6 +208,84 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int8_t *__restrict__
     if (l == 0) player[b] = (int8_t)nxt;
 }
 
+// Board.get_symmetries (SplendorLogicNumba.py:349-395) for E examples, one wave per
+// example. Variant k of K = 10 + 2n: 0 = identity; 1..9 = tier t = (k-1)/3 visible cards
+// permuted by cards_symmetries[(k-1)%3] (SplendorLogic.py:283) with buy/reserve actions
+// permuted alike; 10 + 2p + q = player p's reserved cards permuted by
+// reserve_symmetries[#reserved][q] (:284-295; present only when defined), buy-reserve
+// actions permuted for p == 0. present[e][k] marks emitted variants (reference order).
+__constant__ int8_t K_CARD_SYM[3][4] = {{1, 3, 0, 2}, {2, 0, 3, 1}, {3, 2, 1, 0}};
+__constant__ int8_t K_RSV_SYM[4][2][3] = {{{-1, -1, -1}, {-1, -1, -1}}, {{-1, -1, -1}, {-1, -1, -1}},
+                                          {{1, 0, 2}, {-1, -1, -1}}, {{1, 2, 0}, {2, 0, 1}}};
+
+template <int N>
+__global__ __launch_bounds__(THREADS) void k_symmetries(int E, const int8_t *__restrict__ state,
+                                                        const float *__restrict__ pi,
+                                                        const uint64_t *__restrict__ valid,
+                                                        int8_t *__restrict__ ostate, float *__restrict__ opi,
+                                                        uint64_t *__restrict__ ovalid,
+                                                        uint8_t *__restrict__ present) {
+    using Lx = Lay<N>;
+    constexpr int K = 10 + 2 * N;
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    const int w = threadIdx.x >> 6, e = blockIdx.x * WAVES + w;
+    if (e >= E) return;
+    const int l = lane_id();
+    int8_t *s = lds[w];
+    wave_copy_board<N>(s, state + (size_t)e * Lx::S);
+    int nres[N];
+#pragma unroll
+    for (int p = 0; p < N; p++) {        // _nb_of_reserved_cards (:770-774)
+        nres[p] = 3;
+        for (int c = 2; c >= 0; c--)
+            if (sum5(s + 7 * (Lx::RSV + 6 * p + 2 * c)) == 0) nres[p] = c;
+    }
+    for (int k = 0; k < K; k++) {
+        int tier = -1, p = -1;
+        const int8_t *perm = nullptr;
+        if (k >= 1 && k <= 9) { tier = (k - 1) / 3; perm = K_CARD_SYM[(k - 1) % 3]; }
+        if (k >= 10) {
+            p = (k - 10) / 2;
+            perm = K_RSV_SYM[nres[p]][(k - 10) % 2];
+            if (perm[0] < 0) { if (l == 0) present[(size_t)e * K + k] = 0; continue; }
+        }
+        if (l == 0) present[(size_t)e * K + k] = 1;
+        int8_t *os = ostate + ((size_t)e * K + k) * Lx::S;
+        // state bytes: rows of the permuted block come from the source row pair
+        for (int i = l; i < Lx::S; i += 64) {
+            int src = i;
+            const int r = i / 7, c = i - 7 * (i / 7);
+            if (tier >= 0 && r >= Lx::TIERS + 8 * tier && r < Lx::TIERS + 8 * tier + 8) {
+                const int rr = r - Lx::TIERS - 8 * tier;
+                src = 7 * (Lx::TIERS + 8 * tier + 2 * perm[rr >> 1] + (rr & 1)) + c;
+            }
+            if (p >= 0 && r >= Lx::RSV + 6 * p && r < Lx::RSV + 6 * p + 6) {
+                const int rr = r - Lx::RSV - 6 * p;
+                src = 7 * (Lx::RSV + 6 * p + 2 * perm[rr >> 1] + (rr & 1)) + c;
+            }
+            os[i] = s[src];
+        }
+        // policy and legality: action a takes the source action's entry
+        const float *ip = pi + (size_t)e * SPL_ACTIONS;
+        float *op = opi + ((size_t)e * K + k) * SPL_ACTIONS;
+        const uint64_t *iv = valid + (size_t)e * 7;
+#pragma unroll
+        for (int ch = 0; ch < 7; ch++) {
+            const int a = 64 * ch + l;
+            int src = a;
+            if (tier >= 0) {
+                if (a >= 4 * tier && a < 4 * tier + 4) src = 4 * tier + perm[a - 4 * tier];
+                if (a >= 12 + 4 * tier && a < 16 + 4 * tier) src = 12 + 4 * tier + perm[a - 12 - 4 * tier];
+            }
+            if (p == 0 && a >= 27 && a < 30) src = 27 + perm[a - 27];
+            if (a < SPL_ACTIONS) op[a] = ip[src];
+            const bool bit = a < SPL_ACTIONS && ((iv[src >> 6] >> (src & 63)) & 1);
+            const uint64_t word = __ballot(bit);
+            if (l == 0) ovalid[((size_t)e * K + k) * 7 + ch] = word;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- launch helpers
 inline int check_launch() { return hipGetLastError() == hipSuccess ? 0 : SPL_EDEVICE; }
 inline dim3 wave_grid(int B) { return dim3((unsigned)((B + WAVES - 1) / WAVES)); }
@@ -315,6 +393,25 @@ int spl_tree_step(const spl_ctx *c, int B, const int8_t *parent, const int16_t *
     if (!B) return 0;
     SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_tree_step<N>, wave_grid(B), dim3(THREADS), 0,
                                           (hipStream_t)hs, B, parent, action, child, err));
+    return check_launch();
+}
+
+int spl_ctx_set_token_limit(spl_ctx *c, int token_limit) {
+    if (!ok_ctx(c) || token_limit < 3 || token_limit > 100) return SPL_EINVAL;
+    c->token_limit = token_limit;
+    return 0;
+}
+
+int spl_symmetries(const spl_ctx *c, int E, const int8_t *state, const float *pi,
+                   const uint64_t *valid, int8_t *out_state, float *out_pi, uint64_t *out_valid,
+                   uint8_t *present, void *hs) {
+    if (!ok_ctx(c) || E < 0 || (E && (!state || !pi || !valid || !out_state || !out_pi || !out_valid ||
+                                      !present)))
+        return SPL_EINVAL;
+    if (!E) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_symmetries<N>, wave_grid(E), dim3(THREADS), 0,
+                                          (hipStream_t)hs, E, state, pi, valid, out_state, out_pi,
+                                          out_valid, present));
     return check_launch();
 }
 

@@ -29,6 +29,8 @@ _SIGS = {
     "spl_abi_version": ([], C.c_int),
     "spl_ctx_create": ([C.c_int, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
     "spl_ctx_destroy": ([C.c_void_p], C.c_int),
+    "spl_ctx_set_token_limit": ([C.c_void_p, C.c_int], C.c_int),
+    "spl_symmetries": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_state_rows": ([C.c_void_p], C.c_int),
     "spl_state_bytes": ([C.c_void_p], C.c_int),
     "spl_init": ([C.c_void_p, C.c_int, _vp, _vp, _vp, C.c_int, C.c_uint64, C.c_uint32, C.c_uint32,
@@ -49,7 +51,7 @@ _SIGS = {
     "spl_mcts_set_roots": ([C.c_void_p, _vp, C.c_int, C.c_int, _vp], C.c_int),
     "spl_mcts_select": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_backup": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
-    "spl_mcts_root_stats": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_mcts_root_stats": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_headers": ([C.c_void_p, _vp, _vp], C.c_int),
     "spl_mcts_reset_games": ([C.c_void_p, _vp], C.c_int),
     "spl_mcts_commit": ([C.c_void_p, _vp], C.c_int),

@@ -1,0 +1,74 @@
+"""Coach plug-in: Coach.executeEpisode (Coach.py:50-100) for many games at once.
+
+`Coach(game, nnet, args, batch=B).executeEpisodes(k)` plays self-play games on B device
+trees concurrently (splendor.selfplay.SelfPlay) until k games have finished, expands every
+recorded position with getSymmetries (Coach.py:77-80, device kernel spl_symmetries) and
+returns the reference's example records (board, pi, winner, scdiff, valids, surprise)
+(Coach.py:91-98). `executeEpisode()` is the one-game form. Training (`learn`) is out of
+scope.
+"""
+import numpy as np
+import torch
+
+from .env import unpack_mask
+from .search import evaluator_for
+from .selfplay import SelfPlay, gather_examples
+
+
+def _arg(args, k, default=None):
+    if isinstance(args, dict):
+        return args.get(k, default)
+    return getattr(args, k, default)
+
+
+def expand_symmetries(engine, ex):
+    """Apply Board.get_symmetries to drained examples (device tensors, reference order);
+    winner / scdiff / surprise are shared by all variants of a position."""
+    if ex["board"].shape[0] == 0:
+        return ex
+    s, p, v, present = engine.symmetries(ex["board"], ex["pi"], ex["valids"])
+    keep = present.bool()
+    idx = torch.arange(ex["board"].shape[0], device=keep.device).unsqueeze(1).expand_as(keep)[keep]
+    out = {"board": s[keep], "pi": p[keep], "valids": v[keep]}
+    for k in ("winner", "scdiff", "surprise"):
+        out[k] = ex[k][idx]
+    return out
+
+
+class Coach:
+    def __init__(self, game, nnet, args, batch=None, seed=0x5EED, board_base=0):
+        self.game, self.nnet, self.args = game, nnet, args
+        B = int(batch or _arg(args, "numEps", 1))
+        self.B = B
+        self.sp = SelfPlay(game.engine, B, args, evaluator=evaluator_for(game.engine, nnet, B),
+                           dirichlet_noise=float(_arg(args, "dirichletAlpha", 0.0)) > 0, seed=seed,
+                           board_base=board_base)
+        self.sp.reset()
+
+    def run_iterations(self, k, use_graph=False):
+        for _ in range(k):
+            self.sp.step(use_graph=use_graph)
+
+    def executeEpisodes(self, num_games, with_symmetries=True, as_tuples=True, gather=False):
+        collected, done = [], 0
+        while done < num_games:
+            self.run_iterations(32)
+            ex = self.sp.drain()
+            if ex["board"].shape[0]:
+                collected.append(ex)
+            done = self.sp.stats()["games_done"]
+        ex = {k: torch.cat([c[k] for c in collected]) for k in collected[0]} if collected else self.sp.drain()
+        if gather:
+            ex = gather_examples(ex)
+        if with_symmetries:
+            ex = expand_symmetries(self.game.engine, ex)
+        if not as_tuples:
+            return ex
+        boards = ex["board"].cpu().numpy()
+        pis = ex["pi"].cpu().numpy()
+        valids = unpack_mask(ex["valids"]).cpu().numpy()
+        win, sd, sur = (ex[k].cpu().numpy() for k in ("winner", "scdiff", "surprise"))
+        return [(boards[i], pis[i], win[i], sd[i], valids[i], sur[i]) for i in range(len(boards))]
+
+    def executeEpisode(self):
+        return self.executeEpisodes(1)

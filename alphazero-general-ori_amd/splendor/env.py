@@ -33,12 +33,12 @@ _BIT = None
 
 
 def unpack_mask(mask):
-    """[B,7] packed words -> bool [B,409] (on the same device)."""
+    """[...,7] packed words -> bool [...,409] (on the same device)."""
     global _BIT
     if _BIT is None or _BIT.device != mask.device:
         _BIT = torch.arange(64, device=mask.device, dtype=torch.int64)
     bits = (mask.to(torch.int64).unsqueeze(-1) >> _BIT) & 1
-    return bits.reshape(mask.shape[0], MASK_WORDS * 64)[:, :ACTIONS].bool()
+    return bits.reshape(*mask.shape[:-1], MASK_WORDS * 64)[..., :ACTIONS].bool()
 
 
 class SplendorEngine:
@@ -127,6 +127,23 @@ class SplendorEngine:
         _lib.check(self.L.spl_tree_step(self.ctx, parent.shape[0], _ptr(parent), _ptr(action), _ptr(child),
                                         _ptr(err), self._s()), "spl_tree_step")
         return child
+
+    def set_token_limit(self, n):
+        """Board.setNumTokenLim (SplendorLogicNumba.py:214-215)."""
+        _lib.check(self.L.spl_ctx_set_token_limit(self.ctx, int(n)), "spl_ctx_set_token_limit")
+
+    def symmetries(self, state, pi, valid):
+        """Board.get_symmetries for E examples -> (state [E,K,R,7], pi [E,K,409],
+        valid [E,K,7], present [E,K]) with K = 10 + 2n (reference order)."""
+        E, K = state.shape[0], 10 + 2 * self.n
+        dev = self.device
+        os_ = torch.empty((E, K, self.rows, 7), dtype=torch.int8, device=dev)
+        op = torch.empty((E, K, ACTIONS), dtype=torch.float32, device=dev)
+        ov = torch.empty((E, K, MASK_WORDS), dtype=torch.int64, device=dev)
+        pr = torch.empty((E, K), dtype=torch.uint8, device=dev)
+        _lib.check(self.L.spl_symmetries(self.ctx, E, _ptr(state), _ptr(pi.contiguous()), _ptr(valid.contiguous()),
+                                         _ptr(os_), _ptr(op), _ptr(ov), _ptr(pr), self._s()), "spl_symmetries")
+        return os_, op, ov, pr
 
     def rollout_step(self, state, player, mask_out, action_out, ended_out, games_done, seed, step,
                      board_base=0):

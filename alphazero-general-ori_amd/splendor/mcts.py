@@ -123,15 +123,16 @@ class BatchedMCTS:
         _lib.check(self.L.spl_mcts_headers(self.h, _ptr(self._hdr), self.e._s()), "spl_mcts_headers")
         return self._hdr.cpu().numpy().view(HDR_DTYPE).reshape(self.B)
 
-    def root_stats(self):
+    def root_stats(self, adjusted=False):
         B, dev = self.B, self.e.device
         counts = torch.empty((B, ACTIONS), dtype=torch.int64, device=dev)
         qsa = torch.empty((B, ACTIONS), dtype=torch.float64, device=dev)
         probs = torch.empty((B, ACTIONS), dtype=torch.float64, device=dev)
         q = torch.empty((B, self.e.n), dtype=torch.float64, device=dev)
+        adj = torch.empty((B, ACTIONS), dtype=torch.int64, device=dev) if adjusted else None
         _lib.check(self.L.spl_mcts_root_stats(self.h, _ptr(counts), _ptr(qsa), _ptr(probs), _ptr(q),
-                                              self.e._s()), "spl_mcts_root_stats")
-        return counts, qsa, probs, q
+                                              _ptr(adj), self.e._s()), "spl_mcts_root_stats")
+        return (counts, qsa, probs, q, adj) if adjusted else (counts, qsa, probs, q)
 
     # ---------------------------------------------------------------- reference API
     def get_action_prob(self, canonical_boards, force_full_search=True, keep_tree=True):

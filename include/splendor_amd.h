@@ -46,6 +46,8 @@ int spl_abi_version(void);
  * token_limit = NUM_TOKEN_LIMIT (default 10; Board.setNumTokenLim, :214-215). */
 int spl_ctx_create(int n_players, int token_limit, spl_ctx **out);
 int spl_ctx_destroy(spl_ctx *ctx);
+/* Board.setNumTokenLim (SplendorLogicNumba.py:214-215; Arena.py:116 handicap games) */
+int spl_ctx_set_token_limit(spl_ctx *ctx, int token_limit);
 /* observation_size (SplendorLogicNumba.py:26-27): rows R; bytes per board 7*R */
 int spl_state_rows(const spl_ctx *ctx);
 int spl_state_bytes(const spl_ctx *ctx);
@@ -88,6 +90,15 @@ int spl_round(const spl_ctx *ctx, int B, const int8_t *state, int32_t *out, void
  * child = swap_players(make_move(copy(parent), a, 0, deterministic=True)). */
 int spl_tree_step(const spl_ctx *ctx, int B, const int8_t *parent, const int16_t *action,
                   int8_t *child, int32_t *err, void *hip_stream);
+
+/* SplendorGame.getSymmetries (SplendorGame.py:59-61) -> Board.get_symmetries
+ * (SplendorLogicNumba.py:349-395) for E examples (state E x S, pi E x 409 f32, valid E x 7
+ * u64). Outputs K = 10 + 2n variant slots per example in the reference's order: identity,
+ * 3 tiers x 3 card permutations, then per player up to 2 reserve permutations;
+ * present[E][K] = 1 for emitted slots (reserve permutations depend on #reserved cards). */
+int spl_symmetries(const spl_ctx *ctx, int E, const int8_t *state, const float *pi,
+                   const uint64_t *valid, int8_t *out_state, float *out_pi, uint64_t *out_valid,
+                   uint8_t *present, void *hip_stream);
 
 /* One fused random-policy self-play step per board (BASELINE config 2; the move loop of
  * Coach.executeEpisode, Coach.py:71-100, with a uniform random policy):
@@ -145,10 +156,11 @@ int spl_mcts_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_
 /* pi: B x 409 f32 (policy over all actions, as predict returns), v: B x n f32 */
 int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v,
                     void *hip_stream);
-/* counts B x 409 i64, qsa B x 409 f64 (-42 = unvisited), probs B x 409 f64, q B x n f64;
- * any may be NULL */
+/* counts B x 409 i64 (root visit counts Nsa), qsa B x 409 f64 (-42 = unvisited), probs
+ * B x 409 f64 (temp = 1), q B x n f64, adjusted B x 409 i64 (counts after policy-target
+ * pruning, MCTS.py:69-74; = counts without forced playouts); any may be NULL */
 int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs, double *q,
-                        void *hip_stream);
+                        int64_t *adjusted, void *hip_stream);
 /* ---- self-play (Coach.executeEpisode, Coach.py:50-100), selfplay=1 only ----
  * reset_games: deal B new games (Board.init_game via Philox) and start their searches.
  * commit: for every tree whose search budget is spent, play the move on device:
