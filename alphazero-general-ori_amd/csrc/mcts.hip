@@ -388,10 +388,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
             pi[ea[i]] = (float)((double)POLICY_COUNT(i) / (double)tot);
         uint64_t m[7];
         wave_valid_moves<N>(s, 0, lim, m);
-        uint64_t mv = m[0];
-#pragma unroll
-        for (int k = 1; k < 7; k++) mv = l == k ? m[k] : mv;
-        if (l < 7) P.ex_valid[x * 7 + l] = mv;
+        store_mask(P.ex_valid + x * 7, m);
         if (l == 0) {
             const double q0 = P.nqs[nb + root];
             P.ex_player[x] = player;
@@ -593,10 +590,7 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
         wave_copy_board<N>(leaf_state + (size_t)t * Lx::S, s);
         uint64_t m[7];
         wave_valid_moves<N>(s, 0, lim, m);                   // MCTS.py:136
-        uint64_t mv = m[0];
-#pragma unroll
-        for (int k = 1; k < 7; k++) mv = l == k ? m[k] : mv;
-        if (l < 7) leaf_mask[(size_t)t * 7 + l] = mv;
+        store_mask(leaf_mask + (size_t)t * 7, m);
     }
     if (l == 0) {
         H->depth = depth;

@@ -241,17 +241,25 @@ __device__ __forceinline__ bool deck_card(int8_t *s, int tier, Chance &ch, int8_
     int8_t *cnt = s + 7 * (Lx::DECKS + 2 * tier), *bits = cnt + 7;
     const int tot = sum5(cnt);
     if (tot == 0) return false;
-    double p[8];
+    // searchsorted(cumsum(cnt / tot), u, 'right'), evaluated on the fly (no local arrays)
+    const double u0 = ch.draw();
+    int color = 4;
+    double c = 0.0;
 #pragma unroll
-    for (int c = 0; c < 5; c++) p[c] = (double)cnt[c] / (double)tot;
-    int color = rand_choice(p, 5, ch.draw());
-    if (color > 4) color = 4;                    // cumsum < u: prob ~1e-16, see DESIGN.md
-    uint32_t b = (uint8_t)bits[color];
-    const int nb = __builtin_popcount(b);
+    for (int k = 0; k < 5; k++) {
+        c += (double)cnt[k] / (double)tot;
+        if (c > u0) { color = k; break; }
+    }
+    const uint32_t b = (uint8_t)bits[color];
+    const double nbits = (double)__builtin_popcount(b);
+    const double u1 = ch.draw();
+    int idx = 7;
+    c = 0.0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) p[k] = (double)((b >> (7 - k)) & 1) / (double)nb;
-    int idx = rand_choice(p, 8, ch.draw());
-    if (idx > 7) idx = 7;
+    for (int k = 0; k < 8; k++) {
+        c += (double)((b >> (7 - k)) & 1) / nbits;
+        if (c > u1) { idx = k; break; }
+    }
     bits[color] = (int8_t)(b & ~(1u << (7 - idx)));
     cnt[color] = (int8_t)(cnt[color] - 1);
     const int8_t *cd = K_CARDS[tier * 40 + color * 8 + idx];
@@ -437,11 +445,8 @@ __device__ __forceinline__ int get_score(const int8_t *s, int p) {
 // Board.init_game (:222-246). Card draws use the chance source; the noble draw is a
 // partial Fisher-Yates on the same stream (the reference's np.random.choice is unseeded).
 template <int N>
-__device__ __forceinline__ void init_game(int8_t *s, Chance &ch) {
+__device__ __forceinline__ void init_fill(int8_t *s, Chance &ch) {   // s already zeroed
     using Lx = Lay<N>;
-    const int l = lane_id();
-    for (int i = l; i < Lx::S; i += 64) s[i] = 0;
-    __builtin_amdgcn_wave_barrier();
     const int g = N == 2 ? 4 : (N == 3 ? 5 : 7);
 #pragma unroll
     for (int c = 0; c < 5; c++) s[c] = (int8_t)g;
@@ -458,34 +463,63 @@ __device__ __forceinline__ void init_game(int8_t *s, Chance &ch) {
     }
     for (int t = 0; t < 3; t++)
         for (int i = 0; i < 4; i++) fill_new_card<N>(s, t, i, false, ch);
-    int perm[10];
-#pragma unroll
-    for (int i = 0; i < 10; i++) perm[i] = i;
+    uint64_t perm = 0x9876543210ull;              // 10 nibbles: partial Fisher-Yates
     for (int i = 0; i < Lx::NN; i++) {
-        int j = i + (int)floor(ch.draw() * (double)(10 - i));
-        int t = perm[i]; perm[i] = perm[j]; perm[j] = t;
+        const int j = i + (int)floor(ch.draw() * (double)(10 - i));
+        const uint64_t pi = (perm >> (4 * i)) & 15, pj = (perm >> (4 * j)) & 15;
+        perm &= ~((15ull << (4 * i)) | (15ull << (4 * j)));
+        perm |= (pj << (4 * i)) | (pi << (4 * j));
     }
     for (int i = 0; i < Lx::NN; i++) {
         int8_t *r = s + 7 * (Lx::NOBLES + i);
-        const int8_t *nb = K_NOBLES[perm[i]];
+        const int8_t *nb = K_NOBLES[(perm >> (4 * i)) & 15];
 #pragma unroll
         for (int c = 0; c < 7; c++) r[c] = nb[c];
     }
+}
+
+// wave-collective new game
+template <int N>
+__device__ __forceinline__ void init_game(int8_t *s, Chance &ch) {
+    const int l = lane_id();
+    for (int i = l; i < Lay<N>::S; i += 64) s[i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    init_fill<N>(s, ch);
     __builtin_amdgcn_wave_barrier();
 }
 
-// k-th set bit of the packed mask (k < popcount), wave-uniform
+// single-lane new game (lane-per-board code paths)
+template <int N>
+__device__ __forceinline__ void init_game_lane(int8_t *s, Chance &ch) {
+    for (int i = 0; i < Lay<N>::S; i++) s[i] = 0;
+    init_fill<N>(s, ch);
+}
+
+// store a wave-uniform packed mask (7 words) from lane 0 (no per-lane word selection:
+// selecting w[lane] makes hipcc spill the array to scratch)
+__device__ __forceinline__ void store_mask(uint64_t *dst, const uint64_t w[7]) {
+    if (lane_id() == 0) {
+#pragma unroll
+        for (int k = 0; k < 7; k++) dst[k] = w[k];
+    }
+}
+
+// k-th set bit of the packed mask (k < popcount); fully unrolled (no runtime indexing)
 __device__ __forceinline__ int select_bit(const uint64_t w[7], int k) {
+    int res = 408;
+    bool done = false;
+#pragma unroll
     for (int j = 0; j < 7; j++) {
-        int c = __popcll(w[j]);
-        if (k < c) {
+        const int c = __popcll(w[j]);
+        if (!done && k < c) {
             uint64_t x = w[j];
             for (int t = 0; t < k; t++) x &= x - 1;
-            return 64 * j + __ffsll((unsigned long long)x) - 1;
+            res = 64 * j + __ffsll((unsigned long long)x) - 1;
+            done = true;
         }
-        k -= c;
+        if (!done) k -= c;
     }
-    return 408;
+    return res;
 }
 
 }  // namespace spl

@@ -23,13 +23,6 @@ namespace {
 constexpr int WAVES = 4;            // boards per workgroup
 constexpr int THREADS = 64 * WAVES;
 
-__device__ __forceinline__ uint64_t pick_word(const uint64_t w[7], int j) {
-    uint64_t v = w[0];
-#pragma unroll
-    for (int k = 1; k < 7; k++) v = j == k ? w[k] : v;
-    return v;
-}
-
 template <int N>
 __device__ __forceinline__ void store_board(int8_t *dst, const int8_t *lds) {
     wave_copy_board<N>(dst, lds);
@@ -65,8 +58,7 @@ __global__ __launch_bounds__(THREADS) void k_valid(int B, const int8_t *__restri
     const int p = player ? player[b] : 0;
     uint64_t m[7];
     wave_valid_moves<N>(s, p, lim, m);
-    const int l = lane_id();
-    if (l < 7) mask[(size_t)b * 7 + l] = pick_word(m, l);
+    store_mask(mask + (size_t)b * 7, m);
 }
 
 template <int N>
@@ -160,7 +152,25 @@ __global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__re
     store_board<N>(child + (size_t)b * Lx::S, s);
 }
 
-// Fused random-policy self-play step (see splendor_amd.h spl_rollout_step)
+// Fused random-policy self-play step (see splendor_amd.h spl_rollout_step).
+// A 256-thread workgroup owns RB = 64 consecutive boards, staged in LDS at an odd-dword
+// stride (conflict-free lane-per-board access):
+//   phase 1  all threads: coalesced dword load of the 64 boards (+ players)
+//   phase 2  wave w, boards 16w..16w+15, one board at a time: 409-action mask (ballots) on
+//            the real board for the player to move (== the canonical form's mask: it only
+//            reads player p's rows), mask store, uniform action draw
+//   phase 3  lane b of wave 0 = board b: make_move with chance, end check, auto-reset —
+//            the serial rule logic runs 64 boards per wave instead of one
+//   phase 4  all threads: coalesced store
+constexpr int RB = 64;
+#ifndef ROLLOUT_ABLATE
+#define ROLLOUT_ABLATE 0   // diagnostic builds only (tools/ablate_rollout.hip): 1 = skip mask, 2 = skip step
+#endif
+template <int N>
+struct RolloutLds {
+    static constexpr int STRIDE = ((Lay<N>::S + 3) / 4) % 2 ? (Lay<N>::S + 3) / 4 * 4 : (Lay<N>::S + 3) / 4 * 4 + 4;
+};
+
 template <int N>
 __global__ __launch_bounds__(THREADS) void k_rollout(int B, int8_t *__restrict__ state,
                                                      int8_t *__restrict__ player, int lim,
@@ -170,42 +180,86 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int8_t *__restrict__
                                                      int32_t *__restrict__ games_done,
                                                      uint64_t seed, uint32_t step, uint32_t bbase) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][2][Lx::SPAD];
-    const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
-    if (b >= B) return;
-    const int l = lane_id();
-    int8_t *s = lds[w][0], *c = lds[w][1];
-    int8_t *g = state + (size_t)b * Lx::S;
-    wave_copy_board<N>(s, g);
-    const int p = player[b];
-    wave_roll_players<N>(c, s, p);                       // getCanonicalForm
-    uint64_t m[7];
-    wave_valid_moves<N>(c, 0, lim, m);                   // getValidMoves(canonical, 0)
-    if (l < 7) mask_out[(size_t)b * 7 + l] = pick_word(m, l);
-    int cnt = 0;
-#pragma unroll
-    for (int j = 0; j < 7; j++) cnt += __popcll(m[j]);
-    const uint32_t gb = bbase + (uint32_t)b;
-    const int k = (int)(philox_u01(seed, gb, step, 0) * (double)cnt);
-    const int a = select_bit(m, k);
-    Chance ch{nullptr, seed, gb, step, 1};
-    int nxt = make_move<N>(s, a, p, false, ch);          // getNextState (chance)
-    __builtin_amdgcn_wave_barrier();
-    float e[N];
-    check_end<N>(s, e);                                  // getGameEnded
-    bool ended = false;
-#pragma unroll
-    for (int i = 0; i < N; i++) ended |= e[i] != 0.f;
-    if (l < N) ended_out[(size_t)b * N + l] = e[l < N ? l : 0];
-    if (l == 0) action_out[b] = (int16_t)a;
-    if (ended) {                                         // auto-reset finished games
-        Chance ch2{nullptr, seed, gb, step, 3};
-        init_game<N>(s, ch2);
-        nxt = 0;
-        if (games_done && l == 0) games_done[b] += 1;
+    constexpr int ST = RolloutLds<N>::STRIDE;
+    __shared__ __align__(16) int8_t lds[RB * ST];
+    __shared__ int16_t act[RB];
+    __shared__ int8_t pl[RB];
+    const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
+    const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
+    // phase 1
+    if constexpr (Lx::S % 4 == 0) {
+        const int32_t *g = reinterpret_cast<const int32_t *>(state + (size_t)b0 * Lx::S);
+        constexpr int W = Lx::S / 4;
+        for (int i = tid; i < nb * W; i += THREADS) {
+            const int b = i / W, k = i - b * W;
+            *reinterpret_cast<int32_t *>(lds + b * ST + 4 * k) = g[i];
+        }
+    } else {
+        const int8_t *g = state + (size_t)b0 * Lx::S;
+        for (int i = tid; i < nb * Lx::S; i += THREADS) {
+            const int b = i / Lx::S, k = i - b * Lx::S;
+            lds[b * ST + k] = g[i];
+        }
     }
-    store_board<N>(g, s);
-    if (l == 0) player[b] = (int8_t)nxt;
+    if (tid < nb) pl[tid] = player[b0 + tid];
+    __syncthreads();
+    // phase 2
+    for (int j = 0; j < RB / WAVES && ROLLOUT_ABLATE != 1; j++) {
+        const int b = w * (RB / WAVES) + j;
+        if (b >= nb) break;
+        const int8_t *s = lds + b * ST;
+        uint64_t m[7];
+        wave_valid_moves<N>(s, pl[b], lim, m);
+        store_mask(mask_out + (size_t)(b0 + b) * 7, m);
+        int cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) cnt += __popcll(m[k]);
+        const int kk = (int)(philox_u01(seed, bbase + (uint32_t)(b0 + b), step, 0) * (double)cnt);
+        const int a = select_bit(m, kk);
+        if (l == 0) act[b] = (int16_t)a;
+    }
+    __syncthreads();
+    if (ROLLOUT_ABLATE == 1 && tid < nb) act[tid] = 30 + (int)((step + tid) % 5);
+    // phase 3
+    if (w == 0 && l < nb && ROLLOUT_ABLATE != 2) {
+        const int b = l, gb = b0 + b;
+        int8_t *s = lds + b * ST;
+        const int a = act[b];
+        Chance ch{nullptr, seed, bbase + (uint32_t)gb, step, 1};
+        int nxt = make_move<N>(s, a, pl[b], false, ch);
+        float e[N];
+        check_end<N>(s, e);
+        bool ended = false;
+#pragma unroll
+        for (int i = 0; i < N; i++) {
+            ended |= e[i] != 0.f;
+            ended_out[(size_t)gb * N + i] = e[i];
+        }
+        action_out[gb] = (int16_t)a;
+        if (ended) {
+            Chance ch2{nullptr, seed, bbase + (uint32_t)gb, step, 3};
+            init_game_lane<N>(s, ch2);
+            nxt = 0;
+            if (games_done) games_done[gb] += 1;
+        }
+        player[gb] = (int8_t)nxt;
+    }
+    __syncthreads();
+    // phase 4
+    if constexpr (Lx::S % 4 == 0) {
+        int32_t *g = reinterpret_cast<int32_t *>(state + (size_t)b0 * Lx::S);
+        constexpr int W = Lx::S / 4;
+        for (int i = tid; i < nb * W; i += THREADS) {
+            const int b = i / W, k = i - b * W;
+            g[i] = *reinterpret_cast<const int32_t *>(lds + b * ST + 4 * k);
+        }
+    } else {
+        int8_t *g = state + (size_t)b0 * Lx::S;
+        for (int i = tid; i < nb * Lx::S; i += THREADS) {
+            const int b = i / Lx::S, k = i - b * Lx::S;
+            g[i] = lds[b * ST + k];
+        }
+    }
 }
 
 // Board.get_symmetries (SplendorLogicNumba.py:349-395) for E examples, one wave per
@@ -422,7 +476,7 @@ int spl_rollout_step(const spl_ctx *c, int B, int8_t *state, int8_t *player, uin
         (B && (!state || !player || !mask_out || !action_out || !ended_out)))
         return SPL_EINVAL;
     if (!B) return 0;
-    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_rollout<N>, wave_grid(B), dim3(THREADS), 0,
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_rollout<N>, dim3((unsigned)((B + RB - 1) / RB)), dim3(THREADS), 0,
                                           (hipStream_t)hs, B, state, player, c->token_limit,
                                           mask_out, action_out, ended_out, games_done, seed,
                                           step, board_base));
