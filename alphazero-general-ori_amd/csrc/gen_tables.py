@@ -166,6 +166,36 @@ def main():
     out.append(arr("static __constant__ uint32_t K_ACTION_DESC[409]", None, action_table(), lambda x: f"0x{x:06x}u"))
     out.append("// exchange actions 60..404: take id, give id, give id (255 none), reserve index (255 none)")
     out.append(arr("static __constant__ uint8_t K_EXCHANGE[345][4]", None, exchange_table()))
+    # ---- packed forms for the 8-byte-row LDS layout (splendor_device.h)
+    def pack(vals):
+        v = 0
+        for i, x in enumerate(vals):
+            v |= (x & 0xFF) << (8 * i)
+        return v
+    rows = []
+    for tier, tab in enumerate((TIER1, TIER2, TIER3)):
+        for col in range(5):
+            for k in range(8):
+                if k < len(tab[col]):
+                    cost = list(tab[col][k][:5])
+                    gain = [0] * 7
+                    gain[GAIN[col]] = 1
+                    gain[6] = tab[col][k][5]
+                    rows.append((pack(cost), pack(gain)))
+                else:
+                    rows.append((0, 0))
+    out.append("// [tier*40 + deckcol*8 + k] -> (cost row, gain row) as packed 8-byte rows")
+    out.append(arr("static __constant__ uint64_t K_CARD_ROWS[120][2]", None, rows, lambda x: f"0x{x:016x}ull"))
+    out.append(arr("static __constant__ uint64_t K_NOBLE_ROWS[10]", None, [pack(list(n) + [0, 3]) for n in NOBLES],
+                   lambda x: f"0x{x:016x}ull"))
+    out.append(arr("static __constant__ uint64_t K_TAKE_ROW[30]", None, [pack(v) for v in TAKE], lambda x: f"0x{x:016x}ull"))
+    out.append(arr("static __constant__ uint64_t K_GIVE_ROW[20]", None, [pack(v) for v in GIVE], lambda x: f"0x{x:016x}ull"))
+    out.append(arr("static __constant__ uint64_t K_SPEC3_ROW[40]", None, [pack(v) for v in SPEC3], lambda x: f"0x{x:016x}ull"))
+    out.append("// exact IEEE quotients for the deck draw: K_QUOT[tot][cnt] = cnt / tot, K_RECIP[n] = 1 / n")
+    quot = [[(c / t if t else 0.0) for c in range(9)] for t in range(41)]
+    out.append(arr("static __constant__ double K_QUOT[41][9]", None, quot, lambda x: float(x).hex()))
+    out.append(arr("static __constant__ double K_RECIP[9]", None, [0.0] + [1.0 / n for n in range(1, 9)],
+                   lambda x: float(x).hex()))
     print("\n".join(out))
 
 

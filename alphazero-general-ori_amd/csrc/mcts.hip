@@ -250,13 +250,13 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
     using Lx = Lay<N>;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
-    wave_copy_board<N>(P.root_state + (size_t)t * Lx::S, s);
+    wave_store_board<N>(P.root_state + (size_t)t * Lx::S, s);
     int root = -1;
     if (keep && H->node_count > 0) {
         uint64_t k0, k1;
         wave_fingerprint<N>(s, k0, k1);
         root = hash_lookup(P, t, k0, k1);
-        root = compact_tree(P, t, root, (uint8_t)s[6]);
+        root = compact_tree(P, t, root, (uint8_t)bt(row(s, 0), 6));
     } else {
         int32_t *hs = P.hslot + (size_t)t * P.hcap;
         for (int i = l; i < P.hcap; i += 64) hs[i] = -1;
@@ -286,23 +286,22 @@ __global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int
                                                        const int8_t *__restrict__ roots, int keep,
                                                        int force_full) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     int8_t *s = lds[w];
-    for (int i = Lx::S + lane_id(); i < Lx::SPAD; i += 64) s[i] = 0;
-    wave_copy_board<N>(s, roots + (size_t)t * Lx::S);
+    wave_load_board<N>(s, roots + (size_t)t * Lx::S);
     begin_search<N>(P, C, t, s, keep != 0, force_full != 0);
 }
 
 // ------------------------------------------------------------ self-play
 // New game on tree t: Board.init_game with ST_DEAL draws, player 0, fresh tree.
 template <int N>
-__device__ void deal_game(const Pools &P, const SearchCfg &C, int t, int8_t *b) {
+__device__ void deal_game(const Pools &P, const SearchCfg &C, int t, int8_t *b, double *ub) {
     TreeHdr *H = P.hdr + t;
     const int g = H->game_no;
-    Chance ch{nullptr, C.seed, C.board_base + (uint32_t)t, ST_DEAL | (uint32_t)g, 0};
-    init_game<N>(b, ch);
+    wave_philox_uniforms(ub, C.seed, C.board_base + (uint32_t)t, ST_DEAL | (uint32_t)g, 0, DEAL_DRAWS);
+    wave_init_game<N>(b, ub);
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     if (lane_id() == 0) {
@@ -318,13 +317,13 @@ __device__ void deal_game(const Pools &P, const SearchCfg &C, int t, int8_t *b) 
 template <int N>
 __global__ __launch_bounds__(THREADS) void k_reset_games(Pools P, SearchCfg C, int B) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
+    __shared__ double ub[WAVES][DEAL_DRAWS];
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     int8_t *b = lds[w];
-    for (int i = Lx::S + lane_id(); i < Lx::SPAD; i += 64) b[i] = 0;
-    deal_game<N>(P, C, t, b);
-    wave_copy_board<N>(P.board + (size_t)t * Lx::S, b);
+    deal_game<N>(P, C, t, b, ub[w]);
+    wave_store_board<N>(P.board + (size_t)t * Lx::S, b);
     begin_search<N>(P, C, t, b, false, false);
 }
 
@@ -341,7 +340,8 @@ __device__ __forceinline__ long long pruned_count(long long c, int best, bool fo
 template <int N>
 __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B, int lim) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][2][Lx::SPAD];
+    __shared__ __align__(16) int8_t lds[WAVES][2][Lx::LS];
+    __shared__ double ub[WAVES][DEAL_DRAWS];
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
@@ -373,13 +373,12 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     const int step = H->episode_step + 1;
     const int player = H->player;
     int8_t *s = lds[w][0], *b = lds[w][1];
-    for (int i = Lx::S + l; i < Lx::SPAD; i += 64) { s[i] = 0; b[i] = 0; }
     // training example (Coach.py:76-80): canonical board, player, pi, valids, q
     int nex = H->n_examples;
     if (H->full && nex < P.excap) {
         const size_t x = (size_t)t * P.excap + nex;
-        wave_copy_board<N>(s, P.root_state + (size_t)t * Lx::S);
-        wave_copy_board<N>(P.ex_state + x * Lx::S, s);
+        wave_load_board<N>(s, P.root_state + (size_t)t * Lx::S);
+        wave_store_board<N>(P.ex_state + x * Lx::S, s);
         float *pi = P.ex_pi + x * SPL_ACTIONS;
         for (int a = l; a < SPL_ACTIONS; a += 64) pi[a] = 0.f;
         __threadfence_block();
@@ -418,7 +417,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     action = __shfl(action, 0, 64);
 #undef POLICY_COUNT
     // getNextState with chance (Coach.py:86), getGameEnded (:88)
-    wave_copy_board<N>(b, P.board + (size_t)t * Lx::S);
+    wave_load_board<N>(b, P.board + (size_t)t * Lx::S);
     Chance ch{nullptr, C.seed, gb, ST_MOVE | (uint32_t)cm, 0};
     int nxt = make_move<N>(b, action, player, false, ch);
     __builtin_amdgcn_wave_barrier();
@@ -444,7 +443,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
                 continue;
             }
             const int px = P.ex_player[x];
-            wave_copy_board<N>(P.out_state + (size_t)slot * Lx::S, P.ex_state + x * Lx::S);
+            wave_copy_bytes(P.out_state + (size_t)slot * Lx::S, P.ex_state + x * Lx::S, Lx::S);
             for (int a = l; a < SPL_ACTIONS; a += 64)
                 P.out_pi[(size_t)slot * SPL_ACTIONS + a] = P.ex_pi[x * SPL_ACTIONS + a];
             if (l < 7) P.out_valid[(size_t)slot * 7 + l] = P.ex_valid[x * 7 + l];
@@ -460,7 +459,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         if (l == 0) H->games_done += 1;
-        deal_game<N>(P, C, t, b);                               // next episode
+        deal_game<N>(P, C, t, b, ub[w]);                        // next episode
         nxt = 0;
     } else if (l == 0) {
         H->player = nxt;
@@ -468,7 +467,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    wave_copy_board<N>(P.board + (size_t)t * Lx::S, b);
+    wave_store_board<N>(P.board + (size_t)t * Lx::S, b);
     wave_roll_players<N>(s, b, nxt);                            // getCanonicalForm (:73)
     begin_search<N>(P, C, t, s, !ended, false);
 }
@@ -507,7 +506,7 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
                                                     uint64_t *__restrict__ leaf_mask,
                                                     uint8_t *__restrict__ leaf_valid) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
@@ -518,8 +517,7 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
         return;
     }
     int8_t *s = lds[w];
-    for (int i = Lx::S + l; i < Lx::SPAD; i += 64) s[i] = 0;
-    wave_copy_board<N>(s, P.root_state + (size_t)t * Lx::S);
+    wave_load_board<N>(s, P.root_state + (size_t)t * Lx::S);
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     int32_t *path = P.path + (size_t)t * P.pcap * 2;
     int node = H->root, depth = 0, kind = LEAF_NN;
@@ -570,7 +568,7 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
                 if (l == 0) {
                     P.nkey0[nb + id] = k0; P.nkey1[nb + id] = k1; P.neb[nb + id] = 0;
                     P.nec[nb + id] = 0; P.nns[nb + id] = 0; P.nqs[nb + id] = 0;
-                    P.nround[nb + id] = (uint8_t)s[6]; P.nterm[nb + id] = 1;
+                    P.nround[nb + id] = (uint8_t)bt(row(s, 0), 6); P.nterm[nb + id] = 1;
 #pragma unroll
                     for (int i = 0; i < 4; i++) P.nes[(nb + id) * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
                     hash_insert(P, t, k0, id);
@@ -587,7 +585,7 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
     }
     __builtin_amdgcn_wave_barrier();
     if (kind == LEAF_NN) {
-        wave_copy_board<N>(leaf_state + (size_t)t * Lx::S, s);
+        wave_store_board<N>(leaf_state + (size_t)t * Lx::S, s);
         uint64_t m[7];
         wave_valid_moves<N>(s, 0, lim, m);                   // MCTS.py:136
         store_mask(leaf_mask + (size_t)t * 7, m);
@@ -596,7 +594,7 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
         H->depth = depth;
         H->leaf_kind = kind;
         H->leaf_k0 = k0; H->leaf_k1 = k1;
-        H->leaf_round = (uint8_t)s[6];
+        H->leaf_round = (uint8_t)bt(row(s, 0), 6);
 #pragma unroll
         for (int i = 0; i < 4; i++) H->leaf_v[i] = val[i];
         leaf_valid[t] = kind == LEAF_NN;

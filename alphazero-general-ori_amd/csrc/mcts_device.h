@@ -95,14 +95,15 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-// 128-bit fingerprint of the S-byte state staged in LDS (zero padded to SPAD); the
-// transposition key of MCTS.py:119 (board.tobytes()). Wave-collective.
+// 128-bit fingerprint of the state staged in LDS (8-byte rows, zero pad byte); the
+// transposition key of MCTS.py:119 (board.tobytes()). Row r enters as its 7 bytes with r
+// in the pad byte. Wave-collective.
 template <int N>
 __device__ __forceinline__ void wave_fingerprint(const int8_t *s, uint64_t &k0, uint64_t &k1) {
     const int l = lane_id();
     uint64_t a = 0, b = 0;
-    for (int i = l; i < Lay<N>::SPAD / 4; i += 64) {
-        uint64_t x = (uint32_t)reinterpret_cast<const int32_t *>(s)[i] | ((uint64_t)i << 32);
+    for (int i = l; i < Lay<N>::ROWS; i += 64) {
+        const uint64_t x = row(s, i) | ((uint64_t)i << 56);
         a ^= mix64(x ^ 0x243F6A8885A308D3ull);
         b ^= mix64(x ^ 0x13198A2E03707344ull);
     }

@@ -1,14 +1,19 @@
 // splendor_device.h — gfx950 device implementation of the Splendor rules.
 //
-// Execution model: ONE WAVE (64 lanes) PER BOARD. The board record (7*R int8, the
-// reference's (R,7) state, SplendorLogicNumba.py:291-303) is staged in LDS; the wave
-// evaluates the 409-action legality mask as 7 x 64-lane chunks and packs each with a
-// ballot, and applies a transition with wave-uniform control flow (no divergence, every
-// lane runs the same instructions on broadcast LDS reads).
+// Board representation on chip: the reference's int8 (R,7) state (SplendorLogicNumba.py:
+// 291-303; 7 bytes per row in HBM, identical to board.tobytes()) is staged in LDS as
+// R x 8-byte rows (7 columns + a zero pad byte). Every row is one aligned 64-bit word, so
+// a row read/write/copy is a single ds_read_b64/ds_write_b64 and gem arithmetic is
+// byte-wise SIMD-within-a-register on whole rows.
 //
-// Semantics follow the reference bit-for-bit (incl. Numba int8 wraps); each function
-// cites the reference lines it restates. Parity is checked against the CPU oracle
-// (oracle/) which is itself pinned to golden vectors recorded from the reference.
+// Kernels use two mappings: WAVE-per-board (the 409-action legality mask is 7 chunks of
+// 64 lanes packed by ballots) and LANE-per-board (transitions: the serial rule logic of 64
+// boards runs in one wave). Functions named wave_* are wave-collective; all others are
+// per-lane and run either uniformly across a wave or one board per lane.
+//
+// Semantics follow the reference bit for bit (incl. the Numba int8 wraps); every function
+// cites the lines it restates. Parity: tests/ compare against the CPU oracle (oracle/),
+// itself pinned to golden vectors recorded from the reference.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,8 +30,8 @@ template <int N>
 struct Lay {  // row offsets of the (R,7) state (SplendorLogicNumba.py:296-303)
     static constexpr int NN = N + 1;                 // nobles on the table
     static constexpr int ROWS = 32 + 10 * N + N * N;
-    static constexpr int S = 7 * ROWS;               // bytes per board
-    static constexpr int SPAD = (S + 15) & ~15;      // LDS slot (16-B aligned)
+    static constexpr int S = 7 * ROWS;               // bytes per board in HBM (7-byte rows)
+    static constexpr int LS = 8 * ROWS;              // bytes per board in LDS (8-byte rows)
     static constexpr int BANK = 0, TIERS = 1, DECKS = 25, NOBLES = 31;
     static constexpr int GEMS = 32 + N, PNOB = 32 + 2 * N, CARDS = 32 + 3 * N + N * N;
     static constexpr int RSV = 32 + 4 * N + N * N;
@@ -36,111 +41,189 @@ struct Lay {  // row offsets of the (R,7) state (SplendorLogicNumba.py:296-303)
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
-__device__ __forceinline__ int sum5(const int8_t *r) { return r[0] + r[1] + r[2] + r[3] + r[4]; }
-__device__ __forceinline__ int sum7(const int8_t *r) { return sum5(r) + r[5] + r[6]; }
+// ------------------------------------------------------------------ row words
+__device__ __forceinline__ uint64_t &row(int8_t *s, int r) { return *reinterpret_cast<uint64_t *>(s + 8 * r); }
+__device__ __forceinline__ uint64_t row(const int8_t *s, int r) { return *reinterpret_cast<const uint64_t *>(s + 8 * r); }
+__device__ __forceinline__ int bt(uint64_t w, int c) { return (int8_t)(uint8_t)(w >> (8 * c)); }
+__device__ __forceinline__ uint64_t with_bt(uint64_t w, int c, int v) {
+    return (w & ~(0xFFull << (8 * c))) | ((uint64_t)(uint8_t)v << (8 * c));
+}
+__device__ __forceinline__ int sum5(uint64_t w) { return bt(w, 0) + bt(w, 1) + bt(w, 2) + bt(w, 3) + bt(w, 4); }
+__device__ __forceinline__ int sum7(uint64_t w) { return sum5(w) + bt(w, 5) + bt(w, 6); }
+// byte-wise add / sub modulo 256 in every byte (the int8 wrap), no carries between bytes
+__device__ __forceinline__ uint64_t bytes_add(uint64_t a, uint64_t b) {
+    const uint64_t H = 0x8080808080808080ull;
+    return ((a & ~H) + (b & ~H)) ^ ((a ^ b) & H);
+}
+__device__ __forceinline__ uint64_t bytes_sub(uint64_t a, uint64_t b) {
+    const uint64_t H = 0x8080808080808080ull;
+    return ((a | H) - (b & ~H)) ^ ((a ^ ~b) & H);
+}
+// each of the first 5 signed bytes of x >= the matching signed byte of v
+__device__ __forceinline__ bool ge5(uint64_t x, uint64_t v) {
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < 5; c++) ok &= bt(x, c) >= bt(v, c);
+    return ok;
+}
 
 // ------------------------------------------------------------------ chance source
-// Philox4x32-10 (Salmon et al. 2011); identical to oracle/splendor_oracle.c or_philox4x32.
-__device__ __forceinline__ double philox_u01(uint64_t seed, uint32_t board, uint32_t stream,
-                                             uint32_t draw) {
-    uint32_t c0 = draw, c1 = board, c2 = stream, c3 = 0x53504C44u;
+// Philox4x32-10 (Salmon et al. 2011); identical to oracle/splendor_oracle.c. Uniform d of
+// a (seed, board, stream) sequence is one half of counter block d/2: output words (0,1)
+// for even d, (2,3) for odd d, 53 bits each.
+__device__ __forceinline__ void philox_pair(uint64_t seed, uint32_t board, uint32_t stream,
+                                            uint32_t blk, double &a, double &b) {
+    uint32_t c0 = blk, c1 = board, c2 = stream, c3 = 0x53504C44u;
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
     for (int r = 0; r < 10; r++) {
-        uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
         c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
-    return ((double)(c0 >> 5) * 67108864.0 + (double)(c1 >> 6)) * (1.0 / 9007199254740992.0);
+    a = ((double)(c0 >> 5) * 67108864.0 + (double)(c1 >> 6)) * (1.0 / 9007199254740992.0);
+    b = ((double)(c2 >> 5) * 67108864.0 + (double)(c3 >> 6)) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ double philox_u01(uint64_t seed, uint32_t board, uint32_t stream, uint32_t d) {
+    double a, b;
+    philox_pair(seed, board, stream, d >> 1, a, b);
+    return (d & 1) ? b : a;
 }
 
 // Either an explicit stream of doubles (parity with recorded reference draws) or Philox.
+// Sequential draws reuse the second half of a Philox block.
 struct Chance {
     const double *u;   // explicit uniforms for this board, or nullptr -> Philox
     uint64_t seed;
     uint32_t board, stream, next;
+    double spare = 0.0;
+    bool have_spare = false;
     __device__ __forceinline__ double draw() {
-        double r = u ? u[next] : philox_u01(seed, board, stream, next);
+        if (u) return u[next++];
+        double r;
+        if ((next & 1) && have_spare) {
+            r = spare;
+        } else {
+            double a, b;
+            philox_pair(seed, board, stream, next >> 1, a, b);
+            r = (next & 1) ? b : a;
+            spare = b;
+        }
+        have_spare = !(next & 1);
         ++next;
         return r;
     }
 };
 
-// my_random_choice: searchsorted(cumsum(prob), U, side="right") (SplendorLogicNumba.py:39-41)
-__device__ __forceinline__ int rand_choice(const double *p, int len, double u) {
-    double c = 0.0;
-    for (int i = 0; i < len; i++) {
-        c += p[i];
-        if (c > u) return i;
-    }
-    return len;
-}
-
-// ------------------------------------------------------------------ gem vectors
-__device__ __forceinline__ void move_gems(int8_t *bank, int8_t *gems, const int8_t *v, int sign) {
+// ------------------------------------------------------------------ HBM <-> LDS
+// HBM boards have 7-byte rows; LDS boards 8-byte rows with a zero pad byte. Four rows are
+// 28 HBM bytes = 7 dwords; one lane converts such a quad in registers (funnel shifts), so
+// a board moves as 7-dword global accesses and 64-bit LDS accesses. Boards whose row count
+// is not a multiple of 4 (3 players) go byte by byte.
+__device__ __forceinline__ void quad_to_rows(const uint32_t *g, uint64_t *o) {
+    uint32_t d[7];
 #pragma unroll
-    for (int c = 0; c < 5; c++) {
-        bank[c] = (int8_t)(bank[c] - sign * v[c]);
-        gems[c] = (int8_t)(gems[c] + sign * v[c]);
+    for (int k = 0; k < 7; k++) d[k] = g[k];
+    const uint64_t M = 0x00FFFFFFFFFFFFFFull;
+    o[0] = ((uint64_t)d[0] | (uint64_t)d[1] << 32) & M;
+    o[1] = ((uint64_t)d[1] >> 24 | (uint64_t)d[2] << 8 | (uint64_t)d[3] << 40) & M;
+    o[2] = ((uint64_t)d[3] >> 16 | (uint64_t)d[4] << 16 | (uint64_t)d[5] << 48) & M;
+    o[3] = ((uint64_t)d[5] >> 8 | (uint64_t)d[6] << 24) & M;
+}
+__device__ __forceinline__ void rows_to_quad(const uint64_t *r, uint32_t *g) {
+    const uint64_t r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+    g[0] = (uint32_t)r0;
+    g[1] = (uint32_t)(r0 >> 32 | r1 << 24);
+    g[2] = (uint32_t)(r1 >> 8);
+    g[3] = (uint32_t)(r1 >> 40 | r2 << 16);
+    g[4] = (uint32_t)(r2 >> 16);
+    g[5] = (uint32_t)(r2 >> 48 | r3 << 8);
+    g[6] = (uint32_t)(r3 >> 24);
+}
+// quad-or-byte unit u of a board (units per board: Conv<N>::UNITS)
+template <int N>
+struct Conv {
+    static constexpr bool QUAD = Lay<N>::ROWS % 4 == 0;
+    static constexpr int UNITS = QUAD ? Lay<N>::ROWS / 4 : Lay<N>::S;
+    static __device__ __forceinline__ void load(int8_t *lds, const int8_t *g, int u) {
+        if constexpr (QUAD) {
+            quad_to_rows(reinterpret_cast<const uint32_t *>(g) + 7 * u, reinterpret_cast<uint64_t *>(lds) + 4 * u);
+        } else {
+            lds[8 * (u / 7) + u % 7] = g[u];
+            if (u % 7 == 6) lds[8 * (u / 7) + 7] = 0;
+        }
     }
-}
-
-// ------------------------------------------------------------------ wave helpers
-// copy `bytes` (multiple of 4, 4-aligned) between global and LDS with dword lanes
-__device__ __forceinline__ void wave_copy4(int8_t *dst, const int8_t *src, int bytes) {
-    const int l = lane_id();
-    for (int i = 4 * l; i < bytes; i += 256)
-        *reinterpret_cast<int32_t *>(dst + i) = *reinterpret_cast<const int32_t *>(src + i);
-}
-__device__ __forceinline__ void wave_copy1(int8_t *dst, const int8_t *src, int bytes) {
-    const int l = lane_id();
-    for (int i = l; i < bytes; i += 64) dst[i] = src[i];
+    static __device__ __forceinline__ void store(int8_t *g, const int8_t *lds, int u) {
+        if constexpr (QUAD) rows_to_quad(reinterpret_cast<const uint64_t *>(lds) + 4 * u, reinterpret_cast<uint32_t *>(g) + 7 * u);
+        else g[u] = lds[8 * (u / 7) + u % 7];
+    }
+};
+template <int N>
+__device__ __forceinline__ void wave_load_board(int8_t *lds, const int8_t *g) {
+    for (int u = lane_id(); u < Conv<N>::UNITS; u += 64) Conv<N>::load(lds, g, u);
+    __builtin_amdgcn_wave_barrier();
 }
 template <int N>
-__device__ __forceinline__ void wave_copy_board(int8_t *dst, const int8_t *src) {
-    if constexpr (Lay<N>::S % 4 == 0) wave_copy4(dst, src, Lay<N>::S);
-    else wave_copy1(dst, src, Lay<N>::S);
+__device__ __forceinline__ void wave_store_board(int8_t *g, const int8_t *lds) {
+    __builtin_amdgcn_wave_barrier();
+    for (int u = lane_id(); u < Conv<N>::UNITS; u += 64) Conv<N>::store(g, lds, u);
+}
+// plain byte copies in one layout (HBM->HBM, or byte-permuting kernels)
+__device__ __forceinline__ void wave_copy_bytes(int8_t *dst, const int8_t *src, int bytes) {
+    const int l = lane_id();
+    if ((bytes & 3) == 0 && ((uintptr_t)dst & 3) == 0 && ((uintptr_t)src & 3) == 0) {
+        for (int i = 4 * l; i < bytes; i += 256)
+            *reinterpret_cast<int32_t *>(dst + i) = *reinterpret_cast<const int32_t *>(src + i);
+    } else {
+        for (int i = l; i < bytes; i += 64) dst[i] = src[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+// LDS -> LDS board copy (8-byte rows)
+template <int N>
+__device__ __forceinline__ void wave_copy_lds_board(int8_t *dst, const int8_t *src) {
+    for (int r = lane_id(); r < Lay<N>::ROWS; r += 64) row(dst, r) = row(src, r);
     __builtin_amdgcn_wave_barrier();
 }
 
 // swap_players (SplendorLogicNumba.py:338-347): roll each player block so that player k
-// becomes player 0. Noble block rolls by 3k (hard-coded 3, :345). dst may equal src.
+// becomes player 0 (gems by k, nobles by 3k — hard-coded 3, :345 —, cards by k, reserved
+// by 6k). Wave: one lane per row. dst may equal src.
 template <int N>
 __device__ __forceinline__ void wave_roll_players(int8_t *dst, const int8_t *src, int k) {
     using Lx = Lay<N>;
-    constexpr int PB = 7 * Lx::PROWS;
-    constexpr int ITER = (PB + 63) / 64;
+    constexpr int IT = (Lx::ROWS + 63) / 64;
     const int l = lane_id();
-    int8_t v[ITER];
+    uint64_t v[IT];
 #pragma unroll
-    for (int j = 0; j < ITER; j++) {
-        int i = l + 64 * j;
+    for (int j = 0; j < IT; j++) {
+        const int r = l + 64 * j;
         v[j] = 0;
-        if (i < PB) {
-            int r = i / 7, c = i - 7 * (i / 7), sr;
-            if (r < N) sr = (r + k) % N;
-            else if (r < N + N * Lx::NN) sr = N + (r - N + 3 * k) % (N * Lx::NN);
-            else if (r < 2 * N + N * Lx::NN) sr = N + N * Lx::NN + (r - N - N * Lx::NN + k) % N;
-            else sr = 2 * N + N * Lx::NN + (r - 2 * N - N * Lx::NN + 6 * k) % (6 * N);
-            v[j] = src[7 * (Lx::GEMS + sr) + c];
+        if (r < Lx::ROWS) {
+            int sr = r;
+            const int q = r - Lx::GEMS;
+            if (q >= 0) {
+                if (q < N) sr = Lx::GEMS + (q + k) % N;
+                else if (q < N + N * Lx::NN) sr = Lx::GEMS + N + (q - N + 3 * k) % (N * Lx::NN);
+                else if (q < 2 * N + N * Lx::NN) sr = Lx::GEMS + N + N * Lx::NN + (q - N - N * Lx::NN + k) % N;
+                else sr = Lx::GEMS + 2 * N + N * Lx::NN + (q - 2 * N - N * Lx::NN + 6 * k) % (6 * N);
+            }
+            v[j] = row(src, sr);
         }
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int j = 0; j < ITER; j++) {
-        int i = l + 64 * j;
-        if (i < PB) dst[7 * Lx::GEMS + i] = v[j];
-    }
-    if (dst != src) {  // shared (non-player) rows
-        for (int i = l; i < 7 * Lx::GEMS; i += 64) dst[i] = src[i];
+    for (int j = 0; j < IT; j++) {
+        const int r = l + 64 * j;
+        if (r < Lx::ROWS && (dst != src || r >= Lx::GEMS)) row(dst, r) = v[j];
     }
     __builtin_amdgcn_wave_barrier();
 }
 
 // ------------------------------------------------------------------ legality mask
-// Board.valid_moves (SplendorLogicNumba.py:251-265). Wave-collective; returns the packed
-// 409-bit mask in w[0..6] (bit a%64 of word a/64), identical in every lane.
+// Board.valid_moves (SplendorLogicNumba.py:251-265). Wave-collective over an LDS board;
+// returns the packed 409-bit mask in w[0..6] (bit a%64 of word a/64), same in every lane.
 //
 // Phase 1 packs 120 per-board predicates into two ballots:
 //   F0: 0-11 _valid_buy (:476-501)  12-26 _valid_reserve(is_limit=False) (:508-515)
@@ -150,64 +233,62 @@ __device__ __forceinline__ void wave_roll_players(int8_t *dst, const int8_t *src
 // Phase 2 evaluates one action per lane from K_ACTION_DESC: flag0 & flag1 & condition,
 // the conditions restating the token-count branches of _valid_get_gems (:570-574) and
 // _valid_exchange (:615-680). Pass (408) is set iff nothing else is legal (:263).
+// Board-independent per-lane operands of the mask (action descriptors and the gem vector
+// each predicate lane compares against), loaded once per kernel instead of per board.
+struct MaskLane {
+    uint32_t desc[7];
+    uint64_t take, give;
+    __device__ __forceinline__ static MaskLane load() {
+        const int l = lane_id();
+        MaskLane m;
+#pragma unroll
+        for (int k = 0; k < 7; k++) m.desc[k] = 64 * k + l < 409 ? K_ACTION_DESC[64 * k + l] : (uint32_t)(C_NEVER << 16);
+        m.take = l >= 30 && l < 55 ? K_TAKE_ROW[l - 30] : 0;
+        m.give = l < 15 ? K_GIVE_ROW[l] : (l >= 20 && l < 60 ? K_SPEC3_ROW[l - 20] : 0);
+        return m;
+    }
+};
+
 template <int N>
-__device__ __forceinline__ void wave_valid_moves(const int8_t *s, int p, int lim, uint64_t w[7]) {
+__device__ __forceinline__ void wave_valid_moves(const int8_t *s, int p, int lim, uint64_t w[7], const MaskLane &ml) {
     using Lx = Lay<N>;
     const int l = lane_id();
-    const int8_t *bank = s;
-    const int8_t *gems = s + 7 * (Lx::GEMS + p);
-    const int8_t *cards = s + 7 * (Lx::CARDS + p);
-    const int8_t *rsv = s + 7 * (Lx::RSV + 6 * p);
-    const int T = sum7(gems), gold = gems[5], bgold = bank[5];
+    const uint64_t bank = row(s, Lx::BANK), gems = row(s, Lx::GEMS + p), cards = row(s, Lx::CARDS + p);
+    const int T = sum7(gems), gold = bt(gems, 5), bgold = bt(bank, 5);
     int nspec = 0;
 #pragma unroll
-    for (int c = 0; c < 5; c++) nspec += bank[c] != 0;
-    const bool slot_free = sum5(rsv + 35) == 0;   // third slot's gain row (:514)
+    for (int c = 0; c < 5; c++) nspec += bt(bank, c) != 0;
+    const bool slot_free = sum5(row(s, Lx::RSV + 6 * p + 5)) == 0;   // third slot's gain row (:514)
 
     bool f = false;
-    if (l < 12 || (l >= 27 && l < 30)) {          // affordability (cards or reserved)
-        const int8_t *cost = l < 12 ? s + 7 * (Lx::TIERS + 2 * l) : rsv + 14 * (l - 27);
-        int miss = 0, tot = 0;
+    if (l < 12 || (l >= 27 && l < 30)) {          // affordability (visible or reserved card)
+        const uint64_t cost = row(s, l < 12 ? Lx::TIERS + 2 * l : Lx::RSV + 6 * p + 2 * (l - 27));
+        int miss = 0;
 #pragma unroll
         for (int c = 0; c < 5; c++) {
-            int d = cost[c] - gems[c] - cards[c];
+            const int d = bt(cost, c) - bt(gems, c) - bt(cards, c);
             miss += d > 0 ? d : 0;
-            tot += cost[c];
         }
-        f = miss <= gold && tot != 0;
+        f = miss <= gold && sum5(cost) != 0;
     } else if (l < 27) {                          // reservable slot non-empty
-        int i = l - 12;
-        const int8_t *row = i < 12 ? s + 7 * (Lx::TIERS + 2 * i) : s + 7 * (Lx::DECKS + 2 * (i - 12));
-        f = sum5(row) != 0 && slot_free;
+        const int i = l - 12;
+        f = sum5(row(s, i < 12 ? Lx::TIERS + 2 * i : Lx::DECKS + 2 * (i - 12))) != 0 && slot_free;
     } else if (l < 55) {                          // bank can supply take vector
-        const int8_t *v = K_TAKE[l - 30];
-        bool ok = true;
-#pragma unroll
-        for (int c = 0; c < 5; c++) ok &= (bank[c] - v[c]) >= 0;
-        f = ok;
+        f = ge5(bank, ml.take);
     } else if (l < 60) {
-        f = bank[l - 55] >= 4;
+        f = bt(bank, l - 55) >= 4;
     }
     const uint64_t F0 = __ballot(f);
     f = false;
-    if (l >= 15 && l < 20) {                      // two identical gems
-        f = gems[l - 15] >= 2;
-    } else if (l < 60) {                          // player can give back vector
-        const int8_t *v = l < 15 ? K_GIVE[l] : K_SPEC3[l - 20];
-        bool ok = true;
-#pragma unroll
-        for (int c = 0; c < 5; c++) ok &= (gems[c] - v[c]) >= 0;
-        f = ok;
-    }
+    if (l >= 15 && l < 20) f = bt(gems, l - 15) >= 2;                 // two identical gems
+    else if (l < 60) f = ge5(gems, ml.give);
     const uint64_t F1 = __ballot(f);
 
-    // wave-uniform condition bits, indexed by condition code
     const bool ex_any = T > 7;
     const bool ex8 = ex_any && T == lim - 2;
     const bool ex9 = ex_any && !ex8 && T == lim - 1;
     const bool ex10 = ex_any && !ex8 && !ex9;
-    uint32_t cond = 0;
-    cond |= 1u << C_ALWAYS;
+    uint32_t cond = 1u << C_ALWAYS;
     cond |= (uint32_t)(!(T == lim && bgold > 0)) << C_RSV_LIMIT;
     cond |= (uint32_t)(T + 1 <= lim && (T == 9 || nspec == 1)) << C_TAKE1;
     cond |= (uint32_t)(T + 2 <= lim && (T == 8 || nspec == 2)) << C_TAKE2D;
@@ -221,8 +302,7 @@ __device__ __forceinline__ void wave_valid_moves(const int8_t *s, int p, int lim
     uint64_t any = 0;
 #pragma unroll
     for (int k = 0; k < 7; k++) {
-        const int a = 64 * k + l;
-        const uint32_t d = a < 409 ? K_ACTION_DESC[a] : (uint32_t)(C_NEVER << 16);
+        const uint32_t d = ml.desc[k];
         const bool f0 = !((d >> 6) & 1) || ((F0 >> (d & 63)) & 1);
         const bool f1 = !((d >> 14) & 1) || ((F1 >> ((d >> 8) & 63)) & 1);
         const bool c = (cond >> ((d >> 16) & 15)) & 1;
@@ -231,133 +311,151 @@ __device__ __forceinline__ void wave_valid_moves(const int8_t *s, int p, int lim
     }
     if (!any) w[6] |= 1ull << (408 - 384);
 }
+template <int N>
+__device__ __forceinline__ void wave_valid_moves(const int8_t *s, int p, int lim, uint64_t w[7]) {
+    wave_valid_moves<N>(s, p, lim, w, MaskLane::load());
+}
 
 // ------------------------------------------------------------------ transition
 // _get_deck_card (SplendorLogicNumba.py:400-420): colour ~ remaining count, then card ~
-// remaining bit; bitfield stored as int8 (packbits wrap, :44-46). Returns false if empty.
+// remaining bit, each by searchsorted(cumsum(p), U, 'right') (:39-41). The probabilities
+// come from K_QUOT / K_RECIP, which hold the correctly rounded quotients the reference
+// divides out (out-of-table counts — unreachable boards — divide). The bitfield is stored
+// as int8 (packbits wrap, :44-46). Returns false if the tier's deck is empty.
+// colour pick with true divisions, for counts outside K_QUOT (unreachable boards); kept out
+// of line so the common path carries no division code
+__device__ __noinline__ int pick_color_div(uint64_t cnt, int tot, double u) {
+    double c = 0.0;
+    for (int k = 0; k < 5; k++) {
+        c += (double)bt(cnt, k) / (double)tot;
+        if (c > u) return k;
+    }
+    return 4;
+}
+
 template <int N>
-__device__ __forceinline__ bool deck_card(int8_t *s, int tier, Chance &ch, int8_t out[14]) {
+__device__ __forceinline__ bool deck_card(int8_t *s, int tier, Chance &ch, uint64_t &cost, uint64_t &gain) {
     using Lx = Lay<N>;
-    int8_t *cnt = s + 7 * (Lx::DECKS + 2 * tier), *bits = cnt + 7;
+    const uint64_t cnt = row(s, Lx::DECKS + 2 * tier), bits = row(s, Lx::DECKS + 2 * tier + 1);
     const int tot = sum5(cnt);
     if (tot == 0) return false;
-    // searchsorted(cumsum(cnt / tot), u, 'right'), evaluated on the fly (no local arrays)
-    const double u0 = ch.draw();
-    int color = 4;
-    double c = 0.0;
+    bool dom = true;
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
-        c += (double)cnt[k] / (double)tot;
-        if (c > u0) { color = k; break; }
+    for (int k = 0; k < 5; k++) dom &= (unsigned)bt(cnt, k) <= 8u;
+    const double u0 = ch.draw();
+    int color = 4;                                  // cumsum stays below u: last colour
+    if (dom) {
+        const double *q = K_QUOT[tot];
+        double c = 0.0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            c += q[bt(cnt, k)];
+            if (c > u0) { color = k; break; }
+        }
+    } else {
+        color = pick_color_div(cnt, tot, u0);
     }
-    const uint32_t b = (uint8_t)bits[color];
-    const double nbits = (double)__builtin_popcount(b);
+    double c;
+    const uint32_t b = (uint8_t)bt(bits, color);
+    const int nb = __builtin_popcount(b);
+    const double inv = K_RECIP[nb];
     const double u1 = ch.draw();
     int idx = 7;
-    c = 0.0;
+    if (nb) {                                       // nb == 0: every term 0/0 = NaN -> idx 7
+        c = 0.0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-        c += (double)((b >> (7 - k)) & 1) / nbits;
-        if (c > u1) { idx = k; break; }
+        for (int k = 0; k < 8; k++) {
+            c += ((b >> (7 - k)) & 1) ? inv : 0.0;
+            if (c > u1) { idx = k; break; }
+        }
     }
-    bits[color] = (int8_t)(b & ~(1u << (7 - idx)));
-    cnt[color] = (int8_t)(cnt[color] - 1);
-    const int8_t *cd = K_CARDS[tier * 40 + color * 8 + idx];
-#pragma unroll
-    for (int c = 0; c < 14; c++) out[c] = 0;
-#pragma unroll
-    for (int c = 0; c < 5; c++) out[c] = cd[c];
-    out[7 + cd[5]] = 1;
-    out[13] = cd[6];
+    row(s, Lx::DECKS + 2 * tier + 1) = with_bt(bits, color, (int)(b & ~(1u << (7 - idx))));
+    row(s, Lx::DECKS + 2 * tier) = with_bt(cnt, color, bt(cnt, color) - 1);
+    cost = K_CARD_ROWS[tier * 40 + color * 8 + idx][0];
+    gain = K_CARD_ROWS[tier * 40 + color * 8 + idx][1];
     return true;
 }
 
 template <int N>
 __device__ __forceinline__ void fill_new_card(int8_t *s, int tier, int idx, bool det, Chance &ch) {
-    int8_t *slot = s + 7 * (Lay<N>::TIERS + 8 * tier + 2 * idx);
-    int8_t c[14];
-    const bool got = !det && deck_card<N>(s, tier, ch, c);
-#pragma unroll
-    for (int i = 0; i < 14; i++) slot[i] = got ? c[i] : 0;   // _fill_new_card (:445-450)
+    const int r = Lay<N>::TIERS + 8 * tier + 2 * idx;
+    uint64_t cost = 0, gain = 0;
+    if (!det) deck_card<N>(s, tier, ch, cost, gain);   // _fill_new_card (:445-450)
+    row(s, r) = cost;
+    row(s, r + 1) = gain;
 }
 
 // _give_nobles_if_earned (:763-768): every qualifying noble, stored at row nn*p+i
 template <int N>
 __device__ __forceinline__ void give_nobles(int8_t *s, int p) {
     using Lx = Lay<N>;
-    const int8_t *cards = s + 7 * (Lx::CARDS + p);
+    const uint64_t cards = row(s, Lx::CARDS + p);
     for (int i = 0; i < Lx::NN; i++) {
-        int8_t *nob = s + 7 * (Lx::NOBLES + i);
-        bool ok = sum5(nob) > 0;
-#pragma unroll
-        for (int c = 0; c < 5; c++) ok &= cards[c] >= nob[c];
-        if (ok) {
-            int8_t *dst = s + 7 * (Lx::PNOB + Lx::NN * p + i);
-#pragma unroll
-            for (int c = 0; c < 7; c++) { dst[c] = nob[c]; }
-#pragma unroll
-            for (int c = 0; c < 7; c++) nob[c] = 0;
+        const uint64_t nob = row(s, Lx::NOBLES + i);
+        if (sum5(nob) > 0 && ge5(cards, nob)) {
+            row(s, Lx::PNOB + Lx::NN * p + i) = nob;
+            row(s, Lx::NOBLES + i) = 0;
         }
     }
 }
 
-// _buy_card (:458-474)
+// _buy_card (:458-474): pay coloured gems, then gold for what is missing; take the gain
 template <int N>
 __device__ __forceinline__ void buy_card(int8_t *s, int cost_row, int p) {
     using Lx = Lay<N>;
-    int8_t *bank = s, *gems = s + 7 * (Lx::GEMS + p), *cards = s + 7 * (Lx::CARDS + p);
-    int8_t cost[5], gain[7];
-#pragma unroll
-    for (int c = 0; c < 5; c++) cost[c] = s[7 * cost_row + c];
-#pragma unroll
-    for (int c = 0; c < 7; c++) gain[c] = s[7 * cost_row + 7 + c];
+    const uint64_t cost = row(s, cost_row), gain = row(s, cost_row + 1);
+    uint64_t gems = row(s, Lx::GEMS + p), bank = row(s, Lx::BANK);
+    const uint64_t cards = row(s, Lx::CARDS + p);
     int miss = 0;
+    uint64_t paid = 0;
 #pragma unroll
     for (int c = 0; c < 5; c++) {
-        int d = cost[c] - gems[c] - cards[c];
+        const int cc = bt(cost, c), gc = bt(gems, c), kc = bt(cards, c);
+        const int d = cc - gc - kc;
         miss += d > 0 ? d : 0;
-    }
-#pragma unroll
-    for (int c = 0; c < 5; c++) {
-        int need = cost[c] - cards[c];
+        int need = cc - kc;
         need = need > 0 ? need : 0;
-        int paid = need < gems[c] ? need : gems[c];
-        gems[c] = (int8_t)(gems[c] - paid);
-        bank[c] = (int8_t)(bank[c] + paid);
+        paid |= (uint64_t)(uint8_t)(need < gc ? need : gc) << (8 * c);
     }
-    gems[5] = (int8_t)(gems[5] - miss);
-    bank[5] = (int8_t)(bank[5] + miss);
-#pragma unroll
-    for (int c = 0; c < 7; c++) cards[c] = (int8_t)(cards[c] + gain[c]);
+    gems = bytes_sub(gems, paid);
+    bank = bytes_add(bank, paid);
+    row(s, Lx::GEMS + p) = with_bt(gems, 5, bt(gems, 5) - miss);
+    row(s, Lx::BANK) = with_bt(bank, 5, bt(bank, 5) + miss);
+    row(s, Lx::CARDS + p) = bytes_add(cards, gain);
     give_nobles<N>(s, p);
 }
 
-// _reserve (:517-536)
+// _reserve (:517-536): first empty slot; reserving from the deck in the tree
+// (deterministic) reserves nothing; +1 gold if the bank has any
 template <int N>
 __device__ __forceinline__ void reserve(int8_t *s, int i, int p, bool det, Chance &ch) {
     using Lx = Lay<N>;
     int slot = -1;
     for (int k = 2; k >= 0; k--)
-        if (sum5(s + 7 * (Lx::RSV + 6 * p + 2 * k)) == 0) slot = Lx::RSV + 6 * p + 2 * k;
+        if (sum5(row(s, Lx::RSV + 6 * p + 2 * k)) == 0) slot = Lx::RSV + 6 * p + 2 * k;
     if (i < 12) {
-        const int tier = i >> 2, idx = i & 3;
-        const int8_t *src = s + 7 * (Lx::TIERS + 8 * tier + 2 * idx);
-        if (slot >= 0) {
-#pragma unroll
-            for (int c = 0; c < 14; c++) s[7 * slot + c] = src[c];
-        }
+        const int tier = i >> 2, idx = i & 3, r = Lx::TIERS + 8 * tier + 2 * idx;
+        if (slot >= 0) { row(s, slot) = row(s, r); row(s, slot + 1) = row(s, r + 1); }
         fill_new_card<N>(s, tier, idx, det, ch);
     } else if (!det) {
-        int8_t c14[14];
-        if (deck_card<N>(s, i - 12, ch, c14) && slot >= 0) {
-#pragma unroll
-            for (int c = 0; c < 14; c++) s[7 * slot + c] = c14[c];
-        }
+        uint64_t cost, gain;
+        if (deck_card<N>(s, i - 12, ch, cost, gain) && slot >= 0) { row(s, slot) = cost; row(s, slot + 1) = gain; }
     }
-    if (s[5] > 0) {
-        s[7 * (Lx::GEMS + p) + 5] += 1;
-        s[5] -= 1;
+    const uint64_t bank = row(s, Lx::BANK);
+    if (bt(bank, 5) > 0) {
+        const uint64_t gems = row(s, Lx::GEMS + p);
+        row(s, Lx::GEMS + p) = with_bt(gems, 5, bt(gems, 5) + 1);
+        row(s, Lx::BANK) = with_bt(bank, 5, bt(bank, 5) - 1);
     }
+}
+
+// take (_get_gems :585-593) or give back (_give_gems :685-694) a gem vector
+template <int N>
+__device__ __forceinline__ void move_gems(int8_t *s, int p, uint64_t v, bool take) {
+    using Lx = Lay<N>;
+    const uint64_t gems = row(s, Lx::GEMS + p), bank = row(s, Lx::BANK);
+    row(s, Lx::GEMS + p) = take ? bytes_add(gems, v) : bytes_sub(gems, v);
+    row(s, Lx::BANK) = take ? bytes_sub(bank, v) : bytes_add(bank, v);
 }
 
 // Board.make_move (:267-289); actions 405..408 are a no-op + round increment (the
@@ -366,48 +464,67 @@ __device__ __forceinline__ void reserve(int8_t *s, int i, int p, bool det, Chanc
 template <int N>
 __device__ __forceinline__ int make_move(int8_t *s, int a, int p, bool det, Chance &ch) {
     using Lx = Lay<N>;
-    int8_t *bank = s, *gems = s + 7 * (Lx::GEMS + p);
     if (a < 12) {
         buy_card<N>(s, Lx::TIERS + 2 * a, p);
         fill_new_card<N>(s, a >> 2, a & 3, det, ch);
     } else if (a < 27) {
         reserve<N>(s, a - 12, p, det, ch);
     } else if (a < 30) {                                   // _buy_reserve (:554-560)
-        const int i = a - 27, st = Lx::RSV + 6 * p + 2 * i;
+        const int st = Lx::RSV + 6 * p + 2 * (a - 27);
         buy_card<N>(s, st, p);
-        for (int r = st; r < Lx::RSV + 6 * p + 4; r++)
-#pragma unroll
-            for (int c = 0; c < 7; c++) s[7 * r + c] = s[7 * (r + 2) + c];
-#pragma unroll
-        for (int c = 0; c < 14; c++) s[7 * (Lx::RSV + 6 * p + 4) + c] = 0;
-    } else if (a < 60) {                                   // _get_gems (:585-593)
-        move_gems(bank, gems, K_TAKE[a - 30], +1);
+        for (int r = st; r < Lx::RSV + 6 * p + 4; r++) row(s, r) = row(s, r + 2);
+        row(s, Lx::RSV + 6 * p + 4) = 0;
+        row(s, Lx::RSV + 6 * p + 5) = 0;
+    } else if (a < 60) {
+        move_gems<N>(s, p, K_TAKE_ROW[a - 30], true);
     } else if (a < 405) {                                  // exchanges (:697-761)
         const uint8_t *e = K_EXCHANGE[a - 60];
         if (e[3] != 255) reserve<N>(s, e[3], p, det, ch);
-        if (e[0] != 255) move_gems(bank, gems, K_TAKE[e[0]], +1);
-        move_gems(bank, gems, K_GIVE[e[1]], -1);
-        if (e[2] != 255) move_gems(bank, gems, K_GIVE[e[2]], -1);
+        if (e[0] != 255) move_gems<N>(s, p, K_TAKE_ROW[e[0]], true);
+        move_gems<N>(s, p, K_GIVE_ROW[e[1]], false);
+        if (e[2] != 255) move_gems<N>(s, p, K_GIVE_ROW[e[2]], false);
     }
-    s[6] = (int8_t)(s[6] + 1);                             // round counter (:287)
+    const uint64_t bank = row(s, Lx::BANK);
+    row(s, Lx::BANK) = with_bt(bank, 6, bt(bank, 6) + 1);  // round counter, int8 (:287)
     return (p + 1) % N;
 }
 
 // ------------------------------------------------------------------ end of game
-// check_end_game + judge + get_score (:320-334, :306-318, :217-220)
-template <int N>
-__device__ __forceinline__ void check_end(const int8_t *s, float out[N]) {
+// Row views: an LDS board (8-byte rows) or an HBM board (7-byte rows, byte-assembled).
+struct LdsRows {
+    const int8_t *s;
+    __device__ __forceinline__ uint64_t operator()(int r) const { return row(s, r); }
+};
+struct HbmRows {
+    const int8_t *s;
+    __device__ __forceinline__ uint64_t operator()(int r) const {
+        uint64_t v = 0;
+#pragma unroll
+        for (int c = 0; c < 7; c++) v |= (uint64_t)(uint8_t)s[7 * r + c] << (8 * c);
+        return v;
+    }
+};
+
+template <int N, class V>
+__device__ __forceinline__ int score_rows(const V &rows, int p) {   // :217-220 (hard-coded 3)
+    using Lx = Lay<N>;
+    int v = bt(rows(Lx::CARDS + p), 6);
+    for (int i = 0; i < 3; i++) v += bt(rows(Lx::PNOB + 3 * p + i), 6);
+    return v;
+}
+
+// check_end_game + judge (:320-334, :306-318)
+template <int N, class V>
+__device__ __forceinline__ void check_end_rows(const V &rows, float out[N]) {
     using Lx = Lay<N>;
 #pragma unroll
     for (int i = 0; i < N; i++) out[i] = 0.f;
-    const int r = (uint8_t)s[6];
+    const int r = (uint8_t)bt(rows(Lx::BANK), 6);
     if (r % N != 0) return;
     int sc[N], mx = -1000;
 #pragma unroll
     for (int p = 0; p < N; p++) {
-        int v = s[7 * (Lx::CARDS + p) + 6];
-        for (int i = 0; i < 3; i++) v += s[7 * (Lx::PNOB + 3 * p + i) + 6];  // hard-coded 3
-        sc[p] = (int8_t)v;
+        sc[p] = (int8_t)score_rows<N>(rows, p);
         mx = sc[p] > mx ? sc[p] : mx;
     }
     if (!(mx >= 15 || r >= Lx::MAXMOVES)) return;
@@ -422,7 +539,7 @@ __device__ __forceinline__ void check_end(const int8_t *s, float out[N]) {
     int m[N], mn = 127;
 #pragma unroll
     for (int p = 0; p < N; p++) {
-        m[p] = (int8_t)sum5(s + 7 * (Lx::CARDS + p));
+        m[p] = (int8_t)sum5(rows(Lx::CARDS + p));
         if (sc[p] < mx) m[p] = -25;                          // int8(999) (:313)
         mn = m[p] < mn ? m[p] : mn;
     }
@@ -432,67 +549,68 @@ __device__ __forceinline__ void check_end(const int8_t *s, float out[N]) {
 #pragma unroll
     for (int p = 0; p < N; p++) out[p] = m[p] == mn ? (cnt > 1 ? 0.01f : 1.f) : -1.f;
 }
-
 template <int N>
-__device__ __forceinline__ int get_score(const int8_t *s, int p) {
-    using Lx = Lay<N>;
-    int v = s[7 * (Lx::CARDS + p) + 6];
-    for (int i = 0; i < 3; i++) v += s[7 * (Lx::PNOB + 3 * p + i) + 6];
-    return v;
-}
+__device__ __forceinline__ void check_end(const int8_t *lds, float out[N]) { check_end_rows<N>(LdsRows{lds}, out); }
+template <int N>
+__device__ __forceinline__ int get_score(const int8_t *lds, int p) { return score_rows<N>(LdsRows{lds}, p); }
 
 // ------------------------------------------------------------------ new game
-// Board.init_game (:222-246). Card draws use the chance source; the noble draw is a
-// partial Fisher-Yates on the same stream (the reference's np.random.choice is unseeded).
+// Board.init_game (:222-246) on a zeroed board. Card draws use the chance source; the
+// noble draw is a partial Fisher-Yates on the same stream (the reference's
+// np.random.choice is unseeded). The decks start full, so each of the 12 visible cards
+// takes exactly two draws: uniforms 8t..8t+7 deal tier t, 24..24+nn-1 pick the nobles.
+// The four parts touch disjoint rows and are dealt concurrently by lanes 0-3.
+constexpr int DEAL_DRAWS = 29;                    // 24 card draws + up to 5 nobles
+
 template <int N>
-__device__ __forceinline__ void init_fill(int8_t *s, Chance &ch) {   // s already zeroed
+__device__ __forceinline__ void deal_tier(int8_t *s, int t, const double *u) {
     using Lx = Lay<N>;
-    const int g = N == 2 ? 4 : (N == 3 ? 5 : 7);
-#pragma unroll
-    for (int c = 0; c < 5; c++) s[c] = (int8_t)g;
-    s[5] = 5;
-#pragma unroll
-    for (int t = 0; t < 3; t++) {
-        const int len = t == 0 ? 8 : (t == 1 ? 6 : 4);
-        const int8_t bits = (int8_t)(uint8_t)(0xFFu << (8 - len));
-#pragma unroll
-        for (int c = 0; c < 5; c++) {
-            s[7 * (Lx::DECKS + 2 * t) + c] = (int8_t)len;
-            s[7 * (Lx::DECKS + 2 * t + 1) + c] = bits;
-        }
-    }
-    for (int t = 0; t < 3; t++)
-        for (int i = 0; i < 4; i++) fill_new_card<N>(s, t, i, false, ch);
+    const uint64_t len = t == 0 ? 8 : (t == 1 ? 6 : 4);
+    const uint64_t bits = (uint8_t)(0xFFu << (8 - len));
+    row(s, Lx::DECKS + 2 * t) = len * 0x0000000101010101ull;
+    row(s, Lx::DECKS + 2 * t + 1) = bits * 0x0000000101010101ull;
+    Chance ch{u + 8 * t, 0, 0, 0, 0};
+    for (int i = 0; i < 4; i++) fill_new_card<N>(s, t, i, false, ch);
+}
+template <int N>
+__device__ __forceinline__ void deal_nobles_bank(int8_t *s, const double *u) {
+    using Lx = Lay<N>;
+    const uint64_t g = N == 2 ? 4 : (N == 3 ? 5 : 7);
+    row(s, Lx::BANK) = g * 0x0000000101010101ull | (5ull << 40);
     uint64_t perm = 0x9876543210ull;              // 10 nibbles: partial Fisher-Yates
     for (int i = 0; i < Lx::NN; i++) {
-        const int j = i + (int)floor(ch.draw() * (double)(10 - i));
+        const int j = i + (int)floor(u[24 + i] * (double)(10 - i));
         const uint64_t pi = (perm >> (4 * i)) & 15, pj = (perm >> (4 * j)) & 15;
         perm &= ~((15ull << (4 * i)) | (15ull << (4 * j)));
         perm |= (pj << (4 * i)) | (pi << (4 * j));
     }
-    for (int i = 0; i < Lx::NN; i++) {
-        int8_t *r = s + 7 * (Lx::NOBLES + i);
-        const int8_t *nb = K_NOBLES[(perm >> (4 * i)) & 15];
-#pragma unroll
-        for (int c = 0; c < 7; c++) r[c] = nb[c];
-    }
+    for (int i = 0; i < Lx::NN; i++) row(s, Lx::NOBLES + i) = K_NOBLE_ROWS[(perm >> (4 * i)) & 15];
 }
 
-// wave-collective new game
-template <int N>
-__device__ __forceinline__ void init_game(int8_t *s, Chance &ch) {
+// uniforms d0 .. d0+n-1 of a Philox sequence into dst (n <= 126), one block per lane
+__device__ __forceinline__ void wave_philox_uniforms(double *dst, uint64_t seed, uint32_t board,
+                                                     uint32_t stream, uint32_t d0, int n) {
     const int l = lane_id();
-    for (int i = l; i < Lay<N>::S; i += 64) s[i] = 0;
-    __builtin_amdgcn_wave_barrier();
-    init_fill<N>(s, ch);
+    const uint32_t blk = (d0 >> 1) + l;
+    if ((int)(2 * blk) < (int)(d0 + n)) {
+        double a, b;
+        philox_pair(seed, board, stream, blk, a, b);
+        const int i = (int)(2 * blk) - (int)d0;
+        if (i >= 0) dst[i] = a;
+        if (i + 1 < n) dst[i + 1] = b;
+    }
     __builtin_amdgcn_wave_barrier();
 }
 
-// single-lane new game (lane-per-board code paths)
+// wave-collective new game from DEAL_DRAWS uniforms u (LDS or HBM)
 template <int N>
-__device__ __forceinline__ void init_game_lane(int8_t *s, Chance &ch) {
-    for (int i = 0; i < Lay<N>::S; i++) s[i] = 0;
-    init_fill<N>(s, ch);
+__device__ __forceinline__ void wave_init_game(int8_t *s, const double *u) {
+    const int l = lane_id();
+    for (int r = l; r < Lay<N>::ROWS; r += 64) row(s, r) = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (l < 3) deal_tier<N>(s, l, u);
+    else if (l == 3) deal_nobles_bank<N>(s, u);
+    __builtin_amdgcn_wave_barrier();
 }
 
 // store a wave-uniform packed mask (7 words) from lane 0 (no per-lane word selection:

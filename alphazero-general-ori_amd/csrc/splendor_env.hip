@@ -2,8 +2,9 @@
 // declared in include/splendor_amd.h.
 //
 // Mapping: one 64-lane wave per board, 4 boards per 256-thread workgroup; each wave stages
-// its board in its own LDS slot (Lay<N>::SPAD bytes), so boards never share LDS and no
-// workgroup barrier is needed (waves exit independently). Device logic: splendor_device.h.
+// its board in its own LDS slot (Lay<N>::LS bytes, 8-byte rows), so boards never share LDS
+// and no workgroup barrier is needed (waves exit independently). The fused rollout kernel
+// instead owns 64 boards per workgroup (see k_rollout). Device logic: splendor_device.h.
 #include <hip/hip_runtime.h>
 
 #include <new>
@@ -23,11 +24,6 @@ namespace {
 constexpr int WAVES = 4;            // boards per workgroup
 constexpr int THREADS = 64 * WAVES;
 
-template <int N>
-__device__ __forceinline__ void store_board(int8_t *dst, const int8_t *lds) {
-    wave_copy_board<N>(dst, lds);
-}
-
 // ---------------------------------------------------------------- kernels
 template <int N>
 __global__ __launch_bounds__(THREADS) void k_init(int B, int8_t *__restrict__ state,
@@ -35,13 +31,15 @@ __global__ __launch_bounds__(THREADS) void k_init(int B, int8_t *__restrict__ st
                                                   const double *__restrict__ u, int ustride,
                                                   uint64_t seed, uint32_t stream, uint32_t bbase) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
+    __shared__ double ub[WAVES][DEAL_DRAWS];
     const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
     if (b >= B) return;
     int8_t *s = lds[w];
-    Chance ch{u ? u + (size_t)b * ustride : nullptr, seed, bbase + (uint32_t)b, stream, 0};
-    init_game<N>(s, ch);
-    store_board<N>(state + (size_t)b * Lx::S, s);
+    const double *du = u ? u + (size_t)b * ustride : ub[w];
+    if (!u) wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)b, stream, 0, DEAL_DRAWS);
+    wave_init_game<N>(s, du);
+    wave_store_board<N>(state + (size_t)b * Lx::S, s);
     if (player && lane_id() == 0) player[b] = 0;
 }
 
@@ -50,11 +48,11 @@ __global__ __launch_bounds__(THREADS) void k_valid(int B, const int8_t *__restri
                                                    const int8_t *__restrict__ player, int lim,
                                                    uint64_t *__restrict__ mask) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
     const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
     if (b >= B) return;
     int8_t *s = lds[w];
-    wave_copy_board<N>(s, state + (size_t)b * Lx::S);
+    wave_load_board<N>(s, state + (size_t)b * Lx::S);
     const int p = player ? player[b] : 0;
     uint64_t m[7];
     wave_valid_moves<N>(s, p, lim, m);
@@ -70,7 +68,7 @@ __global__ __launch_bounds__(THREADS) void k_step(int B, int8_t *__restrict__ st
                                                   uint64_t seed, uint32_t stream, uint32_t bbase,
                                                   int32_t *err) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
     const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
     if (b >= B) return;
     const int a = action[b];
@@ -82,11 +80,11 @@ __global__ __launch_bounds__(THREADS) void k_step(int B, int8_t *__restrict__ st
     }
     int8_t *s = lds[w];
     int8_t *g = state + (size_t)b * Lx::S;
-    wave_copy_board<N>(s, g);
+    wave_load_board<N>(s, g);
     Chance ch{u ? u + (size_t)b * ustride : nullptr, seed, bbase + (uint32_t)b, stream, 0};
     const int nxt = make_move<N>(s, a, p, det != 0, ch);
     __builtin_amdgcn_wave_barrier();
-    store_board<N>(g, s);
+    wave_store_board<N>(g, s);
     if (next_player && lane_id() == 0) next_player[b] = (int8_t)nxt;
 }
 
@@ -97,7 +95,7 @@ __global__ __launch_bounds__(256) void k_ended(int B, const int8_t *__restrict__
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= B) return;
     float e[N];
-    check_end<N>(state + (size_t)b * Lay<N>::S, e);
+    check_end_rows<N>(HbmRows{state + (size_t)b * Lay<N>::S}, e);
 #pragma unroll
     for (int i = 0; i < N; i++) out[(size_t)b * N + i] = e[i];
 }
@@ -111,7 +109,7 @@ __global__ __launch_bounds__(256) void k_score_round(int B, const int8_t *__rest
     const int8_t *s = state + (size_t)b * Lay<N>::S;
     if (score)
 #pragma unroll
-        for (int p = 0; p < N; p++) score[(size_t)b * N + p] = get_score<N>(s, p);
+        for (int p = 0; p < N; p++) score[(size_t)b * N + p] = score_rows<N>(HbmRows{s}, p);
     if (round) round[b] = (uint8_t)s[6];
 }
 
@@ -120,14 +118,14 @@ __global__ __launch_bounds__(THREADS) void k_canonical(int B, const int8_t *__re
                                                        const int8_t *__restrict__ player,
                                                        int8_t *out) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
     const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
     if (b >= B) return;
     int8_t *s = lds[w];
-    wave_copy_board<N>(s, state + (size_t)b * Lx::S);
+    wave_load_board<N>(s, state + (size_t)b * Lx::S);
     const int p = player ? player[b] : 0;
     if (p) wave_roll_players<N>(s, s, p);
-    store_board<N>(out + (size_t)b * Lx::S, s);
+    wave_store_board<N>(out + (size_t)b * Lx::S, s);
 }
 
 template <int N>
@@ -135,11 +133,11 @@ __global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__re
                                                        const int16_t *__restrict__ action,
                                                        int8_t *__restrict__ child, int32_t *err) {
     using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
     const int w = threadIdx.x >> 6, b = blockIdx.x * WAVES + w;
     if (b >= B) return;
     int8_t *s = lds[w];
-    wave_copy_board<N>(s, parent + (size_t)b * Lx::S);
+    wave_load_board<N>(s, parent + (size_t)b * Lx::S);
     const int a = action[b];
     if (a < 0 || a >= SPL_ACTIONS) {
         if (err && lane_id() == 0) atomicOr(err, SPL_ERR_BAD_ACTION);
@@ -149,26 +147,26 @@ __global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__re
         __builtin_amdgcn_wave_barrier();
         if (nxt) wave_roll_players<N>(s, s, nxt);
     }
-    store_board<N>(child + (size_t)b * Lx::S, s);
+    wave_store_board<N>(child + (size_t)b * Lx::S, s);
 }
 
 // Fused random-policy self-play step (see splendor_amd.h spl_rollout_step).
-// A 256-thread workgroup owns RB = 64 consecutive boards, staged in LDS at an odd-dword
-// stride (conflict-free lane-per-board access):
-//   phase 1  all threads: coalesced dword load of the 64 boards (+ players)
+// A 256-thread workgroup owns RB = 64 consecutive boards, staged in LDS as 8-byte rows at
+// an odd-qword stride (conflict-free ds_read_b64 / ds_write_b64 in lane-per-board code):
+//   phase 1  all threads: HBM -> LDS, one 4-row quad per thread (7 dwords -> 4 qwords)
 //   phase 2  wave w, boards 16w..16w+15, one board at a time: 409-action mask (ballots) on
 //            the real board for the player to move (== the canonical form's mask: it only
 //            reads player p's rows), mask store, uniform action draw
 //   phase 3  lane b of wave 0 = board b: make_move with chance, end check, auto-reset —
 //            the serial rule logic runs 64 boards per wave instead of one
-//   phase 4  all threads: coalesced store
+//   phase 4  all threads: LDS -> HBM
 constexpr int RB = 64;
 #ifndef ROLLOUT_ABLATE
 #define ROLLOUT_ABLATE 0   // diagnostic builds only (tools/ablate_rollout.hip): 1 = skip mask, 2 = skip step
 #endif
 template <int N>
 struct RolloutLds {
-    static constexpr int STRIDE = ((Lay<N>::S + 3) / 4) % 2 ? (Lay<N>::S + 3) / 4 * 4 : (Lay<N>::S + 3) / 4 * 4 + 4;
+    static constexpr int STRIDE = (Lay<N>::ROWS % 2 ? Lay<N>::ROWS : Lay<N>::ROWS + 1) * 8;
 };
 
 template <int N>
@@ -180,85 +178,88 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int8_t *__restrict__
                                                      int32_t *__restrict__ games_done,
                                                      uint64_t seed, uint32_t step, uint32_t bbase) {
     using Lx = Lay<N>;
+    using Cv = Conv<N>;
     constexpr int ST = RolloutLds<N>::STRIDE;
     __shared__ __align__(16) int8_t lds[RB * ST];
     __shared__ int16_t act[RB];
     __shared__ int8_t pl[RB];
+    __shared__ double u0s[RB], u1s[RB]; // action draw block: u0 picks the action, u1 = draw 1
+    __shared__ double ub[WAVES][DEAL_DRAWS];
+    __shared__ uint64_t reset_mask;
     const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
+    int8_t *const gst = state + (size_t)b0 * Lx::S;
     // phase 1
-    if constexpr (Lx::S % 4 == 0) {
-        const int32_t *g = reinterpret_cast<const int32_t *>(state + (size_t)b0 * Lx::S);
-        constexpr int W = Lx::S / 4;
-        for (int i = tid; i < nb * W; i += THREADS) {
-            const int b = i / W, k = i - b * W;
-            *reinterpret_cast<int32_t *>(lds + b * ST + 4 * k) = g[i];
-        }
-    } else {
-        const int8_t *g = state + (size_t)b0 * Lx::S;
-        for (int i = tid; i < nb * Lx::S; i += THREADS) {
-            const int b = i / Lx::S, k = i - b * Lx::S;
-            lds[b * ST + k] = g[i];
-        }
+    for (int i = tid; i < nb * Cv::UNITS; i += THREADS) {
+        const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
+        Cv::load(lds + b * ST, gst + (size_t)b * Lx::S, u);
     }
-    if (tid < nb) pl[tid] = player[b0 + tid];
+    if (tid < nb) {
+        pl[tid] = player[b0 + tid];
+        philox_pair(seed, bbase + (uint32_t)(b0 + tid), step, 0, u0s[tid], u1s[tid]);
+    }
     __syncthreads();
     // phase 2
-    for (int j = 0; j < RB / WAVES && ROLLOUT_ABLATE != 1; j++) {
-        const int b = w * (RB / WAVES) + j;
-        if (b >= nb) break;
-        const int8_t *s = lds + b * ST;
-        uint64_t m[7];
-        wave_valid_moves<N>(s, pl[b], lim, m);
-        store_mask(mask_out + (size_t)(b0 + b) * 7, m);
-        int cnt = 0;
+    if (ROLLOUT_ABLATE != 1) {
+        const MaskLane ml = MaskLane::load();
+        for (int j = 0; j < RB / WAVES; j++) {
+            const int b = w * (RB / WAVES) + j;
+            if (b >= nb) break;
+            const int8_t *s = lds + b * ST;
+            uint64_t m[7];
+            wave_valid_moves<N>(s, pl[b], lim, m, ml);
+            store_mask(mask_out + (size_t)(b0 + b) * 7, m);
+            int cnt = 0;
 #pragma unroll
-        for (int k = 0; k < 7; k++) cnt += __popcll(m[k]);
-        const int kk = (int)(philox_u01(seed, bbase + (uint32_t)(b0 + b), step, 0) * (double)cnt);
-        const int a = select_bit(m, kk);
-        if (l == 0) act[b] = (int16_t)a;
+            for (int k = 0; k < 7; k++) cnt += __popcll(m[k]);
+            const int a = select_bit(m, (int)(u0s[b] * (double)cnt));
+            if (l == 0) act[b] = (int16_t)a;
+        }
     }
     __syncthreads();
     if (ROLLOUT_ABLATE == 1 && tid < nb) act[tid] = 30 + (int)((step + tid) % 5);
     // phase 3
-    if (w == 0 && l < nb && ROLLOUT_ABLATE != 2) {
-        const int b = l, gb = b0 + b;
-        int8_t *s = lds + b * ST;
-        const int a = act[b];
-        Chance ch{nullptr, seed, bbase + (uint32_t)gb, step, 1};
-        int nxt = make_move<N>(s, a, pl[b], false, ch);
-        float e[N];
-        check_end<N>(s, e);
+    if (w == 0 && ROLLOUT_ABLATE != 2) {
         bool ended = false;
+        if (l < nb) {
+            const int b = l, gb = b0 + b;
+            int8_t *s = lds + b * ST;
+            const int a = act[b];
+            Chance ch{nullptr, seed, bbase + (uint32_t)gb, step, 1, u1s[b], true};
+            int nxt = make_move<N>(s, a, pl[b], false, ch);
+            float e[N];
+            check_end<N>(s, e);
 #pragma unroll
-        for (int i = 0; i < N; i++) {
-            ended |= e[i] != 0.f;
-            ended_out[(size_t)gb * N + i] = e[i];
+            for (int i = 0; i < N; i++) {
+                ended |= e[i] != 0.f;
+                ended_out[(size_t)gb * N + i] = e[i];
+            }
+            action_out[gb] = (int16_t)a;
+            if (ended) {
+                nxt = 0;
+                if (games_done) games_done[gb] += 1;
+            }
+            player[gb] = (int8_t)nxt;
         }
-        action_out[gb] = (int16_t)a;
-        if (ended) {
-            Chance ch2{nullptr, seed, bbase + (uint32_t)gb, step, 3};
-            init_game_lane<N>(s, ch2);
-            nxt = 0;
-            if (games_done) games_done[gb] += 1;
+        const uint64_t rm = __ballot(ended);
+        if (l == 0) reset_mask = rm;
+    }
+    __syncthreads();
+    // phase 3b: finished boards are re-dealt (draws 3..), one board per wave at a time
+    if (ROLLOUT_ABLATE != 2) {
+        uint64_t rm = reset_mask;
+        for (int i = 0; rm; i++, rm &= rm - 1) {
+            if ((i & (WAVES - 1)) != w) continue;
+            const int b = __ffsll((unsigned long long)rm) - 1;
+            wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)(b0 + b), step, 3, DEAL_DRAWS);
+            wave_init_game<N>(lds + b * ST, ub[w]);
         }
-        player[gb] = (int8_t)nxt;
     }
     __syncthreads();
     // phase 4
-    if constexpr (Lx::S % 4 == 0) {
-        int32_t *g = reinterpret_cast<int32_t *>(state + (size_t)b0 * Lx::S);
-        constexpr int W = Lx::S / 4;
-        for (int i = tid; i < nb * W; i += THREADS) {
-            const int b = i / W, k = i - b * W;
-            g[i] = *reinterpret_cast<const int32_t *>(lds + b * ST + 4 * k);
-        }
-    } else {
-        int8_t *g = state + (size_t)b0 * Lx::S;
-        for (int i = tid; i < nb * Lx::S; i += THREADS) {
-            const int b = i / Lx::S, k = i - b * Lx::S;
-            g[i] = lds[b * ST + k];
-        }
+    for (int i = tid; i < nb * Cv::UNITS; i += THREADS) {
+        const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
+        Cv::store(gst + (size_t)b * Lx::S, lds + b * ST, u);
     }
 }
 
@@ -281,18 +282,18 @@ __global__ __launch_bounds__(THREADS) void k_symmetries(int E, const int8_t *__r
                                                         uint8_t *__restrict__ present) {
     using Lx = Lay<N>;
     constexpr int K = 10 + 2 * N;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::SPAD];
+    __shared__ __align__(16) int8_t lds[WAVES][(Lx::S + 15) & ~15];   // raw 7-byte rows
     const int w = threadIdx.x >> 6, e = blockIdx.x * WAVES + w;
     if (e >= E) return;
     const int l = lane_id();
     int8_t *s = lds[w];
-    wave_copy_board<N>(s, state + (size_t)e * Lx::S);
+    wave_copy_bytes(s, state + (size_t)e * Lx::S, Lx::S);
     int nres[N];
 #pragma unroll
     for (int p = 0; p < N; p++) {        // _nb_of_reserved_cards (:770-774)
         nres[p] = 3;
         for (int c = 2; c >= 0; c--)
-            if (sum5(s + 7 * (Lx::RSV + 6 * p + 2 * c)) == 0) nres[p] = c;
+            if (sum5(HbmRows{s}(Lx::RSV + 6 * p + 2 * c)) == 0) nres[p] = c;
     }
     for (int k = 0; k < K; k++) {
         int tier = -1, p = -1;

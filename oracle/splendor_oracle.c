@@ -488,10 +488,13 @@ void or_philox4x32(uint32_t k0, uint32_t k1, const uint32_t in[4], uint32_t out[
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+/* uniform d of a (seed, board, stream) sequence: half of counter block d/2 (words 0,1 for
+ * even d, 2,3 for odd d), 53 bits */
 double or_uniform(uint64_t seed, uint32_t board, uint32_t stream, uint32_t d) {
-    uint32_t ctr[4] = {d, board, stream, 0x53504C44u /* 'SPLD' */}, o[4];
+    uint32_t ctr[4] = {d >> 1, board, stream, 0x53504C44u /* 'SPLD' */}, o[4];
     or_philox4x32((uint32_t)seed, (uint32_t)(seed >> 32), ctr, o);
-    return ((double)(o[0] >> 5) * 67108864.0 + (double)(o[1] >> 6)) * (1.0 / 9007199254740992.0);
+    const uint32_t *w = o + 2 * (d & 1);
+    return ((double)(w[0] >> 5) * 67108864.0 + (double)(w[1] >> 6)) * (1.0 / 9007199254740992.0);
 }
 
 /* ------------------------------------------------------------------ fake NN */

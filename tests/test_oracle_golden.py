@@ -147,6 +147,11 @@ def test_philox_known_answer():
     assert list(out) == [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
     us = [O.uniform(123, b, s, k) for b in range(4) for s in range(4) for k in range(4)]
     assert all(0.0 <= u < 1.0 for u in us) and len(set(us)) == len(us)
+    # uniform d = half d&1 of counter block d>>1 (53 bits from two words)
+    for d in range(6):
+        L.or_philox4x32(7, 0, (C.c_uint32 * 4)(d >> 1, 3, 5, 0x53504C44), out)
+        w = list(out)[2 * (d & 1):2 * (d & 1) + 2]
+        assert O.uniform(7, 3, 5, d) == ((w[0] >> 5) * 67108864.0 + (w[1] >> 6)) / 9007199254740992.0
 
 
 def test_symmetries_shapes():
