@@ -196,6 +196,19 @@ def main():
     out.append(arr("static __constant__ double K_QUOT[41][9]", None, quot, lambda x: float(x).hex()))
     out.append(arr("static __constant__ double K_RECIP[9]", None, [0.0] + [1.0 / n for n in range(1, 9)],
                    lambda x: float(x).hex()))
+    # ---- compile-time forms for the lane-per-board mask (splendor_device.h lane_predicates)
+    # threshold masks: bit 5t+c <-> value_c >= t (t = 0..4); a predicate "x >= v in every
+    # colour" holds iff REQ(v) & ~THRESH(x) == 0
+    def req(v):
+        assert max(v) <= 4
+        return sum(1 << (5 * t + c) for c in range(5) for t in range(v[c] + 1))
+    req0 = [0] * 30 + [req(TAKE[i]) for i in range(25)] + [1 << (20 + c) for c in range(5)]
+    req1 = [req(GIVE[i]) for i in range(15)] + [1 << (10 + c) for c in range(5)] + [req(v) for v in SPEC3]
+    out.append("// compile-time copies for fully unrolled lane-per-board evaluation")
+    out.append(arr("static constexpr uint32_t KC_ACTION_DESC[409]", None, action_table(), lambda x: f"0x{x:06x}u"))
+    out.append("// F0 bits 30..59 / F1 bits 0..59: required threshold bits (bit 5t+c: colour c >= t)")
+    out.append(arr("static constexpr uint32_t KC_REQ0[60]", None, req0, lambda x: f"0x{x:07x}u"))
+    out.append(arr("static constexpr uint32_t KC_REQ1[60]", None, req1, lambda x: f"0x{x:07x}u"))
     print("\n".join(out))
 
 

@@ -92,13 +92,16 @@ __device__ __forceinline__ double philox_u01(uint64_t seed, uint32_t board, uint
 }
 
 // Either an explicit stream of doubles (parity with recorded reference draws) or Philox.
-// Sequential draws reuse the second half of a Philox block.
+// Sequential draws reuse the second half of a Philox block. The deck-draw tables travel
+// with the chance source so a kernel can serve them from LDS.
 struct Chance {
     const double *u;   // explicit uniforms for this board, or nullptr -> Philox
     uint64_t seed;
     uint32_t board, stream, next;
     double spare = 0.0;
     bool have_spare = false;
+    const double (*quot)[9] = K_QUOT;
+    const uint64_t (*cards)[2] = K_CARD_ROWS;
     __device__ __forceinline__ double draw() {
         if (u) return u[next++];
         double r;
@@ -316,6 +319,119 @@ __device__ __forceinline__ void wave_valid_moves(const int8_t *s, int p, int lim
     wave_valid_moves<N>(s, p, lim, w, MaskLane::load());
 }
 
+// Lane-per-board form of the same mask: one lane evaluates every predicate and action of
+// its own board with compile-time bit positions (KC_* tables), ~20x fewer instructions
+// per board than the wave form; used where 64 boards share a wave.
+struct LanePred {
+    uint64_t F0, F1;   // the two predicate sets of wave_valid_moves
+    uint32_t C;        // condition bits, indexed by condition code
+};
+
+// threshold mask of the 5 colours of a row: bit 5t+c <-> byte c >= t (t = 0..4)
+__device__ __forceinline__ uint32_t thresh5(uint64_t w) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        const int v = bt(w, c);
+#pragma unroll
+        for (int t = 0; t < 5; t++) m |= (uint32_t)(v >= t) << (5 * t + c);
+    }
+    return m;
+}
+
+template <int N>
+__device__ __forceinline__ LanePred lane_predicates(const int8_t *s, int p, int lim) {
+    using Lx = Lay<N>;
+    const uint64_t bank = row(s, Lx::BANK), gems = row(s, Lx::GEMS + p), cards = row(s, Lx::CARDS + p);
+    const int T = sum7(gems), gold = bt(gems, 5), bgold = bt(bank, 5);
+    int nspec = 0, have[5];
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        nspec += bt(bank, c) != 0;
+        have[c] = bt(gems, c) + bt(cards, c);
+    }
+    const bool slot_free = sum5(row(s, Lx::RSV + 6 * p + 5)) == 0;
+    LanePred P{0, 0, 0};
+    // F0 0-11 buy a visible card, 12-23 reserve it (:476-515)
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+        const uint64_t cost = row(s, Lx::TIERS + 2 * i);
+        int miss = 0;
+#pragma unroll
+        for (int c = 0; c < 5; c++) {
+            const int d = bt(cost, c) - have[c];
+            miss += d > 0 ? d : 0;
+        }
+        const bool any = sum5(cost) != 0;
+        P.F0 |= (uint64_t)(miss <= gold && any) << i;
+        P.F0 |= (uint64_t)(any && slot_free) << (12 + i);
+    }
+    // F0 24-26 reserve from a deck, 27-29 buy a reserved card (:508-552)
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+        P.F0 |= (uint64_t)(sum5(row(s, Lx::DECKS + 2 * t)) != 0 && slot_free) << (24 + t);
+        const uint64_t cost = row(s, Lx::RSV + 6 * p + 2 * t);
+        int miss = 0;
+#pragma unroll
+        for (int c = 0; c < 5; c++) {
+            const int d = bt(cost, c) - have[c];
+            miss += d > 0 ? d : 0;
+        }
+        P.F0 |= (uint64_t)(miss <= gold && sum5(cost) != 0) << (27 + t);
+    }
+    // F0 30-59 bank supplies, F1 0-59 player can give (threshold masks, KC_REQ*)
+    const uint32_t nb = ~thresh5(bank), ng = ~thresh5(gems);
+#pragma unroll
+    for (int i = 30; i < 60; i++) P.F0 |= (uint64_t)((KC_REQ0[i] & nb) == 0) << i;
+#pragma unroll
+    for (int i = 0; i < 60; i++) P.F1 |= (uint64_t)((KC_REQ1[i] & ng) == 0) << i;
+    // condition bits (same as wave_valid_moves)
+    const bool ex_any = T > 7;
+    const bool ex8 = ex_any && T == lim - 2;
+    const bool ex9 = ex_any && !ex8 && T == lim - 1;
+    const bool ex10 = ex_any && !ex8 && !ex9;
+    uint32_t C = 1u << C_ALWAYS;
+    C |= (uint32_t)(!(T == lim && bgold > 0)) << C_RSV_LIMIT;
+    C |= (uint32_t)(T + 1 <= lim && (T == 9 || nspec == 1)) << C_TAKE1;
+    C |= (uint32_t)(T + 2 <= lim && (T == 8 || nspec == 2)) << C_TAKE2D;
+    C |= (uint32_t)(T + 3 <= lim) << C_TAKE3;
+    C |= (uint32_t)(T + 2 <= lim) << C_TAKE2S;
+    C |= (uint32_t)ex8 << C_EX8;
+    C |= (uint32_t)ex9 << C_EX9;
+    C |= (uint32_t)ex10 << C_EX10;
+    C |= (uint32_t)(ex10 && bgold > 0) << C_EX10G;
+    P.C = C;
+    return P;
+}
+
+// mask word K (actions 64K .. 64K+63) from the predicates; the pass bit is not included
+template <int K>
+__device__ __forceinline__ uint64_t lane_mask_word(const LanePred &P) {
+    uint64_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        const int a = 64 * K + j;
+        if (a >= 405) break;                       // 405-408: never set here
+        const uint32_t d = KC_ACTION_DESC[a];
+        uint64_t bit = (uint64_t)(P.C >> ((d >> 16) & 15));
+        if ((d >> 6) & 1) bit &= P.F0 >> (d & 63);
+        if ((d >> 14) & 1) bit &= P.F1 >> ((d >> 8) & 63);
+        w |= (bit & 1) << j;
+    }
+    return w;
+}
+
+// k-th set bit (k < popcount) of a lane-private 64-bit word, by halving
+__device__ __forceinline__ int kth_bit64(uint64_t x, int k) {
+    int pos = 0;
+#pragma unroll
+    for (int h = 32; h >= 1; h >>= 1) {
+        const int c = __popcll(x & ((1ull << h) - 1));
+        if (k >= c) { k -= c; x >>= h; pos += h; }
+    }
+    return pos;
+}
+
 // ------------------------------------------------------------------ transition
 // _get_deck_card (SplendorLogicNumba.py:400-420): colour ~ remaining count, then card ~
 // remaining bit, each by searchsorted(cumsum(p), U, 'right') (:39-41). The probabilities
@@ -345,7 +461,7 @@ __device__ __forceinline__ bool deck_card(int8_t *s, int tier, Chance &ch, uint6
     const double u0 = ch.draw();
     int color = 4;                                  // cumsum stays below u: last colour
     if (dom) {
-        const double *q = K_QUOT[tot];
+        const double *q = ch.quot[tot];
         double c = 0.0;
 #pragma unroll
         for (int k = 0; k < 5; k++) {
@@ -371,8 +487,8 @@ __device__ __forceinline__ bool deck_card(int8_t *s, int tier, Chance &ch, uint6
     }
     row(s, Lx::DECKS + 2 * tier + 1) = with_bt(bits, color, (int)(b & ~(1u << (7 - idx))));
     row(s, Lx::DECKS + 2 * tier) = with_bt(cnt, color, bt(cnt, color) - 1);
-    cost = K_CARD_ROWS[tier * 40 + color * 8 + idx][0];
-    gain = K_CARD_ROWS[tier * 40 + color * 8 + idx][1];
+    cost = ch.cards[tier * 40 + color * 8 + idx][0];
+    gain = ch.cards[tier * 40 + color * 8 + idx][1];
     return true;
 }
 
@@ -630,9 +746,7 @@ __device__ __forceinline__ int select_bit(const uint64_t w[7], int k) {
     for (int j = 0; j < 7; j++) {
         const int c = __popcll(w[j]);
         if (!done && k < c) {
-            uint64_t x = w[j];
-            for (int t = 0; t < k; t++) x &= x - 1;
-            res = 64 * j + __ffsll((unsigned long long)x) - 1;
+            res = 64 * j + kth_bit64(w[j], k);
             done = true;
         }
         if (!done) k -= c;

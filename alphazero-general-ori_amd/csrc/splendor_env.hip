@@ -153,16 +153,29 @@ __global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__re
 // Fused random-policy self-play step (see splendor_amd.h spl_rollout_step).
 // A 256-thread workgroup owns RB = 64 consecutive boards, staged in LDS as 8-byte rows at
 // an odd-qword stride (conflict-free ds_read_b64 / ds_write_b64 in lane-per-board code):
-//   phase 1  all threads: HBM -> LDS, one 4-row quad per thread (7 dwords -> 4 qwords)
-//   phase 2  wave w, boards 16w..16w+15, one board at a time: 409-action mask (ballots) on
-//            the real board for the player to move (== the canonical form's mask: it only
-//            reads player p's rows), mask store, uniform action draw
-//   phase 3  lane b of wave 0 = board b: make_move with chance, end check, auto-reset —
-//            the serial rule logic runs 64 boards per wave instead of one
-//   phase 4  all threads: LDS -> HBM
+//   phase 1  all threads: HBM -> LDS, one 4-row quad per thread (7 dwords -> 4 qwords);
+//            Philox blocks 0-1 of every board's step stream (draw 0 picks the action,
+//            1-2 feed a deck draw), deck-draw tables into LDS
+//   phase 2  lane per board: predicates + mask words w, w+4 of the 409-action mask in wave
+//            w, on the real board for the player to move (== the canonical form's mask: it
+//            only reads player p's rows)
+//   phase 3  lane l < 16 of wave w = board 16w + l: pass bit, uniform action draw,
+//            make_move with chance, end check — the serial rule logic runs 16 boards per wave
+//   phase 3b finished games are re-dealt wave-parallel (draws 3.., Philox per lane)
+//   phase 4  all threads: boards and masks LDS -> HBM
 constexpr int RB = 64;
 #ifndef ROLLOUT_ABLATE
 #define ROLLOUT_ABLATE 0   // diagnostic builds only (tools/ablate_rollout.hip): 1 = skip mask, 2 = skip step
+#endif
+#ifndef ROLLOUT_TIMING
+#define ROLLOUT_TIMING 0   // diagnostic builds only: per-block phase timestamps into g_rollout_timing
+#endif
+#if ROLLOUT_TIMING
+__device__ uint64_t *g_rollout_timing;
+#define RT_MARK(k)                                                                          \
+    if (threadIdx.x == 0) g_rollout_timing[(size_t)blockIdx.x * 8 + (k)] = (k) == 0 || (k) == 6 ? wall_clock64() : clock64();
+#else
+#define RT_MARK(k)
 #endif
 template <int N>
 struct RolloutLds {
@@ -181,51 +194,62 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int8_t *__restrict__
     using Cv = Conv<N>;
     constexpr int ST = RolloutLds<N>::STRIDE;
     __shared__ __align__(16) int8_t lds[RB * ST];
-    __shared__ int16_t act[RB];
+    __shared__ uint64_t msk[RB][7];    // legality masks (odd qword stride: conflict-free)
     __shared__ int8_t pl[RB];
-    __shared__ double u0s[RB], u1s[RB]; // action draw block: u0 picks the action, u1 = draw 1
+    __shared__ double ud[RB][4];       // draws 0..3 of each board's step stream
     __shared__ double ub[WAVES][DEAL_DRAWS];
-    __shared__ uint64_t reset_mask;
+    __shared__ double quot[41][9];
+    __shared__ uint64_t cards[120][2];
+    __shared__ uint16_t reset16[WAVES];
     const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
     int8_t *const gst = state + (size_t)b0 * Lx::S;
-    // phase 1
+    RT_MARK(0) RT_MARK(1)
+    // phase 1: boards, players, the step's first two Philox blocks, deck tables
     for (int i = tid; i < nb * Cv::UNITS; i += THREADS) {
         const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
         Cv::load(lds + b * ST, gst + (size_t)b * Lx::S, u);
     }
-    if (tid < nb) {
-        pl[tid] = player[b0 + tid];
-        philox_pair(seed, bbase + (uint32_t)(b0 + tid), step, 0, u0s[tid], u1s[tid]);
+    if (tid < 2 * RB && (tid & (RB - 1)) < nb) {
+        const int b = tid & (RB - 1), k = tid / RB;
+        philox_pair(seed, bbase + (uint32_t)(b0 + b), step, k, ud[b][2 * k], ud[b][2 * k + 1]);
+    }
+    if (tid < nb) pl[tid] = player[b0 + tid];
+    for (int i = tid; i < 41 * 9; i += THREADS) (&quot[0][0])[i] = (&K_QUOT[0][0])[i];
+    for (int i = tid; i < 240; i += THREADS) (&cards[0][0])[i] = (&K_CARD_ROWS[0][0])[i];
+    __syncthreads();
+    RT_MARK(2)
+    // phase 2: masks, lane per board; wave w evaluates words w and w+4 of all 64 boards
+    if (ROLLOUT_ABLATE != 1 && l < nb) {
+        const LanePred P = lane_predicates<N>(lds + l * ST, pl[l], lim);
+        if (w == 0) { msk[l][0] = lane_mask_word<0>(P); msk[l][4] = lane_mask_word<4>(P); }
+        else if (w == 1) { msk[l][1] = lane_mask_word<1>(P); msk[l][5] = lane_mask_word<5>(P); }
+        else if (w == 2) { msk[l][2] = lane_mask_word<2>(P); msk[l][6] = lane_mask_word<6>(P); }
+        else { msk[l][3] = lane_mask_word<3>(P); }
     }
     __syncthreads();
-    // phase 2
-    if (ROLLOUT_ABLATE != 1) {
-        const MaskLane ml = MaskLane::load();
-        for (int j = 0; j < RB / WAVES; j++) {
-            const int b = w * (RB / WAVES) + j;
-            if (b >= nb) break;
-            const int8_t *s = lds + b * ST;
-            uint64_t m[7];
-            wave_valid_moves<N>(s, pl[b], lim, m, ml);
-            store_mask(mask_out + (size_t)(b0 + b) * 7, m);
-            int cnt = 0;
-#pragma unroll
-            for (int k = 0; k < 7; k++) cnt += __popcll(m[k]);
-            const int a = select_bit(m, (int)(u0s[b] * (double)cnt));
-            if (l == 0) act[b] = (int16_t)a;
-        }
-    }
-    __syncthreads();
-    if (ROLLOUT_ABLATE == 1 && tid < nb) act[tid] = 30 + (int)((step + tid) % 5);
-    // phase 3
-    if (w == 0 && ROLLOUT_ABLATE != 2) {
+    RT_MARK(3)
+    // phase 3: lane l < 16 of wave w = board 16w + l: pass bit (:263), uniform action draw,
+    // make_move with chance (a move takes at most draws 1-2), end check
+    if (ROLLOUT_ABLATE != 2) {
+        constexpr int PER = RB / WAVES;
         bool ended = false;
-        if (l < nb) {
-            const int b = l, gb = b0 + b;
+        const int b = w * PER + l;
+        if (l < PER && b < nb) {
+            const int gb = b0 + b;
+            int a;
+            if (ROLLOUT_ABLATE == 1) {
+                a = 30 + (int)((step + b) % 5);
+            } else {
+                uint64_t m[7];
+                int cnt = 0;
+#pragma unroll
+                for (int k = 0; k < 7; k++) { m[k] = msk[b][k]; cnt += __popcll(m[k]); }
+                if (!cnt) { m[6] |= 1ull << (408 - 384); msk[b][6] = m[6]; cnt = 1; }
+                a = select_bit(m, (int)(ud[b][0] * (double)cnt));
+            }
             int8_t *s = lds + b * ST;
-            const int a = act[b];
-            Chance ch{nullptr, seed, bbase + (uint32_t)gb, step, 1, u1s[b], true};
+            Chance ch{&ud[b][0], 0, 0, 0, 1, 0.0, false, quot, cards};
             int nxt = make_move<N>(s, a, pl[b], false, ch);
             float e[N];
             check_end<N>(s, e);
@@ -242,12 +266,15 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int8_t *__restrict__
             player[gb] = (int8_t)nxt;
         }
         const uint64_t rm = __ballot(ended);
-        if (l == 0) reset_mask = rm;
+        if (l == 0) reset16[w] = (uint16_t)rm;
     }
     __syncthreads();
+    RT_MARK(4)
     // phase 3b: finished boards are re-dealt (draws 3..), one board per wave at a time
     if (ROLLOUT_ABLATE != 2) {
-        uint64_t rm = reset_mask;
+        uint64_t rm = 0;
+#pragma unroll
+        for (int k = 0; k < WAVES; k++) rm |= (uint64_t)reset16[k] << (16 * k);
         for (int i = 0; rm; i++, rm &= rm - 1) {
             if ((i & (WAVES - 1)) != w) continue;
             const int b = __ffsll((unsigned long long)rm) - 1;
@@ -256,11 +283,24 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int8_t *__restrict__
         }
     }
     __syncthreads();
+    RT_MARK(5)
     // phase 4
     for (int i = tid; i < nb * Cv::UNITS; i += THREADS) {
         const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
         Cv::store(gst + (size_t)b * Lx::S, lds + b * ST, u);
     }
+    if (ROLLOUT_ABLATE != 1)
+        for (int i = tid; i < nb * 7; i += THREADS) mask_out[(size_t)b0 * 7 + i] = (&msk[0][0])[i];
+#if ROLLOUT_TIMING
+    __syncthreads();
+    RT_MARK(6)
+    if (threadIdx.x == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_rollout_timing[(size_t)blockIdx.x * 8 + 7] = ((uint64_t)xcc << 32) | hw;
+    }
+#endif
 }
 
 // Board.get_symmetries (SplendorLogicNumba.py:349-395) for E examples, one wave per
