@@ -196,6 +196,25 @@ def main():
     out.append(arr("static __constant__ double K_QUOT[41][9]", None, quot, lambda x: float(x).hex()))
     out.append(arr("static __constant__ double K_RECIP[9]", None, [0.0] + [1.0 / n for n in range(1, 9)],
                    lambda x: float(x).hex()))
+    # ---- per-action gem vectors for the flattened make_move: take / give rows (give = sum of
+    # the exchange's give vectors) and the reserve index (-1: none)
+    act_take, act_give, act_rsv = [0] * 409, [0] * 409, [-1] * 409
+    for a in range(12, 27):
+        act_rsv[a] = a - 12
+    for a in range(30, 60):
+        act_take[a] = pack(TAKE[a - 30])
+    for a, (tk, g1, g2, rv) in zip(range(60, 405), exchange_table()):
+        if tk != 255:
+            act_take[a] = pack(TAKE[tk])
+        gv = [GIVE[g1][c] + (GIVE[g2][c] if g2 != 255 else 0) for c in range(5)]
+        assert max(gv) < 128
+        act_give[a] = pack(gv)
+        if rv != 255:
+            act_rsv[a] = rv
+    out.append("// per action: gems taken / given back (packed rows) and reserve index (-1 none)")
+    out.append(arr("static __constant__ uint64_t K_ACT_TAKE[409]", None, act_take, lambda x: f"0x{x:016x}ull"))
+    out.append(arr("static __constant__ uint64_t K_ACT_GIVE[409]", None, act_give, lambda x: f"0x{x:016x}ull"))
+    out.append(arr("static __constant__ int8_t K_ACT_RSV[409]", None, act_rsv))
     # ---- compile-time forms for the lane-per-board mask (splendor_device.h lane_predicates)
     # threshold masks: bit 5t+c <-> value_c >= t (t = 0..4); a predicate "x >= v in every
     # colour" holds iff REQ(v) & ~THRESH(x) == 0

@@ -92,8 +92,9 @@ __device__ __forceinline__ double philox_u01(uint64_t seed, uint32_t board, uint
 }
 
 // Either an explicit stream of doubles (parity with recorded reference draws) or Philox.
-// Sequential draws reuse the second half of a Philox block. The deck-draw tables travel
-// with the chance source so a kernel can serve them from LDS.
+// Sequential draws reuse the second half of a Philox block. The transition tables (deck
+// draws, per-action gem vectors) travel with the chance source so a kernel can serve them
+// from LDS.
 struct Chance {
     const double *u;   // explicit uniforms for this board, or nullptr -> Philox
     uint64_t seed;
@@ -102,6 +103,8 @@ struct Chance {
     bool have_spare = false;
     const double (*quot)[9] = K_QUOT;
     const uint64_t (*cards)[2] = K_CARD_ROWS;
+    const uint64_t *act_take = K_ACT_TAKE, *act_give = K_ACT_GIVE;
+    const int8_t *act_rsv = K_ACT_RSV;
     __device__ __forceinline__ double draw() {
         if (u) return u[next++];
         double r;
@@ -541,67 +544,66 @@ __device__ __forceinline__ void buy_card(int8_t *s, int cost_row, int p) {
     give_nobles<N>(s, p);
 }
 
-// _reserve (:517-536): first empty slot; reserving from the deck in the tree
-// (deterministic) reserves nothing; +1 gold if the bank has any
-template <int N>
-__device__ __forceinline__ void reserve(int8_t *s, int i, int p, bool det, Chance &ch) {
-    using Lx = Lay<N>;
-    int slot = -1;
-    for (int k = 2; k >= 0; k--)
-        if (sum5(row(s, Lx::RSV + 6 * p + 2 * k)) == 0) slot = Lx::RSV + 6 * p + 2 * k;
-    if (i < 12) {
-        const int tier = i >> 2, idx = i & 3, r = Lx::TIERS + 8 * tier + 2 * idx;
-        if (slot >= 0) { row(s, slot) = row(s, r); row(s, slot + 1) = row(s, r + 1); }
-        fill_new_card<N>(s, tier, idx, det, ch);
-    } else if (!det) {
-        uint64_t cost, gain;
-        if (deck_card<N>(s, i - 12, ch, cost, gain) && slot >= 0) { row(s, slot) = cost; row(s, slot + 1) = gain; }
-    }
-    const uint64_t bank = row(s, Lx::BANK);
-    if (bt(bank, 5) > 0) {
-        const uint64_t gems = row(s, Lx::GEMS + p);
-        row(s, Lx::GEMS + p) = with_bt(gems, 5, bt(gems, 5) + 1);
-        row(s, Lx::BANK) = with_bt(bank, 5, bt(bank, 5) - 1);
-    }
-}
-
-// take (_get_gems :585-593) or give back (_give_gems :685-694) a gem vector
-template <int N>
-__device__ __forceinline__ void move_gems(int8_t *s, int p, uint64_t v, bool take) {
-    using Lx = Lay<N>;
-    const uint64_t gems = row(s, Lx::GEMS + p), bank = row(s, Lx::BANK);
-    row(s, Lx::GEMS + p) = take ? bytes_add(gems, v) : bytes_sub(gems, v);
-    row(s, Lx::BANK) = take ? bytes_sub(bank, v) : bytes_add(bank, v);
-}
-
-// Board.make_move (:267-289); actions 405..408 are a no-op + round increment (the
-// reference's select-noble stub does not parse and pass reads give_ids3 out of bounds;
-// see DESIGN.md "Defined deviations"). Returns the next player.
+// Board.make_move (:267-289) as one fixed pipeline of row operations, so boards that take
+// different kinds of moves share every stage (lane-per-board kernels run the pipeline once,
+// not once per move kind):
+//   buy     _buy_card (:458-474) for a visible (0-11) or reserved (27-29) card
+//   reserve _reserve (:517-536): first empty slot; a visible card moves there
+//   draw    one deck draw: refill the bought / reserved visible slot (_fill_new_card,
+//           zeros when the deck is empty or in the tree), or a deck reserve into the slot
+//           (nothing in the tree: deterministic reserve-from-deck draws no card)
+//   shift   _buy_reserve (:554-560) closes the bought card's slot
+//   gems    reserving grants a gold if the bank has one; then the action's take vector
+//           (_get_gems :585-593) and summed give-back vectors (_give_gems :685-694,
+//           exchanges :697-761) as one byte-wise row update
+//   round   round counter +1, int8 (:287)
+// Actions 405..408 are a no-op + round increment (the reference's select-noble stub does
+// not parse and pass reads give_ids3 out of bounds; DESIGN.md "Defined deviations").
+// Returns the next player.
 template <int N>
 __device__ __forceinline__ int make_move(int8_t *s, int a, int p, bool det, Chance &ch) {
     using Lx = Lay<N>;
-    if (a < 12) {
-        buy_card<N>(s, Lx::TIERS + 2 * a, p);
-        fill_new_card<N>(s, a >> 2, a & 3, det, ch);
-    } else if (a < 27) {
-        reserve<N>(s, a - 12, p, det, ch);
-    } else if (a < 30) {                                   // _buy_reserve (:554-560)
-        const int st = Lx::RSV + 6 * p + 2 * (a - 27);
-        buy_card<N>(s, st, p);
-        for (int r = st; r < Lx::RSV + 6 * p + 4; r++) row(s, r) = row(s, r + 2);
+    const int rsv = ch.act_rsv[a];
+    const uint64_t take = ch.act_take[a], give = ch.act_give[a];
+    const bool buy_vis = a < 12, buy_rsv = a >= 27 && a < 30;
+    if (buy_vis || buy_rsv) buy_card<N>(s, buy_vis ? Lx::TIERS + 2 * a : Lx::RSV + 6 * p + 2 * (a - 27), p);
+    int slot = -1;
+    if (rsv >= 0) {
+        for (int k = 2; k >= 0; k--)
+            if (sum5(row(s, Lx::RSV + 6 * p + 2 * k)) == 0) slot = Lx::RSV + 6 * p + 2 * k;
+        if (rsv < 12 && slot >= 0) {
+            const int r = Lx::TIERS + 2 * rsv;
+            row(s, slot) = row(s, r);
+            row(s, slot + 1) = row(s, r + 1);
+        }
+    }
+    const int tier = buy_vis ? a >> 2 : (rsv >= 0 ? (rsv < 12 ? rsv >> 2 : rsv - 12) : -1);
+    if (tier >= 0) {
+        uint64_t cost = 0, gain = 0;
+        const bool got = !det && deck_card<N>(s, tier, ch, cost, gain);
+        if (buy_vis || rsv < 12) {
+            const int r = Lx::TIERS + 2 * (buy_vis ? a : rsv);
+            row(s, r) = cost;
+            row(s, r + 1) = gain;
+        } else if (got && slot >= 0) {
+            row(s, slot) = cost;
+            row(s, slot + 1) = gain;
+        }
+    }
+    if (buy_rsv) {
+        for (int r = Lx::RSV + 6 * p + 2 * (a - 27); r < Lx::RSV + 6 * p + 4; r++) row(s, r) = row(s, r + 2);
         row(s, Lx::RSV + 6 * p + 4) = 0;
         row(s, Lx::RSV + 6 * p + 5) = 0;
-    } else if (a < 60) {
-        move_gems<N>(s, p, K_TAKE_ROW[a - 30], true);
-    } else if (a < 405) {                                  // exchanges (:697-761)
-        const uint8_t *e = K_EXCHANGE[a - 60];
-        if (e[3] != 255) reserve<N>(s, e[3], p, det, ch);
-        if (e[0] != 255) move_gems<N>(s, p, K_TAKE_ROW[e[0]], true);
-        move_gems<N>(s, p, K_GIVE_ROW[e[1]], false);
-        if (e[2] != 255) move_gems<N>(s, p, K_GIVE_ROW[e[2]], false);
     }
-    const uint64_t bank = row(s, Lx::BANK);
-    row(s, Lx::BANK) = with_bt(bank, 6, bt(bank, 6) + 1);  // round counter, int8 (:287)
+    uint64_t bank = row(s, Lx::BANK), gems = row(s, Lx::GEMS + p);
+    if (rsv >= 0 && bt(bank, 5) > 0) {
+        gems = with_bt(gems, 5, bt(gems, 5) + 1);
+        bank = with_bt(bank, 5, bt(bank, 5) - 1);
+    }
+    gems = bytes_sub(bytes_add(gems, take), give);
+    bank = bytes_add(bytes_sub(bank, take), give);
+    row(s, Lx::GEMS + p) = gems;
+    row(s, Lx::BANK) = with_bt(bank, 6, bt(bank, 6) + 1);
     return (p + 1) % N;
 }
 

@@ -150,30 +150,32 @@ __global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__re
     wave_store_board<N>(child + (size_t)b * Lx::S, s);
 }
 
-// Fused random-policy self-play step (see splendor_amd.h spl_rollout_step).
-// A 256-thread workgroup owns RB = 64 consecutive boards, staged in LDS as 8-byte rows at
-// an odd-qword stride (conflict-free ds_read_b64 / ds_write_b64 in lane-per-board code):
-//   phase 1  all threads: HBM -> LDS, one 4-row quad per thread (7 dwords -> 4 qwords);
-//            Philox blocks 0-1 of every board's step stream (draw 0 picks the action,
-//            1-2 feed a deck draw), deck-draw tables into LDS
-//   phase 2  lane per board: predicates + mask words w, w+4 of the 409-action mask in wave
-//            w, on the real board for the player to move (== the canonical form's mask: it
-//            only reads player p's rows)
-//   phase 3  lane l < 16 of wave w = board 16w + l: pass bit, uniform action draw,
-//            make_move with chance, end check — the serial rule logic runs 16 boards per wave
-//   phase 3b finished games are re-dealt wave-parallel (draws 3.., Philox per lane)
-//   phase 4  all threads: boards and masks LDS -> HBM
+// Fused random-policy self-play (splendor_amd.h spl_rollout_step / spl_rollout_run).
+// A 256-thread workgroup owns RB = 64 consecutive boards and keeps them in LDS, as 8-byte
+// rows at an odd-qword stride (conflict-free lane-per-board ds_read_b64/ds_write_b64), for
+// all K moves of the launch:
+//   load     HBM -> LDS, one 4-row quad per thread (7 dwords -> 4 qwords), deck tables
+//   per move t (step = step0 + t):
+//     mask   Philox blocks 0-1 of every board's step stream (draw 0 picks the action, 1-2
+//            feed a deck draw); lane-per-board legality predicates + mask words w, w+4 in
+//            wave w, on the real board for the player to move (== the canonical form's
+//            mask: it only reads player p's rows)
+//     move   lane l < 16 of wave w = board 16w + l: pass bit (:263), uniform action draw,
+//            make_move with chance, end check; per-move outputs
+//     reset  finished games are re-dealt wave-parallel (draws 3.., Philox per lane); the
+//            move's masks go to HBM
+//   store    boards, players, game counters LDS -> HBM
 constexpr int RB = 64;
 #ifndef ROLLOUT_ABLATE
-#define ROLLOUT_ABLATE 0   // diagnostic builds only (tools/ablate_rollout.hip): 1 = skip mask, 2 = skip step
+#define ROLLOUT_ABLATE 0   // diagnostic builds only (tools/ablate_rollout.hip): 1 = skip mask, 2 = skip move
 #endif
 #ifndef ROLLOUT_TIMING
-#define ROLLOUT_TIMING 0   // diagnostic builds only: per-block phase timestamps into g_rollout_timing
+#define ROLLOUT_TIMING 0   // diagnostic builds only: per-block phase cycle totals into g_rollout_timing
 #endif
 #if ROLLOUT_TIMING
 __device__ uint64_t *g_rollout_timing;
 #define RT_MARK(k)                                                                          \
-    if (threadIdx.x == 0) g_rollout_timing[(size_t)blockIdx.x * 8 + (k)] = (k) == 0 || (k) == 6 ? wall_clock64() : clock64();
+    if (threadIdx.x == 0) { const uint64_t c_ = clock64(); rt[k] += c_ - rt_last; rt_last = c_; }
 #else
 #define RT_MARK(k)
 #endif
@@ -183,60 +185,71 @@ struct RolloutLds {
 };
 
 template <int N>
-__global__ __launch_bounds__(THREADS) void k_rollout(int B, int8_t *__restrict__ state,
+__global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__restrict__ state,
                                                      int8_t *__restrict__ player, int lim,
                                                      uint64_t *__restrict__ mask_out,
                                                      int16_t *__restrict__ action_out,
                                                      float *__restrict__ ended_out,
                                                      int32_t *__restrict__ games_done,
-                                                     uint64_t seed, uint32_t step, uint32_t bbase) {
+                                                     uint64_t seed, uint32_t step0, uint32_t bbase) {
     using Lx = Lay<N>;
     using Cv = Conv<N>;
     constexpr int ST = RolloutLds<N>::STRIDE;
+    constexpr int PER = RB / WAVES;
     __shared__ __align__(16) int8_t lds[RB * ST];
     __shared__ uint64_t msk[RB][7];    // legality masks (odd qword stride: conflict-free)
     __shared__ int8_t pl[RB];
+    __shared__ int32_t gdone[RB];
     __shared__ double ud[RB][4];       // draws 0..3 of each board's step stream
     __shared__ double ub[WAVES][DEAL_DRAWS];
     __shared__ double quot[41][9];
     __shared__ uint64_t cards[120][2];
+    __shared__ uint64_t act_take[409], act_give[409];
+    __shared__ int8_t act_rsv[409];
     __shared__ uint16_t reset16[WAVES];
     const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
     int8_t *const gst = state + (size_t)b0 * Lx::S;
-    RT_MARK(0) RT_MARK(1)
-    // phase 1: boards, players, the step's first two Philox blocks, deck tables
+#if ROLLOUT_TIMING
+    uint64_t rt[6] = {0, 0, 0, 0, 0, 0}, rt_last = clock64();
+    const uint64_t wall0 = wall_clock64();
+#endif
     for (int i = tid; i < nb * Cv::UNITS; i += THREADS) {
         const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
         Cv::load(lds + b * ST, gst + (size_t)b * Lx::S, u);
     }
-    if (tid < 2 * RB && (tid & (RB - 1)) < nb) {
-        const int b = tid & (RB - 1), k = tid / RB;
-        philox_pair(seed, bbase + (uint32_t)(b0 + b), step, k, ud[b][2 * k], ud[b][2 * k + 1]);
+    if (tid < nb) {
+        pl[tid] = player[b0 + tid];
+        gdone[tid] = games_done ? games_done[b0 + tid] : 0;
     }
-    if (tid < nb) pl[tid] = player[b0 + tid];
     for (int i = tid; i < 41 * 9; i += THREADS) (&quot[0][0])[i] = (&K_QUOT[0][0])[i];
     for (int i = tid; i < 240; i += THREADS) (&cards[0][0])[i] = (&K_CARD_ROWS[0][0])[i];
-    __syncthreads();
-    RT_MARK(2)
-    // phase 2: masks, lane per board; wave w evaluates words w and w+4 of all 64 boards
-    if (ROLLOUT_ABLATE != 1 && l < nb) {
-        const LanePred P = lane_predicates<N>(lds + l * ST, pl[l], lim);
-        if (w == 0) { msk[l][0] = lane_mask_word<0>(P); msk[l][4] = lane_mask_word<4>(P); }
-        else if (w == 1) { msk[l][1] = lane_mask_word<1>(P); msk[l][5] = lane_mask_word<5>(P); }
-        else if (w == 2) { msk[l][2] = lane_mask_word<2>(P); msk[l][6] = lane_mask_word<6>(P); }
-        else { msk[l][3] = lane_mask_word<3>(P); }
+    for (int i = tid; i < 409; i += THREADS) {
+        act_take[i] = K_ACT_TAKE[i];
+        act_give[i] = K_ACT_GIVE[i];
+        act_rsv[i] = K_ACT_RSV[i];
     }
     __syncthreads();
-    RT_MARK(3)
-    // phase 3: lane l < 16 of wave w = board 16w + l: pass bit (:263), uniform action draw,
-    // make_move with chance (a move takes at most draws 1-2), end check
-    if (ROLLOUT_ABLATE != 2) {
-        constexpr int PER = RB / WAVES;
+    RT_MARK(0)
+    for (int t = 0; t < K; t++) {
+        const uint32_t step = step0 + (uint32_t)t;
+        const size_t ob = (size_t)t * B + b0;            // this move's output row base
+        if (tid < 2 * RB && (tid & (RB - 1)) < nb) {
+            const int b = tid & (RB - 1), k = tid / RB;
+            philox_pair(seed, bbase + (uint32_t)(b0 + b), step, k, ud[b][2 * k], ud[b][2 * k + 1]);
+        }
+        if (ROLLOUT_ABLATE != 1 && l < nb) {
+            const LanePred P = lane_predicates<N>(lds + l * ST, pl[l], lim);
+            if (w == 0) { msk[l][0] = lane_mask_word<0>(P); msk[l][4] = lane_mask_word<4>(P); }
+            else if (w == 1) { msk[l][1] = lane_mask_word<1>(P); msk[l][5] = lane_mask_word<5>(P); }
+            else if (w == 2) { msk[l][2] = lane_mask_word<2>(P); msk[l][6] = lane_mask_word<6>(P); }
+            else { msk[l][3] = lane_mask_word<3>(P); }
+        }
+        __syncthreads();
+        RT_MARK(1)
         bool ended = false;
         const int b = w * PER + l;
-        if (l < PER && b < nb) {
-            const int gb = b0 + b;
+        if (ROLLOUT_ABLATE != 2 && l < PER && b < nb) {
             int a;
             if (ROLLOUT_ABLATE == 1) {
                 a = 30 + (int)((step + b) % 5);
@@ -249,56 +262,60 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int8_t *__restrict__
                 a = select_bit(m, (int)(ud[b][0] * (double)cnt));
             }
             int8_t *s = lds + b * ST;
-            Chance ch{&ud[b][0], 0, 0, 0, 1, 0.0, false, quot, cards};
+            Chance ch{&ud[b][0], 0, 0, 0, 1, 0.0, false, quot, cards, act_take, act_give, act_rsv};
             int nxt = make_move<N>(s, a, pl[b], false, ch);
             float e[N];
             check_end<N>(s, e);
 #pragma unroll
             for (int i = 0; i < N; i++) {
                 ended |= e[i] != 0.f;
-                ended_out[(size_t)gb * N + i] = e[i];
+                ended_out[(ob + b) * N + i] = e[i];
             }
-            action_out[gb] = (int16_t)a;
+            action_out[ob + b] = (int16_t)a;
             if (ended) {
                 nxt = 0;
-                if (games_done) games_done[gb] += 1;
+                gdone[b] += 1;
             }
-            player[gb] = (int8_t)nxt;
+            pl[b] = (int8_t)nxt;
         }
-        const uint64_t rm = __ballot(ended);
-        if (l == 0) reset16[w] = (uint16_t)rm;
-    }
-    __syncthreads();
-    RT_MARK(4)
-    // phase 3b: finished boards are re-dealt (draws 3..), one board per wave at a time
-    if (ROLLOUT_ABLATE != 2) {
+        const uint64_t rm16 = __ballot(ended);
+        if (l == 0) reset16[w] = (uint16_t)rm16;
+        __syncthreads();
+        RT_MARK(2)
         uint64_t rm = 0;
 #pragma unroll
         for (int k = 0; k < WAVES; k++) rm |= (uint64_t)reset16[k] << (16 * k);
         for (int i = 0; rm; i++, rm &= rm - 1) {
             if ((i & (WAVES - 1)) != w) continue;
-            const int b = __ffsll((unsigned long long)rm) - 1;
-            wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)(b0 + b), step, 3, DEAL_DRAWS);
-            wave_init_game<N>(lds + b * ST, ub[w]);
+            const int rb = __ffsll((unsigned long long)rm) - 1;
+            wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)(b0 + rb), step, 3, DEAL_DRAWS);
+            wave_init_game<N>(lds + rb * ST, ub[w]);
         }
+        if (mask_out && ROLLOUT_ABLATE != 1)
+            for (int i = tid; i < nb * 7; i += THREADS) mask_out[ob * 7 + i] = (&msk[0][0])[i];
+        __syncthreads();
+        RT_MARK(3)
     }
-    __syncthreads();
-    RT_MARK(5)
-    // phase 4
     for (int i = tid; i < nb * Cv::UNITS; i += THREADS) {
         const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
         Cv::store(gst + (size_t)b * Lx::S, lds + b * ST, u);
     }
-    if (ROLLOUT_ABLATE != 1)
-        for (int i = tid; i < nb * 7; i += THREADS) mask_out[(size_t)b0 * 7 + i] = (&msk[0][0])[i];
+    if (tid < nb) {
+        player[b0 + tid] = pl[tid];
+        if (games_done) games_done[b0 + tid] = gdone[tid];
+    }
 #if ROLLOUT_TIMING
     __syncthreads();
-    RT_MARK(6)
+    RT_MARK(4)
     if (threadIdx.x == 0) {
+        uint64_t *o = g_rollout_timing + (size_t)blockIdx.x * 8;
+        for (int k = 0; k < 5; k++) o[k] = rt[k];
+        o[5] = wall0;
+        o[6] = wall_clock64();
         uint32_t hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        g_rollout_timing[(size_t)blockIdx.x * 8 + 7] = ((uint64_t)xcc << 32) | hw;
+        o[7] = ((uint64_t)xcc << 32) | hw;
     }
 #endif
 }
@@ -510,18 +527,25 @@ int spl_symmetries(const spl_ctx *c, int E, const int8_t *state, const float *pi
     return check_launch();
 }
 
+int spl_rollout_run(const spl_ctx *c, int B, int K, int8_t *state, int8_t *player, uint64_t *mask_out,
+                    int16_t *action_out, float *ended_out, int32_t *games_done, uint64_t seed,
+                    uint32_t step0, uint32_t board_base, void *hs) {
+    if (!ok_ctx(c) || B < 0 || K < 0 || (B && K && (!state || !player || !action_out || !ended_out)))
+        return SPL_EINVAL;
+    if (!B || !K) return 0;
+    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_rollout<N>, dim3((unsigned)((B + RB - 1) / RB)), dim3(THREADS), 0,
+                                          (hipStream_t)hs, B, K, state, player, c->token_limit,
+                                          mask_out, action_out, ended_out, games_done, seed,
+                                          step0, board_base));
+    return check_launch();
+}
+
 int spl_rollout_step(const spl_ctx *c, int B, int8_t *state, int8_t *player, uint64_t *mask_out,
                      int16_t *action_out, float *ended_out, int32_t *games_done, uint64_t seed,
                      uint32_t step, uint32_t board_base, void *hs) {
-    if (!ok_ctx(c) || B < 0 ||
-        (B && (!state || !player || !mask_out || !action_out || !ended_out)))
-        return SPL_EINVAL;
-    if (!B) return 0;
-    SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_rollout<N>, dim3((unsigned)((B + RB - 1) / RB)), dim3(THREADS), 0,
-                                          (hipStream_t)hs, B, state, player, c->token_limit,
-                                          mask_out, action_out, ended_out, games_done, seed,
-                                          step, board_base));
-    return check_launch();
+    if (B && !mask_out) return SPL_EINVAL;
+    return spl_rollout_run(c, B, 1, state, player, mask_out, action_out, ended_out, games_done, seed,
+                           step, board_base, hs);
 }
 
 }  // extern "C"

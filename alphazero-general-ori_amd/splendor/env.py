@@ -152,6 +152,14 @@ class SplendorEngine:
                                            _ptr(games_done), seed, step, board_base, self._s()),
                    "spl_rollout_step")
 
+    def rollout_run(self, K, state, player, mask_out, action_out, ended_out, games_done, seed, step0,
+                    board_base=0):
+        """K fused moves in one launch; outputs stacked by move ([K][B]...)."""
+        _lib.check(self.L.spl_rollout_run(self.ctx, state.shape[0], int(K), _ptr(state), _ptr(player),
+                                          _ptr(mask_out), _ptr(action_out), _ptr(ended_out),
+                                          _ptr(games_done), seed, step0, board_base, self._s()),
+                   "spl_rollout_run")
+
 
 class RolloutBatch:
     """B boards of random-policy self-play, stepped by one fused launch per step
@@ -176,3 +184,16 @@ class RolloutBatch:
         self.e.rollout_step(self.state, self.player, self.mask, self.action, self.ended, self.games,
                             self.seed, self.t, self.board_base)
         self.t += 1
+
+    def run(self, K, masks=True, out=None):
+        """K moves in one launch (boards stay on chip); returns the stacked per-move outputs
+        {"mask": [K,B,7] or None, "action": [K,B], "ended": [K,B,n]} (reused if `out`)."""
+        B, dev, n = self.B, self.e.device, self.e.n
+        if out is None or out["action"].shape[0] != K:
+            out = {"mask": torch.empty((K, B, MASK_WORDS), dtype=torch.int64, device=dev) if masks else None,
+                   "action": torch.empty((K, B), dtype=torch.int16, device=dev),
+                   "ended": torch.empty((K, B, n), dtype=torch.float32, device=dev)}
+        self.e.rollout_run(K, self.state, self.player, out["mask"], out["action"], out["ended"], self.games,
+                           self.seed, self.t, self.board_base)
+        self.t += K
+        return out

@@ -111,6 +111,16 @@ int spl_rollout_step(const spl_ctx *ctx, int B, int8_t *state, int8_t *player,
                      int32_t *games_done, uint64_t seed, uint32_t step, uint32_t board_base,
                      void *hip_stream);
 
+/* K consecutive spl_rollout_step calls (steps step0 .. step0+K-1) in one launch: each
+ * workgroup keeps its boards on chip for all K moves, so board bytes cross HBM once per
+ * launch. Per-move outputs are stacked by move: mask_out [K][B][7] (may be NULL),
+ * action_out [K][B], ended_out [K][B][n]; state, player and games_done hold the result
+ * after move K. Bit-identical to K spl_rollout_step calls. */
+int spl_rollout_run(const spl_ctx *ctx, int B, int K, int8_t *state, int8_t *player,
+                    uint64_t *mask_out, int16_t *action_out, float *ended_out,
+                    int32_t *games_done, uint64_t seed, uint32_t step0, uint32_t board_base,
+                    void *hip_stream);
+
 
 /* ===================================================================== MCTS
  * Device-resident batched PUCT search (MCTS.py), one tree per board/game, B trees.

@@ -20,7 +20,7 @@ def declared():
 def test_header_declares_entry_points():
     names = declared()
     for must in ("spl_init", "spl_valid_moves", "spl_step", "spl_game_ended", "spl_canonical",
-                 "spl_tree_step", "spl_rollout_step"):
+                 "spl_tree_step", "spl_rollout_step", "spl_rollout_run"):
         assert must in names
 
 

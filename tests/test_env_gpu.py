@@ -121,6 +121,35 @@ def test_fused_rollout_matches_oracle(engines, n):
     np.testing.assert_array_equal(rb.games.cpu().numpy(), ref["games"])
 
 
+@pytest.mark.parametrize("n", NS)
+def test_rollout_run_matches_oracle(engines, n):
+    """spl_rollout_run (K moves per launch, boards kept on chip) == the oracle's move loop,
+    across launch boundaries (chunks 1, 40, 55), incl. every move's legality mask."""
+    from splendor.env import RolloutBatch
+    B, seed = 1000, 0x5EED + 7 * n          # ragged: last workgroup holds 40 boards
+    chunks = (1, 40, 55)
+    T = sum(chunks)
+    ref = O.rollout_run(n, B, T, seed)
+    rb = RolloutBatch(engines[n], B, seed=seed)
+    acts, ends, masks = [], [], []
+    for K in chunks:
+        o = rb.run(K)
+        acts.append(o["action"].cpu().numpy()); ends.append(o["ended"].cpu().numpy())
+        masks.append(o["mask"].cpu().numpy().view(np.uint64))
+    act, end, msk = np.concatenate(acts), np.concatenate(ends), np.concatenate(masks)
+    np.testing.assert_array_equal(act, ref["action"])
+    np.testing.assert_array_equal(end, ref["ended"])
+    fold = np.zeros(B, np.uint64)
+    with np.errstate(over="ignore"):
+        for t in range(T):
+            for j in range(7):
+                fold ^= (msk[t, :, j] * np.uint64(2 * j + 1)) ^ np.uint64(t << 40)
+    np.testing.assert_array_equal(fold, ref["mask_fold"])
+    np.testing.assert_array_equal(rb.state.cpu().numpy(), ref["state"])
+    np.testing.assert_array_equal(rb.player.cpu().numpy(), ref["player"])
+    np.testing.assert_array_equal(rb.games.cpu().numpy(), ref["games"])
+
+
 def _invariants(n, st, gems_in_play):
     R = 32 + 10 * n + n * n
     gems = 32 + n
