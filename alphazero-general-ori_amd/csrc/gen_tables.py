@@ -223,6 +223,16 @@ def main():
         return sum(1 << (5 * t + c) for c in range(5) for t in range(v[c] + 1))
     req0 = [0] * 30 + [req(TAKE[i]) for i in range(25)] + [1 << (20 + c) for c in range(5)]
     req1 = [req(GIVE[i]) for i in range(15)] + [1 << (10 + c) for c in range(5)] + [req(v) for v in SPEC3]
+    # subset / level lookup tables for non-negative gem rows (lane_predicates fast path):
+    # LUT_DIFF[m] bit i <-> DIFF[i] within colour set m; LUT_SPEC3[l] bit j <-> SPEC3[j] <=
+    # levels l (2 bits per colour: min(count, 3))
+    lut_diff = [sum(1 << i for i, v in enumerate(DIFF) if all(v[c] <= ((m >> c) & 1) for c in range(5)))
+                for m in range(32)]
+    assert max(max(v) for v in SPEC3) <= 3
+    lut_s3 = [sum(1 << j for j, v in enumerate(SPEC3) if all(v[c] <= ((l >> (2 * c)) & 3) for c in range(5)))
+              for l in range(1024)]
+    out.append(arr("static __constant__ uint32_t K_LUT_DIFF[32]", None, lut_diff, lambda x: f"0x{x:07x}u"))
+    out.append(arr("static __constant__ uint64_t K_LUT_SPEC3[1024]", None, lut_s3, lambda x: f"0x{x:010x}ull"))
     out.append("// compile-time copies for fully unrolled lane-per-board evaluation")
     out.append(arr("static constexpr uint32_t KC_ACTION_DESC[409]", None, action_table(), lambda x: f"0x{x:06x}u"))
     out.append("// F0 bits 30..59 / F1 bits 0..59: required threshold bits (bit 5t+c: colour c >= t)")

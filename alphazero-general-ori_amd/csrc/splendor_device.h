@@ -342,8 +342,28 @@ __device__ __forceinline__ uint32_t thresh5(uint64_t w) {
     return m;
 }
 
+// condition bits (the token-count branches of wave_valid_moves)
+__device__ __forceinline__ uint32_t lane_cond(int T, int lim, int nspec, int bgold) {
+    const bool ex_any = T > 7;
+    const bool ex8 = ex_any && T == lim - 2;
+    const bool ex9 = ex_any && !ex8 && T == lim - 1;
+    const bool ex10 = ex_any && !ex8 && !ex9;
+    uint32_t C = 1u << C_ALWAYS;
+    C |= (uint32_t)(!(T == lim && bgold > 0)) << C_RSV_LIMIT;
+    C |= (uint32_t)(T + 1 <= lim && (T == 9 || nspec == 1)) << C_TAKE1;
+    C |= (uint32_t)(T + 2 <= lim && (T == 8 || nspec == 2)) << C_TAKE2D;
+    C |= (uint32_t)(T + 3 <= lim) << C_TAKE3;
+    C |= (uint32_t)(T + 2 <= lim) << C_TAKE2S;
+    C |= (uint32_t)ex8 << C_EX8;
+    C |= (uint32_t)ex9 << C_EX9;
+    C |= (uint32_t)ex10 << C_EX10;
+    C |= (uint32_t)(ex10 && bgold > 0) << C_EX10G;
+    return C;
+}
+
+// exact predicates for any int8 board (threshold masks over signed bytes)
 template <int N>
-__device__ __forceinline__ LanePred lane_predicates(const int8_t *s, int p, int lim) {
+__device__ __noinline__ LanePred lane_predicates_exact(const int8_t *s, int p, int lim) {
     using Lx = Lay<N>;
     const uint64_t bank = row(s, Lx::BANK), gems = row(s, Lx::GEMS + p), cards = row(s, Lx::CARDS + p);
     const int T = sum7(gems), gold = bt(gems, 5), bgold = bt(bank, 5);
@@ -388,22 +408,74 @@ __device__ __forceinline__ LanePred lane_predicates(const int8_t *s, int p, int 
     for (int i = 30; i < 60; i++) P.F0 |= (uint64_t)((KC_REQ0[i] & nb) == 0) << i;
 #pragma unroll
     for (int i = 0; i < 60; i++) P.F1 |= (uint64_t)((KC_REQ1[i] & ng) == 0) << i;
-    // condition bits (same as wave_valid_moves)
-    const bool ex_any = T > 7;
-    const bool ex8 = ex_any && T == lim - 2;
-    const bool ex9 = ex_any && !ex8 && T == lim - 1;
-    const bool ex10 = ex_any && !ex8 && !ex9;
-    uint32_t C = 1u << C_ALWAYS;
-    C |= (uint32_t)(!(T == lim && bgold > 0)) << C_RSV_LIMIT;
-    C |= (uint32_t)(T + 1 <= lim && (T == 9 || nspec == 1)) << C_TAKE1;
-    C |= (uint32_t)(T + 2 <= lim && (T == 8 || nspec == 2)) << C_TAKE2D;
-    C |= (uint32_t)(T + 3 <= lim) << C_TAKE3;
-    C |= (uint32_t)(T + 2 <= lim) << C_TAKE2S;
-    C |= (uint32_t)ex8 << C_EX8;
-    C |= (uint32_t)ex9 << C_EX9;
-    C |= (uint32_t)ex10 << C_EX10;
-    C |= (uint32_t)(ex10 && bgold > 0) << C_EX10G;
-    P.C = C;
+    P.C = lane_cond(T, lim, nspec, bgold);
+    return P;
+}
+
+// colours whose byte is >= t
+__device__ __forceinline__ uint32_t ge_set(uint64_t w, int t) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < 5; c++) m |= (uint32_t)(bt(w, c) >= t) << c;
+    return m;
+}
+
+// Predicates of lane_predicates_exact, computed with byte arithmetic for boards whose
+// colour bytes (bank, the player's gems and cards, card costs, deck counts, reserve slot)
+// are non-negative — every board reachable from init_game. Affordability uses byte SADs:
+// sum max(cost - have, 0) = (sum |cost - have| + sum cost - sum have) / 2; the gem-vector
+// predicates are subset / level table lookups (K_LUT_DIFF, K_LUT_SPEC3). Other boards take
+// the exact path.
+template <int N>
+__device__ __forceinline__ LanePred lane_predicates(const int8_t *s, int p, int lim,
+                                                    const uint32_t *lut_diff = K_LUT_DIFF,
+                                                    const uint64_t *lut_s3 = K_LUT_SPEC3) {
+    using Lx = Lay<N>;
+    constexpr uint64_t M5 = 0xFFFFFFFFFFull, H5 = 0x8080808080ull;
+    const uint64_t bank = row(s, Lx::BANK), gems = row(s, Lx::GEMS + p), cards = row(s, Lx::CARDS + p);
+    const uint64_t slot5 = row(s, Lx::RSV + 6 * p + 5);
+    uint64_t cost[15], deck[3];
+    uint64_t any = bank | gems | cards | slot5;
+#pragma unroll
+    for (int i = 0; i < 15; i++) {
+        cost[i] = row(s, i < 12 ? Lx::TIERS + 2 * i : Lx::RSV + 6 * p + 2 * (i - 12));
+        any |= cost[i];
+    }
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+        deck[t] = row(s, Lx::DECKS + 2 * t);
+        any |= deck[t];
+    }
+    if (any & H5) return lane_predicates_exact<N>(s, p, lim);
+    const uint64_t have = (gems & M5) + (cards & M5);          // bytes < 256: no carries
+    const uint32_t hlo = (uint32_t)have, hhi = (uint32_t)(have >> 32);
+    const int gold = bt(gems, 5);
+    const int rhs = 2 * gold + (int)__builtin_amdgcn_sad_u8(hlo, 0u, hhi);
+    const bool slot_free = (slot5 & M5) == 0;
+    LanePred P{0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 15; i++) {
+        const uint32_t clo = (uint32_t)cost[i], chi = (uint32_t)(cost[i] >> 32) & 0xFF;
+        const uint32_t absd = __builtin_amdgcn_sad_u8(clo, hlo, __builtin_amdgcn_sad_u8(chi, hhi, 0u));
+        const int lhs = (int)__builtin_amdgcn_sad_u8(clo, 0u, absd + chi);   // sum|c-h| + sum c
+        const bool nz = (cost[i] & M5) != 0;
+        const bool buy = lhs <= rhs && nz;
+        if (i < 12) {
+            P.F0 |= (uint64_t)buy << i;
+            P.F0 |= (uint64_t)(nz && slot_free) << (12 + i);
+        } else {
+            P.F0 |= (uint64_t)buy << (27 + i - 12);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 3; t++) P.F0 |= (uint64_t)((deck[t] & M5) != 0 && slot_free) << (24 + t);
+    const uint32_t b1 = ge_set(bank, 1), g1 = ge_set(gems, 1);
+    uint32_t lvl = 0;
+#pragma unroll
+    for (int c = 0; c < 5; c++) lvl |= (uint32_t)min(bt(gems, c), 3) << (2 * c);
+    P.F0 |= (uint64_t)lut_diff[b1] << 30 | (uint64_t)ge_set(bank, 4) << 55;
+    P.F1 = (uint64_t)(lut_diff[g1] & 0x7FFFu) | (uint64_t)ge_set(gems, 2) << 15 | lut_s3[lvl] << 20;
+    P.C = lane_cond(sum7(gems), lim, __popc(b1), bt(bank, 5));
     return P;
 }
 

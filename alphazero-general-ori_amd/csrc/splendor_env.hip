@@ -206,6 +206,8 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     __shared__ uint64_t cards[120][2];
     __shared__ uint64_t act_take[409], act_give[409];
     __shared__ int8_t act_rsv[409];
+    __shared__ uint32_t lut_diff[32];
+    __shared__ uint64_t lut_s3[1024];
     __shared__ uint16_t reset16[WAVES];
     const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
@@ -229,6 +231,8 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         act_give[i] = K_ACT_GIVE[i];
         act_rsv[i] = K_ACT_RSV[i];
     }
+    for (int i = tid; i < 1024; i += THREADS) lut_s3[i] = K_LUT_SPEC3[i];
+    if (tid < 32) lut_diff[tid] = K_LUT_DIFF[tid];
     __syncthreads();
     RT_MARK(0)
     for (int t = 0; t < K; t++) {
@@ -239,7 +243,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
             philox_pair(seed, bbase + (uint32_t)(b0 + b), step, k, ud[b][2 * k], ud[b][2 * k + 1]);
         }
         if (ROLLOUT_ABLATE != 1 && l < nb) {
-            const LanePred P = lane_predicates<N>(lds + l * ST, pl[l], lim);
+            const LanePred P = lane_predicates<N>(lds + l * ST, pl[l], lim, lut_diff, lut_s3);
             if (w == 0) { msk[l][0] = lane_mask_word<0>(P); msk[l][4] = lane_mask_word<4>(P); }
             else if (w == 1) { msk[l][1] = lane_mask_word<1>(P); msk[l][5] = lane_mask_word<5>(P); }
             else if (w == 2) { msk[l][2] = lane_mask_word<2>(P); msk[l][6] = lane_mask_word<6>(P); }

@@ -2,10 +2,12 @@
 """Benchmark of the MI355X Splendor self-play hot path (BASELINE.json).
 
 Default workload = BASELINE config 2: 2-player Splendor, 32,768 concurrent boards per GPU,
-random-policy self-play, one fused HIP launch per step over every board (canonical form ->
-409-action legality mask -> action -> chance transition -> end check -> auto-reset).
-A "rollout" here is one board-step of that loop (BASELINE.md units). Data are synthetic:
-boards start from Philox-seeded deals (seed 0x5EED, board id) and reset on game end.
+random-policy self-play by the fused HIP rollout kernel (canonical form -> 409-action
+legality mask -> action -> chance transition -> end check -> auto-reset). One bench "step"
+is one move of every board; a launch runs --chunk moves with the boards kept on chip and
+writes every move's mask, action and end result to HBM. A "rollout" is one board-move
+(BASELINE.md units). Data are synthetic: boards start from Philox-seeded deals (seed
+0x5EED, board id) and reset on game end.
 
 Contract: `python bench.py --gpus N --steps K --warmup W`; for N>1 launched by
 torch.distributed.run, one rank per GPU; boards are sharded by board id (board_base =
@@ -27,11 +29,12 @@ METRIC = "self-play rollouts/sec (32k boards, 2p Splendor) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 
 
-def bytes_per_board_step(n):
-    """Algorithmic HBM bytes of one fused rollout step for one board:
-    state read + write (2S), player read + write (2), packed mask (56), action (2), ended (4n)."""
+def bytes_per_board_launch(n, moves):
+    """Algorithmic HBM bytes of one rollout launch for one board: state read +
+    write (2S), player read + write (2), game counter read + write (8), and per move the
+    packed mask (56), action (2) and end result (4n)."""
     S = 7 * (32 + 10 * n + n * n)
-    return 2 * S + 2 + 56 + 2 + 4 * n
+    return 2 * S + 2 + 8 + moves * (56 + 2 + 4 * n)
 
 
 def cpu_baseline(n, seed, target_s=10.0):
@@ -144,6 +147,7 @@ def main():
     ap.add_argument("--no-selfplay", action="store_true",
                     help="env workload: skip the secondary config-3 self-play measurement")
     ap.add_argument("--selfplay-steps", type=int, default=100)
+    ap.add_argument("--chunk", type=int, default=50, help="env: moves per rollout launch")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,22 +194,29 @@ def main():
     eng = SplendorEngine(args.players, device=dev)
     B = args.boards
     rb = RolloutBatch(eng, B, seed=args.seed, board_base=rank * B)
-    for _ in range(args.warmup):
-        rb.step()
+    K, chunk = args.steps, max(1, min(args.chunk, args.steps))
+    launches = [chunk] * (K // chunk) + ([K % chunk] if K % chunk else [])
+    outs = {}
+    def run(k):
+        outs[k] = rb.run(k, out=outs.get(k))
+    w = args.warmup
+    while w > 0:
+        run(min(chunk, w))
+        w -= chunk
+    for k in set(launches):
+        run(k)                                 # output buffers of every launch size exist
     torch.cuda.synchronize(dev)
 
-    K = args.steps
     # HIP events on the stream the kernel is launched on (torch's current stream): one
-    # pair around the K back-to-back launches -> average launch duration (incl. the
-    # ~1-2 us inter-launch gap; rocprofv3 --stats gives the pure kernel time)
+    # pair around the back-to-back launches -> average launch duration
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record()
-    for _ in range(K):
-        rb.step()
+    for k in launches:
+        run(k)
     ev1.record()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -214,7 +225,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms = ev0.elapsed_time(ev1) / K
+    kernel_ms = ev0.elapsed_time(ev1) / len(launches)
     games = int(rb.games.sum().item())
 
     secondary = None
@@ -234,7 +245,7 @@ def main():
                      "tree_device_bytes": r["device_bytes"]}
 
     if rank == 0:
-        per = bytes_per_board_step(args.players)
+        per = bytes_per_board_launch(args.players, chunk)
         achieved = per * B / (kernel_ms * 1e-3) / 1e9
         traffic = load_traffic(args.traffic_json, B)
         out = {
@@ -253,11 +264,13 @@ def main():
             "config": {"workload": "config2: env-step-only random-policy self-play, fused "
                                    "canonical+mask+action+chance step+end check+auto-reset",
                        "players": args.players, "boards_per_gpu": B, "global_boards": world * B,
+                       "moves_per_launch": chunk,
                        "parallelism": f"dp{world} (board shards, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rollout<2>", "kernel_avg_us": kernel_ms * 1e3,
-                         "bytes_per_board_step": per},
+                         "kernel": f"k_rollout<{args.players}>", "kernel_avg_us": kernel_ms * 1e3,
+                         "moves_per_launch": chunk, "bytes_per_board_launch": per,
+                         "note": "VALU-issue bound, not HBM bound: see DESIGN.md §5"},
             "cpu_baseline": cpu,
             "games_completed": games,
             "config3_selfplay": secondary,

@@ -150,6 +150,35 @@ def test_rollout_run_matches_oracle(engines, n):
     np.testing.assert_array_equal(rb.games.cpu().numpy(), ref["games"])
 
 
+@pytest.mark.parametrize("n", NS)
+def test_rollout_masks_on_perturbed_boards(engines, n):
+    """The fused kernel's lane-per-board mask (byte-SAD / lookup fast path and the exact
+    path for boards with negative bytes) == the oracle's valid_moves, on golden states whose
+    bank / gem / card / cost / deck bytes are randomly overwritten (arbitrary int8)."""
+    from splendor.env import MASK_WORDS
+    d = load(f"env_{n}p.npz")
+    rng = np.random.default_rng(11 + n)
+    R = O.rows(n)
+    st = np.repeat(d["state"], 3, axis=0)[:600].copy()
+    pl = np.repeat(d["player"], 3, axis=0)[:600].astype(np.int8)
+    B = len(st)
+    rows_hit = np.array([0] + list(range(1, 31)) + list(range(32 + n, R)))
+    for b in range(B):
+        k = rng.integers(1, 6)
+        for _ in range(k):
+            r, c = rng.choice(rows_hit), rng.integers(0, 7)
+            lo = -128 if b % 3 == 0 else 0           # a third of the boards leave the fast domain
+            st[b, r, c] = rng.integers(lo, 12)
+    want = np.stack([O.valid_moves(n, st[b], int(pl[b])) for b in range(B)]).astype(np.uint8)
+    e = engines[n]
+    dst, dpl = dev(st), dev(pl)
+    mask = torch.zeros((B, MASK_WORDS), dtype=torch.int64, device="cuda")
+    act = torch.zeros(B, dtype=torch.int16, device="cuda")
+    end = torch.zeros((B, n), dtype=torch.float32, device="cuda")
+    e.rollout_step(dst, dpl, mask, act, end, None, 0x5EED, 0)
+    np.testing.assert_array_equal(host_mask(mask), want)
+
+
 def _invariants(n, st, gems_in_play):
     R = 32 + 10 * n + n * n
     gems = 32 + n
