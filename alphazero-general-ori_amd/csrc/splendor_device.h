@@ -20,6 +20,10 @@
 
 #include "splendor_tables.h"
 
+#ifndef SPL_PROBE
+#define SPL_PROBE(k)   // diagnostic cycle probes (tools/time_rollout.hip); empty in product builds
+#endif
+
 namespace spl {
 
 // condition codes of K_ACTION_DESC (gen_tables.py)
@@ -91,20 +95,45 @@ __device__ __forceinline__ double philox_u01(uint64_t seed, uint32_t board, uint
     return (d & 1) ? b : a;
 }
 
+// The transition tables (deck draws, per-action gem vectors). Default: constant memory;
+// a kernel may stage them in LDS (stage_tabs) and pass the LDS copy.
+struct Tabs {
+    const double (*quot)[9] = K_QUOT;
+    const double *recip = K_RECIP;
+    const uint64_t (*cards)[2] = K_CARD_ROWS;
+    const uint64_t *act_take = K_ACT_TAKE, *act_give = K_ACT_GIVE;
+    const int8_t *act_rsv = K_ACT_RSV;
+};
+struct TabsLds {          // LDS image of Tabs
+    double quot[41][9];
+    double recip[9];
+    uint64_t cards[120][2];
+    uint64_t act_take[409], act_give[409];
+    int8_t act_rsv[409];
+    __device__ __forceinline__ Tabs view() const { return Tabs{quot, recip, cards, act_take, act_give, act_rsv}; }
+};
+// cooperative copy of the tables into LDS by `nthreads` threads (caller synchronises)
+__device__ __forceinline__ void stage_tabs(TabsLds &t, int tid, int nthreads) {
+    for (int i = tid; i < 41 * 9; i += nthreads) (&t.quot[0][0])[i] = (&K_QUOT[0][0])[i];
+    for (int i = tid; i < 240; i += nthreads) (&t.cards[0][0])[i] = (&K_CARD_ROWS[0][0])[i];
+    for (int i = tid; i < 409; i += nthreads) {
+        t.act_take[i] = K_ACT_TAKE[i];
+        t.act_give[i] = K_ACT_GIVE[i];
+        t.act_rsv[i] = K_ACT_RSV[i];
+    }
+    if (tid < 9) t.recip[tid] = K_RECIP[tid];
+}
+
 // Either an explicit stream of doubles (parity with recorded reference draws) or Philox.
-// Sequential draws reuse the second half of a Philox block. The transition tables (deck
-// draws, per-action gem vectors) travel with the chance source so a kernel can serve them
-// from LDS.
+// Sequential draws reuse the second half of a Philox block. The transition tables travel
+// with the chance source.
 struct Chance {
     const double *u;   // explicit uniforms for this board, or nullptr -> Philox
     uint64_t seed;
     uint32_t board, stream, next;
     double spare = 0.0;
     bool have_spare = false;
-    const double (*quot)[9] = K_QUOT;
-    const uint64_t (*cards)[2] = K_CARD_ROWS;
-    const uint64_t *act_take = K_ACT_TAKE, *act_give = K_ACT_GIVE;
-    const int8_t *act_rsv = K_ACT_RSV;
+    Tabs tab = Tabs{};
     __device__ __forceinline__ double draw() {
         if (u) return u[next++];
         double r;
@@ -509,12 +538,11 @@ __device__ __forceinline__ int kth_bit64(uint64_t x, int k) {
 
 // ------------------------------------------------------------------ transition
 // _get_deck_card (SplendorLogicNumba.py:400-420): colour ~ remaining count, then card ~
-// remaining bit, each by searchsorted(cumsum(p), U, 'right') (:39-41). The probabilities
-// come from K_QUOT / K_RECIP, which hold the correctly rounded quotients the reference
-// divides out (out-of-table counts — unreachable boards — divide). The bitfield is stored
+// remaining bit, each by searchsorted(cumsum(p), U, 'right') (:39-41); K_QUOT / K_RECIP
+// hold the correctly rounded quotients the reference divides out. The bitfield is stored
 // as int8 (packbits wrap, :44-46). Returns false if the tier's deck is empty.
-// colour pick with true divisions, for counts outside K_QUOT (unreachable boards); kept out
-// of line so the common path carries no division code
+// Colour pick with true divisions, for counts outside K_QUOT (unreachable boards); kept out
+// of line so the common path carries no division code.
 __device__ __noinline__ int pick_color_div(uint64_t cnt, int tot, double u) {
     double c = 0.0;
     for (int k = 0; k < 5; k++) {
@@ -522,6 +550,30 @@ __device__ __noinline__ int pick_color_div(uint64_t cnt, int tot, double u) {
         if (c > u) return k;
     }
     return 4;
+}
+
+// Colour / card picks of _get_deck_card. The reference compares fp cumulative sums of the
+// quotients cnt_k / tot (and 1 / nbits) with u; those sums equal the exact fractions
+// C_k / tot to within 1e-15, so away from a boundary the pick is the integer count of
+// prefix sums C_k <= u * tot. Draws within 1e-9 of a boundary (|C_k - u * tot| < 1e-9;
+// about one in 1e9) take the reference's fp sums over the exact quotient tables instead.
+__device__ __noinline__ int pick_color_fp(uint64_t cnt, int tot, double u, const double (*quot)[9]) {
+    const double *q = quot[tot];
+    double c = 0.0;
+    for (int k = 0; k < 5; k++) {
+        c += q[bt(cnt, k)];
+        if (c > u) return k;
+    }
+    return 4;
+}
+__device__ __noinline__ int pick_card_fp(uint32_t b, double u, const double *recip) {
+    const double inv = recip[__builtin_popcount(b)];
+    double c = 0.0;
+    for (int k = 0; k < 8; k++) {
+        c += ((b >> (7 - k)) & 1) ? inv : 0.0;
+        if (c > u) return k;
+    }
+    return 7;
 }
 
 template <int N>
@@ -534,36 +586,40 @@ __device__ __forceinline__ bool deck_card(int8_t *s, int tier, Chance &ch, uint6
 #pragma unroll
     for (int k = 0; k < 5; k++) dom &= (unsigned)bt(cnt, k) <= 8u;
     const double u0 = ch.draw();
-    int color = 4;                                  // cumsum stays below u: last colour
+    int color;
     if (dom) {
-        const double *q = ch.quot[tot];
-        double c = 0.0;
+        const double x = u0 * (double)tot;
+        int ck = 0, n_le = 0;
+        bool amb = false;
 #pragma unroll
         for (int k = 0; k < 5; k++) {
-            c += q[bt(cnt, k)];
-            if (c > u0) { color = k; break; }
+            ck += bt(cnt, k);
+            n_le += (double)ck <= x;
+            amb |= fabs((double)ck - x) < 1e-9;
         }
+        color = amb ? pick_color_fp(cnt, tot, u0, ch.tab.quot) : min(n_le, 4);
     } else {
         color = pick_color_div(cnt, tot, u0);
     }
-    double c;
     const uint32_t b = (uint8_t)bt(bits, color);
     const int nb = __builtin_popcount(b);
-    const double inv = K_RECIP[nb];
     const double u1 = ch.draw();
-    int idx = 7;
-    if (nb) {                                       // nb == 0: every term 0/0 = NaN -> idx 7
-        c = 0.0;
+    const double x = u1 * (double)nb;
+    int pk = 0, n_le = 0;
+    bool amb = false;
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            c += ((b >> (7 - k)) & 1) ? inv : 0.0;
-            if (c > u1) { idx = k; break; }
-        }
+    for (int k = 0; k < 8; k++) {
+        pk += (b >> (7 - k)) & 1;
+        n_le += (double)pk <= x;
+        amb |= fabs((double)pk - x) < 1e-9;
     }
+    // nb == 0 (reference: 0/0 sums, no index above u -> the last card) is ambiguous here
+    // and resolved by the fp path, which returns the last card as well
+    const int idx = amb ? pick_card_fp(b, u1, ch.tab.recip) : min(n_le, 7);
     row(s, Lx::DECKS + 2 * tier + 1) = with_bt(bits, color, (int)(b & ~(1u << (7 - idx))));
     row(s, Lx::DECKS + 2 * tier) = with_bt(cnt, color, bt(cnt, color) - 1);
-    cost = ch.cards[tier * 40 + color * 8 + idx][0];
-    gain = ch.cards[tier * 40 + color * 8 + idx][1];
+    cost = ch.tab.cards[tier * 40 + color * 8 + idx][0];
+    gain = ch.tab.cards[tier * 40 + color * 8 + idx][1];
     return true;
 }
 
@@ -613,6 +669,7 @@ __device__ __forceinline__ void buy_card(int8_t *s, int cost_row, int p) {
     row(s, Lx::GEMS + p) = with_bt(gems, 5, bt(gems, 5) - miss);
     row(s, Lx::BANK) = with_bt(bank, 5, bt(bank, 5) + miss);
     row(s, Lx::CARDS + p) = bytes_add(cards, gain);
+    SPL_PROBE(15)
     give_nobles<N>(s, p);
 }
 
@@ -635,10 +692,12 @@ __device__ __forceinline__ void buy_card(int8_t *s, int cost_row, int p) {
 template <int N>
 __device__ __forceinline__ int make_move(int8_t *s, int a, int p, bool det, Chance &ch) {
     using Lx = Lay<N>;
-    const int rsv = ch.act_rsv[a];
-    const uint64_t take = ch.act_take[a], give = ch.act_give[a];
+    const int rsv = ch.tab.act_rsv[a];
+    const uint64_t take = ch.tab.act_take[a], give = ch.tab.act_give[a];
     const bool buy_vis = a < 12, buy_rsv = a >= 27 && a < 30;
+    SPL_PROBE(10)
     if (buy_vis || buy_rsv) buy_card<N>(s, buy_vis ? Lx::TIERS + 2 * a : Lx::RSV + 6 * p + 2 * (a - 27), p);
+    SPL_PROBE(11)
     int slot = -1;
     if (rsv >= 0) {
         for (int k = 2; k >= 0; k--)
@@ -649,6 +708,7 @@ __device__ __forceinline__ int make_move(int8_t *s, int a, int p, bool det, Chan
             row(s, slot + 1) = row(s, r + 1);
         }
     }
+    SPL_PROBE(12)
     const int tier = buy_vis ? a >> 2 : (rsv >= 0 ? (rsv < 12 ? rsv >> 2 : rsv - 12) : -1);
     if (tier >= 0) {
         uint64_t cost = 0, gain = 0;
@@ -662,6 +722,7 @@ __device__ __forceinline__ int make_move(int8_t *s, int a, int p, bool det, Chan
             row(s, slot + 1) = gain;
         }
     }
+    SPL_PROBE(13)
     if (buy_rsv) {
         for (int r = Lx::RSV + 6 * p + 2 * (a - 27); r < Lx::RSV + 6 * p + 4; r++) row(s, r) = row(s, r + 2);
         row(s, Lx::RSV + 6 * p + 4) = 0;
@@ -676,6 +737,7 @@ __device__ __forceinline__ int make_move(int8_t *s, int a, int p, bool det, Chan
     bank = bytes_add(bytes_sub(bank, take), give);
     row(s, Lx::GEMS + p) = gems;
     row(s, Lx::BANK) = with_bt(bank, 6, bt(bank, 6) + 1);
+    SPL_PROBE(14)
     return (p + 1) % N;
 }
 
@@ -753,13 +815,13 @@ __device__ __forceinline__ int get_score(const int8_t *lds, int p) { return scor
 constexpr int DEAL_DRAWS = 29;                    // 24 card draws + up to 5 nobles
 
 template <int N>
-__device__ __forceinline__ void deal_tier(int8_t *s, int t, const double *u) {
+__device__ __forceinline__ void deal_tier(int8_t *s, int t, const double *u, const Tabs &tab) {
     using Lx = Lay<N>;
     const uint64_t len = t == 0 ? 8 : (t == 1 ? 6 : 4);
     const uint64_t bits = (uint8_t)(0xFFu << (8 - len));
     row(s, Lx::DECKS + 2 * t) = len * 0x0000000101010101ull;
     row(s, Lx::DECKS + 2 * t + 1) = bits * 0x0000000101010101ull;
-    Chance ch{u + 8 * t, 0, 0, 0, 0};
+    Chance ch{u + 8 * t, 0, 0, 0, 0, 0.0, false, tab};
     for (int i = 0; i < 4; i++) fill_new_card<N>(s, t, i, false, ch);
 }
 template <int N>
@@ -794,11 +856,11 @@ __device__ __forceinline__ void wave_philox_uniforms(double *dst, uint64_t seed,
 
 // wave-collective new game from DEAL_DRAWS uniforms u (LDS or HBM)
 template <int N>
-__device__ __forceinline__ void wave_init_game(int8_t *s, const double *u) {
+__device__ __forceinline__ void wave_init_game(int8_t *s, const double *u, const Tabs &tab = Tabs{}) {
     const int l = lane_id();
     for (int r = l; r < Lay<N>::ROWS; r += 64) row(s, r) = 0;
     __builtin_amdgcn_wave_barrier();
-    if (l < 3) deal_tier<N>(s, l, u);
+    if (l < 3) deal_tier<N>(s, l, u, tab);
     else if (l == 3) deal_nobles_bank<N>(s, u);
     __builtin_amdgcn_wave_barrier();
 }
@@ -812,20 +874,23 @@ __device__ __forceinline__ void store_mask(uint64_t *dst, const uint64_t w[7]) {
     }
 }
 
-// k-th set bit of the packed mask (k < popcount); fully unrolled (no runtime indexing)
+// k-th set bit of the packed mask (k < popcount): the word by prefix popcounts, then one
+// halving search inside it (no runtime-indexed arrays: those go to scratch)
 __device__ __forceinline__ int select_bit(const uint64_t w[7], int k) {
-    int res = 408;
-    bool done = false;
+    uint64_t x = w[6];
+    int base = 384, rem = k;
+    int pre = 0;
 #pragma unroll
-    for (int j = 0; j < 7; j++) {
+    for (int j = 0; j < 6; j++) {
         const int c = __popcll(w[j]);
-        if (!done && k < c) {
-            res = 64 * j + kth_bit64(w[j], k);
-            done = true;
-        }
-        if (!done) k -= c;
+        const bool here = k >= pre && k < pre + c;
+        x = here ? w[j] : x;
+        base = here ? 64 * j : base;
+        rem = here ? k - pre : rem;
+        pre += c;
     }
-    return res;
+    if (base == 384) rem = k - pre;
+    return base + kth_bit64(x, rem);
 }
 
 }  // namespace spl

@@ -10,6 +10,26 @@
 #include <new>
 
 #include "../../include/splendor_amd.h"
+
+#ifndef ROLLOUT_ABLATE
+#define ROLLOUT_ABLATE 0   // diagnostic builds only (tools/ablate_rollout.hip): 1 = skip mask, 2 = skip move
+#endif
+#ifndef ROLLOUT_TIMING
+#define ROLLOUT_TIMING 0   // diagnostic builds only (tools/time_rollout.hip): per-block cycle totals
+#endif
+#if ROLLOUT_TIMING
+// block-shared cycle accumulators; SPL_PROBE(k) charges the cycles since the previous probe
+// to slot k (thread 0's view; in product builds SPL_PROBE expands to nothing)
+__shared__ uint64_t spl_probe_acc[24];
+__shared__ uint64_t spl_probe_last;
+#define SPL_PROBE(k)                                                                       \
+    if (threadIdx.x == 0) {                                                                \
+        const uint64_t c_ = clock64();                                                     \
+        spl_probe_acc[k] += c_ - spl_probe_last;                                           \
+        spl_probe_last = c_;                                                               \
+    }
+__device__ uint64_t *g_rollout_timing;
+#endif
 #include "splendor_device.h"
 
 using namespace spl;
@@ -166,19 +186,7 @@ __global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__re
 //            move's masks go to HBM
 //   store    boards, players, game counters LDS -> HBM
 constexpr int RB = 64;
-#ifndef ROLLOUT_ABLATE
-#define ROLLOUT_ABLATE 0   // diagnostic builds only (tools/ablate_rollout.hip): 1 = skip mask, 2 = skip move
-#endif
-#ifndef ROLLOUT_TIMING
-#define ROLLOUT_TIMING 0   // diagnostic builds only: per-block phase cycle totals into g_rollout_timing
-#endif
-#if ROLLOUT_TIMING
-__device__ uint64_t *g_rollout_timing;
-#define RT_MARK(k)                                                                          \
-    if (threadIdx.x == 0) { const uint64_t c_ = clock64(); rt[k] += c_ - rt_last; rt_last = c_; }
-#else
-#define RT_MARK(k)
-#endif
+#define RT_MARK(k) SPL_PROBE(k)
 template <int N>
 struct RolloutLds {
     static constexpr int STRIDE = (Lay<N>::ROWS % 2 ? Lay<N>::ROWS : Lay<N>::ROWS + 1) * 8;
@@ -202,10 +210,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     __shared__ int32_t gdone[RB];
     __shared__ double ud[RB][4];       // draws 0..3 of each board's step stream
     __shared__ double ub[WAVES][DEAL_DRAWS];
-    __shared__ double quot[41][9];
-    __shared__ uint64_t cards[120][2];
-    __shared__ uint64_t act_take[409], act_give[409];
-    __shared__ int8_t act_rsv[409];
+    __shared__ TabsLds tabs;
     __shared__ uint32_t lut_diff[32];
     __shared__ uint64_t lut_s3[1024];
     __shared__ uint16_t reset16[WAVES];
@@ -213,7 +218,8 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
     int8_t *const gst = state + (size_t)b0 * Lx::S;
 #if ROLLOUT_TIMING
-    uint64_t rt[6] = {0, 0, 0, 0, 0, 0}, rt_last = clock64();
+    if (tid < 24) spl_probe_acc[tid] = 0;
+    if (tid == 0) spl_probe_last = clock64();
     const uint64_t wall0 = wall_clock64();
 #endif
     for (int i = tid; i < nb * Cv::UNITS; i += THREADS) {
@@ -224,13 +230,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         pl[tid] = player[b0 + tid];
         gdone[tid] = games_done ? games_done[b0 + tid] : 0;
     }
-    for (int i = tid; i < 41 * 9; i += THREADS) (&quot[0][0])[i] = (&K_QUOT[0][0])[i];
-    for (int i = tid; i < 240; i += THREADS) (&cards[0][0])[i] = (&K_CARD_ROWS[0][0])[i];
-    for (int i = tid; i < 409; i += THREADS) {
-        act_take[i] = K_ACT_TAKE[i];
-        act_give[i] = K_ACT_GIVE[i];
-        act_rsv[i] = K_ACT_RSV[i];
-    }
+    stage_tabs(tabs, tid, THREADS);
     for (int i = tid; i < 1024; i += THREADS) lut_s3[i] = K_LUT_SPEC3[i];
     if (tid < 32) lut_diff[tid] = K_LUT_DIFF[tid];
     __syncthreads();
@@ -265,9 +265,11 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                 if (!cnt) { m[6] |= 1ull << (408 - 384); msk[b][6] = m[6]; cnt = 1; }
                 a = select_bit(m, (int)(ud[b][0] * (double)cnt));
             }
+            RT_MARK(5)
             int8_t *s = lds + b * ST;
-            Chance ch{&ud[b][0], 0, 0, 0, 1, 0.0, false, quot, cards, act_take, act_give, act_rsv};
+            Chance ch{&ud[b][0], 0, 0, 0, 1, 0.0, false, tabs.view()};
             int nxt = make_move<N>(s, a, pl[b], false, ch);
+            RT_MARK(6)
             float e[N];
             check_end<N>(s, e);
 #pragma unroll
@@ -275,6 +277,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                 ended |= e[i] != 0.f;
                 ended_out[(ob + b) * N + i] = e[i];
             }
+            RT_MARK(7)
             action_out[ob + b] = (int16_t)a;
             if (ended) {
                 nxt = 0;
@@ -293,7 +296,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
             if ((i & (WAVES - 1)) != w) continue;
             const int rb = __ffsll((unsigned long long)rm) - 1;
             wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)(b0 + rb), step, 3, DEAL_DRAWS);
-            wave_init_game<N>(lds + rb * ST, ub[w]);
+            wave_init_game<N>(lds + rb * ST, ub[w], tabs.view());
         }
         if (mask_out && ROLLOUT_ABLATE != 1)
             for (int i = tid; i < nb * 7; i += THREADS) mask_out[ob * 7 + i] = (&msk[0][0])[i];
@@ -312,14 +315,10 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     __syncthreads();
     RT_MARK(4)
     if (threadIdx.x == 0) {
-        uint64_t *o = g_rollout_timing + (size_t)blockIdx.x * 8;
-        for (int k = 0; k < 5; k++) o[k] = rt[k];
-        o[5] = wall0;
-        o[6] = wall_clock64();
-        uint32_t hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        o[7] = ((uint64_t)xcc << 32) | hw;
+        uint64_t *o = g_rollout_timing + (size_t)blockIdx.x * 32;
+        for (int k = 0; k < 24; k++) o[k] = spl_probe_acc[k];
+        o[24] = wall0;
+        o[25] = wall_clock64();
     }
 #endif
 }

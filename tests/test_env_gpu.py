@@ -82,6 +82,32 @@ def test_chance_step_matches_reference(engines, n):
 
 
 @pytest.mark.parametrize("n", NS)
+def test_deck_draw_boundary_uniforms(engines, n):
+    """Deck draws with uniforms on (and one ulp around) the cumulative-fraction boundaries
+    k / tot and k / nbits, where the device's integer pick defers to the reference's fp
+    cumulative sums: every visible-card buy and every deck reserve of the golden states."""
+    e, d = engines[n], load(f"env_{n}p.npz")
+    base = [j / t for t in range(1, 41) for j in range(t)] + [1 - 2 ** -53]
+    cand = np.unique(np.concatenate([base, np.nextafter(base, 0), np.nextafter(base, 1)]))
+    cand = cand[(cand >= 0) & (cand < 1)]
+    rng = np.random.default_rng(5 + n)
+    st0, pl0 = d["state"], d["player"]
+    states, players, acts, us = [], [], [], []
+    for i in range(len(st0)):
+        m = O.valid_moves(n, st0[i], int(pl0[i]))
+        for a in np.flatnonzero(m[:27]):             # buys of visible cards and reserves
+            for _ in range(3):
+                states.append(st0[i]); players.append(pl0[i]); acts.append(a)
+                us.append(rng.choice(cand, 2))
+    B = len(states)
+    st, pl, ac, u = np.stack(states), np.array(players, np.int8), np.array(acts, np.int16), np.stack(us)
+    want = np.stack([O.make_move(n, st[b], int(ac[b]), int(pl[b]), False, u[b])[0] for b in range(B)])
+    dst = dev(st)
+    e.step(dst, dev(ac), dev(pl), None, deterministic=False, uniforms=dev(np.ascontiguousarray(u)))
+    np.testing.assert_array_equal(dst.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("n", NS)
 def test_tree_step_matches_reference(engines, n):
     e, d = engines[n], load(f"env_{n}p.npz")
     parents = d["canon"][d["det_src"]]

@@ -12,31 +12,38 @@ int main() {
     int8_t *st, *pl; uint64_t *mk; int16_t *ac; float *en; int32_t *gd; uint64_t *tm;
     (void)hipMalloc(&st, (size_t)B * 392); (void)hipMalloc(&pl, B); (void)hipMalloc(&mk, (size_t)K * B * 56);
     (void)hipMalloc(&ac, (size_t)K * 2 * B); (void)hipMalloc(&en, (size_t)K * 8 * B); (void)hipMalloc(&gd, 4 * B);
-    (void)hipMalloc(&tm, (size_t)NB * 8 * 8);
+    (void)hipMalloc(&tm, (size_t)NB * 32 * 8);
     (void)hipMemset(gd, 0, 4 * B);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rollout_timing), &tm, sizeof(tm));
     spl_init(c, B, st, pl, nullptr, 0, 0x5EED, 0xFFFFFFFFu, 0, nullptr);
     for (int k = 0; k < 5; k++) spl_rollout_run(c, B, K, st, pl, mk, ac, en, gd, 0x5EED, K * k, 0, nullptr);
     (void)hipDeviceSynchronize();
-    std::vector<uint64_t> h((size_t)NB * 8);
-    const char *names[] = {"load", "mask/move", "move/step", "reset+mask store", "store"};
+    std::vector<uint64_t> h((size_t)NB * 32);
+    // probe slots (splendor_env.hip / splendor_device.h SPL_PROBE)
+    const int slots[] = {0, 1, 5, 10, 15, 11, 12, 13, 14, 7, 2, 3, 4};
+    const char *names[] = {"load", "mask", "move: select", "move: decode", "move: buy (pay)",
+                           "move: buy (nobles)", "move: reserve slot", "move: deck draw",
+                           "move: shift+gems", "move: end+outputs", "move: tail to sync",
+                           "reset+mask store", "store"};
+    const bool per_move[] = {false, true, true, true, true, true, true, true, true, true, true, true, false};
+    const int NS = 13;
     for (int rep = 0; rep < 2; rep++) {
         spl_rollout_run(c, B, K, st, pl, mk, ac, en, gd, 0x5EED, 200 + K * rep, 0, nullptr);
         (void)hipDeviceSynchronize();
         (void)hipMemcpy(h.data(), tm, h.size() * 8, hipMemcpyDeviceToHost);
         uint64_t w0 = ~0ull, w1 = 0;
-        std::vector<double> ph[5], life;
+        std::vector<double> ph[NS], life;
         for (int b = 0; b < NB; b++) {
-            const uint64_t *r = &h[(size_t)b * 8];
-            w0 = std::min(w0, r[5]); w1 = std::max(w1, r[6]);
-            for (int k = 0; k < 5; k++) ph[k].push_back((double)r[k] / (k >= 1 && k <= 3 ? K : 1));
-            life.push_back((double)(r[6] - r[5]) / 100.0);
+            const uint64_t *r = &h[(size_t)b * 32];
+            w0 = std::min(w0, r[24]); w1 = std::max(w1, r[25]);
+            for (int k = 0; k < NS; k++) ph[k].push_back((double)r[slots[k]] / (per_move[k] ? K : 1));
+            life.push_back((double)(r[25] - r[24]) / 100.0);
         }
         printf("rep %d: K=%d moves, kernel span %.2f us (%.2f us/move)\n", rep, K, (w1 - w0) / 100.0, (w1 - w0) / 100.0 / K);
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NS; k++) {
             std::sort(ph[k].begin(), ph[k].end());
-            printf("  %-18s cycles%s p10 %8.0f  p50 %8.0f  p90 %8.0f  max %8.0f\n", names[k],
-                   k >= 1 && k <= 3 ? "/move" : "     ", ph[k][NB / 10], ph[k][NB / 2], ph[k][NB * 9 / 10], ph[k][NB - 1]);
+            printf("  %-22s cycles%s p10 %8.0f  p50 %8.0f  p90 %8.0f  max %8.0f\n", names[k],
+                   per_move[k] ? "/move" : "     ", ph[k][NB / 10], ph[k][NB / 2], ph[k][NB * 9 / 10], ph[k][NB - 1]);
         }
         std::sort(life.begin(), life.end());
         printf("  block life us p10 %.2f p50 %.2f p90 %.2f max %.2f\n", life[NB / 10], life[NB / 2], life[NB * 9 / 10], life[NB - 1]);
