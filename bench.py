@@ -116,9 +116,10 @@ def run_selfplay(args, rank, world, dev, dist):
             "device_bytes": sp.device_bytes}
 
 
-def load_traffic(path, B):
-    """Measured HBM bytes per launch from the newest committed rocprofv3 --pmc summary
-    (profiles/rNN_rollout_pmc.json, corrected as DESIGN.md §6 describes), if any."""
+def load_traffic(path, B, moves):
+    """The newest committed rocprofv3 --pmc summary of this workload (profiles/
+    rNN_rollout_pmc.json, tools/pmc_rollout.sh; HBM bytes corrected as DESIGN.md §6
+    describes), if it was taken at this board count and launch size."""
     if not path:
         import glob
         found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_rollout_pmc.json")))
@@ -127,9 +128,9 @@ def load_traffic(path, B):
         return None
     with open(path) as f:
         d = json.load(f)
-    if d.get("boards") != B:
+    if d.get("boards") != B or d.get("moves_per_launch", 1) != moves:
         return None
-    return d.get("hbm_bytes_per_launch")
+    return d
 
 
 def main():
@@ -247,7 +248,10 @@ def main():
     if rank == 0:
         per = bytes_per_board_launch(args.players, chunk)
         achieved = per * B / (kernel_ms * 1e-3) / 1e9
-        traffic = load_traffic(args.traffic_json, B)
+        prof = load_traffic(args.traffic_json, B, chunk)
+        traffic = prof.get("hbm_bytes_per_launch") if prof else None
+        issue = ({k: prof.get(k) for k in ("valu_insts_per_board_move", "valu_issue_frac", "effective_clock_ghz")}
+                 if prof else None)
         out = {
             "metric": METRIC,
             "value": world * B * K / elapsed,
@@ -270,6 +274,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"k_rollout<{args.players}>", "kernel_avg_us": kernel_ms * 1e3,
                          "moves_per_launch": chunk, "bytes_per_board_launch": per,
+                         "valu_issue": issue,
                          "note": "VALU-issue bound, not HBM bound: see DESIGN.md §5"},
             "cpu_baseline": cpu,
             "games_completed": games,
