@@ -45,6 +45,8 @@ _SIGS = {
     "spl_tree_step": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_rollout_step": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.c_uint32,
                           C.c_uint32, _vp], C.c_int),
+    "spl_nn_packed_floats": ([C.c_int], C.c_int),
+    "spl_nn_forward": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_rollout_run": ([C.c_void_p, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64,
                          C.c_uint32, C.c_uint32, _vp], C.c_int),
     "spl_mcts_create": ([C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)], C.c_int),

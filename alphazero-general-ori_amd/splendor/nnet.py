@@ -6,8 +6,9 @@ heads). Parameter names follow the reference's state_dict keys so checkpoints sa
 state_dicts load with torch.load(weights_only=True).
 
 Inference path (`LeafEvaluator`): eval-mode BatchNorms are folded into per-channel affine
-terms once, the score-diff head (training-only) is skipped, and the whole
-"int8 leaves -> pi, v" computation is captured in a HIP graph at a fixed batch.
+terms once, the score-diff head (training-only) is skipped, and "int8 leaves -> pi, v" runs
+as one fused HIP kernel (csrc/nnet.hip, spl_nn_forward; fp32 MFMA) — or, for reference,
+as the PyTorch-ROCm FoldedNet, optionally captured in a HIP graph at a fixed batch.
 Returns exp(masked log_softmax(pi)) and tanh(v) like GenericNNetWrapper.predict (:141-168).
 """
 import ctypes as C
@@ -156,6 +157,56 @@ class FoldedNet(nn.Module):
         return pi, v
 
 
+def pack_weights(folded, n_players):
+    """Pack a FoldedNet into the layout k_nn_forward reads (include/splendor_amd.h,
+    spl_nn_forward): per layer the MFMA B-fragment order [NT][S/4][64][4] with
+    element (nt, q, l, j) = W[32 nt + (l & 31)][4 q + j + (l >> 5) S], then the 0-padded
+    bias; finally the per-column BN affines s1, t1, sp1, tp1."""
+    f = folded
+    layers = [(f.w1, f.b1), (f.w2, f.b2), (f.wp1, f.bp1), (f.w3, f.b3), (f.w4, f.b4), (f.wp4, f.bp4),
+              (f.w5a, f.b5a), (f.w5b, f.b5b), (f.wp5, f.bp5), (f.wpi1, f.bpi1), (f.wpi2, f.bpi2),
+              (f.wv1, f.bv1), (f.wv2, f.bv2)]
+    parts = []
+    with torch.no_grad():
+        for w, b in layers:
+            N, K = w.shape
+            kp = (K + 7) // 8 * 8
+            S, NT = kp // 2, (N + 31) // 32
+            wp = torch.zeros((NT * 32, kp), dtype=torch.float32, device=w.device)
+            wp[:N, :K] = w
+            # [nt][col][h][q][j] -> [nt][q][h][col][j]; lane = 32 h + col
+            wr = wp.view(NT, 32, 2, S // 4, 4).permute(0, 3, 2, 1, 4)
+            parts.append(wr.reshape(-1))
+            bp = torch.zeros(NT * 32, dtype=torch.float32, device=w.device)
+            bp[:N] = b
+            parts.append(bp)
+        parts += [f.s1.reshape(7), f.t1.reshape(7), f.sp1.reshape(7), f.tp1.reshape(7)]
+        out = torch.cat([p.float() for p in parts]).contiguous()
+    want = _lib.lib().spl_nn_packed_floats(n_players)
+    if out.numel() != want:
+        raise _lib.EngineError(f"packed network has {out.numel()} floats, engine expects {want}")
+    return out
+
+
+class FusedNet:
+    """SplendorNNet inference through the fused HIP kernel (spl_nn_forward): int8 leaf
+    boards + packed masks -> (softmax policy, tanh value), all fp32."""
+
+    def __init__(self, net, n_players, device):
+        self.n = n_players
+        self.device = torch.device(device)
+        self.w = pack_weights(FoldedNet(net).to(self.device).eval(), n_players)
+
+    def __call__(self, leaf_state, leaf_mask, pi=None, v=None):
+        B = leaf_state.shape[0]
+        pi = pi if pi is not None else torch.empty((B, ACTIONS), dtype=torch.float32, device=self.device)
+        v = v if v is not None else torch.empty((B, self.n), dtype=torch.float32, device=self.device)
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(_lib.lib().spl_nn_forward(self.n, B, _ptr(leaf_state), _ptr(leaf_mask), _ptr(self.w), _ptr(pi),
+                                             _ptr(v), s), "spl_nn_forward")
+        return pi, v
+
+
 def random_net(n_players=2, seed=0, device="cuda"):
     """Seeded random-init SplendorNNet (no pretrained weights load safely)."""
     g = torch.random.fork_rng(devices=[])
@@ -167,13 +218,21 @@ def random_net(n_players=2, seed=0, device="cuda"):
 
 class LeafEvaluator:
     """Batched nnet.predict for the search (GenericNNetWrapper.predict, :141-168): int8 leaf
-    boards + packed masks -> (pi f32 [B,409], v f32 [B,n]); optional HIP-graph capture."""
+    boards + packed masks -> (pi f32 [B,409], v f32 [B,n]).
 
-    def __init__(self, engine, net, B, use_graph=True):
+    fused=True (default): one spl_nn_forward launch (the fused HIP network kernel).
+    fused=False: the PyTorch-ROCm FoldedNet (hipBLASLt GEMMs; reference for the tests),
+    optionally captured in a HIP graph."""
+
+    def __init__(self, engine, net, B, use_graph=True, fused=True):
         self.e = engine
         self.B = B
+        self.fused = FusedNet(net, engine.n, engine.device) if fused else None
         self.net = FoldedNet(net).to(engine.device).eval()
         dev = engine.device
+        if fused:
+            self.pi_buf = torch.empty((B, ACTIONS), dtype=torch.float32, device=dev)
+            self.v_buf = torch.empty((B, engine.n), dtype=torch.float32, device=dev)
         self.x = torch.zeros((B, 7, engine.rows), dtype=torch.float32, device=dev)   # transposed
         self.valid = torch.zeros((B, ACTIONS), dtype=torch.bool, device=dev)
         self.use_graph = use_graph
@@ -193,6 +252,8 @@ class LeafEvaluator:
 
     @torch.no_grad()
     def __call__(self, leaf_state, leaf_mask, leaf_valid=None):
+        if self.fused is not None:
+            return self.fused(leaf_state, leaf_mask, self.pi_buf, self.v_buf)
         if not self.use_graph:
             return self._run(leaf_state, leaf_mask)
         key = (leaf_state.data_ptr(), leaf_mask.data_ptr())

@@ -18,7 +18,8 @@
  *   - player arrays are int8 (0..n-1); a NULL player pointer means "player 0 everywhere".
  *   - chance: either explicit uniforms (u != NULL: board b consumes u[b*u_stride + k],
  *     k = 0,1,.. in the reference's draw order) or counter-based Philox4x32-10 with
- *     key = seed and counter = (k, board_base + b, stream, 'SPLD').
+ *     key = seed: uniform k is half (k & 1) of the block at counter
+ *     (k >> 1, board_base + b, stream, 'SPLD'), 53 bits from words (0,1) or (2,3).
  *   - hip_stream: a hipStream_t (NULL = default stream).
  *   - Return value: 0 ok; SPL_EINVAL bad argument; SPL_EDEVICE HIP launch/runtime error.
  *     Per-board errors found on device (action out of range) are OR-ed into *err when
@@ -202,6 +203,27 @@ int spl_nn_input(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t 
  * tree-only throughput runs */
 int spl_hash_eval(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask,
                   float *pi, float *v, void *hip_stream);
+
+/* ===================================================================== network
+ * SplendorNNet inference (SplendorNNet.py:56-159 in eval mode; GenericNNetWrapper.predict
+ * :141-168 minus the host round trip) as one fused kernel: int8 boards [B][R][7] + packed
+ * masks [B][7] -> pi [B][409] = softmax(masked logits, invalid -> -1e8) and v [B][n] =
+ * tanh(value head). fp32 throughout (products and accumulation in f32, MFMA).
+ *
+ * packed_weights: spl_nn_packed_floats(n) floats, 16-byte aligned, the eval-mode network
+ * with BatchNorms folded (splendor/nnet.py pack_weights). For each of the 13 linear layers
+ * (N outputs, K inputs) in the order dense2d_1[0], dense2d_1[3], partialgpool_1 dense,
+ * dense2d_3, dense1d_4, partialgpool_4 dense, dense1d_5[0], dense1d_5[3], partialgpool_5
+ * dense, output_layers_PI[0], [1], output_layers_V[0], [1]:
+ *     Kp = K rounded up to 8, S = Kp / 2, NT = ceil(N / 32)
+ *     weights [NT][S/4][64][4]: element (nt, q, l, j) = W[32 nt + (l & 31)][4 q + j + (l >> 5) S]
+ *             (0 outside N x K)
+ *     bias    [32 NT] (0-padded)
+ * then the per-board-column BatchNorm affines of dense2d_1 and partialgpool_1:
+ * s1[7], t1[7], sp1[7], tp1[7] (y = x * s + t). Returns the float count or SPL_EINVAL. */
+int spl_nn_packed_floats(int n_players);
+int spl_nn_forward(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
+                   const float *packed_weights, float *pi, float *v, void *hip_stream);
 
 #ifdef __cplusplus
 }
