@@ -2,10 +2,13 @@
 // gfx950 kernel: int8 leaf boards + packed legality masks in, masked softmax policy and
 // tanh values out (GenericNNetWrapper.predict, :141-168). C ABI: include/splendor_amd.h.
 //
-// One 256-thread workgroup evaluates ML = 32 leaves through all 13 dense layers with every
+// One 512-thread workgroup (8 waves, two per SIMD so one wave's LDS / L2 latency hides
+// behind the other's MFMAs) evaluates ML = 32 leaves through all 13 dense layers with every
 // activation on chip:
 //   * GEMMs on v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation: the reference
-//     network's precision). Wave w owns output columns [32w, 32w+32) of a 128-wide layer.
+//     network's precision). Wave w owns output columns [32(w&3), 32(w&3)+32) of a 128-wide
+//     layer; the two wave groups (w>>2) split the token tiles of the per-column layers and
+//     the K range of the per-leaf layers (partial sums combined through LDS).
 //   * The per-board-column layers (dense2d_1, dense2d_3, partialgpool_1) treat the 7 board
 //     columns of the 32 leaves as 7 token tiles of 32 (channel-major), so the per-column
 //     BatchNorm affine is uniform across an MFMA tile.
@@ -23,7 +26,7 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int NNT = 256;       // threads per workgroup (4 waves)
+constexpr int NNT = 512;       // threads per workgroup (8 waves)
 constexpr int ML = 32;         // leaves per workgroup
 constexpr int XS = 132;        // activation row stride (floats)
 constexpr int LS = 420;        // logits row stride (floats)
@@ -67,10 +70,11 @@ __device__ __forceinline__ void mfma4(const float4 &a, const float4 &b, f32x16 &
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
 }
 
-// T token tiles x one N tile (column block nt) over K = 2S: acc[t] = A_t . W^T
+// token tiles t0 .. t0+nt_tok-1 (<= T) x one N tile (column block nt) over K = 2S
 // wp: packed weights of the layer; afetch(t, col) -> float4 of A[token tile t][lane row][col..col+3]
 template <int T, int S, class AF>
-__device__ __forceinline__ void gemm_tiles(const float *__restrict__ wp, int nt, AF afetch, f32x16 acc[T]) {
+__device__ __forceinline__ void gemm_tiles(const float *__restrict__ wp, int nt, int t0, int nt_tok, AF afetch,
+                                           f32x16 acc[T]) {
     const int lane = threadIdx.x & 63, h = lane >> 5;
     const float4 *w4 = reinterpret_cast<const float4 *>(wp) + (size_t)nt * (S / 4) * 64 + lane;
 #pragma unroll
@@ -81,20 +85,22 @@ __device__ __forceinline__ void gemm_tiles(const float *__restrict__ wp, int nt,
         const float4 b = bn;
         if (s4 + 1 < S / 4) bn = w4[(s4 + 1) * 64];
 #pragma unroll
-        for (int t = 0; t < T; t++) mfma4(afetch(t, h * S + 4 * s4), b, acc[t]);
+        for (int t = 0; t < T; t++)
+            if (t < nt_tok) mfma4(afetch(t0 + t, h * S + 4 * s4), b, acc[t]);
     }
 }
 
-// one token tile x up to NT column blocks {nt0, nt0 + step, ...} < ntot (shared A operand)
+// one token tile x up to NT column blocks {nt0, nt0 + step, ...} < ntot (shared A operand),
+// over the step range [q0, q1) of the S/4 float4 steps
 template <int NT, int S, class AF>
-__device__ __forceinline__ void gemm_cols(const float *__restrict__ wp, int nt0, int step, int ntot, AF afetch,
-                                          f32x16 acc[NT]) {
+__device__ __forceinline__ void gemm_cols(const float *__restrict__ wp, int nt0, int step, int ntot, int q0, int q1,
+                                          AF afetch, f32x16 acc[NT]) {
     const int lane = threadIdx.x & 63, h = lane >> 5;
 #pragma unroll
     for (int j = 0; j < NT; j++) acc[j] = zero16();
     const float4 *w4 = reinterpret_cast<const float4 *>(wp) + lane;
 #pragma unroll 2
-    for (int s4 = 0; s4 < S / 4; s4++) {
+    for (int s4 = q0; s4 < q1; s4++) {
         const float4 a = afetch(0, h * S + 4 * s4);
 #pragma unroll
         for (int j = 0; j < NT; j++) {
@@ -121,8 +127,11 @@ __global__ __launch_bounds__(NNT) void k_nn_forward(int B, const int8_t *__restr
     __shared__ __align__(16) float bufP[ML * XS];          // per-leaf ping
     __shared__ __align__(16) float bufQ[ML * XS];          // per-leaf pong
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 31;
+    const int wc = w & 3, wg = w >> 2;                     // column block, wave group
     const int b0 = blockIdx.x * ML, nb = min(ML, B - b0);
     const float *aff = W + Nt::AFF;                        // s1, t1, sp1, tp1
+    float *scratch = bufA + 7 * ML * XS - 4 * 16 * 64;     // split-K partials (per-leaf layers)
+    const int t0 = 4 * wg, ntok = wg ? 3 : 4;              // this wave's token tiles (per-column layers)
 
     // ---- input: x[column c][leaf i][row r] = state[leaf][r][c] as int8 (token c*32+i)
     int8_t *x0 = reinterpret_cast<int8_t *>(bufA);
@@ -134,82 +143,75 @@ __global__ __launch_bounds__(NNT) void k_nn_forward(int B, const int8_t *__restr
     }
     __syncthreads();
 
-    f32x16 acc7[7];
+    f32x16 acc[4];
+    const int col = 32 * wc + acc_col();
+    // per-column epilogue over this wave's token tiles: dst = f(acc, t, n)
+    auto store_tiles = [&](int coloff, auto f) {
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            if (t < ntok)
+#pragma unroll
+                for (int r = 0; r < 16; r++)
+                    bufA[((t0 + t) * ML + acc_row(r)) * XS + coloff] = f(acc[t][r], t0 + t);
+    };
+    auto fetchA = [&](int col0) {
+        return [&, col0](int t, int c) { return ld4(bufA + (t * ML + li) * XS + col0 + c); };
+    };
     // ---- dense2d_1: relu(s1[c] * (W1 x + b1) + t1[c])
     {
         constexpr int S = kpad(R) / 2;
-        gemm_tiles<7, S>(W + Nt::woff(0), w, [&](int t, int col) {
-            const int v = *reinterpret_cast<const int32_t *>(x0 + (t * ML + li) * X0S + col);
+        gemm_tiles<4, S>(W + Nt::woff(0), wc, t0, ntok, [&](int t, int c) {
+            const int v = *reinterpret_cast<const int32_t *>(x0 + (t * ML + li) * X0S + c);
             return make_float4((float)(int8_t)v, (float)(int8_t)(v >> 8), (float)(int8_t)(v >> 16), (float)(v >> 24));
-        }, acc7);
+        }, acc);
         __syncthreads();
-        const float bias = W[Nt::boff(0) + 32 * w + acc_col()];
-#pragma unroll
-        for (int t = 0; t < 7; t++) {
-            const float s = aff[t], o = aff[7 + t];
-#pragma unroll
-            for (int r = 0; r < 16; r++)
-                bufA[(t * ML + acc_row(r)) * XS + 32 * w + acc_col()] = fmaxf((acc7[t][r] + bias) * s + o, 0.f);
-        }
+        const float bias = W[Nt::boff(0) + col];
+        store_tiles(col, [&](float x, int t) { return fmaxf((x + bias) * aff[t] + aff[7 + t], 0.f); });
         __syncthreads();
     }
-    auto fetchA = [&](int col0) {
-        return [&, col0](int t, int col) { return ld4(bufA + (t * ML + li) * XS + col0 + col); };
-    };
     // ---- dense2d_1[3]: relu(W2 x + b2)
     {
-        gemm_tiles<7, 64>(W + Nt::woff(1), w, fetchA(0), acc7);
+        gemm_tiles<4, 64>(W + Nt::woff(1), wc, t0, ntok, fetchA(0), acc);
         __syncthreads();
-        const float bias = W[Nt::boff(1) + 32 * w + acc_col()];
-#pragma unroll
-        for (int t = 0; t < 7; t++)
-#pragma unroll
-            for (int r = 0; r < 16; r++)
-                bufA[(t * ML + acc_row(r)) * XS + 32 * w + acc_col()] = fmaxf(acc7[t][r] + bias, 0.f);
+        const float bias = W[Nt::boff(1) + col];
+        store_tiles(col, [&](float x, int) { return fmaxf(x + bias, 0.f); });
         __syncthreads();
     }
     // ---- partialgpool_1: [max, mean over 4 groups of 8 of x[0:32]] ++ relu(BN(Wp1 x[32:] + bp1))
     {
-        gemm_tiles<7, 48>(W + Nt::woff(2), w, fetchA(32), acc7);
-        float pv[7];
+        gemm_tiles<4, 48>(W + Nt::woff(2), wc, t0, ntok, fetchA(32), acc);
+        constexpr int NQ = (7 * ML * 8 + NNT - 1) / NNT;
+        float pv[NQ];
 #pragma unroll
-        for (int q = 0; q < 7; q++) {
+        for (int q = 0; q < NQ; q++) {
             const int item = tid + NNT * q, tok = item >> 3, j = item & 7, g = j & 3;
-            const float *p = bufA + tok * XS + 8 * g;
-            float m = p[0], s = p[0];
+            pv[q] = 0.f;
+            if (item < 7 * ML * 8) {
+                const float *p = bufA + tok * XS + 8 * g;
+                float m = p[0], s = p[0];
 #pragma unroll
-            for (int k = 1; k < 8; k++) { m = fmaxf(m, p[k]); s += p[k]; }
-            pv[q] = j < 4 ? m : s / 8.f;
+                for (int k = 1; k < 8; k++) { m = fmaxf(m, p[k]); s += p[k]; }
+                pv[q] = j < 4 ? m : s / 8.f;
+            }
         }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 7; q++) {
+        for (int q = 0; q < NQ; q++) {
             const int item = tid + NNT * q;
-            bufA[(item >> 3) * XS + (item & 7)] = pv[q];
+            if (item < 7 * ML * 8) bufA[(item >> 3) * XS + (item & 7)] = pv[q];
         }
-        const int n = 32 * w + acc_col();
-        if (n < 120) {
-            const float bias = W[Nt::boff(2) + n];
-#pragma unroll
-            for (int t = 0; t < 7; t++) {
-                const float s = aff[14 + t], o = aff[21 + t];
-#pragma unroll
-                for (int r = 0; r < 16; r++)
-                    bufA[(t * ML + acc_row(r)) * XS + 8 + n] = fmaxf((acc7[t][r] + bias) * s + o, 0.f);
-            }
+        if (col < 120) {
+            const float bias = W[Nt::boff(2) + col];
+            store_tiles(8 + col, [&](float x, int t) { return fmaxf((x + bias) * aff[14 + t] + aff[21 + t], 0.f); });
         }
         __syncthreads();
     }
     // ---- dense2d_3: relu(W3 x + b3)
     {
-        gemm_tiles<7, 64>(W + Nt::woff(3), w, fetchA(0), acc7);
+        gemm_tiles<4, 64>(W + Nt::woff(3), wc, t0, ntok, fetchA(0), acc);
         __syncthreads();
-        const float bias = W[Nt::boff(3) + 32 * w + acc_col()];
-#pragma unroll
-        for (int t = 0; t < 7; t++)
-#pragma unroll
-            for (int r = 0; r < 16; r++)
-                bufA[(t * ML + acc_row(r)) * XS + 32 * w + acc_col()] = fmaxf(acc7[t][r] + bias, 0.f);
+        const float bias = W[Nt::boff(3) + col];
+        store_tiles(col, [&](float x, int) { return fmaxf(x + bias, 0.f); });
         __syncthreads();
     }
     // ---- FlattenAndPartialGPool(64, 5): pool[i] = [max_c<5 x[c][i][0:64], mean_c<5 ...]
@@ -226,96 +228,106 @@ __global__ __launch_bounds__(NNT) void k_nn_forward(int B, const int8_t *__restr
         bufP[i * XS + 64 + f] = s / 5.f;
     }
     __syncthreads();
-    f32x16 acc4[4];
+    // per-leaf layer, 4 column blocks, K split between the wave groups; the summed tile goes to
+    // group 0, which applies f(x, n) and writes dst (f returns NaN-free values only for n < nmax)
+    auto leaf_layer = [&](auto gemm, float *dst, int dst_off, int nmax, auto f) {
+        gemm();
+        __syncthreads();
+        if (wg) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) scratch[(wc * 16 + r) * 64 + lane] = acc[0][r];
+        }
+        __syncthreads();
+        if (!wg && col < nmax) {
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                dst[acc_row(r) * XS + dst_off + col] = f(acc[0][r] + scratch[(wc * 16 + r) * 64 + lane]);
+        }
+        __syncthreads();
+    };
     // ---- dense1d_4 over the 704 flattened features: [pool 128][x[5][:64]][x[6][:64]][x[c][64:128], c<7]
     {
-        gemm_cols<1, 352>(W + Nt::woff(4), w, 4, 4, [&](int, int k) {
-            if (k < 128) return ld4(bufP + li * XS + k);
-            if (k < 256) return ld4(bufA + ((5 + ((k - 128) >> 6)) * ML + li) * XS + ((k - 128) & 63));
-            return ld4(bufA + (((k - 256) >> 6) * ML + li) * XS + 64 + ((k - 256) & 63));
-        }, acc4);
-        __syncthreads();
-        const float bias = W[Nt::boff(4) + 32 * w + acc_col()];
-#pragma unroll
-        for (int r = 0; r < 16; r++) bufQ[acc_row(r) * XS + 32 * w + acc_col()] = fmaxf(acc4[0][r] + bias, 0.f);
-        __syncthreads();
+        const float bias = W[Nt::boff(4) + col];
+        leaf_layer([&] {
+            gemm_cols<1, 352>(W + Nt::woff(4), wc, 4, 4, 44 * wg, 44 * wg + 44, [&](int, int k) {
+                if (k < 128) return ld4(bufP + li * XS + k);
+                if (k < 256) return ld4(bufA + ((5 + ((k - 128) >> 6)) * ML + li) * XS + ((k - 128) & 63));
+                return ld4(bufA + (((k - 256) >> 6) * ML + li) * XS + 64 + ((k - 256) & 63));
+            }, acc);
+        }, bufQ, 0, 128, [&](float x) { return fmaxf(x + bias, 0.f); });
     }
     // partial pool over 4 groups of 4 of x[0:16] ++ relu(Wp x[16:] + bp) (BN folded): src -> dst
     auto pool44 = [&](const float *src, float *dst, int layer) {
-        gemm_cols<1, 56>(W + Nt::woff(layer), w, 4, 4, [&](int, int col) { return ld4(src + li * XS + 16 + col); }, acc4);
-        const int i = tid >> 3, j = tid & 7, g = j & 3;
-        const float *p = src + i * XS + 4 * g;
-        const float pv = j < 4 ? fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3])) : (p[0] + p[1] + p[2] + p[3]) / 4.f;
-        __syncthreads();
-        dst[i * XS + j] = pv;
-        const int n = 32 * w + acc_col();
-        if (n < 120) {
-            const float bias = W[Nt::boff(layer) + n];
-#pragma unroll
-            for (int r = 0; r < 16; r++) dst[acc_row(r) * XS + 8 + n] = fmaxf(acc4[0][r] + bias, 0.f);
+        float pv = 0.f;
+        if (tid < ML * 8) {
+            const int i = tid >> 3, j = tid & 7, g = j & 3;
+            const float *p = src + i * XS + 4 * g;
+            pv = j < 4 ? fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3])) : (p[0] + p[1] + p[2] + p[3]) / 4.f;
         }
+        const float bias = col < 120 ? W[Nt::boff(layer) + col] : 0.f;
+        leaf_layer([&] {
+            gemm_cols<1, 56>(W + Nt::woff(layer), wc, 4, 4, 7 * wg, 7 * wg + 7,
+                             [&](int, int c) { return ld4(src + li * XS + 16 + c); }, acc);
+        }, dst, 8, 120, [&](float x) { return fmaxf(x + bias, 0.f); });
+        if (tid < ML * 8) dst[(tid >> 3) * XS + (tid & 7)] = pv;
         __syncthreads();
     };
-    auto dense128 = [&](const float *src, float *dst, int layer, bool relu) {
-        gemm_cols<1, 64>(W + Nt::woff(layer), w, 4, 4, [&](int, int col) { return ld4(src + li * XS + col); }, acc4);
-        __syncthreads();
-        const float bias = W[Nt::boff(layer) + 32 * w + acc_col()];
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const float x = acc4[0][r] + bias;
-            dst[acc_row(r) * XS + 32 * w + acc_col()] = relu ? fmaxf(x, 0.f) : x;
-        }
-        __syncthreads();
+    auto dense128 = [&](const float *src, float *dst, int layer) {
+        const float bias = W[Nt::boff(layer) + col];
+        leaf_layer([&] {
+            gemm_cols<1, 64>(W + Nt::woff(layer), wc, 4, 4, 8 * wg, 8 * wg + 8,
+                             [&](int, int c) { return ld4(src + li * XS + c); }, acc);
+        }, dst, 0, 128, [&](float x) { return fmaxf(x + bias, 0.f); });
     };
     pool44(bufQ, bufP, 5);                  // partialgpool_4
-    dense128(bufP, bufQ, 6, true);          // dense1d_5[0] (+BN folded)
-    dense128(bufQ, bufP, 7, true);          // dense1d_5[3]
+    dense128(bufP, bufQ, 6);                // dense1d_5[0] (+BN folded)
+    dense128(bufQ, bufP, 7);                // dense1d_5[3]
     pool44(bufP, bufQ, 8);                  // partialgpool_5 -> trunk output in bufQ
-    // ---- heads: PI[0] and V[0] (no activation)
+    // ---- heads: PI[0] (group 0) and V[0] (group 1), no activation
     {
-        f32x16 a2[2];
-        gemm_cols<1, 64>(W + Nt::woff(9), w, 4, 4, [&](int, int col) { return ld4(bufQ + li * XS + col); }, a2);
-        gemm_cols<1, 64>(W + Nt::woff(11), w, 4, 4, [&](int, int col) { return ld4(bufQ + li * XS + col); }, a2 + 1);
+        const int layer = wg ? 11 : 9;
+        gemm_cols<1, 64>(W + Nt::woff(layer), wc, 4, 4, 0, 16, [&](int, int c) { return ld4(bufQ + li * XS + c); },
+                         acc);
         __syncthreads();
-        const float bp = W[Nt::boff(9) + 32 * w + acc_col()], bv = W[Nt::boff(11) + 32 * w + acc_col()];
+        const float bias = W[Nt::boff(layer) + col];
+        float *dst = wg ? bufA : bufP;
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-            bufP[acc_row(r) * XS + 32 * w + acc_col()] = a2[0][r] + bp;
-            bufA[acc_row(r) * XS + 32 * w + acc_col()] = a2[1][r] + bv;
-        }
+        for (int r = 0; r < 16; r++) dst[acc_row(r) * XS + col] = acc[0][r] + bias;
         __syncthreads();
     }
     float *logits = bufA + ML * XS;
-    // ---- PI[1] (409 outputs, 13 column blocks over 4 waves) and V[1] (NP outputs, wave 3)
+    // ---- PI[1] (409 outputs, 13 column blocks over 8 waves) and V[1] (NP outputs, wave 7)
     {
-        gemm_cols<4, 64>(W + Nt::woff(10), w, 4, ntiles(ACT), [&](int, int col) { return ld4(bufP + li * XS + col); },
-                         acc4);
+        gemm_cols<2, 64>(W + Nt::woff(10), w, 8, ntiles(ACT), 0, 16, [&](int, int c) { return ld4(bufP + li * XS + c); },
+                         acc);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int nt = w + 4 * j;
+        for (int j = 0; j < 2; j++) {
+            const int nt = w + 8 * j;
             if (nt < ntiles(ACT)) {
                 const int n = 32 * nt + acc_col();
                 const float bias = W[Nt::boff(10) + n];
 #pragma unroll
-                for (int r = 0; r < 16; r++) logits[acc_row(r) * LS + n] = acc4[j][r] + bias;
+                for (int r = 0; r < 16; r++) logits[acc_row(r) * LS + n] = acc[j][r] + bias;
             }
         }
-        if (w == 3) {
-            gemm_cols<1, 64>(W + Nt::woff(12), 0, 1, 1, [&](int, int col) { return ld4(bufA + li * XS + col); }, acc4);
+        if (w == 7) {
+            gemm_cols<1, 64>(W + Nt::woff(12), 0, 1, 1, 0, 16, [&](int, int c) { return ld4(bufA + li * XS + c); },
+                             acc);
             const int n = acc_col();
             if (n < NP) {
                 const float bias = W[Nt::boff(12) + n];
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
                     const int i = acc_row(r);
-                    if (i < nb) v_out[(size_t)(b0 + i) * NP + n] = tanhf(acc4[0][r] + bias);
+                    if (i < nb) v_out[(size_t)(b0 + i) * NP + n] = tanhf(acc[0][r] + bias);
                 }
             }
         }
         __syncthreads();
     }
     // ---- masked softmax (invalid -> -1e8, as the reference's masked_fill + log_softmax)
-    for (int i = w * (ML / 4); i < (w + 1) * (ML / 4); i++) {
+    constexpr int PERW = ML / (NNT / 64);
+    for (int i = w * PERW; i < (w + 1) * PERW; i++) {
         if (i >= nb) break;
         const uint64_t *mk = mask + (size_t)(b0 + i) * 7;
         float x[7];
