@@ -7,6 +7,21 @@
 #include <new>
 
 #include "../../include/splendor_amd.h"
+
+#ifndef MCTS_TIMING
+#define MCTS_TIMING 0      // diagnostic builds only (tools/time_select.hip): k_select cycle probes
+#endif
+#if MCTS_TIMING
+__shared__ uint64_t spl_probe_acc[24];
+__shared__ uint64_t spl_probe_last;
+#define SPL_PROBE(k)                                                                       \
+    if (threadIdx.x == 0) {                                                                \
+        const uint64_t c_ = clock64();                                                     \
+        spl_probe_acc[k] += c_ - spl_probe_last;                                           \
+        spl_probe_last = c_;                                                               \
+    }
+__device__ unsigned long long g_select_timing[24];
+#endif
 #include "mcts_device.h"
 
 using namespace spl;
@@ -34,42 +49,82 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 }
 
 // ------------------------------------------------------------ edge selection
-// pick_highest_UCB (MCTS.py:199-219) over the CSR edges of `node`; forced playouts
-// return the first edge (action order) with N < int(sqrt(0.5 * P * step)).
-__device__ __forceinline__ int pick_edge(const Pools &P, const SearchCfg &C, int t, int node,
-                                         bool forced, int step) {
+// pick_edge for the descent: every edge's (P, N, Q, action, child) is requested in one go
+// (up to 2 x 64 edges in registers — more would cost occupancy; wider nodes loop over the
+// rest), so a tree level costs one round trip for the edges; the chosen edge's action and
+// child come from its lane by shuffle.
+struct Pick {
+    int e, a, child;
+};
+__device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &C, int t, int eb, int ec,
+                                               int ns, double qs, bool forced, int step) {
     const int l = lane_id();
-    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
-    const int eb = P.neb[nb + node], ec = P.nec[nb + node], ns = P.nns[nb + node];
-    const double qs = P.nqs[nb + node];
-    const float *ep = P.ep + e0 + eb;
-    const int32_t *en = P.en + e0 + eb;
-    const double *eq = P.eq + e0 + eb;
-    if (forced) {
-        for (int base = 0; base < ec; base += 64) {
+    const size_t e0 = (size_t)t * P.ecap + eb;
+    float p[2];
+    int n[2], a[2], c[2];
+    double q[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int i = 64 * j + l;
+        const bool in = i < ec;
+        p[j] = in ? P.ep[e0 + i] : 0.f;
+        n[j] = in ? P.en[e0 + i] : 0;
+        q[j] = in ? P.eq[e0 + i] : Q_UNSET;
+        a[j] = in ? (int)P.ea[e0 + i] : 0;
+        c[j] = in ? P.echild[e0 + i] : -1;
+    }
+    int bi = -1;
+    if (forced) {                               // MCTS.py:208-213: first under-visited edge
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int i = 64 * j + l;
+            const bool f = i < ec && (long long)n[j] < (long long)sqrt(0.5 * (double)p[j] * (double)step);
+            const uint64_t b = __ballot(f);
+            if (bi < 0 && b) bi = 64 * j + __ffsll((unsigned long long)b) - 1;
+        }
+        for (int base = 128; bi < 0 && base < ec; base += 64) {
             const int i = base + l;
             bool f = false;
-            if (i < ec) f = (long long)en[i] < (long long)sqrt(0.5 * (double)ep[i] * (double)step);
+            if (i < ec) f = (long long)P.en[e0 + i] < (long long)sqrt(0.5 * (double)P.ep[e0 + i] * (double)step);
             const uint64_t b = __ballot(f);
-            if (b) return base + __ffsll((unsigned long long)b) - 1;
+            if (b) bi = base + __ffsll((unsigned long long)b) - 1;
         }
     }
-    const double fpu_init = C.fpu > 0 ? qs - C.fpu : C.fpu;
-    const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
-    double bu = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int base = 0; base < ec; base += 64) {
-        const int i = base + l;
-        if (i < ec) {
-            const double p = (double)ep[i], q = eq[i];
-            double u;
-            if (q != Q_UNSET) u = q + C.cpuct * p * sq / (double)(1 + en[i]);
-            else u = fpu_init + C.cpuct * p * sq_eps;
-            if (u > bu) { bu = u; bi = i; }
+    if (bi < 0) {                               // pick_highest_UCB (MCTS.py:199-219)
+        const double fpu_init = C.fpu > 0 ? qs - C.fpu : C.fpu;
+        const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
+        double bu = -INFINITY;
+        int bj = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int i = 64 * j + l;
+            if (i < ec) {
+                const double u = q[j] != Q_UNSET ? q[j] + C.cpuct * (double)p[j] * sq / (double)(1 + n[j])
+                                                 : fpu_init + C.cpuct * (double)p[j] * sq_eps;
+                if (u > bu) { bu = u; bj = i; }
+            }
         }
+        for (int base = 128; base < ec; base += 64) {
+            const int i = base + l;
+            if (i < ec) {
+                const double qq = P.eq[e0 + i], pp = (double)P.ep[e0 + i];
+                const double u = qq != Q_UNSET ? qq + C.cpuct * pp * sq / (double)(1 + P.en[e0 + i])
+                                               : fpu_init + C.cpuct * pp * sq_eps;
+                if (u > bu) { bu = u; bj = i; }
+            }
+        }
+        wave_argmax(bu, bj);
+        bi = bj;
     }
-    wave_argmax(bu, bi);
-    return bi;
+    const int jb = bi >> 6;
+    int av = a[0], cv = c[0];
+#pragma unroll
+    for (int j = 1; j < 2; j++)
+        if (jb == j) { av = a[j]; cv = c[j]; }
+    av = __shfl(av, bi & 63, 64);
+    cv = __shfl(cv, bi & 63, 64);
+    if (bi >= 128) { av = P.ea[e0 + bi]; cv = P.echild[e0 + bi]; }
+    return {bi, av, cv};
 }
 
 // ------------------------------------------------------------ Dirichlet root noise
@@ -516,10 +571,18 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
         if (l == 0) { leaf_valid[t] = 0; H->leaf_kind = LEAF_NONE; }
         return;
     }
+#if MCTS_TIMING
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < 24; k++) spl_probe_acc[k] = 0;
+        spl_probe_last = clock64();
+    }
+#endif
+    const MaskLane ml = MaskLane::load();                // constant-table operands of the leaf mask
     int8_t *s = lds[w];
     wave_load_board<N>(s, P.root_state + (size_t)t * Lx::S);
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     int32_t *path = P.path + (size_t)t * P.pcap * 2;
+    SPL_PROBE(0)
     int node = H->root, depth = 0, kind = LEAF_NN;
     uint64_t k0 = 0, k1 = 0;
     float val[4] = {0, 0, 0, 0};
@@ -530,29 +593,39 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
             apply_root_noise(P, C, t, P.neb[nb + node], P.nec[nb + node], ST_DIR | (uint32_t)H->move_no);
         const bool forced = H->forced;
         for (;;) {
+            // node record: CSR range, visit stats and (below the root) the terminal flag, in
+            // one round trip; a terminal child found on the previous level ends the descent
+            SPL_PROBE(1)
+            const int eb = P.neb[nb + node], ec = P.nec[nb + node], ns = P.nns[nb + node];
+            const double qs = P.nqs[nb + node];
+            if (depth > 0 && P.nterm[nb + node]) {
+                kind = LEAF_TERMINAL;
+#pragma unroll
+                for (int i = 0; i < 4; i++) val[i] = P.nes[(nb + node) * 4 + i];
+                break;
+            }
             if (depth >= P.pcap) { kind = LEAF_NONE; if (l == 0) H->overflow = 2; break; }
-            const int e = pick_edge(P, C, t, node, forced && depth == 0, sims);
-            const int ge = P.neb[nb + node] + e;
+            const Pick pk = pick_edge_desc(P, C, t, eb, ec, ns, qs, forced && depth == 0, sims);
+            const int ge = eb + pk.e;
             if (l == 0) { path[2 * depth] = node; path[2 * depth + 1] = ge; }
             depth++;
-            const int a = P.ea[e0 + ge];
-            int child = P.echild[e0 + ge];
+            int child = pk.child;
+            SPL_PROBE(2)
             Chance ch{nullptr, 0, 0, 0, 0};
-            const int nxt = make_move<N>(s, a, 0, true, ch);   // MCTS.py:227-235
+            const int nxt = make_move<N>(s, pk.a, 0, true, ch);   // MCTS.py:227-235
             __builtin_amdgcn_wave_barrier();
             if (nxt) wave_roll_players<N>(s, s, nxt);
+            SPL_PROBE(3)
             if (child < 0) {
                 wave_fingerprint<N>(s, k0, k1);
                 child = hash_lookup(P, t, k0, k1);
                 if (child >= 0 && l == 0) P.echild[e0 + ge] = child;
             }
+            SPL_PROBE(4)
+#if MCTS_TIMING
+            if (threadIdx.x == 0) spl_probe_acc[20] += 1;
+#endif
             if (child >= 0) {
-                if (P.nterm[nb + child]) {
-                    kind = LEAF_TERMINAL;
-#pragma unroll
-                    for (int i = 0; i < 4; i++) val[i] = P.nes[(nb + child) * 4 + i];
-                    break;
-                }
                 node = child;
                 continue;
             }
@@ -584,12 +657,14 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
         }
     }
     __builtin_amdgcn_wave_barrier();
+    SPL_PROBE(5)
     if (kind == LEAF_NN) {
         wave_store_board<N>(leaf_state + (size_t)t * Lx::S, s);
         uint64_t m[7];
-        wave_valid_moves<N>(s, 0, lim, m);                   // MCTS.py:136
+        wave_valid_moves<N>(s, 0, lim, m, ml);               // MCTS.py:136
         store_mask(leaf_mask + (size_t)t * 7, m);
     }
+    SPL_PROBE(6)
     if (l == 0) {
         H->depth = depth;
         H->leaf_kind = kind;
@@ -599,6 +674,13 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
         for (int i = 0; i < 4; i++) H->leaf_v[i] = val[i];
         leaf_valid[t] = kind == LEAF_NN;
     }
+#if MCTS_TIMING
+    SPL_PROBE(7)
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < 24; k++) atomicAdd(&g_select_timing[k], (unsigned long long)spl_probe_acc[k]);
+        atomicAdd(&g_select_timing[21], 1ull);
+    }
+#endif
 }
 
 // ------------------------------------------------------------ expand + backup
