@@ -508,6 +508,75 @@ __device__ __forceinline__ LanePred lane_predicates(const int8_t *s, int p, int 
     return P;
 }
 
+// One quarter of lane_predicates' fast path, so four waves can share a board's predicate
+// work: PART 0 / 1 = buy and reserve bits of visible cards 0-5 / 6-11, PART 2 = reserved
+// cards, deck reserves and the condition bits, PART 3 = the gem-vector lookups. The parts
+// OR together to lane_predicates' F0 / F1 / C; `bad` flags rows outside the fast domain
+// (the caller then uses lane_predicates_exact for the board).
+template <int N, int PART>
+__device__ __forceinline__ void lane_predicates_part(const int8_t *s, int p, int lim, const uint32_t *lut_diff,
+                                                     const uint64_t *lut_s3, uint64_t &F0, uint64_t &F1,
+                                                     uint32_t &C, bool &bad) {
+    using Lx = Lay<N>;
+    constexpr uint64_t M5 = 0xFFFFFFFFFFull, H5 = 0x8080808080ull;
+    const uint64_t bank = row(s, Lx::BANK), gems = row(s, Lx::GEMS + p);
+    F0 = 0; F1 = 0; C = 0;
+    if constexpr (PART == 3) {
+        bad = ((bank | gems) & H5) != 0;
+        const uint32_t b1 = ge_set(bank, 1), g1 = ge_set(gems, 1);
+        uint32_t lvl = 0;
+#pragma unroll
+        for (int c = 0; c < 5; c++) lvl |= (uint32_t)min(bt(gems, c), 3) << (2 * c);
+        F0 = (uint64_t)lut_diff[b1] << 30 | (uint64_t)ge_set(bank, 4) << 55;
+        F1 = (uint64_t)(lut_diff[g1] & 0x7FFFu) | (uint64_t)ge_set(gems, 2) << 15 | lut_s3[lvl] << 20;
+    } else {
+        constexpr int I0 = PART == 0 ? 0 : (PART == 1 ? 6 : 12), NI = PART == 2 ? 3 : 6;
+        const uint64_t cards = row(s, Lx::CARDS + p), slot5 = row(s, Lx::RSV + 6 * p + 5);
+        uint64_t cost[NI];
+        uint64_t any = gems | cards | slot5;
+#pragma unroll
+        for (int k = 0; k < NI; k++) {
+            const int i = I0 + k;
+            cost[k] = row(s, i < 12 ? Lx::TIERS + 2 * i : Lx::RSV + 6 * p + 2 * (i - 12));
+            any |= cost[k];
+        }
+        uint64_t deck[3] = {0, 0, 0};
+        if constexpr (PART == 2) {
+#pragma unroll
+            for (int t = 0; t < 3; t++) {
+                deck[t] = row(s, Lx::DECKS + 2 * t);
+                any |= deck[t];
+            }
+            any |= bank;
+        }
+        bad = (any & H5) != 0;
+        const uint64_t have = (gems & M5) + (cards & M5);
+        const uint32_t hlo = (uint32_t)have, hhi = (uint32_t)(have >> 32);
+        const int rhs = 2 * bt(gems, 5) + (int)__builtin_amdgcn_sad_u8(hlo, 0u, hhi);
+        const bool slot_free = (slot5 & M5) == 0;
+#pragma unroll
+        for (int k = 0; k < NI; k++) {
+            const int i = I0 + k;
+            const uint32_t clo = (uint32_t)cost[k], chi = (uint32_t)(cost[k] >> 32) & 0xFF;
+            const uint32_t absd = __builtin_amdgcn_sad_u8(clo, hlo, __builtin_amdgcn_sad_u8(chi, hhi, 0u));
+            const int lhs = (int)__builtin_amdgcn_sad_u8(clo, 0u, absd + chi);
+            const bool nz = (cost[k] & M5) != 0;
+            const bool buy = lhs <= rhs && nz;
+            if (i < 12) {
+                F0 |= (uint64_t)buy << i;
+                F0 |= (uint64_t)(nz && slot_free) << (12 + i);
+            } else {
+                F0 |= (uint64_t)buy << (27 + i - 12);
+            }
+        }
+        if constexpr (PART == 2) {
+#pragma unroll
+            for (int t = 0; t < 3; t++) F0 |= (uint64_t)((deck[t] & M5) != 0 && slot_free) << (24 + t);
+            C = lane_cond(sum7(gems), lim, __popc(ge_set(bank, 1)), bt(bank, 5));
+        }
+    }
+}
+
 // mask word K (actions 64K .. 64K+63) from the predicates; the pass bit is not included
 template <int K>
 __device__ __forceinline__ uint64_t lane_mask_word(const LanePred &P) {
@@ -689,12 +758,22 @@ __device__ __forceinline__ void buy_card(int8_t *s, int cost_row, int p) {
 // Actions 405..408 are a no-op + round increment (the reference's select-noble stub does
 // not parse and pass reads give_ids3 out of bounds; DESIGN.md "Defined deviations").
 // Returns the next player.
-template <int N>
+// KIND (move_kind) >= 0 specialises the pipeline to one kind of move when the caller knows
+// it: the stages that kind never uses are compiled out.
+enum { MK_GEMS = 0, MK_BUY = 1, MK_RESERVE = 2, MK_BUY_RESERVED = 3 };
+__device__ __forceinline__ int move_kind(int a, const int8_t *act_rsv) {
+    return a < 12 ? MK_BUY : (a >= 27 && a < 30 ? MK_BUY_RESERVED : (act_rsv[a] >= 0 ? MK_RESERVE : MK_GEMS));
+}
+
+template <int N, int KIND = -1>
 __device__ __forceinline__ int make_move(int8_t *s, int a, int p, bool det, Chance &ch) {
     using Lx = Lay<N>;
-    const int rsv = ch.tab.act_rsv[a];
-    const uint64_t take = ch.tab.act_take[a], give = ch.tab.act_give[a];
-    const bool buy_vis = a < 12, buy_rsv = a >= 27 && a < 30;
+    constexpr bool ANY = KIND < 0;
+    const int rsv = ANY || KIND == MK_RESERVE ? (int)ch.tab.act_rsv[a] : -1;
+    const bool vec = ANY || KIND == MK_GEMS || KIND == MK_RESERVE;
+    const uint64_t take = vec ? ch.tab.act_take[a] : 0, give = vec ? ch.tab.act_give[a] : 0;
+    const bool buy_vis = ANY ? a < 12 : KIND == MK_BUY;
+    const bool buy_rsv = ANY ? (a >= 27 && a < 30) : KIND == MK_BUY_RESERVED;
     SPL_PROBE(10)
     if (buy_vis || buy_rsv) buy_card<N>(s, buy_vis ? Lx::TIERS + 2 * a : Lx::RSV + 6 * p + 2 * (a - 27), p);
     SPL_PROBE(11)

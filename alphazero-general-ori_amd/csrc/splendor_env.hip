@@ -180,8 +180,10 @@ __global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__re
 //            feed a deck draw); lane-per-board legality predicates + mask words w, w+4 in
 //            wave w, on the real board for the player to move (== the canonical form's
 //            mask: it only reads player p's rows)
-//     move   lane l < 16 of wave w = board 16w + l: pass bit (:263), uniform action draw,
-//            make_move with chance, end check; per-move outputs
+//     select lane l < 16 of wave w = board 16w + l: pass bit (:263), uniform action draw;
+//            boards filed by move kind
+//     move   wave k makes the moves of kind k (gem vectors / buy / reserve / buy reserved),
+//            lane per board, chance, end check; per-move outputs
 //     reset  finished games are re-dealt wave-parallel (draws 3.., Philox per lane); the
 //            move's masks go to HBM
 //   store    boards, players, game counters LDS -> HBM
@@ -213,7 +215,12 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     __shared__ TabsLds tabs;
     __shared__ uint32_t lut_diff[32];
     __shared__ uint64_t lut_s3[1024];
-    __shared__ uint16_t reset16[WAVES];
+    __shared__ int16_t act[RB];
+    __shared__ uint8_t klist[4][RB], rflag[RB];
+    __shared__ int kcount[4];
+    __shared__ uint64_t pf0[WAVES][RB], pf1[RB];
+    __shared__ uint32_t pcond[RB];
+    __shared__ uint8_t pbad[WAVES][RB];
     const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
     int8_t *const gst = state + (size_t)b0 * Lx::S;
@@ -230,6 +237,8 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         pl[tid] = player[b0 + tid];
         gdone[tid] = games_done ? games_done[b0 + tid] : 0;
     }
+    if (tid < RB) rflag[tid] = 0;
+    if (tid < 4) kcount[tid] = 0;
     stage_tabs(tabs, tid, THREADS);
     for (int i = tid; i < 1024; i += THREADS) lut_s3[i] = K_LUT_SPEC3[i];
     if (tid < 32) lut_diff[tid] = K_LUT_DIFF[tid];
@@ -242,8 +251,34 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
             const int b = tid & (RB - 1), k = tid / RB;
             philox_pair(seed, bbase + (uint32_t)(b0 + b), step, k, ud[b][2 * k], ud[b][2 * k + 1]);
         }
+        // predicates: wave w computes part w of every board's predicate set (lane per board)
         if (ROLLOUT_ABLATE != 1 && l < nb) {
-            const LanePred P = lane_predicates<N>(lds + l * ST, pl[l], lim, lut_diff, lut_s3);
+            uint64_t f0, f1;
+            uint32_t cc;
+            bool bad;
+            const int8_t *s = lds + l * ST;
+            switch (w) {
+                case 0: lane_predicates_part<N, 0>(s, pl[l], lim, lut_diff, lut_s3, f0, f1, cc, bad); break;
+                case 1: lane_predicates_part<N, 1>(s, pl[l], lim, lut_diff, lut_s3, f0, f1, cc, bad); break;
+                case 2: lane_predicates_part<N, 2>(s, pl[l], lim, lut_diff, lut_s3, f0, f1, cc, bad); break;
+                default: lane_predicates_part<N, 3>(s, pl[l], lim, lut_diff, lut_s3, f0, f1, cc, bad); break;
+            }
+            pf0[w][l] = f0;
+            if (w == 3) pf1[l] = f1;
+            if (w == 2) pcond[l] = cc;
+            pbad[w][l] = bad;
+        }
+        __syncthreads();
+        // mask words w and w+4 of every board from the combined predicates
+        if (ROLLOUT_ABLATE != 1 && l < nb) {
+            LanePred P;
+            if (pbad[0][l] | pbad[1][l] | pbad[2][l] | pbad[3][l]) {
+                P = lane_predicates_exact<N>(lds + l * ST, pl[l], lim);
+            } else {
+                P.F0 = pf0[0][l] | pf0[1][l] | pf0[2][l] | pf0[3][l];
+                P.F1 = pf1[l];
+                P.C = pcond[l];
+            }
             if (w == 0) { msk[l][0] = lane_mask_word<0>(P); msk[l][4] = lane_mask_word<4>(P); }
             else if (w == 1) { msk[l][1] = lane_mask_word<1>(P); msk[l][5] = lane_mask_word<5>(P); }
             else if (w == 2) { msk[l][2] = lane_mask_word<2>(P); msk[l][6] = lane_mask_word<6>(P); }
@@ -251,27 +286,45 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         }
         __syncthreads();
         RT_MARK(1)
-        bool ended = false;
-        const int b = w * PER + l;
-        if (ROLLOUT_ABLATE != 2 && l < PER && b < nb) {
-            int a;
-            if (ROLLOUT_ABLATE == 1) {
-                a = 30 + (int)((step + b) % 5);
-            } else {
-                uint64_t m[7];
-                int cnt = 0;
+        // select: lane l < 16 of wave w: pass bit (:263), uniform pick, filed by move kind
+        {
+            const int b = w * PER + l;
+            if (ROLLOUT_ABLATE != 2 && l < PER && b < nb) {
+                int a;
+                if (ROLLOUT_ABLATE == 1) {
+                    a = 30 + (int)((step + b) % 5);
+                } else {
+                    uint64_t m[7];
+                    int cnt = 0;
 #pragma unroll
-                for (int k = 0; k < 7; k++) { m[k] = msk[b][k]; cnt += __popcll(m[k]); }
-                if (!cnt) { m[6] |= 1ull << (408 - 384); msk[b][6] = m[6]; cnt = 1; }
-                a = select_bit(m, (int)(ud[b][0] * (double)cnt));
+                    for (int k = 0; k < 7; k++) { m[k] = msk[b][k]; cnt += __popcll(m[k]); }
+                    if (!cnt) { m[6] |= 1ull << (408 - 384); msk[b][6] = m[6]; cnt = 1; }
+                    a = select_bit(m, (int)(ud[b][0] * (double)cnt));
+                }
+                act[b] = (int16_t)a;
+                const int kind = move_kind(a, tabs.act_rsv);
+                klist[kind][atomicAdd(&kcount[kind], 1)] = (uint8_t)b;
             }
-            RT_MARK(5)
+        }
+        __syncthreads();
+        RT_MARK(5)
+        // move: wave w makes every move of kind w (one pipeline specialisation per wave, so no
+        // wave carries the stages of other kinds); chance draws 1-2; end check; outputs
+        if (ROLLOUT_ABLATE != 2 && l < kcount[w]) {
+            const int b = klist[w][l], a = act[b];
             int8_t *s = lds + b * ST;
             Chance ch{&ud[b][0], 0, 0, 0, 1, 0.0, false, tabs.view()};
-            int nxt = make_move<N>(s, a, pl[b], false, ch);
+            int nxt;
+            switch (w) {
+                case MK_GEMS: nxt = make_move<N, MK_GEMS>(s, a, pl[b], false, ch); break;
+                case MK_BUY: nxt = make_move<N, MK_BUY>(s, a, pl[b], false, ch); break;
+                case MK_RESERVE: nxt = make_move<N, MK_RESERVE>(s, a, pl[b], false, ch); break;
+                default: nxt = make_move<N, MK_BUY_RESERVED>(s, a, pl[b], false, ch); break;
+            }
             RT_MARK(6)
             float e[N];
             check_end<N>(s, e);
+            bool ended = false;
 #pragma unroll
             for (int i = 0; i < N; i++) {
                 ended |= e[i] != 0.f;
@@ -284,14 +337,12 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                 gdone[b] += 1;
             }
             pl[b] = (int8_t)nxt;
+            rflag[b] = ended;
         }
-        const uint64_t rm16 = __ballot(ended);
-        if (l == 0) reset16[w] = (uint16_t)rm16;
         __syncthreads();
         RT_MARK(2)
-        uint64_t rm = 0;
-#pragma unroll
-        for (int k = 0; k < WAVES; k++) rm |= (uint64_t)reset16[k] << (16 * k);
+        if (tid < 4) kcount[tid] = 0;
+        uint64_t rm = __ballot(l < nb && rflag[l]);
         for (int i = 0; rm; i++, rm &= rm - 1) {
             if ((i & (WAVES - 1)) != w) continue;
             const int rb = __ffsll((unsigned long long)rm) - 1;
