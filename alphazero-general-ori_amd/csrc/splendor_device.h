@@ -706,10 +706,13 @@ template <int N>
 __device__ __forceinline__ void give_nobles(int8_t *s, int p) {
     using Lx = Lay<N>;
     const uint64_t cards = row(s, Lx::CARDS + p);
+    uint64_t nob[Lx::NN];                    // all noble rows read before any write
+#pragma unroll
+    for (int i = 0; i < Lx::NN; i++) nob[i] = row(s, Lx::NOBLES + i);
+#pragma unroll
     for (int i = 0; i < Lx::NN; i++) {
-        const uint64_t nob = row(s, Lx::NOBLES + i);
-        if (sum5(nob) > 0 && ge5(cards, nob)) {
-            row(s, Lx::PNOB + Lx::NN * p + i) = nob;
+        if (sum5(nob[i]) > 0 && ge5(cards, nob[i])) {
+            row(s, Lx::PNOB + Lx::NN * p + i) = nob[i];
             row(s, Lx::NOBLES + i) = 0;
         }
     }

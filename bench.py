@@ -148,7 +148,7 @@ def main():
     ap.add_argument("--no-selfplay", action="store_true",
                     help="env workload: skip the secondary config-3 self-play measurement")
     ap.add_argument("--selfplay-steps", type=int, default=100)
-    ap.add_argument("--chunk", type=int, default=50, help="env: moves per rollout launch")
+    ap.add_argument("--chunk", type=int, default=100, help="env: moves per rollout launch")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

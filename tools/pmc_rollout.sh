@@ -8,7 +8,7 @@ OUT=${1:-gpurun_out/pmc}
 ROUND=${2:-r01}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
-CMD=(python3 bench.py --steps 100 --warmup 50 --chunk 50 --no-cpu-baseline --no-selfplay)
+CMD=(python3 bench.py --steps 200 --warmup 100 --chunk 100 --no-cpu-baseline --no-selfplay)
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- "${CMD[@]}" > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- "${CMD[@]}" > "$OUT/write.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE \

@@ -44,12 +44,12 @@ def main():
         for r in csv.DictReader(open(f)):
             if KERNEL in r["Name"]:
                 avg_ns = float(r["AverageNs"])
-    B, moves, n = 32768, 50, 2
+    B, moves, n = 32768, 100, 2
     S = 7 * (32 + 10 * n + n * n)
     alg = B * (2 * S + 2 + 8 + moves * (56 + 2 + 4 * n))
     res = {"kernel": KERNEL, "boards": B, "moves_per_launch": moves, "round": rnd,
            "command": "tools/pmc_rollout.sh: rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE | --pmc SQ_* "
-                      "(separate passes) -- python3 bench.py --steps 100 --warmup 50 --chunk 50",
+                      "(separate passes) -- python3 bench.py --steps 200 --warmup 100 --chunk 100",
            "dispatches_used": [n1, n2], "kernel_avg_us_rocprof": avg_ns / 1e3 if avg_ns else None,
            "FETCH_SIZE_KB_avg": fetch_kb, "WRITE_SIZE_KB_avg": write_kb}
     if fetch_kb is not None and write_kb is not None:
