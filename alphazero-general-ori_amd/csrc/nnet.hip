@@ -43,10 +43,20 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int NNT = 512;       // threads per workgroup (8 waves)
+#ifndef NN_PF1
+#define NN_PF1 4               // weight-prefetch depth (k steps) of the per-leaf GEMMs
+#endif
+constexpr int NNT = 512;      // threads per workgroup (8 waves)
 constexpr int ML = 32;         // leaves per workgroup
 constexpr int XS = 132;        // activation row stride (floats)
 constexpr int LS = 420;        // logits row stride (floats)
+// per-leaf operands are read by ds_read_b128 with lane l on row l & 15 and k group l >> 4
+// 4 floats apart: with rows 8 banks apart, the groups {0-3,12-15,20-27}, ... that share an
+// LDS cycle land on disjoint banks (MI355X_MICROARCH.md §LDS)
+constexpr int PS = 136;        // per-leaf activation row stride (floats)
+constexpr int ZS = 712;        // flattened trunk row stride (704 features)
+static_assert(ML * ZS <= 7 * ML * XS && ML * (PS + LS) <= 7 * ML * XS, "bufA overlays");
+static_assert(2 * 64 * ML <= ML * PS, "dense2d_3 pool partials fit bufP");
 constexpr int ACT = 409;
 
 __host__ __device__ constexpr int kpad(int K) { return (K + 7) / 8 * 8; }
@@ -93,103 +103,148 @@ __device__ __forceinline__ void mfma4(const float4 &a, const float4 &b, f32x16 &
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
 }
 
-// token tiles t0 .. t0+nt_tok-1 (<= T) x one N tile (column block nt) over K = 2S
-// wp: packed weights of the layer; afetch(t, col) -> float4 of A[token tile t][lane row][col..col+3]
-template <int T, int S, class AF>
-__device__ __forceinline__ void gemm_tiles(const float *__restrict__ wp, int nt, int t0, int nt_tok, AF afetch,
-                                           f32x16 acc[T]) {
-    const int lane = threadIdx.x & 63, h = lane >> 5;
-    const float4 *w4 = reinterpret_cast<const float4 *>(wp) + (size_t)nt * (S / 4) * 64 + lane;
+template <int V> struct IntC {
+    static constexpr int value = V;
+};
+
+// weight-fragment ring of the per-column GEMMs (a k-step is 4 T MFMAs of 64 cycles)
+constexpr int PFC = 2;
+typedef float4 RingC[PFC];
+
+// first PFC k-steps of column block nt of a per-column layer (K = 2S) into the ring
+template <int S>
+__device__ __forceinline__ void ringc_load(const float *__restrict__ wp, int nt, RingC &bq) {
+    const float4 *w4 = reinterpret_cast<const float4 *>(wp) + (size_t)nt * (S / 4) * 64 + (threadIdx.x & 63);
 #pragma unroll
-    for (int t = 0; t < T; t++) acc[t] = zero16();
-    float4 bn = w4[0];
-#pragma unroll 2
-    for (int s4 = 0; s4 < S / 4; s4++) {
-        const float4 b = bn;
-        if (s4 + 1 < S / 4) bn = w4[(s4 + 1) * 64];
-#pragma unroll
-        for (int t = 0; t < T; t++)
-            if (t < nt_tok) mfma4(afetch(t0 + t, h * S + 4 * s4), b, acc[t]);
-    }
+    for (int p = 0; p < PFC; p++) bq[p] = w4[(p < S / 4 ? p : S / 4 - 1) * 64];
 }
 
-// one token tile x up to NT column blocks {nt0, nt0 + step, ...} < ntot (shared A operand),
-// over the step range [q0, q1) of the S/4 float4 steps
-template <int NT, int S, class AF>
-__device__ __forceinline__ void gemm_cols(const float *__restrict__ wp, int nt0, int step, int ntot, int q0, int q1,
-                                          AF afetch, f32x16 acc[NT]) {
+// token tiles t0 .. t0+T-1 x one N tile (column block nt) over K = 2S; bq holds the first
+// PFC steps (ringc_load); afetch(t, col) -> float4 of A[token tile t][lane row][col..col+3];
+// next() runs after the last MFMA is issued. Unrolled and branch-free like gemm16.
+template <int T, int S, class AF, class NX>
+__device__ __forceinline__ void gemm_tiles(const float *__restrict__ wp, int nt, int t0, RingC &bq, AF afetch,
+                                           f32x16 *acc, NX next) {
+    constexpr int Q = S / 4;
     const int lane = threadIdx.x & 63, h = lane >> 5;
+    const float4 *w4 = reinterpret_cast<const float4 *>(wp) + (size_t)nt * Q * 64 + lane;
 #pragma unroll
-    for (int j = 0; j < NT; j++) acc[j] = zero16();
-    const float4 *w4 = reinterpret_cast<const float4 *>(wp) + lane;
-#pragma unroll 2
-    for (int s4 = q0; s4 < q1; s4++) {
-        const float4 a = afetch(0, h * S + 4 * s4);
+    for (int t = 0; t < T; t++) acc[t] = zero16();
+    float4 a[T];
 #pragma unroll
-        for (int j = 0; j < NT; j++) {
-            const int nt = nt0 + j * step;
-            if (nt < ntot) mfma4(a, w4[((size_t)nt * (S / 4) + s4) * 64], acc[j]);
-        }
+    for (int t = 0; t < T; t++) a[t] = afetch(t0 + t, h * S);
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+        float4 x[T];
+#pragma unroll
+        for (int t = 0; t < T; t++) x[t] = a[t];
+        if (q + 1 < Q)
+#pragma unroll
+            for (int t = 0; t < T; t++) a[t] = afetch(t0 + t, h * S + 4 * (q + 1));
+        const float4 b = bq[q % PFC];
+        if (q + PFC < Q) bq[q % PFC] = w4[(q + PFC) * 64];
+#pragma unroll
+        for (int t = 0; t < T; t++) mfma4(x[t], b, acc[t]);
+        __builtin_amdgcn_sched_barrier(0);
     }
+    next();
+    __builtin_amdgcn_sched_barrier(0);
 }
+
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void mfma4_16(const float4 &a, const float4 &b, f32x4 &acc) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+// both row tiles against one B fragment, alternating accumulators: a 16x16x4 f32 MFMA
+// issues every 32 cycles but its result is ready for a dependent one only after 40
+// (MI355X_MICROARCH.md, cycle constants)
+__device__ __forceinline__ void mfma4_16x2(const float4 &a0, const float4 &a1, const float4 &b, f32x4 &c0,
+                                          f32x4 &c1) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b.x, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b.x, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b.y, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b.y, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b.z, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b.z, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b.w, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b.w, c1, 0, 0, 0);
 }
 
-// per-leaf GEMM on v_mfma_f32_16x16x4_f32: the 32 leaves as 2 row tiles of 16 x up to NC
-// 16-column tiles {c0, c0 + cstep, ...} < ctot, K = 16 * Q4 (lane group g = lane >> 4 feeds
-// k = g * 4 Q4 + s at step s). afetch(rt, col) -> float4 of A[row tile rt][lane row][col..+3].
-template <int NC, int Q4, class AF>
-__device__ __forceinline__ void gemm16(const float *__restrict__ wp, int c0, int cstep, int ctot, AF afetch,
-                                       f32x4 acc[NC][2]) {
+// workgroup barrier for LDS traffic only: waits for this wave's LDS operations, not for its
+// global loads, so weight fragments prefetched for the next layer stay in flight across it
+// (__syncthreads() waits vmcnt(0) first); the memory clobber keeps the compiler from moving
+// LDS accesses across it
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// weight-fragment ring of the per-leaf GEMMs: PF16 k-steps x up to 4 column tiles
+constexpr int PF16 = NN_PF1;
+typedef float4 Ring16[PF16][4];
+
+// column tile j of a per-leaf layer: tile min(c0 + j cstep, ctot - 1) (a clamped tile is
+// loaded but never multiplied)
+template <int Q4>
+__device__ __forceinline__ const float4 *tile16(const float *__restrict__ wp, int c0, int cstep, int ctot, int j) {
+    return reinterpret_cast<const float4 *>(wp) + (size_t)min(c0 + j * cstep, ctot - 1) * Q4 * 64 + (threadIdx.x & 63);
+}
+
+// issue the first PF16 k-steps of a per-leaf layer's weight fragments into the ring; a
+// caller does this right after the previous layer's last MFMA, ahead of its epilogue and
+// barrier, so no layer starts on an L2 round trip
+template <int NC, int Q4>
+__device__ __forceinline__ void ring_load(const float *__restrict__ wp, int c0, int cstep, int ctot, Ring16 &bq) {
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+        const float4 *w4 = tile16<Q4>(wp, c0, cstep, ctot, j);
+#pragma unroll
+        for (int p = 0; p < PF16; p++) bq[p][j] = w4[(p < Q4 ? p : Q4 - 1) * 64];
+    }
+}
+
+// per-leaf GEMM on v_mfma_f32_16x16x4_f32: the 32 leaves as 2 row tiles of 16 x NC
+// 16-column tiles {c0, c0 + cstep, ...} (all valid: the caller picks NC for its wave),
+// K = 16 * Q4 (lane group g = lane >> 4 feeds k = 16 q + 4 g + j at step q, MFMA j).
+// bq holds the first PF16 steps (ring_load); afetch(rt, col) -> float4 of
+// A[row tile rt][lane row][col..+3]; next() runs after the last MFMA is issued.
+// The k loop is fully unrolled with no branch in it: a conditional weight load makes the
+// compiler copy the loaded fragment into the ring register under an s_waitcnt vmcnt(0)
+// at once, and every step then pays the whole L2 round trip.
+template <int NC, int Q4, class AF, class NX>
+__device__ __forceinline__ void gemm16(const float *__restrict__ wp, int c0, int cstep, Ring16 &bq, AF afetch,
+                                       f32x4 (*acc)[2], NX next) {
     // a k-step is only 8 NC MFMAs (~256 NC cycles), shorter than an L2 round trip: the
-    // weight fragments are prefetched PF steps ahead, the activations one step ahead
-    constexpr int PF = 4;
+    // weight fragments are prefetched PF16 steps ahead, the activations one step ahead
+    constexpr int PF = PF16;
     const int lane = threadIdx.x & 63, g = lane >> 4;
 #pragma unroll
     for (int j = 0; j < NC; j++)
 #pragma unroll
         for (int r = 0; r < 2; r++) acc[j][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const float4 *w4 = reinterpret_cast<const float4 *>(wp) + lane;
-    float4 bq[PF][NC];
+    const float4 *w4[NC];
 #pragma unroll
-    for (int p = 0; p < PF; p++)
+    for (int j = 0; j < NC; j++) w4[j] = tile16<Q4>(wp, c0, cstep, 1 << 30, j);
+    float4 a0 = afetch(0, 4 * g), a1 = afetch(1, 4 * g);
+#pragma unroll
+    for (int q = 0; q < Q4; q++) {
+        const float4 x0 = a0, x1 = a1;
+        if (q + 1 < Q4) {
+            a0 = afetch(0, 4 * g + 16 * (q + 1));
+            a1 = afetch(1, 4 * g + 16 * (q + 1));
+        }
 #pragma unroll
         for (int j = 0; j < NC; j++) {
-            const int ct = c0 + j * cstep;
-            bq[p][j] = ct < ctot && p < Q4 ? w4[((size_t)ct * Q4 + p) * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 b = bq[q % PF][j];
+            if (q + PF < Q4) bq[q % PF][j] = w4[j][(q + PF) * 64];
+            mfma4_16x2(x0, x1, b, acc[j][0], acc[j][1]);
         }
-    float4 a0 = afetch(0, g * 4 * Q4), a1 = afetch(1, g * 4 * Q4);
-    for (int q0 = 0; q0 < Q4; q0 += PF) {
-#pragma unroll
-        for (int p = 0; p < PF; p++) {
-            const int q = q0 + p;
-            if (q < Q4) {
-                const float4 x0 = a0, x1 = a1;
-                if (q + 1 < Q4) {
-                    a0 = afetch(0, g * 4 * Q4 + 4 * (q + 1));
-                    a1 = afetch(1, g * 4 * Q4 + 4 * (q + 1));
-                }
-#pragma unroll
-                for (int j = 0; j < NC; j++) {
-                    const int ct = c0 + j * cstep;
-                    if (ct < ctot) {
-                        const float4 b = bq[p][j];
-                        if (q + PF < Q4) bq[p][j] = w4[((size_t)ct * Q4 + q + PF) * 64];
-                        mfma4_16(x0, b, acc[j][0]);
-                        mfma4_16(x1, b, acc[j][1]);
-                    }
-                }
-            }
-        }
+        // keep each step's loads in its step: left alone, the scheduler sinks them next to
+        // their MFMAs PF steps later (vmcnt(1) waits, the ring gone)
+        __builtin_amdgcn_sched_barrier(0);
     }
+    next();
+    __builtin_amdgcn_sched_barrier(0);
 }
+struct NoNext {
+    __device__ void operator()() const {}
+};
 // 16x16 accumulator element r of this lane: row (within the row tile) and column
 __device__ __forceinline__ int acc16_row(int r) { return ((threadIdx.x & 63) >> 4) * 4 + r; }
 __device__ __forceinline__ int acc16_col() { return threadIdx.x & 15; }
@@ -201,16 +256,19 @@ __device__ __forceinline__ int acc_col() { return threadIdx.x & 31; }
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
 template <int NP>
-__global__ __launch_bounds__(NNT) void k_nn_forward(int B, const int8_t *__restrict__ state,
+// one workgroup per CU (LDS) = 2 waves per SIMD: the register budget is 256, and without
+// saying so the scheduler sinks the prefetched weight loads next to their MFMAs
+__global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_nn_forward(int B, const int8_t *__restrict__ state,
                                                     const uint64_t *__restrict__ mask,
                                                     const float *__restrict__ W, float *__restrict__ pi_out,
                                                     float *__restrict__ v_out) {
     using Nt = Net<NP>;
     constexpr int R = Nt::R, X0S = Nt::X0S;
     __shared__ __align__(16) float bufA[7 * ML * XS];      // per-column activations / logits
-    __shared__ __align__(16) float bufP[ML * XS];          // per-leaf ping
-    __shared__ __align__(16) float bufQ[ML * XS];          // per-leaf pong
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 31;
+    __shared__ __align__(16) float bufP[ML * PS];          // per-leaf ping
+    __shared__ __align__(16) float bufQ[ML * PS];          // per-leaf pong
+    // wave index in an SGPR: every per-wave choice below is a scalar branch
+    const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, li = lane & 31;
     const int wc = w & 3, wg = w >> 2;                     // column block, wave group
 #if NN_TIMING
     if (tid < 16) nn_probe_acc[tid] = 0;
@@ -219,21 +277,32 @@ __global__ __launch_bounds__(NNT) void k_nn_forward(int B, const int8_t *__restr
     const int b0 = blockIdx.x * ML, nb = min(ML, B - b0);
     const float *aff = W + Nt::AFF;                        // s1, t1, sp1, tp1
     const int t0 = 4 * wg, ntok = wg ? 3 : 4;              // this wave's token tiles (per-column layers)
+    constexpr int S1 = kpad(R) / 2;
+    RingC ringc;                                           // per-column weight fragments, one layer ahead
+    ringc_load<S1>(W + Nt::woff(0), wc, ringc);
 
     // ---- input: x[column c][leaf i][row r] = state[leaf][r][c] as int8 (token c*32+i)
     int8_t *x0 = reinterpret_cast<int8_t *>(bufA);
     for (int j = tid; j < 7 * ML * X0S / 4; j += NNT) reinterpret_cast<int32_t *>(x0)[j] = 0;
-    __syncthreads();
+    lds_barrier();
     for (int j = tid; j < nb * R; j += NNT) {              // one board row (7 bytes) per thread
         const int i = j / R, r = j - i * R;
         const int8_t *src = state + ((size_t)(b0 + i) * R + r) * 7;
 #pragma unroll
         for (int c = 0; c < 7; c++) x0[(c * ML + i) * X0S + r] = src[c];
     }
-    __syncthreads();
+    lds_barrier();
 
     f32x16 acc[4];
     const int col = 32 * wc + acc_col();
+    // this wave's 4 (group 0) or 3 (group 1) token tiles of column block wc
+    auto gemm_col = [&](auto s_const, const float *wp, auto afetch, auto next) {
+        constexpr int S = decltype(s_const)::value;
+        if (wg == 0)
+            gemm_tiles<4, S>(wp, wc, 0, ringc, afetch, acc, next);
+        else
+            gemm_tiles<3, S>(wp, wc, 4, ringc, afetch, acc, next);
+    };
     // per-column epilogue over this wave's token tiles: dst = f(acc, t, n)
     auto store_tiles = [&](int coloff, auto f) {
 #pragma unroll
@@ -248,30 +317,32 @@ __global__ __launch_bounds__(NNT) void k_nn_forward(int B, const int8_t *__restr
     };
     NN_PROBE(0)
     // ---- dense2d_1: relu(s1[c] * (W1 x + b1) + t1[c])
+    // (each layer's bias is read before its GEMM, ahead of the next layer's ring: vmcnt
+    // retires loads in order)
     {
-        constexpr int S = kpad(R) / 2;
-        gemm_tiles<4, S>(W + Nt::woff(0), wc, t0, ntok, [&](int t, int c) {
+        const float bias = W[Nt::boff(0) + col];
+        gemm_col(IntC<S1>(), W + Nt::woff(0), [&](int t, int c) {
             const int v = *reinterpret_cast<const int32_t *>(x0 + (t * ML + li) * X0S + c);
             return make_float4((float)(int8_t)v, (float)(int8_t)(v >> 8), (float)(int8_t)(v >> 16), (float)(v >> 24));
-        }, acc);
-        __syncthreads();
-        const float bias = W[Nt::boff(0) + col];
+        }, [&] { ringc_load<64>(W + Nt::woff(1), wc, ringc); });
+        lds_barrier();
         store_tiles(col, [&](float x, int t) { return fmaxf((x + bias) * aff[t] + aff[7 + t], 0.f); });
-        __syncthreads();
+        lds_barrier();
     }
     NN_PROBE(1)
     // ---- dense2d_1[3]: relu(W2 x + b2)
     {
-        gemm_tiles<4, 64>(W + Nt::woff(1), wc, t0, ntok, fetchA(0), acc);
-        __syncthreads();
         const float bias = W[Nt::boff(1) + col];
+        gemm_col(IntC<64>(), W + Nt::woff(1), fetchA(0), [&] { ringc_load<48>(W + Nt::woff(2), wc, ringc); });
+        lds_barrier();
         store_tiles(col, [&](float x, int) { return fmaxf(x + bias, 0.f); });
-        __syncthreads();
+        lds_barrier();
     }
     NN_PROBE(2)
     // ---- partialgpool_1: [max, mean over 4 groups of 8 of x[0:32]] ++ relu(BN(Wp1 x[32:] + bp1))
     {
-        gemm_tiles<4, 48>(W + Nt::woff(2), wc, t0, ntok, fetchA(32), acc);
+        const float bias = W[Nt::boff(2) + col];  // 0-padded to 128 columns
+        gemm_col(IntC<48>(), W + Nt::woff(2), fetchA(32), [&] { ringc_load<64>(W + Nt::woff(3), wc, ringc); });
         constexpr int NQ = (7 * ML * 8 + NNT - 1) / NNT;
         float pv[NQ];
 #pragma unroll
@@ -286,42 +357,61 @@ __global__ __launch_bounds__(NNT) void k_nn_forward(int B, const int8_t *__restr
                 pv[q] = j < 4 ? m : s / 8.f;
             }
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
             const int item = tid + NNT * q;
             if (item < 7 * ML * 8) bufA[(item >> 3) * XS + (item & 7)] = pv[q];
         }
-        if (col < 120) {
-            const float bias = W[Nt::boff(2) + col];
+        if (col < 120)
             store_tiles(8 + col, [&](float x, int t) { return fmaxf((x + bias) * aff[14 + t] + aff[21 + t], 0.f); });
-        }
-        __syncthreads();
+        lds_barrier();
     }
     NN_PROBE(3)
-    // ---- dense2d_3: relu(W3 x + b3)
+    // ---- dense2d_3: relu(W3 x + b3), written straight into the flattened per-leaf image
+    // Z[leaf][704] = [max_c<5 x[c][:64]][mean_c<5 x[c][:64]][x[5][:64]][x[6][:64]][x[c][64:], c<7]
+    // (FlattenAndPartialGPool(64, 5)), so dense1d_4 reads plain rows
+    float *Z = bufA;
+    Ring16 ring;                           // per-leaf weight fragments, one layer ahead
     {
-        gemm_tiles<4, 64>(W + Nt::woff(3), wc, t0, ntok, fetchA(0), acc);
-        __syncthreads();
         const float bias = W[Nt::boff(3) + col];
-        store_tiles(col, [&](float x, int) { return fmaxf(x + bias, 0.f); });
-        __syncthreads();
+        gemm_col(IntC<64>(), W + Nt::woff(3), fetchA(0), [&] { ring_load<1, 44>(W + Nt::woff(4), w, 8, 8, ring); });
+        lds_barrier();
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[t][r] = fmaxf(acc[t][r] + bias, 0.f);
+        if (col >= 64) {
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                if (t < ntok)
+#pragma unroll
+                    for (int r = 0; r < 16; r++) Z[acc_row(r) * ZS + 256 + 64 * (t0 + t) + col - 64] = acc[t][r];
+        } else if (wg == 0) {              // channels 0-3: partial max / sum -> bufP
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                bufP[acc_row(r) * 128 + col] = fmaxf(fmaxf(acc[0][r], acc[1][r]), fmaxf(acc[2][r], acc[3][r]));
+                bufP[acc_row(r) * 128 + 64 + col] = acc[0][r] + acc[1][r] + acc[2][r] + acc[3][r];
+            }
+        } else {                           // channels 5, 6 pass through
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                Z[acc_row(r) * ZS + 128 + col] = acc[1][r];
+                Z[acc_row(r) * ZS + 192 + col] = acc[2][r];
+            }
+        }
+        lds_barrier();
+        if (col < 64 && wg == 1) {         // channel 4 closes the pool
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int i = acc_row(r);
+                Z[i * ZS + col] = fmaxf(bufP[i * 128 + col], acc[0][r]);
+                Z[i * ZS + 64 + col] = (bufP[i * 128 + 64 + col] + acc[0][r]) / 5.f;
+            }
+        }
+        lds_barrier();
     }
     NN_PROBE(4)
-    // ---- FlattenAndPartialGPool(64, 5): pool[i] = [max_c<5 x[c][i][0:64], mean_c<5 ...]
-    for (int item = tid; item < ML * 64; item += NNT) {
-        const int i = item >> 6, f = item & 63;
-        float m = bufA[i * XS + f], s = m;
-#pragma unroll
-        for (int c = 1; c < 5; c++) {
-            const float x = bufA[(c * ML + i) * XS + f];
-            m = fmaxf(m, x);
-            s += x;
-        }
-        bufP[i * XS + f] = m;
-        bufP[i * XS + 64 + f] = s / 5.f;
-    }
-    __syncthreads();
     // ---- per-leaf layers on 16x16x4 tiles: wave w owns 16-column tile w (both 16-leaf row
     // tiles) of a 128-wide layer; dst[row][dst_off + col] = f(acc, col) for col < nmax
     f32x4 a16[4][2];
@@ -334,82 +424,98 @@ __global__ __launch_bounds__(NNT) void k_nn_forward(int B, const int8_t *__restr
                 for (int r = 0; r < 4; r++) dst[(16 * rt + acc16_row(r)) * stride + dst_off + col] = f(a16[j][rt][r], col);
         }
     };
-    auto leaf_fetch = [&](const float *src, int col0) {
-        return [=](int rt, int c) { return ld4(src + (16 * rt + (lane & 15)) * XS + col0 + c); };
+    auto leaf_fetch = [&](const float *src, int col0, int stride = PS) {
+        return [=](int rt, int c) { return ld4(src + (16 * rt + (lane & 15)) * stride + col0 + c); };
     };
+    // bias of this lane's column in tile ct of a per-leaf layer (biases are 0-padded to whole
+    // tiles). Read before the layer's GEMM: vmcnt retires loads in order, so a bias load
+    // issued behind the next layer's ring prefetch would wait for the whole ring.
+    auto bias16 = [&](int layer, int ct) { return W[Nt::boff(layer) + 16 * ct + acc16_col()]; };
+    auto ring7 = [&](int layer) { return [&, layer] { ring_load<1, 7>(W + Nt::woff(layer), w, 8, 8, ring); }; };
+    auto ring8 = [&](int layer) { return [&, layer] { ring_load<1, 8>(W + Nt::woff(layer), w, 8, 8, ring); }; };
+    constexpr int CT = ntiles16(ACT);      // PI[1] column tiles
+    static_assert(CT > 24 && CT <= 32, "PI[1] tiles: 3 or 4 per wave");
     NN_PROBE(5)
-    // ---- dense1d_4 over the 704 flattened features: [pool 128][x[5][:64]][x[6][:64]][x[c][64:128], c<7]
+    // ---- dense1d_4 over the 704 flattened features Z
     {
-        gemm16<1, 44>(W + Nt::woff(4), w, 8, 8, [&](int rt, int k) {
-            const int i = 16 * rt + (lane & 15);
-            if (k < 128) return ld4(bufP + i * XS + k);
-            if (k < 256) return ld4(bufA + ((5 + ((k - 128) >> 6)) * ML + i) * XS + ((k - 128) & 63));
-            return ld4(bufA + (((k - 256) >> 6) * ML + i) * XS + 64 + ((k - 256) & 63));
-        }, a16);
-        const float *bias = W + Nt::boff(4);
-        store16(0, w, bufQ, XS, 0, 128, [&](float x, int c) { return fmaxf(x + bias[c], 0.f); });
-        __syncthreads();
+        const float bl = bias16(4, w);
+        gemm16<1, 44>(W + Nt::woff(4), w, 8, ring, leaf_fetch(Z, 0, ZS), a16, ring7(5));
+        store16(0, w, bufQ, PS, 0, 128, [&](float x, int) { return fmaxf(x + bl, 0.f); });
+        lds_barrier();
     }
     // partial pool over 4 groups of 4 of x[0:16] ++ relu(Wp x[16:] + bp) (BN folded): src -> dst
-    auto pool44 = [&](const float *src, float *dst, int layer) {
+    auto pool44 = [&](const float *src, float *dst, int layer, auto next) {
+        const float bl = bias16(layer, w);
         float pv = 0.f;
         if (tid < ML * 8) {
             const int i = tid >> 3, j = tid & 7, g = j & 3;
-            const float *p = src + i * XS + 4 * g;
+            const float *p = src + i * PS + 4 * g;
             pv = j < 4 ? fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3])) : (p[0] + p[1] + p[2] + p[3]) / 4.f;
         }
-        gemm16<1, 7>(W + Nt::woff(layer), w, 8, 8, leaf_fetch(src, 16), a16);
-        const float *bias = W + Nt::boff(layer);
-        if (tid < ML * 8) dst[(tid >> 3) * XS + (tid & 7)] = pv;
-        store16(0, w, dst, XS, 8, 120, [&](float x, int c) { return fmaxf(x + bias[c], 0.f); });
-        __syncthreads();
+        gemm16<1, 7>(W + Nt::woff(layer), w, 8, ring, leaf_fetch(src, 16), a16, next);
+        if (tid < ML * 8) dst[(tid >> 3) * PS + (tid & 7)] = pv;
+        store16(0, w, dst, PS, 8, 120, [&](float x, int) { return fmaxf(x + bl, 0.f); });
+        lds_barrier();
     };
-    auto dense128 = [&](const float *src, float *dst, int layer) {
-        gemm16<1, 8>(W + Nt::woff(layer), w, 8, 8, leaf_fetch(src, 0), a16);
-        const float *bias = W + Nt::boff(layer);
-        store16(0, w, dst, XS, 0, 128, [&](float x, int c) { return fmaxf(x + bias[c], 0.f); });
-        __syncthreads();
+    auto dense128 = [&](const float *src, float *dst, int layer, auto next) {
+        const float bl = bias16(layer, w);
+        gemm16<1, 8>(W + Nt::woff(layer), w, 8, ring, leaf_fetch(src, 0), a16, next);
+        store16(0, w, dst, PS, 0, 128, [&](float x, int) { return fmaxf(x + bl, 0.f); });
+        lds_barrier();
     };
     NN_PROBE(6)
-    pool44(bufQ, bufP, 5);                  // partialgpool_4
-    dense128(bufP, bufQ, 6);                // dense1d_5[0] (+BN folded)
-    dense128(bufQ, bufP, 7);                // dense1d_5[3]
-    pool44(bufP, bufQ, 8);                  // partialgpool_5 -> trunk output in bufQ
+    pool44(bufQ, bufP, 5, ring8(6));        // partialgpool_4
+    dense128(bufP, bufQ, 6, ring8(7));      // dense1d_5[0] (+BN folded)
+    dense128(bufQ, bufP, 7, ring7(8));      // dense1d_5[3]
+    pool44(bufP, bufQ, 8, ring8(9));        // partialgpool_5 -> trunk output in bufQ
     NN_PROBE(7)
     // ---- heads: PI[0] -> bufP, V[0] -> bufA (no activation); wave w: column tile w of both
     {
-        gemm16<1, 8>(W + Nt::woff(9), w, 8, 8, leaf_fetch(bufQ, 0), a16);
-        gemm16<1, 8>(W + Nt::woff(11), w, 8, 8, leaf_fetch(bufQ, 0), a16 + 1);
-        const float *bp = W + Nt::boff(9), *bv = W + Nt::boff(11);
-        store16(0, w, bufP, XS, 0, 128, [&](float x, int c) { return x + bp[c]; });
-        store16(1, w, bufA, XS, 0, 128, [&](float x, int c) { return x + bv[c]; });
-        __syncthreads();
+        const float bp = bias16(9, w), bv = bias16(11, w);
+        gemm16<1, 8>(W + Nt::woff(9), w, 8, ring, leaf_fetch(bufQ, 0), a16, ring8(11));
+        gemm16<1, 8>(W + Nt::woff(11), w, 8, ring, leaf_fetch(bufQ, 0), a16 + 1,
+                     [&] { ring_load<4, 8>(W + Nt::woff(10), w, 8, CT, ring); });
+        store16(0, w, bufP, PS, 0, 128, [&](float x, int) { return x + bp; });
+        store16(1, w, bufA, PS, 0, 128, [&](float x, int) { return x + bv; });
+        lds_barrier();
     }
     NN_PROBE(8)
-    float *logits = bufA + ML * XS;
-    // ---- PI[1] (409 outputs, 26 column tiles over 8 waves) and V[1] (NP outputs, wave 7)
+    float *logits = bufA + ML * PS;
+    // ---- PI[1] (409 outputs, 26 column tiles: waves 0-1 take 4, the others 3) and V[1]
+    // (NP outputs, wave 7, whose ring is loaded behind its last PI[1] MFMA)
     {
-        constexpr int CT = ntiles16(ACT);
-        gemm16<4, 8>(W + Nt::woff(10), w, 8, CT, leaf_fetch(bufP, 0), a16);
-        const float *bp = W + Nt::boff(10);
+        float bp[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (w + 8 * j < CT) store16(j, w + 8 * j, logits, LS, 0, 16 * CT, [&](float x, int c) { return x + bp[c]; });
-        if (w == 7) {
-            gemm16<1, 8>(W + Nt::woff(12), 0, 1, 1, leaf_fetch(bufA, 0), a16);
+        for (int j = 0; j < 4; j++) bp[j] = bias16(10, min(w + 8 * j, CT - 1));
+        const float bv = bias16(12, 0);
+        auto store_logits = [&](int nc) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (j < nc) store16(j, w + 8 * j, logits, LS, 0, 16 * CT, [&](float x, int) { return x + bp[j]; });
+        };
+        if (w + 24 < CT) {
+            gemm16<4, 8>(W + Nt::woff(10), w, 8, ring, leaf_fetch(bufP, 0), a16, NoNext());
+            store_logits(4);
+        } else if (w != 7) {
+            gemm16<3, 8>(W + Nt::woff(10), w, 8, ring, leaf_fetch(bufP, 0), a16, NoNext());
+            store_logits(3);
+        } else {
+            gemm16<3, 8>(W + Nt::woff(10), w, 8, ring, leaf_fetch(bufP, 0), a16,
+                         [&] { ring_load<1, 8>(W + Nt::woff(12), 0, 1, 1, ring); });
+            store_logits(3);
+            gemm16<1, 8>(W + Nt::woff(12), 0, 1, ring, leaf_fetch(bufA, 0), a16, NoNext());
             const int n = acc16_col();
             if (n < NP) {
-                const float bias = W[Nt::boff(12) + n];
 #pragma unroll
                 for (int rt = 0; rt < 2; rt++)
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const int i = 16 * rt + acc16_row(r);
-                        if (i < nb) v_out[(size_t)(b0 + i) * NP + n] = tanhf(a16[0][rt][r] + bias);
+                        if (i < nb) v_out[(size_t)(b0 + i) * NP + n] = tanhf(a16[0][rt][r] + bv);
                     }
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
     NN_PROBE(9)
     // ---- masked softmax (invalid -> -1e8, as the reference's masked_fill + log_softmax);

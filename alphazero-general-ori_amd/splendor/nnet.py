@@ -161,8 +161,9 @@ def pack_weights(folded, n_players):
     """Pack a FoldedNet into the layout k_nn_forward reads (include/splendor_amd.h,
     spl_nn_forward): per layer the MFMA B-fragment order — layers 0-3 (32x32x2):
     [NT][S/4][64][4], element (nt, q, l, j) = W[32 nt + (l & 31)][4 q + j + (l >> 5) S],
-    S = Kp/2; layers 4-12 (16x16x4): element (nt, q, l, j) = W[16 nt + (l & 15)][4 q + j +
-    (l >> 4) S], S = Kp/4 — then the 0-padded bias; finally the per-column BN affines."""
+    S = Kp/2; layers 4-12 (16x16x4, Kp % 16 == 0): [NT][Kp/16][64][4], element (nt, q, l, j)
+    = W[16 nt + (l & 15)][16 q + 4 (l >> 4) + j] — then the 0-padded bias; finally the
+    per-column BN affines."""
     f = folded
     layers = [(f.w1, f.b1), (f.w2, f.b2), (f.wp1, f.bp1), (f.w3, f.b3), (f.w4, f.b4), (f.wp4, f.bp4),
               (f.w5a, f.b5a), (f.w5b, f.b5b), (f.wp5, f.bp5), (f.wpi1, f.bpi1), (f.wpi2, f.bpi2),
@@ -172,15 +173,18 @@ def pack_weights(folded, n_players):
         for li, (w, b) in enumerate(layers):
             N, K = w.shape
             kp = (K + 7) // 8 * 8
-            if li < 4:      # per-column layers: 32x32x2 fragments, K in 2 halves
-                T, G = 32, 2
-            else:           # per-leaf layers: 16x16x4 fragments, K in 4 quarters
-                T, G = 16, 4
-            NT, S = (N + T - 1) // T, kp // G
+            T = 32 if li < 4 else 16
+            NT = (N + T - 1) // T
             wp = torch.zeros((NT * T, kp), dtype=torch.float32, device=w.device)
             wp[:N, :K] = w
-            # [nt][col][g][q][j] -> [nt][q][g][col][j]; lane = T g + col
-            wr = wp.view(NT, T, G, S // 4, 4).permute(0, 3, 2, 1, 4)
+            if li < 4:      # per-column layers: 32x32x2 fragments, K in 2 halves
+                # [nt][col][g][q][j] -> [nt][q][g][col][j]; lane = 32 g + col
+                wr = wp.view(NT, T, 2, kp // 8, 4).permute(0, 3, 2, 1, 4)
+            else:           # per-leaf layers: 16x16x4 fragments, k groups interleaved by 4
+                if kp % 16:
+                    raise ValueError(f"per-leaf layer {li}: K={K} is not a multiple of 16")
+                # [nt][col][q][g][j] -> [nt][q][g][col][j]; lane = 16 g + col
+                wr = wp.view(NT, T, kp // 16, 4, 4).permute(0, 2, 3, 1, 4)
             parts.append(wr.reshape(-1))
             bp = torch.zeros(NT * T, dtype=torch.float32, device=w.device)
             bp[:N] = b

@@ -215,11 +215,12 @@ int spl_hash_eval(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t
  * (N outputs, K inputs) in the order dense2d_1[0], dense2d_1[3], partialgpool_1 dense,
  * dense2d_3, dense1d_4, partialgpool_4 dense, dense1d_5[0], dense1d_5[3], partialgpool_5
  * dense, output_layers_PI[0], [1], output_layers_V[0], [1]:
- *     Kp = K rounded up to 8; the first 4 layers use 32-column tiles and 2 K groups
- *     (T = 32, G = 2: v_mfma_f32_32x32x2_f32), the other 9 use T = 16, G = 4
- *     (v_mfma_f32_16x16x4_f32); S = Kp / G, NT = ceil(N / T)
- *     weights [NT][S/4][64][4]: element (nt, q, l, j) = W[T nt + (l % T)][4 q + j + (l / T) S]
- *             (0 outside N x K)
+ *     Kp = K rounded up to 8; NT = ceil(N / T)
+ *     first 4 layers (T = 32, v_mfma_f32_32x32x2_f32, K in 2 halves of S = Kp / 2):
+ *         weights [NT][S/4][64][4]: element (nt, q, l, j) = W[32 nt + l % 32][4 q + j + (l / 32) S]
+ *     other 9 (T = 16, v_mfma_f32_16x16x4_f32, Kp a multiple of 16, k groups interleaved):
+ *         weights [NT][Kp/16][64][4]: element (nt, q, l, j) = W[16 nt + l % 16][16 q + 4 (l / 16) + j]
+ *     (0 outside N x K)
  *     bias    [T NT] (0-padded)
  * then the per-board-column BatchNorm affines of dense2d_1 and partialgpool_1:
  * s1[7], t1[7], sp1[7], tp1[7] (y = x * s + t). Returns the float count or SPL_EINVAL. */
