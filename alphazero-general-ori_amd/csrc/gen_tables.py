@@ -136,6 +136,110 @@ def exchange_table():
     return t
 
 
+def take_need(t):
+    """bank level needed per colour by take t (F0 bit 30 + t): level 1 = >= 1 gem, 2 = >= 4."""
+    return TAKE[t] if t < 25 else tuple(2 if c == t - 25 else 0 for c in range(5))
+
+
+def give_need(g):
+    """gem level (min(gems, 3)) needed per colour by give set g (F1 bit g)."""
+    return GIVE[g] if g < 20 else SPEC3[g - 20]
+
+
+def mask_factors():
+    """Factorised mask words for reachable boards (splendor_device.h lane_mask_word_fast):
+    word K = gate(C) & card(F0 bits 0-29) & U1[bank levels c0-2] & U2[c3-4] & V1[gem levels
+    c0-2] & V2[c3-4]. Bank level = 0 / 1 (1-3 gems) / 2 (>= 4); gem level = min(gems, 3).
+    Returns (per-word table rows, per-word condition masks, card blocks)."""
+    desc = action_table()
+    rows, gates, blocks = [], [], []
+    for K in range(7):
+        acts = [(j, desc[64 * K + j]) for j in range(64) if 64 * K + j < 409]
+
+        def table(colours, base, need_of):
+            out = []
+            for idx in range(base ** len(colours)):
+                lv = [(idx // base ** i) % base for i in range(len(colours))]
+                m = 0
+                for j, d in acts:
+                    need = need_of(d)
+                    if need is None or all(lv[i] >= need[c] for i, c in enumerate(colours)):
+                        m |= 1 << j
+                # bits past action 408 are 1 here; the gates never set them
+                out.append(m | (((1 << 64) - 1) ^ sum(1 << j for j, _ in acts)))
+            return out
+
+        tk = lambda d: take_need((d & 63) - 30) if (d >> 6) & 1 and (d & 63) >= 30 else None
+        gv = lambda d: give_need((d >> 8) & 63) if (d >> 14) & 1 else None
+        rows.append(table((0, 1, 2), 3, tk) + table((3, 4), 3, tk) + table((0, 1, 2), 4, gv) + table((3, 4), 4, gv))
+        gates.append([sum(1 << j for j, d in acts if (d >> 16) & 15 == c) for c in range(11)])
+        # card predicate bits (F0 < 30): runs copied (f0 rises with j) or replicated (same f0)
+        uses = [(j, d & 63) for j, d in acts if (d >> 6) & 1 and (d & 63) < 30]
+        i = 0
+        while i < len(uses):
+            j0, f0 = uses[i]
+            n = 1
+            if i + 1 < len(uses) and uses[i + 1] == (j0 + 1, f0 + 1):
+                while i + n < len(uses) and uses[i + n] == (j0 + n, f0 + n):
+                    n += 1
+                blocks.append((K, j0, n, f0, 0))        # copy F0[f0 .. f0+n) to j0 ..
+            else:
+                while i + n < len(uses) and uses[i + n] == (j0 + n, f0):
+                    n += 1
+                blocks.append((K, j0, n, f0, 1))        # replicate F0[f0] over j0 .. j0+n
+            i += n
+    return rows, gates, blocks
+
+
+def check_mask_factors(rows, gates, blocks, trials=20000):
+    """The factorised words equal the descriptor formula C & F0 & F1 on random predicates."""
+    import random
+    rnd = random.Random(7)
+    desc = action_table()
+    for _ in range(trials):
+        bank = [rnd.randint(0, 7) for _ in range(5)]
+        gems = [rnd.randint(0, 5) for _ in range(5)]
+        cards = rnd.getrandbits(30)
+        C = rnd.getrandbits(10)
+        lam = [0 if b < 1 else (1 if b < 4 else 2) for b in bank]
+        ell = [min(g, 3) for g in gems]
+        F0 = cards
+        for t in range(30):
+            need = take_need(t)
+            if all(bank[c] >= (4 if need[c] == 2 else need[c]) for c in range(5)):
+                F0 |= 1 << (30 + t)
+        F1 = sum(1 << g for g in range(60) if all(gems[c] >= give_need(g)[c] for c in range(5)))
+        for K in range(7):
+            want = 0
+            for j in range(64):
+                a = 64 * K + j
+                if a >= 409:
+                    continue
+                d = desc[a]
+                bit = (C >> ((d >> 16) & 15)) & 1
+                if (d >> 6) & 1:
+                    bit &= F0 >> (d & 63)
+                if (d >> 14) & 1:
+                    bit &= F1 >> ((d >> 8) & 63)
+                want |= (bit & 1) << j
+            r = rows[K]
+            got = r[lam[0] + 3 * lam[1] + 9 * lam[2]] & r[27 + lam[3] + 3 * lam[4]]
+            got &= r[36 + ell[0] + 4 * ell[1] + 16 * ell[2]] & r[100 + ell[3] + 4 * ell[4]]
+            gate = 0
+            for c in range(11):
+                if (C >> c) & 1:
+                    gate |= gates[K][c]
+            card = (1 << 64) - 1
+            for (k, j0, n, f0, rep) in blocks:
+                if k != K:
+                    continue
+                span = ((1 << n) - 1) << j0
+                src = (((cards >> f0) & 1) * ((1 << n) - 1) if rep else (cards >> f0) & ((1 << n) - 1)) << j0
+                card &= ~span | src
+            got &= gate & card
+            assert got == want, (K, hex(got), hex(want))
+
+
 def arr(name, ctype, rows, fmt=str):
     body = ",\n  ".join("{" + ",".join(fmt(x) for x in r) + "}" if isinstance(r, (list, tuple)) else fmt(r)
                         for r in rows)
@@ -238,6 +342,18 @@ def main():
     out.append("// F0 bits 30..59 / F1 bits 0..59: required threshold bits (bit 5t+c: colour c >= t)")
     out.append(arr("static constexpr uint32_t KC_REQ0[60]", None, req0, lambda x: f"0x{x:07x}u"))
     out.append(arr("static constexpr uint32_t KC_REQ1[60]", None, req1, lambda x: f"0x{x:07x}u"))
+    # ---- factorised mask words (lane_mask_word_fast)
+    rows, gates, blocks = mask_factors()
+    check_mask_factors(rows, gates, blocks)
+    out.append("// factorised mask words: per word K, 116 rows = U1[27] (bank levels c0-2, base 3),")
+    out.append("// U2[9] (c3-4), V1[64] (gem levels c0-2, base 4), V2[16] (c3-4); level tables AND to")
+    out.append("// the take / give feasibility of every action of the word (1 where unused)")
+    out.append(arr("static __constant__ uint64_t K_MASK_FACTORS[7][116]", None, rows, lambda x: f"0x{x:016x}ull"))
+    out.append("// per word K: actions gated by condition code c")
+    out.append(arr("static constexpr uint64_t KC_MASK_GATE[7][11]", None, gates, lambda x: f"0x{x:016x}ull"))
+    out.append("// card-predicate runs: word, first bit, length, F0 bit, replicate (1) or copy (0)")
+    out.append(f"static constexpr int KC_CARD_NBLK = {len(blocks)};")
+    out.append(arr(f"static constexpr uint8_t KC_CARD_BLK[{len(blocks)}][5]", None, blocks))
     print("\n".join(out))
 
 

@@ -45,6 +45,13 @@ struct Lay {  // row offsets of the (R,7) state (SplendorLogicNumba.py:296-303)
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// workgroup barrier ordering LDS traffic only: waits for this wave's LDS (and scalar)
+// operations, not its global ones. __syncthreads() first waits vmcnt(0), i.e. for every
+// global store of the wave to be acknowledged by memory (~2K cycles for HBM). Use it where
+// no wave reads global memory another wave wrote before the barrier. The memory clobber
+// keeps the compiler from moving memory accesses across it.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // ------------------------------------------------------------------ row words
 __device__ __forceinline__ uint64_t &row(int8_t *s, int r) { return *reinterpret_cast<uint64_t *>(s + 8 * r); }
 __device__ __forceinline__ uint64_t row(const int8_t *s, int r) { return *reinterpret_cast<const uint64_t *>(s + 8 * r); }
@@ -508,14 +515,54 @@ __device__ __forceinline__ LanePred lane_predicates(const int8_t *s, int p, int 
     return P;
 }
 
+// packed level indices of lane_mask_word_fast: bank levels (0 / 1-3 / >= 4 gems) and gem
+// levels (min(gems, 3)) of colours 0-2 and 3-4, as table row offsets
+__device__ __forceinline__ uint32_t lane_levels(uint64_t bank, uint64_t gems) {
+    int lam[5], ell[5];
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        const int b = bt(bank, c);
+        lam[c] = b >= 4 ? 2 : (b >= 1 ? 1 : 0);
+        ell[c] = min(bt(gems, c), 3);
+    }
+    return (uint32_t)(lam[0] + 3 * lam[1] + 9 * lam[2]) | (uint32_t)(lam[3] + 3 * lam[4]) << 5 |
+           (uint32_t)(ell[0] + 4 * ell[1] + 16 * ell[2]) << 9 | (uint32_t)(ell[3] + 4 * ell[4]) << 15;
+}
+
+// Mask word K of a board in the fast domain from its card predicates (F0 bits 0-29),
+// condition bits C and levels lv (lane_levels): the gem-vector predicates of
+// lane_predicates depend on the board only through the colour levels, so per word they
+// factor into four level-table rows (K_MASK_FACTORS, staged at fac) ANDed with the gates
+// of the word's condition codes and its card-predicate runs (gen_tables.py mask_factors,
+// which checks the factorisation against the descriptor formula of lane_mask_word).
+template <int K>
+__device__ __forceinline__ uint64_t lane_mask_word_fast(uint32_t C, uint64_t F0, uint32_t lv, const uint64_t *fac) {
+    const uint64_t *r = fac + 116 * K;
+    const uint64_t m = r[lv & 31] & r[27 + ((lv >> 5) & 15)] & r[36 + ((lv >> 9) & 63)] & r[100 + ((lv >> 15) & 15)];
+    uint64_t gate = 0;
+#pragma unroll
+    for (int c = 0; c < 11; c++)
+        if (KC_MASK_GATE[K][c]) gate |= ((C >> c) & 1) ? KC_MASK_GATE[K][c] : 0ull;
+    uint64_t card = ~0ull;
+#pragma unroll
+    for (int b = 0; b < KC_CARD_NBLK; b++) {
+        if (KC_CARD_BLK[b][0] != K) continue;
+        const int j0 = KC_CARD_BLK[b][1], n = KC_CARD_BLK[b][2], f0 = KC_CARD_BLK[b][3];
+        const uint64_t span = ((1ull << n) - 1) << j0;
+        const uint64_t src = KC_CARD_BLK[b][4] ? (((F0 >> f0) & 1) ? span : 0ull) : ((F0 >> f0) << j0) & span;
+        card &= ~span | src;
+    }
+    return m & gate & card;
+}
+
 // One quarter of lane_predicates' fast path, so four waves can share a board's predicate
 // work: PART 0 / 1 = buy and reserve bits of visible cards 0-5 / 6-11, PART 2 = reserved
-// cards, deck reserves and the condition bits, PART 3 = the gem-vector lookups. The parts
-// OR together to lane_predicates' F0 / F1 / C; `bad` flags rows outside the fast domain
-// (the caller then uses lane_predicates_exact for the board).
+// cards, deck reserves and the condition bits, PART 3 = the colour levels (returned in F1)
+// that lane_mask_word_fast turns into the gem-vector predicates. F0 / C of the parts OR
+// together; `bad` flags rows outside the fast domain (the caller then uses
+// lane_predicates_exact and lane_mask_word for the board).
 template <int N, int PART>
-__device__ __forceinline__ void lane_predicates_part(const int8_t *s, int p, int lim, const uint32_t *lut_diff,
-                                                     const uint64_t *lut_s3, uint64_t &F0, uint64_t &F1,
+__device__ __forceinline__ void lane_predicates_part(const int8_t *s, int p, int lim, uint64_t &F0, uint64_t &F1,
                                                      uint32_t &C, bool &bad) {
     using Lx = Lay<N>;
     constexpr uint64_t M5 = 0xFFFFFFFFFFull, H5 = 0x8080808080ull;
@@ -523,12 +570,7 @@ __device__ __forceinline__ void lane_predicates_part(const int8_t *s, int p, int
     F0 = 0; F1 = 0; C = 0;
     if constexpr (PART == 3) {
         bad = ((bank | gems) & H5) != 0;
-        const uint32_t b1 = ge_set(bank, 1), g1 = ge_set(gems, 1);
-        uint32_t lvl = 0;
-#pragma unroll
-        for (int c = 0; c < 5; c++) lvl |= (uint32_t)min(bt(gems, c), 3) << (2 * c);
-        F0 = (uint64_t)lut_diff[b1] << 30 | (uint64_t)ge_set(bank, 4) << 55;
-        F1 = (uint64_t)(lut_diff[g1] & 0x7FFFu) | (uint64_t)ge_set(gems, 2) << 15 | lut_s3[lvl] << 20;
+        F1 = lane_levels(bank, gems);
     } else {
         constexpr int I0 = PART == 0 ? 0 : (PART == 1 ? 6 : 12), NI = PART == 2 ? 3 : 6;
         const uint64_t cards = row(s, Lx::CARDS + p), slot5 = row(s, Lx::RSV + 6 * p + 5);
@@ -624,8 +666,9 @@ __device__ __noinline__ int pick_color_div(uint64_t cnt, int tot, double u) {
 // Colour / card picks of _get_deck_card. The reference compares fp cumulative sums of the
 // quotients cnt_k / tot (and 1 / nbits) with u; those sums equal the exact fractions
 // C_k / tot to within 1e-15, so away from a boundary the pick is the integer count of
-// prefix sums C_k <= u * tot. Draws within 1e-9 of a boundary (|C_k - u * tot| < 1e-9;
-// about one in 1e9) take the reference's fp sums over the exact quotient tables instead.
+// prefix sums C_k <= u * tot. Draws with u * tot within 1e-9 of an integer (which covers
+// every boundary |C_k - u * tot| < 1e-9; about 2 in 1e9) take the reference's fp sums over
+// the exact quotient tables instead.
 __device__ __noinline__ int pick_color_fp(uint64_t cnt, int tot, double u, const double (*quot)[9]) {
     const double *q = quot[tot];
     double c = 0.0;
@@ -645,48 +688,70 @@ __device__ __noinline__ int pick_card_fp(uint32_t b, double u, const double *rec
     return 7;
 }
 
-template <int N>
-__device__ __forceinline__ bool deck_card(int8_t *s, int tier, Chance &ch, uint64_t &cost, uint64_t &gain) {
-    using Lx = Lay<N>;
-    const uint64_t cnt = row(s, Lx::DECKS + 2 * tier), bits = row(s, Lx::DECKS + 2 * tier + 1);
+// floor(x) of x >= 0, and whether x lies within 1e-9 of an integer (x - floor(x) and
+// floor(x) + 1 - x are exact in f64). For an integer prefix count C, C <= x iff
+// C <= floor(x), so the picks below count in integers; "near" is a superset of the
+// boundary draws |C_k - x| < 1e-9 and sends them (and ~2e-9 of all draws) to the fp path.
+__device__ __forceinline__ int floor_near(double x, bool &near) {
+    const double f = floor(x);
+    near = x - f < 1e-9 || f + 1.0 - x < 1e-9;
+    return (int)f;
+}
+
+// the colour and card index one draw takes from a tier deck's count / bit rows (tot > 0),
+// given the draw's two uniforms; deck_take removes that card from the rows
+__device__ __forceinline__ void deck_pick(uint64_t cnt, uint64_t bits, double u0, double u1, const Tabs &tab,
+                                          int &color_out, int &idx_out) {
     const int tot = sum5(cnt);
-    if (tot == 0) return false;
     bool dom = true;
 #pragma unroll
     for (int k = 0; k < 5; k++) dom &= (unsigned)bt(cnt, k) <= 8u;
-    const double u0 = ch.draw();
     int color;
     if (dom) {
-        const double x = u0 * (double)tot;
+        bool amb;
+        const int fx = floor_near(u0 * (double)tot, amb);
         int ck = 0, n_le = 0;
-        bool amb = false;
 #pragma unroll
         for (int k = 0; k < 5; k++) {
             ck += bt(cnt, k);
-            n_le += (double)ck <= x;
-            amb |= fabs((double)ck - x) < 1e-9;
+            n_le += ck <= fx;
         }
-        color = amb ? pick_color_fp(cnt, tot, u0, ch.tab.quot) : min(n_le, 4);
+        color = amb ? pick_color_fp(cnt, tot, u0, tab.quot) : min(n_le, 4);
     } else {
         color = pick_color_div(cnt, tot, u0);
     }
     const uint32_t b = (uint8_t)bt(bits, color);
     const int nb = __builtin_popcount(b);
-    const double u1 = ch.draw();
-    const double x = u1 * (double)nb;
+    bool amb;
+    const int fx = floor_near(u1 * (double)nb, amb);
     int pk = 0, n_le = 0;
-    bool amb = false;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         pk += (b >> (7 - k)) & 1;
-        n_le += (double)pk <= x;
-        amb |= fabs((double)pk - x) < 1e-9;
+        n_le += pk <= fx;
     }
-    // nb == 0 (reference: 0/0 sums, no index above u -> the last card) is ambiguous here
-    // and resolved by the fp path, which returns the last card as well
-    const int idx = amb ? pick_card_fp(b, u1, ch.tab.recip) : min(n_le, 7);
-    row(s, Lx::DECKS + 2 * tier + 1) = with_bt(bits, color, (int)(b & ~(1u << (7 - idx))));
-    row(s, Lx::DECKS + 2 * tier) = with_bt(cnt, color, bt(cnt, color) - 1);
+    // nb == 0 (reference: 0/0 sums, no index above u -> the last card) gives x = 0, near an
+    // integer, and is resolved by the fp path, which returns the last card as well
+    color_out = color;
+    idx_out = amb ? pick_card_fp(b, u1, tab.recip) : min(n_le, 7);
+}
+__device__ __forceinline__ void deck_take(uint64_t &cnt, uint64_t &bits, int color, int idx) {
+    bits = with_bt(bits, color, (int)((uint8_t)bt(bits, color) & ~(1u << (7 - idx))));
+    cnt = with_bt(cnt, color, bt(cnt, color) - 1);
+}
+
+template <int N>
+__device__ __forceinline__ bool deck_card(int8_t *s, int tier, Chance &ch, uint64_t &cost, uint64_t &gain) {
+    using Lx = Lay<N>;
+    uint64_t cnt = row(s, Lx::DECKS + 2 * tier), bits = row(s, Lx::DECKS + 2 * tier + 1);
+    if (sum5(cnt) == 0) return false;
+    const double u0 = ch.draw();
+    const double u1 = ch.draw();
+    int color, idx;
+    deck_pick(cnt, bits, u0, u1, ch.tab, color, idx);
+    deck_take(cnt, bits, color, idx);
+    row(s, Lx::DECKS + 2 * tier + 1) = bits;
+    row(s, Lx::DECKS + 2 * tier) = cnt;
     cost = ch.tab.cards[tier * 40 + color * 8 + idx][0];
     gain = ch.tab.cards[tier * 40 + color * 8 + idx][1];
     return true;
@@ -896,15 +961,32 @@ __device__ __forceinline__ int get_score(const int8_t *lds, int p) { return scor
 // The four parts touch disjoint rows and are dealt concurrently by lanes 0-3.
 constexpr int DEAL_DRAWS = 29;                    // 24 card draws + up to 5 nobles
 
+// The four draws of a tier touch only its deck rows: they run on registers (deck rows and
+// the 8 uniforms loaded once), and the deck and visible-card rows are written at the end.
 template <int N>
 __device__ __forceinline__ void deal_tier(int8_t *s, int t, const double *u, const Tabs &tab) {
     using Lx = Lay<N>;
     const uint64_t len = t == 0 ? 8 : (t == 1 ? 6 : 4);
-    const uint64_t bits = (uint8_t)(0xFFu << (8 - len));
-    row(s, Lx::DECKS + 2 * t) = len * 0x0000000101010101ull;
-    row(s, Lx::DECKS + 2 * t + 1) = bits * 0x0000000101010101ull;
-    Chance ch{u + 8 * t, 0, 0, 0, 0, 0.0, false, tab};
-    for (int i = 0; i < 4; i++) fill_new_card<N>(s, t, i, false, ch);
+    uint64_t cnt = len * 0x0000000101010101ull;
+    uint64_t bits = (uint8_t)(0xFFu << (8 - len)) * 0x0000000101010101ull;
+    double uu[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) uu[k] = u[8 * t + k];
+    int card[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int color, idx;
+        deck_pick(cnt, bits, uu[2 * i], uu[2 * i + 1], tab, color, idx);
+        deck_take(cnt, bits, color, idx);
+        card[i] = t * 40 + color * 8 + idx;
+    }
+    row(s, Lx::DECKS + 2 * t) = cnt;
+    row(s, Lx::DECKS + 2 * t + 1) = bits;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        row(s, Lx::TIERS + 8 * t + 2 * i) = tab.cards[card[i]][0];
+        row(s, Lx::TIERS + 8 * t + 2 * i + 1) = tab.cards[card[i]][1];
+    }
 }
 template <int N>
 __device__ __forceinline__ void deal_nobles_bank(int8_t *s, const double *u) {

@@ -213,8 +213,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     __shared__ double ud[RB][4];       // draws 0..3 of each board's step stream
     __shared__ double ub[WAVES][DEAL_DRAWS];
     __shared__ TabsLds tabs;
-    __shared__ uint32_t lut_diff[32];
-    __shared__ uint64_t lut_s3[1024];
+    __shared__ uint64_t mfac[7 * 116];  // K_MASK_FACTORS (lane_mask_word_fast)
     __shared__ int16_t act[RB];
     __shared__ uint8_t klist[4][RB], rflag[RB];
     __shared__ int kcount[4];
@@ -240,9 +239,10 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     if (tid < RB) rflag[tid] = 0;
     if (tid < 4) kcount[tid] = 0;
     stage_tabs(tabs, tid, THREADS);
-    for (int i = tid; i < 1024; i += THREADS) lut_s3[i] = K_LUT_SPEC3[i];
-    if (tid < 32) lut_diff[tid] = K_LUT_DIFF[tid];
-    __syncthreads();
+    for (int i = tid; i < 7 * 116; i += THREADS) mfac[i] = (&K_MASK_FACTORS[0][0])[i];
+    // every barrier of the move loop orders LDS only: the per-move outputs are write-only
+    // HBM streams, and waiting for their stores (__syncthreads) cost ~2K cycles a barrier
+    lds_sync();
     RT_MARK(0)
     for (int t = 0; t < K; t++) {
         const uint32_t step = step0 + (uint32_t)t;
@@ -258,33 +258,55 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
             bool bad;
             const int8_t *s = lds + l * ST;
             switch (w) {
-                case 0: lane_predicates_part<N, 0>(s, pl[l], lim, lut_diff, lut_s3, f0, f1, cc, bad); break;
-                case 1: lane_predicates_part<N, 1>(s, pl[l], lim, lut_diff, lut_s3, f0, f1, cc, bad); break;
-                case 2: lane_predicates_part<N, 2>(s, pl[l], lim, lut_diff, lut_s3, f0, f1, cc, bad); break;
-                default: lane_predicates_part<N, 3>(s, pl[l], lim, lut_diff, lut_s3, f0, f1, cc, bad); break;
+                case 0: lane_predicates_part<N, 0>(s, pl[l], lim, f0, f1, cc, bad); break;
+                case 1: lane_predicates_part<N, 1>(s, pl[l], lim, f0, f1, cc, bad); break;
+                case 2: lane_predicates_part<N, 2>(s, pl[l], lim, f0, f1, cc, bad); break;
+                default: lane_predicates_part<N, 3>(s, pl[l], lim, f0, f1, cc, bad); break;
             }
             pf0[w][l] = f0;
             if (w == 3) pf1[l] = f1;
             if (w == 2) pcond[l] = cc;
             pbad[w][l] = bad;
         }
-        __syncthreads();
-        // mask words w and w+4 of every board from the combined predicates
+        RT_MARK(16)
+        lds_sync();
+        RT_MARK(17)
+        // mask words w and w+4 of every board: factorised words from the card predicates,
+        // condition bits and colour levels; boards outside the fast domain take the exact
+        // predicates and the per-action descriptor words
         if (ROLLOUT_ABLATE != 1 && l < nb) {
-            LanePred P;
-            if (pbad[0][l] | pbad[1][l] | pbad[2][l] | pbad[3][l]) {
-                P = lane_predicates_exact<N>(lds + l * ST, pl[l], lim);
-            } else {
-                P.F0 = pf0[0][l] | pf0[1][l] | pf0[2][l] | pf0[3][l];
-                P.F1 = pf1[l];
-                P.C = pcond[l];
+            const bool bad = pbad[0][l] | pbad[1][l] | pbad[2][l] | pbad[3][l];
+#if ROLLOUT_TIMING
+            {   // diagnostic: waves that take the exact predicate path (slot 18), lanes (19)
+                const uint64_t bm = __ballot(bad);
+                if (l == 0 && bm) { atomicAdd((unsigned long long *)&spl_probe_acc[18], 1ull);
+                                    atomicAdd((unsigned long long *)&spl_probe_acc[19], (unsigned long long)__popcll(bm)); }
             }
-            if (w == 0) { msk[l][0] = lane_mask_word<0>(P); msk[l][4] = lane_mask_word<4>(P); }
-            else if (w == 1) { msk[l][1] = lane_mask_word<1>(P); msk[l][5] = lane_mask_word<5>(P); }
-            else if (w == 2) { msk[l][2] = lane_mask_word<2>(P); msk[l][6] = lane_mask_word<6>(P); }
-            else { msk[l][3] = lane_mask_word<3>(P); }
+#endif
+            if (bad) {
+                const LanePred P = lane_predicates_exact<N>(lds + l * ST, pl[l], lim);
+                if (w == 0) { msk[l][0] = lane_mask_word<0>(P); msk[l][4] = lane_mask_word<4>(P); }
+                else if (w == 1) { msk[l][1] = lane_mask_word<1>(P); msk[l][5] = lane_mask_word<5>(P); }
+                else if (w == 2) { msk[l][2] = lane_mask_word<2>(P); msk[l][6] = lane_mask_word<6>(P); }
+                else { msk[l][3] = lane_mask_word<3>(P); }
+            } else {
+                const uint64_t F0 = pf0[0][l] | pf0[1][l] | pf0[2][l];
+                const uint32_t C = pcond[l], lv = (uint32_t)pf1[l];
+                if (w == 0) {
+                    msk[l][0] = lane_mask_word_fast<0>(C, F0, lv, mfac);
+                    msk[l][4] = lane_mask_word_fast<4>(C, F0, lv, mfac);
+                } else if (w == 1) {
+                    msk[l][1] = lane_mask_word_fast<1>(C, F0, lv, mfac);
+                    msk[l][5] = lane_mask_word_fast<5>(C, F0, lv, mfac);
+                } else if (w == 2) {
+                    msk[l][2] = lane_mask_word_fast<2>(C, F0, lv, mfac);
+                    msk[l][6] = lane_mask_word_fast<6>(C, F0, lv, mfac);
+                } else {
+                    msk[l][3] = lane_mask_word_fast<3>(C, F0, lv, mfac);
+                }
+            }
         }
-        __syncthreads();
+        lds_sync();
         RT_MARK(1)
         // select: lane l < 16 of wave w: pass bit (:263), uniform pick, filed by move kind
         {
@@ -306,7 +328,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                 klist[kind][atomicAdd(&kcount[kind], 1)] = (uint8_t)b;
             }
         }
-        __syncthreads();
+        lds_sync();
         RT_MARK(5)
         // move: wave w makes every move of kind w (one pipeline specialisation per wave, so no
         // wave carries the stages of other kinds); chance draws 1-2; end check; outputs
@@ -339,7 +361,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
             pl[b] = (int8_t)nxt;
             rflag[b] = ended;
         }
-        __syncthreads();
+        lds_sync();
         RT_MARK(2)
         if (tid < 4) kcount[tid] = 0;
         uint64_t rm = __ballot(l < nb && rflag[l]);
@@ -349,9 +371,11 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
             wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)(b0 + rb), step, 3, DEAL_DRAWS);
             wave_init_game<N>(lds + rb * ST, ub[w], tabs.view());
         }
+        RT_MARK(8)
         if (mask_out && ROLLOUT_ABLATE != 1)
             for (int i = tid; i < nb * 7; i += THREADS) mask_out[ob * 7 + i] = (&msk[0][0])[i];
-        __syncthreads();
+        RT_MARK(9)
+        lds_sync();
         RT_MARK(3)
     }
     for (int i = tid; i < nb * Cv::UNITS; i += THREADS) {

@@ -7,7 +7,7 @@
 #include <cstdio>
 #include <vector>
 int main() {
-    const int B = 32768, NB = B / 64, K = 20;
+    const int B = 32768, NB = B / 64, K = 100;
     spl_ctx *c; spl_ctx_create(2, 10, &c);
     int8_t *st, *pl; uint64_t *mk; int16_t *ac; float *en; int32_t *gd; uint64_t *tm;
     (void)hipMalloc(&st, (size_t)B * 392); (void)hipMalloc(&pl, B); (void)hipMalloc(&mk, (size_t)K * B * 56);
@@ -20,13 +20,13 @@ int main() {
     (void)hipDeviceSynchronize();
     std::vector<uint64_t> h((size_t)NB * 32);
     // probe slots (splendor_env.hip / splendor_device.h SPL_PROBE)
-    const int slots[] = {0, 1, 5, 10, 15, 11, 12, 13, 14, 7, 2, 3, 4};
-    const char *names[] = {"load", "mask", "move: select", "move: decode", "move: buy (pay)",
-                           "move: buy (nobles)", "move: reserve slot", "move: deck draw",
-                           "move: shift+gems", "move: end+outputs", "move: tail to sync",
-                           "reset+mask store", "store"};
-    const bool per_move[] = {false, true, true, true, true, true, true, true, true, true, true, true, false};
-    const int NS = 13;
+    // (thread 0 = lane 0 of wave 0: its move-phase slots see the gem-move pipeline)
+    const int slots[] = {0, 16, 17, 1, 5, 6, 7, 2, 8, 9, 3, 4};
+    const char *names[] = {"load", "philox+predicates (w0)", "predicate sync", "mask words+sync", "select",
+                           "make_move (wave 0)", "end check", "outputs+tail to sync", "reset", "mask store",
+                           "barrier", "store"};
+    const bool per_move[] = {false, true, true, true, true, true, true, true, true, true, true, false};
+    const int NS = 12;
     for (int rep = 0; rep < 2; rep++) {
         spl_rollout_run(c, B, K, st, pl, mk, ac, en, gd, 0x5EED, 200 + K * rep, 0, nullptr);
         (void)hipDeviceSynchronize();
@@ -47,6 +47,9 @@ int main() {
         }
         std::sort(life.begin(), life.end());
         printf("  block life us p10 %.2f p50 %.2f p90 %.2f max %.2f\n", life[NB / 10], life[NB / 2], life[NB * 9 / 10], life[NB - 1]);
+        double xw = 0, xl = 0;
+        for (int b = 0; b < NB; b++) { xw += (double)h[(size_t)b * 32 + 18]; xl += (double)h[(size_t)b * 32 + 19]; }
+        printf("  exact-path waves per wave-move %.4f, lanes per board-move %.5f\n", xw / (NB * 4.0 * K), xl / (NB * 64.0 * K));
     }
     return 0;
 }
