@@ -175,17 +175,18 @@ __global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__re
 // rows at an odd-qword stride (conflict-free lane-per-board ds_read_b64/ds_write_b64), for
 // all K moves of the launch:
 //   load     HBM -> LDS, one 4-row quad per thread (7 dwords -> 4 qwords), deck tables
-//   per move t (step = step0 + t):
-//     mask   Philox blocks 0-1 of every board's step stream (draw 0 picks the action, 1-2
-//            feed a deck draw); lane-per-board legality predicates + mask words w, w+4 in
-//            wave w, on the real board for the player to move (== the canonical form's
-//            mask: it only reads player p's rows)
+//   per move t (step = step0 + t), four phases between LDS-only barriers:
+//     preds  lane-per-board legality predicates on the real board for the player to move
+//            (== the canonical form's mask: it only reads player p's rows), part w in wave
+//            w (cards 0-5 / cards 6-11 / reserved cards, decks, conditions / colour
+//            levels); wave 3 also draws Philox blocks 0-1 of every board's step stream
+//            (draw 0 picks the action, 1-2 feed a deck draw)
+//     mask   mask words w, w+4 in wave w (factorised words, lane_mask_word_fast)
 //     select lane l < 16 of wave w = board 16w + l: pass bit (:263), uniform action draw;
 //            boards filed by move kind
-//     move   wave k makes the moves of kind k (gem vectors / buy / reserve / buy reserved),
-//            lane per board, chance, end check; per-move outputs
-//     reset  finished games are re-dealt wave-parallel (draws 3.., Philox per lane); the
-//            move's masks go to HBM
+//     move   the masks go to HBM; wave k makes the moves of kind k (gem vectors / buy /
+//            reserve / buy reserved), lane per board: chance, end check, per-move outputs;
+//            then it re-deals the games its moves finished (wave-collective, draws 3..)
 //   store    boards, players, game counters LDS -> HBM
 constexpr int RB = 64;
 #define RT_MARK(k) SPL_PROBE(k)
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     __shared__ TabsLds tabs;
     __shared__ uint64_t mfac[7 * 116];  // K_MASK_FACTORS (lane_mask_word_fast)
     __shared__ int16_t act[RB];
-    __shared__ uint8_t klist[4][RB], rflag[RB];
+    __shared__ uint8_t klist[4][RB];
     __shared__ int kcount[4];
     __shared__ uint64_t pf0[WAVES][RB], pf1[RB];
     __shared__ uint32_t pcond[RB];
@@ -236,7 +237,6 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         pl[tid] = player[b0 + tid];
         gdone[tid] = games_done ? games_done[b0 + tid] : 0;
     }
-    if (tid < RB) rflag[tid] = 0;
     if (tid < 4) kcount[tid] = 0;
     stage_tabs(tabs, tid, THREADS);
     for (int i = tid; i < 7 * 116; i += THREADS) mfac[i] = (&K_MASK_FACTORS[0][0])[i];
@@ -247,9 +247,12 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     for (int t = 0; t < K; t++) {
         const uint32_t step = step0 + (uint32_t)t;
         const size_t ob = (size_t)t * B + b0;            // this move's output row base
-        if (tid < 2 * RB && (tid & (RB - 1)) < nb) {
-            const int b = tid & (RB - 1), k = tid / RB;
-            philox_pair(seed, bbase + (uint32_t)(b0 + b), step, k, ud[b][2 * k], ud[b][2 * k + 1]);
+        if (tid < 4) kcount[tid] = 0;                    // (last read in the previous move phase)
+        // draws 0-3 of every board's step stream, on wave 3 (its predicate part is the lightest)
+        if (w == 3 && l < nb) {
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+                philox_pair(seed, bbase + (uint32_t)(b0 + l), step, k, ud[l][2 * k], ud[l][2 * k + 1]);
         }
         // predicates: wave w computes part w of every board's predicate set (lane per board)
         if (ROLLOUT_ABLATE != 1 && l < nb) {
@@ -330,51 +333,60 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         }
         lds_sync();
         RT_MARK(5)
-        // move: wave w makes every move of kind w (one pipeline specialisation per wave, so no
-        // wave carries the stages of other kinds); chance draws 1-2; end check; outputs
-        if (ROLLOUT_ABLATE != 2 && l < kcount[w]) {
-            const int b = klist[w][l], a = act[b];
-            int8_t *s = lds + b * ST;
-            Chance ch{&ud[b][0], 0, 0, 0, 1, 0.0, false, tabs.view()};
-            int nxt;
-            switch (w) {
-                case MK_GEMS: nxt = make_move<N, MK_GEMS>(s, a, pl[b], false, ch); break;
-                case MK_BUY: nxt = make_move<N, MK_BUY>(s, a, pl[b], false, ch); break;
-                case MK_RESERVE: nxt = make_move<N, MK_RESERVE>(s, a, pl[b], false, ch); break;
-                default: nxt = make_move<N, MK_BUY_RESERVED>(s, a, pl[b], false, ch); break;
-            }
-            RT_MARK(6)
-            float e[N];
-            check_end<N>(s, e);
-            bool ended = false;
-#pragma unroll
-            for (int i = 0; i < N; i++) {
-                ended |= e[i] != 0.f;
-                ended_out[(ob + b) * N + i] = e[i];
-            }
-            RT_MARK(7)
-            action_out[ob + b] = (int16_t)a;
-            if (ended) {
-                nxt = 0;
-                gdone[b] += 1;
-            }
-            pl[b] = (int8_t)nxt;
-            rflag[b] = ended;
-        }
-        lds_sync();
-        RT_MARK(2)
-        if (tid < 4) kcount[tid] = 0;
-        uint64_t rm = __ballot(l < nb && rflag[l]);
-        for (int i = 0; rm; i++, rm &= rm - 1) {
-            if ((i & (WAVES - 1)) != w) continue;
-            const int rb = __ffsll((unsigned long long)rm) - 1;
-            wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)(b0 + rb), step, 3, DEAL_DRAWS);
-            wave_init_game<N>(lds + rb * ST, ub[w], tabs.view());
-        }
-        RT_MARK(8)
+        // move phase. The move's masks (final since select) go to HBM. Wave w makes every move
+        // of kind w (one pipeline specialisation per wave, so no wave carries the stages of
+        // other kinds): chance draws 1-2, end check, outputs. Then the wave re-deals the games
+        // its own moves finished (wave-collective; draws 3.. of the step stream) — mostly the
+        // gem-move wave, which has the shortest pipeline, so the deals fill its wait for the
+        // other kinds instead of taking a phase of their own.
+#if ROLLOUT_TIMING
+        const uint64_t mv0 = clock64();
+#endif
         if (mask_out && ROLLOUT_ABLATE != 1)
             for (int i = tid; i < nb * 7; i += THREADS) mask_out[ob * 7 + i] = (&msk[0][0])[i];
-        RT_MARK(9)
+        {
+            int b = 0;
+            bool ended = false;
+            if (ROLLOUT_ABLATE != 2 && l < kcount[w]) {
+                b = klist[w][l];
+                const int a = act[b];
+                int8_t *s = lds + b * ST;
+                Chance ch{&ud[b][0], 0, 0, 0, 1, 0.0, false, tabs.view()};
+                int nxt;
+                switch (w) {
+                    case MK_GEMS: nxt = make_move<N, MK_GEMS>(s, a, pl[b], false, ch); break;
+                    case MK_BUY: nxt = make_move<N, MK_BUY>(s, a, pl[b], false, ch); break;
+                    case MK_RESERVE: nxt = make_move<N, MK_RESERVE>(s, a, pl[b], false, ch); break;
+                    default: nxt = make_move<N, MK_BUY_RESERVED>(s, a, pl[b], false, ch); break;
+                }
+                RT_MARK(6)
+                float e[N];
+                check_end<N>(s, e);
+#pragma unroll
+                for (int i = 0; i < N; i++) {
+                    ended |= e[i] != 0.f;
+                    ended_out[(ob + b) * N + i] = e[i];
+                }
+                RT_MARK(7)
+                action_out[ob + b] = (int16_t)a;
+                if (ended) {
+                    nxt = 0;
+                    gdone[b] += 1;
+                }
+                pl[b] = (int8_t)nxt;
+            }
+            RT_MARK(2)
+            for (uint64_t rm = __ballot(ended); rm; rm &= rm - 1) {
+                const int rb = __shfl(b, __ffsll((unsigned long long)rm) - 1);
+                wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)(b0 + rb), step, 3, DEAL_DRAWS);
+                RT_MARK(9)
+                wave_init_game<N>(lds + rb * ST, ub[w], tabs.view());
+                RT_MARK(8)
+            }
+#if ROLLOUT_TIMING
+            if (l == 0) atomicAdd((unsigned long long *)&spl_probe_acc[20 + w], (unsigned long long)(clock64() - mv0));
+#endif
+        }
         lds_sync();
         RT_MARK(3)
     }

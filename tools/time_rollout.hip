@@ -21,10 +21,10 @@ int main() {
     std::vector<uint64_t> h((size_t)NB * 32);
     // probe slots (splendor_env.hip / splendor_device.h SPL_PROBE)
     // (thread 0 = lane 0 of wave 0: its move-phase slots see the gem-move pipeline)
-    const int slots[] = {0, 16, 17, 1, 5, 6, 7, 2, 8, 9, 3, 4};
-    const char *names[] = {"load", "philox+predicates (w0)", "predicate sync", "mask words+sync", "select",
-                           "make_move (wave 0)", "end check", "outputs+tail to sync", "reset", "mask store",
-                           "barrier", "store"};
+    const int slots[] = {0, 16, 17, 1, 5, 6, 7, 2, 9, 8, 3, 4};
+    const char *names[] = {"load", "predicates (w0)", "predicate sync", "mask words+sync", "select",
+                           "mask store+make_move (w0)", "end check (w0)", "outputs (w0)", "deal philox (w0)",
+                           "deal board (w0)", "tail to sync", "store"};
     const bool per_move[] = {false, true, true, true, true, true, true, true, true, true, true, false};
     const int NS = 12;
     for (int rep = 0; rep < 2; rep++) {
@@ -50,6 +50,13 @@ int main() {
         double xw = 0, xl = 0;
         for (int b = 0; b < NB; b++) { xw += (double)h[(size_t)b * 32 + 18]; xl += (double)h[(size_t)b * 32 + 19]; }
         printf("  exact-path waves per wave-move %.4f, lanes per board-move %.5f\n", xw / (NB * 4.0 * K), xl / (NB * 64.0 * K));
+        printf("  move phase per wave (gems / buy / reserve / buy reserved), cycles/move:");
+        for (int k = 0; k < 4; k++) {
+            double x = 0;
+            for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 32 + 20 + k];
+            printf(" %.0f", x / (NB * (double)K));
+        }
+        printf("\n");
     }
     return 0;
 }
