@@ -55,6 +55,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 // child come from its lane by shuffle.
 struct Pick {
     int e, a, child;
+    int2 cr;                                    // child's cached {eb, ec} (valid when child >= 0)
 };
 __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &C, int t, int eb, int ec,
                                                int ns, double qs, bool forced, int step) {
@@ -62,6 +63,7 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
     const size_t e0 = (size_t)t * P.ecap + eb;
     float p[2];
     int n[2], a[2], c[2];
+    int2 r[2];
     double q[2];
 #pragma unroll
     for (int j = 0; j < 2; j++) {
@@ -72,6 +74,7 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         q[j] = in ? P.eq[e0 + i] : Q_UNSET;
         a[j] = in ? (int)P.ea[e0 + i] : 0;
         c[j] = in ? P.echild[e0 + i] : -1;
+        r[j] = in ? P.ecr[e0 + i] : make_int2(0, 0);
     }
     int bi = -1;
     if (forced) {                               // MCTS.py:208-213: first under-visited edge
@@ -117,14 +120,16 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         bi = bj;
     }
     const int jb = bi >> 6;
-    int av = a[0], cv = c[0];
+    int av = a[0], cv = c[0], rx = r[0].x, ry = r[0].y;
 #pragma unroll
     for (int j = 1; j < 2; j++)
-        if (jb == j) { av = a[j]; cv = c[j]; }
+        if (jb == j) { av = a[j]; cv = c[j]; rx = r[j].x; ry = r[j].y; }
     av = __shfl(av, bi & 63, 64);
     cv = __shfl(cv, bi & 63, 64);
-    if (bi >= 128) { av = P.ea[e0 + bi]; cv = P.echild[e0 + bi]; }
-    return {bi, av, cv};
+    rx = __shfl(rx, bi & 63, 64);
+    ry = __shfl(ry, bi & 63, 64);
+    if (bi >= 128) { av = P.ea[e0 + bi]; cv = P.echild[e0 + bi]; const int2 rr = P.ecr[e0 + bi]; rx = rr.x; ry = rr.y; }
+    return {bi, av, cv, make_int2(rx, ry)};
 }
 
 // ------------------------------------------------------------ Dirichlet root noise
@@ -217,6 +222,26 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round) {
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
+    // new CSR base of every kept node (old index -> base), so moved edges can re-point
+    // their cached child record before the child itself has moved
+    int32_t *remap_eb = P.remap_eb + nb;
+    {
+        int run = 0;
+        for (int base = 0; base < nc; base += 64) {
+            const int i = base + l;
+            const int x = i < nc && remap[i] >= 0 ? P.nec[nb + i] : 0;
+            int incl = x;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                int y = __shfl_up(incl, o, 64);
+                if (l >= o) incl += y;
+            }
+            if (i < nc) remap_eb[i] = run + incl - x;
+            run += __shfl(incl, 63, 64);
+        }
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
     int edges = 0;
     for (int base = 0; base < nc; base += 64) {
         const int i = base + l;
@@ -261,15 +286,18 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round) {
                 const int q = base2 + l;
                 const bool in = q < jc;
                 int16_t a = 0; float p = 0; int32_t cnt = 0, ch = -1; double qq = 0;
+                int2 cr = make_int2(0, 0);
                 if (in) {
                     a = P.ea[e0 + jo + q]; p = P.ep[e0 + jo + q]; cnt = P.en[e0 + jo + q];
-                    qq = P.eq[e0 + jo + q]; ch = P.echild[e0 + jo + q];
+                    qq = P.eq[e0 + jo + q]; ch = P.echild[e0 + jo + q]; cr = P.ecr[e0 + jo + q];
                 }
+                const int nch = ch >= 0 ? remap[ch] : -1;
+                if (nch >= 0) cr.x = remap_eb[ch];
                 __threadfence_block();
                 __builtin_amdgcn_wave_barrier();
                 if (in) {
                     P.ea[e0 + jd + q] = a; P.ep[e0 + jd + q] = p; P.en[e0 + jd + q] = cnt;
-                    P.eq[e0 + jd + q] = qq; P.echild[e0 + jd + q] = ch >= 0 ? remap[ch] : -1;
+                    P.eq[e0 + jd + q] = qq; P.echild[e0 + jd + q] = nch; P.ecr[e0 + jd + q] = cr;
                 }
                 __threadfence_block();
                 __builtin_amdgcn_wave_barrier();
@@ -556,13 +584,13 @@ __global__ void k_drain_reset(Pools P, int max, int32_t *n_out) {
 
 // ------------------------------------------------------------ select
 template <int N>
-__global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B, int lim,
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) void k_select(Pools P, SearchCfg C, int B, int lim,
                                                     int8_t *__restrict__ leaf_state,
                                                     uint64_t *__restrict__ leaf_mask,
                                                     uint8_t *__restrict__ leaf_valid) {
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
-    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    const int w = uniform(threadIdx.x >> 6), t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
@@ -592,24 +620,27 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
         if (sims == 0 && H->noise_pending)
             apply_root_noise(P, C, t, P.neb[nb + node], P.nec[nb + node], ST_DIR | (uint32_t)H->move_no);
         const bool forced = H->forced;
+        // CSR range of the current node: the root's from its record, every child's from the
+        // {eb, ec} cached on the edge that led to it, so a level costs ONE round trip (the
+        // node's visit stats travel with its edges); ec < 0 marks a terminal child
+        int eb = P.neb[nb + node], ec = P.nec[nb + node];
         for (;;) {
-            // node record: CSR range, visit stats and (below the root) the terminal flag, in
-            // one round trip; a terminal child found on the previous level ends the descent
             SPL_PROBE(1)
-            const int eb = P.neb[nb + node], ec = P.nec[nb + node], ns = P.nns[nb + node];
-            const double qs = P.nqs[nb + node];
-            if (depth > 0 && P.nterm[nb + node]) {
+            if (depth > 0 && ec < 0) {
                 kind = LEAF_TERMINAL;
 #pragma unroll
                 for (int i = 0; i < 4; i++) val[i] = P.nes[(nb + node) * 4 + i];
                 break;
             }
             if (depth >= P.pcap) { kind = LEAF_NONE; if (l == 0) H->overflow = 2; break; }
+            const int ns = P.nns[nb + node];
+            const double qs = P.nqs[nb + node];
             const Pick pk = pick_edge_desc(P, C, t, eb, ec, ns, qs, forced && depth == 0, sims);
             const int ge = eb + pk.e;
             if (l == 0) { path[2 * depth] = node; path[2 * depth + 1] = ge; }
             depth++;
-            int child = pk.child;
+            int child = uniform(pk.child);
+            int2 cr = make_int2(uniform(pk.cr.x), uniform(pk.cr.y));
             SPL_PROBE(2)
             Chance ch{nullptr, 0, 0, 0, 0};
             const int nxt = make_move<N>(s, pk.a, 0, true, ch);   // MCTS.py:227-235
@@ -618,8 +649,12 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
             SPL_PROBE(3)
             if (child < 0) {
                 wave_fingerprint<N>(s, k0, k1);
-                child = hash_lookup(P, t, k0, k1);
-                if (child >= 0 && l == 0) P.echild[e0 + ge] = child;
+                k0 = uniform64(k0); k1 = uniform64(k1);
+                child = uniform(hash_lookup(P, t, k0, k1));
+                if (child >= 0) {                            // transposition: link + cache
+                    cr = make_int2(P.neb[nb + child], P.nterm[nb + child] ? -1 : P.nec[nb + child]);
+                    if (l == 0) { P.echild[e0 + ge] = child; P.ecr[e0 + ge] = cr; }
+                }
             }
             SPL_PROBE(4)
 #if MCTS_TIMING
@@ -627,6 +662,8 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
 #endif
             if (child >= 0) {
                 node = child;
+                eb = cr.x;
+                ec = cr.y;
                 continue;
             }
             float es[N];
@@ -646,6 +683,7 @@ __global__ __launch_bounds__(THREADS) void k_select(Pools P, SearchCfg C, int B,
                     for (int i = 0; i < 4; i++) P.nes[(nb + id) * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
                     hash_insert(P, t, k0, id);
                     P.echild[e0 + ge] = id;
+                    P.ecr[e0 + ge] = make_int2(0, -1);
                     H->node_count = id + 1;
                 }
                 kind = LEAF_TERMINAL;
@@ -763,7 +801,10 @@ __global__ __launch_bounds__(THREADS) void k_backup(Pools P, SearchCfg C, int B,
             P.nqs[nb + id] = (double)val[0]; P.nround[nb + id] = H->leaf_round; P.nterm[nb + id] = 0;
             hash_insert(P, t, H->leaf_k0, id);
             if (depth == 0) H->root = id;
-            else P.echild[e0 + path[2 * (depth - 1) + 1]] = id;
+            else {
+                P.echild[e0 + path[2 * (depth - 1) + 1]] = id;
+                P.ecr[e0 + path[2 * (depth - 1) + 1]] = make_int2(eb, ec);
+            }
             H->node_count = id + 1;
             H->edge_count = eb + ec;
         }
@@ -938,8 +979,8 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
     acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn); acc(4 * nn);
     acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(2 * ne); acc(4 * ne); acc(4 * ne);
-    acc(4 * ne); acc(8 * ne); acc(4 * (size_t)B * P.hcap); acc(8 * (size_t)B * P.pcap);
-    acc(4 * nn); acc((size_t)B * m->S);
+    acc(4 * ne); acc(8 * ne); acc(8 * ne); acc(4 * (size_t)B * P.hcap); acc(8 * (size_t)B * P.pcap);
+    acc(4 * nn); acc(4 * nn); acc((size_t)B * m->S);
     const int excap = cfg->selfplay ? 62 * ctx->n + 2 : 0;
     const size_t nx = (size_t)B * excap, no = cfg->selfplay ? (size_t)(cfg->out_cap > 0 ? cfg->out_cap : 4 * B) : 0;
     acc((size_t)B * m->S); acc(nx * m->S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
@@ -956,10 +997,10 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.nround = carve<int32_t>(p, nn); P.nqs = carve<double>(p, nn); P.nterm = carve<int8_t>(p, nn);
     P.nes = carve<float>(p, 4 * nn);
     P.ea = carve<int16_t>(p, ne); P.ep = carve<float>(p, ne); P.en = carve<int32_t>(p, ne);
-    P.echild = carve<int32_t>(p, ne); P.eq = carve<double>(p, ne);
+    P.echild = carve<int32_t>(p, ne); P.eq = carve<double>(p, ne); P.ecr = carve<int2>(p, ne);
     P.hslot = carve<int32_t>(p, (size_t)B * P.hcap);
     P.path = carve<int32_t>(p, 2 * (size_t)B * P.pcap);
-    P.remap = carve<int32_t>(p, nn);
+    P.remap = carve<int32_t>(p, nn); P.remap_eb = carve<int32_t>(p, nn);
     P.root_state = carve<int8_t>(p, (size_t)B * m->S);
     P.excap = excap; P.out_cap = (int)no;
     P.board = carve<int8_t>(p, (size_t)B * m->S);
@@ -987,7 +1028,7 @@ int spl_mcts_destroy(spl_mcts *m) {
 long long spl_mcts_device_bytes(const spl_mcts *m) {
     if (!m) return SPL_EINVAL;
     const size_t nn = (size_t)m->B * m->P.ncap, ne = (size_t)m->B * m->P.ecap;
-    return (long long)(nn * 53 + ne * 22 + (size_t)m->B * (4 * m->P.hcap + 8 * m->P.pcap + m->S + sizeof(TreeHdr)));
+    return (long long)(nn * 57 + ne * 30 + (size_t)m->B * (4 * m->P.hcap + 8 * m->P.pcap + m->S + sizeof(TreeHdr)));
 }
 
 int spl_mcts_set_roots(spl_mcts *m, const int8_t *roots, int keep_tree, int force_full, void *hs) {

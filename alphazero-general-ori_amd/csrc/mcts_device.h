@@ -40,10 +40,11 @@ struct Pools {
     int16_t *ea;
     float *ep;
     int32_t *en, *echild;
+    int2 *ecr;                           // cached child record {eb, ec} (ec = -1: terminal child)
     double *eq;
     int32_t *hslot;
     int32_t *path;                       // pcap x 2 (node, edge)
-    int32_t *remap;                      // ncap scratch for compaction
+    int32_t *remap, *remap_eb;           // ncap scratch for compaction (new index, new CSR base)
     int8_t *root_state;                  // B x S (canonical root)
     // self-play (Coach.executeEpisode) state
     int excap, out_cap;                  // staged examples per tree, finished-example queue

@@ -44,6 +44,12 @@ struct Lay {  // row offsets of the (R,7) state (SplendorLogicNumba.py:296-303)
 };
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+// wave-uniform value moved to an SGPR (lets dependent loads use the scalar cache)
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32);
+}
 
 // workgroup barrier ordering LDS traffic only: waits for this wave's LDS (and scalar)
 // operations, not its global ones. __syncthreads() first waits vmcnt(0), i.e. for every

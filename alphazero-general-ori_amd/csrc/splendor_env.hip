@@ -188,7 +188,10 @@ __global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__re
 //            reserve / buy reserved), lane per board: chance, end check, per-move outputs;
 //            then it re-deals the games its moves finished (wave-collective, draws 3..)
 //   store    boards, players, game counters LDS -> HBM
-constexpr int RB = 64;
+#ifndef ROLLOUT_RB
+#define ROLLOUT_RB 64
+#endif
+constexpr int RB = ROLLOUT_RB;   // boards per workgroup (<= 64: lane per board)
 #define RT_MARK(k) SPL_PROBE(k)
 template <int N>
 struct RolloutLds {

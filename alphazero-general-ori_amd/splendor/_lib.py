@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "libsplendor_amd.so")
+LIB_PATH = os.environ.get("SPLENDOR_AMD_LIB") or os.path.join(PKG_ROOT, "libsplendor_amd.so")
 
 ABI_VERSION = 1
 EINVAL, EDEVICE = -1, -2

@@ -7,12 +7,14 @@
 #include "../alphazero-general-ori_amd/csrc/mcts.hip"
 #include <cstdio>
 #include <vector>
-int main() {
+#include <cstdlib>
+int main(int argc, char **argv) {
     const int B = 32768, SIMS = 100, MOVES = 3;
+    const int emul = argc > 1 ? atoi(argv[1]) : 32;   // edge_cap = emul x node_cap
     spl_ctx *c; spl_ctx_create(2, 10, &c);
     spl_mcts_config cfg{};
     cfg.num_sims = SIMS; cfg.ratio_full = 1; cfg.prob_full = 1.0; cfg.cpuct = 2.5; cfg.fpu = 0.3;
-    cfg.node_cap = 4 * SIMS + 64; cfg.edge_cap = 32 * cfg.node_cap; cfg.seed = 0x5EED; cfg.temp_threshold = 10;
+    cfg.node_cap = 4 * SIMS + 64; cfg.edge_cap = emul * cfg.node_cap; cfg.seed = 0x5EED; cfg.temp_threshold = 10;
     cfg.dirichlet_temp = 1.0;
     spl_mcts *m; if (spl_mcts_create(c, B, &cfg, &m)) { printf("create failed\n"); return 1; }
     int8_t *st, *leaf; uint64_t *mk; uint8_t *lv; float *pi, *v;
@@ -40,6 +42,7 @@ int main() {
     const char *names[] = {"root load", "descend: loop top", "pick_edge + edge loads", "make_move + roll",
                            "fingerprint + hash", "node checks (to next level)", "leaf: store + mask", "headers"};
     const double calls = (double)h[21];
+    printf("edge_cap %d, arena %.2f GB\n", cfg.edge_cap, spl_mcts_device_bytes(m) / 1e9);
     printf("%d sims x %d trees: %.1f us per select+hash_eval+backup iteration; %.0f probed waves, %.2f levels/sim\n",
            SIMS, B, ms * 1e3 / SIMS, calls, h[20] / calls);
     for (int k = 0; k < 8; k++) printf("  %-28s %8.0f cycles per select\n", names[k], h[k] / calls);
