@@ -364,14 +364,24 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
     __builtin_amdgcn_wave_barrier();
 }
 
+// active (optional): trees with active[t] == 0 are left as they are, with no search budget
+// (their select/backup are no-ops) — the other player's turn in an Arena game
 template <int N>
 __global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int B,
-                                                       const int8_t *__restrict__ roots, int keep,
+                                                       const int8_t *__restrict__ roots,
+                                                       const uint8_t *__restrict__ active, int keep,
                                                        int force_full) {
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
+    if (active && !active[t]) {
+        if (lane_id() == 0) {
+            TreeHdr *H = P.hdr + t;
+            H->budget = 0; H->sims_done = 0; H->leaf_kind = LEAF_NONE;
+        }
+        return;
+    }
     int8_t *s = lds[w];
     wave_load_board<N>(s, roots + (size_t)t * Lx::S);
     begin_search<N>(P, C, t, s, keep != 0, force_full != 0);
@@ -837,6 +847,65 @@ __global__ __launch_bounds__(THREADS) void k_backup(Pools P, SearchCfg C, int B,
     }
 }
 
+// ------------------------------------------------------------ arena move
+// MCTS.getActionProb(temp=0) (MCTS.py:87-92) followed by Arena's np.argmax of the one-hot:
+// the best root count (after policy-target pruning when forced playouts were on, :68-74),
+// ties broken uniformly (np.random.choice over bestAs) by the Philox draw
+// (seed, board_base + t, ST_BEST | stream, 0) — keyed by the caller's game id and ply, so
+// the choice does not depend on how games are batched onto trees.
+// With every count 0 the reference ties all 409 actions, and so does this.
+__global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int B,
+                                                       const uint8_t *__restrict__ active,
+                                                       uint32_t board_base, uint32_t stream,
+                                                       int16_t *__restrict__ action) {
+    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    if (t >= B || (active && !active[t])) return;
+    const int l = lane_id();
+    TreeHdr *H = P.hdr + t;
+    const int root = H->root;
+    const double u = philox_u01(C.seed, board_base + (uint32_t)t, ST_BEST | (stream & 0xFFFFFFu), 0);
+    if (root < 0) {                                      // no search ran: all counts 0
+        if (l == 0) action[t] = (int16_t)(int)(u * (double)SPL_ACTIONS);
+        return;
+    }
+    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
+    const int eb = P.neb[nb + root], ec = P.nec[nb + root];
+    const int sims = H->budget;
+    const bool forced = H->forced;
+    int best = 0;
+    for (int i = l; i < ec; i += 64) best = max(best, P.en[e0 + eb + i]);
+    for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
+    long long top = 0;
+    for (int i = l; i < ec; i += 64)
+        top = max(top, pruned_count(P.en[e0 + eb + i], best, forced, P.ep[e0 + eb + i], sims));
+    for (int o = 32; o > 0; o >>= 1) top = max(top, (long long)__shfl_xor(top, o, 64));
+    if (top == 0) {
+        if (l == 0) action[t] = (int16_t)(int)(u * (double)SPL_ACTIONS);
+        return;
+    }
+    int nbest = 0;
+    for (int base = 0; base < ec; base += 64) {
+        const int i = base + l;
+        const bool hit = i < ec && pruned_count(P.en[e0 + eb + i], best, forced, P.ep[e0 + eb + i], sims) == top;
+        nbest += __popcll(__ballot(hit));
+    }
+    int k = (int)(u * (double)nbest);                    // k-th best in action order
+    for (int base = 0; base < ec; base += 64) {
+        const int i = base + l;
+        const bool hit = i < ec && pruned_count(P.en[e0 + eb + i], best, forced, P.ep[e0 + eb + i], sims) == top;
+        const uint64_t b = __ballot(hit);
+        const int c = __popcll(b);
+        if (k < c) {
+            uint64_t x = b;
+            for (int j = 0; j < k; j++) x &= x - 1;
+            const int pos = __ffsll((unsigned long long)x) - 1;
+            if (l == 0) action[t] = P.ea[e0 + eb + base + pos];
+            return;
+        }
+        k -= c;
+    }
+}
+
 // ------------------------------------------------------------ results
 // getActionProb tail (MCTS.py:61-97) for temp = 1: root visit counts (with policy-target
 // pruning when forced playouts were on), probs, q.
@@ -1032,10 +1101,23 @@ long long spl_mcts_device_bytes(const spl_mcts *m) {
 }
 
 int spl_mcts_set_roots(spl_mcts *m, const int8_t *roots, int keep_tree, int force_full, void *hs) {
+    return spl_mcts_set_roots_active(m, roots, nullptr, keep_tree, force_full, hs);
+}
+
+int spl_mcts_set_roots_active(spl_mcts *m, const int8_t *roots, const uint8_t *active, int keep_tree,
+                              int force_full, void *hs) {
     if (!m || !roots) return SPL_EINVAL;
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_set_roots<N>, wave_grid(m->B), dim3(THREADS), 0,
-                                          (hipStream_t)hs, m->P, m->cfg, m->B, roots, keep_tree,
+                                          (hipStream_t)hs, m->P, m->cfg, m->B, roots, active, keep_tree,
                                           force_full));
+    return check_launch();
+}
+
+int spl_mcts_pick_best(spl_mcts *m, const uint8_t *active, uint32_t board_base, uint32_t stream,
+                       int16_t *action, void *hs) {
+    if (!m || !action || stream > 0xFFFFFFu) return SPL_EINVAL;
+    hipLaunchKernelGGL(k_pick_best, wave_grid(m->B), dim3(THREADS), 0, (hipStream_t)hs, m->P, m->cfg,
+                       m->B, active, board_base, stream, action);
     return check_launch();
 }
 

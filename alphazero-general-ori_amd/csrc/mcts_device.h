@@ -70,7 +70,7 @@ struct SearchCfg {
 
 // RNG streams for the search / self-play decisions (Philox counter word 2)
 enum : uint32_t { ST_FULL = 1u << 24, ST_DIR = 2u << 24, ST_PICK = 3u << 24, ST_MOVE = 4u << 24,
-                  ST_DEAL = 5u << 24 };
+                  ST_DEAL = 5u << 24, ST_BEST = 6u << 24 };
 
 // --------------------------------------------------------------- wave reductions
 __device__ __forceinline__ uint64_t wave_xor64(uint64_t x) {

@@ -10,7 +10,7 @@ import os
 import numpy as np
 import torch
 
-from .nnet import SplendorNNet
+from .nnet import SplendorNNet, remap_policy_head
 
 
 class NNetWrapper:
@@ -43,6 +43,6 @@ class NNetWrapper:
         except Exception as e:  # refused by the safe loader: never fall back to unpickling
             raise RuntimeError(f"{path}: not loadable with torch.load(weights_only=True) ({type(e).__name__})") from e
         sd = data["state_dict"] if isinstance(data, dict) and "state_dict" in data else data
-        self.nnet.load_state_dict(sd)
+        self.nnet.load_state_dict(remap_policy_head(sd))   # 406-action checkpoints -> 409
         self.nnet.eval()
         return data

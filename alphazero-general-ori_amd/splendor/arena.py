@@ -1,0 +1,147 @@
+"""Batched Arena gate: Arena.playGames (Arena.py:175-227) for many games at once on the
+device MCTS, as Coach.learn uses it to accept or reject a new network (Coach.py:150-159).
+
+Reference semantics kept:
+* two players, each an MCTS over its own network with a search tree that persists through
+  a game and is reset between games (Arena.py:163, MCTS.reset_all_search_trees);
+* a move is np.argmax(mcts.getActionProb(canonical, temp=0, force_full_search=True)[0])
+  (Coach.py:152-153): the best root visit count, ties broken uniformly
+  (MCTS.py:87-92; here the Philox draw (seed, game id, ply), spl_mcts_pick_best);
+* game i is played "1 vs 2" (player 1 moves first) when i % 4 in (0, 3), else "2 vs 1"
+  (Arena.py:200-203); getNextState with chance (deterministic=False), the result is
+  getGameEnded(board)[0], player 0's entry (Arena.py:163-165);
+* oneWon / twoWon / draws are counted as at Arena.py:204-214.
+
+Batched form: game slots play in lockstep (every game's mover is ply % n). Each player owns
+one BatchedMCTS with one tree per game slot; at each ply only the trees of the games where
+that player is to move search (spl_mcts_set_roots_active), the others stay untouched.
+Finished games idle (their boards take the no-op pass move, never read again). Chance is
+Philox keyed (seed, global game id, ply); deals (seed, game id, 0xFFFFFFFF).
+For n > 2 players the reference's player list is [p1, p2] only (Arena.py:86-90, an
+IndexError at n = 3 without player3); here seat 0 plays one side and every other seat
+the other ([p1] + [p2] * (n-1) and its mirror, the form commented in Arena.py:77-84).
+"""
+import numpy as np
+import torch
+
+from .env import ACTIONS, unpack_mask
+from .mcts import BatchedMCTS
+from .search import evaluator_for
+
+PASS = 408
+DEAL_STREAM = 0xFFFFFFFF
+
+
+def _arg(args, k, default=None):
+    if isinstance(args, dict):
+        return args.get(k, default)
+    return getattr(args, k, default)
+
+
+def one_vs_two(i):
+    """Arena.py:200-203: 1 2 2 1  1 2 2 1 ..."""
+    return (i % 4 == 0) or (i % 4 == 3)
+
+
+class Arena:
+    def __init__(self, game, nnet1, nnet2, args, batch=None, seed=0x5EED, game_base=0,
+                 evaluators=None, check_valid=True):
+        self.game, self.args = game, args
+        self.e = game.engine
+        self.n = self.e.n
+        self.B = int(batch or _arg(args, "arenaCompare", 1))
+        self.seed, self.game_base = int(seed), int(game_base)
+        self.check_valid = check_valid
+        if evaluators is None:
+            evaluators = (evaluator_for(self.e, nnet1, self.B), evaluator_for(self.e, nnet2, self.B))
+        margs = dict(numMCTSSims=int(_arg(args, "numMCTSSims", 100)), cpuct=float(_arg(args, "cpuct", 1.0)),
+                     fpu=float(_arg(args, "fpu", 0.0)), prob_fullMCTS=1.0,
+                     ratio_fullMCTS=int(_arg(args, "ratio_fullMCTS", 5) or 1),
+                     forced_playouts=bool(_arg(args, "forced_playouts", False)), dirichletAlpha=0.0,
+                     temperature=list(_arg(args, "temperature", [1.25, 0.8])),
+                     tempThreshold=int(_arg(args, "tempThreshold", 10)))
+        self.mcts = [BatchedMCTS(self.e, self.B, margs, evaluators[k], dirichlet_noise=False,
+                                 seed=self.mcts_seed(k), board_base=self.game_base) for k in range(2)]
+        self.last = None
+
+    def mcts_seed(self, k):
+        return self.seed ^ (k + 1)
+
+    def seats(self, first):
+        """seat -> player (0 = player1, 1 = player2) for the games in `first` order."""
+        n = self.n
+        s = np.where(np.asarray(first)[:, None], np.array([0] + [1] * (n - 1))[None, :],
+                     np.array([1] + [0] * (n - 1))[None, :])
+        return s
+
+    # ---------------------------------------------------------------- one batch
+    def _play_batch(self, g0, G):
+        e, B, n, dev = self.e, self.B, self.n, self.e.device
+        gid = np.arange(g0, g0 + B)
+        alive = torch.from_numpy(np.arange(B) < G).to(dev)
+        first = np.array([one_vs_two(int(i)) for i in gid])
+        seat_player = torch.from_numpy(self.seats(first)).to(dev)            # [B, n]
+        base = self.game_base + g0
+        boards = e.new_state(B)
+        e.init(boards, None, seed=self.seed, stream=DEAL_STREAM, board_base=base)
+        for m in self.mcts:                                                   # fresh trees
+            m.set_roots(boards, keep_tree=False, force_full=True)
+        done = torch.zeros(B, dtype=torch.bool, device=dev)
+        result = torch.zeros((B, n), dtype=torch.float32, device=dev)
+        plies = torch.zeros(B, dtype=torch.int32, device=dev)
+        action = torch.full((B,), PASS, dtype=torch.int16, device=dev)
+        max_plies = 62 * n * 2 + 8                                             # round cap (:322)
+        for ply in range(max_plies):
+            cur = ply % n
+            player = torch.full((B,), cur, dtype=torch.int8, device=dev)
+            canon = e.canonical(boards, player)
+            live = alive & ~done
+            action.fill_(PASS)
+            for k in range(2):
+                act = live & (seat_player[:, cur] == k)
+                if not bool(act.any()):
+                    continue
+                a8 = act.to(torch.uint8)
+                m = self.mcts[k]
+                m.set_roots_active(canon, a8, keep_tree=True, force_full=True)
+                m.search()
+                m.pick_best(a8, board_base=base, stream=ply, out=action)
+            if self.check_valid:                                               # Arena.py:158-159
+                valid = unpack_mask(e.valid_moves(canon))
+                ok = valid.gather(1, action.long().clamp(0, ACTIONS - 1).unsqueeze(1)).squeeze(1)
+                bad = live & ~ok
+                if bool(bad.any()):
+                    raise AssertionError(f"invalid arena action in games {gid[bad.cpu().numpy()].tolist()}")
+            action = torch.where(live, action, torch.full_like(action, PASS))
+            e.step(boards, action, player=player, deterministic=False, seed=self.seed, stream=ply,
+                   board_base=base)
+            ended = e.game_ended(boards)
+            newly = live & (ended != 0).any(1)
+            result[newly] = ended[newly]
+            plies[newly] = ply + 1
+            done |= newly
+            if not bool((alive & ~done).any()):
+                break
+        return {"game": gid[:G], "one_vs_two": first[:G], "result": result[:G].cpu().numpy(),
+                "plies": plies[:G].cpu().numpy(), "score": e.score(boards)[:G].cpu().numpy()}
+
+    # ---------------------------------------------------------------- reference API
+    def playGames(self, num, verbose=False):
+        """Arena.playGames: (oneWon, twoWon, draws) over `num` games; per-game records in
+        self.last (game id, one_vs_two, result vector, plies, final scores)."""
+        recs = []
+        for g0 in range(0, num, self.B):
+            recs.append(self._play_batch(g0, min(self.B, num - g0)))
+        last = {k: np.concatenate([r[k] for r in recs]) for k in recs[0]}
+        r0 = last["result"][:, 0]
+        ovt = last["one_vs_two"]
+        one = int(np.sum(np.where(ovt, r0 == 1.0, r0 == -1.0)))
+        two = int(np.sum(np.where(ovt, r0 == -1.0, r0 == 1.0)))
+        self.last = last
+        return one, two, int(len(r0) - one - two)
+
+
+def accept_new_network(nwins, pwins, update_threshold):
+    """Coach.learn gate (Coach.py:157-164): accept iff pwins + nwins > 0 and
+    nwins / (pwins + nwins) >= updateThreshold."""
+    return not (pwins + nwins == 0 or float(nwins) / (pwins + nwins) < update_threshold)

@@ -4,13 +4,16 @@
 trees concurrently (splendor.selfplay.SelfPlay) until k games have finished, expands every
 recorded position with getSymmetries (Coach.py:77-80, device kernel spl_symmetries) and
 returns the reference's example records (board, pi, winner, scdiff, valids, surprise)
-(Coach.py:91-98). `executeEpisode()` is the one-game form. Training (`learn`) is out of
-scope.
+(Coach.py:91-98). `executeEpisode()` is the one-game form. `executeIteration(k)` returns
+the same examples as a columnar `ExampleSet` and appends it to `trainExamplesHistory`
+(an `ExampleHistory`, saved as .npz by `saveTrainExamples`, Coach.py:167-190). Training
+(`learn`) is out of scope.
 """
 import numpy as np
 import torch
 
 from .env import unpack_mask
+from .examples import ExampleHistory, ExampleSet
 from .search import evaluator_for
 from .selfplay import SelfPlay, gather_examples
 
@@ -44,6 +47,7 @@ class Coach:
                            dirichlet_noise=float(_arg(args, "dirichletAlpha", 0.0)) > 0, seed=seed,
                            board_base=board_base)
         self.sp.reset()
+        self.trainExamplesHistory = ExampleHistory(_arg(args, "numItersHistory"))
 
     def run_iterations(self, k, use_graph=False):
         for _ in range(k):
@@ -72,3 +76,21 @@ class Coach:
 
     def executeEpisode(self):
         return self.executeEpisodes(1)
+
+    def executeIteration(self, num_games, with_symmetries=True, gather=False):
+        """Self-play examples of one iteration (Coach.learn's executeEpisode loop,
+        Coach.py:123-132) as an ExampleSet, appended to trainExamplesHistory."""
+        ex = self.executeEpisodes(num_games, with_symmetries=with_symmetries, as_tuples=False,
+                                  gather=gather)
+        exset = ExampleSet.from_drain(ex)
+        self.trainExamplesHistory.append(exset)
+        return exset
+
+    def saveTrainExamples(self, folder=None):
+        """Coach.saveTrainExamples (:167-173) without pickle: checkpoint.examples.npz."""
+        return self.trainExamplesHistory.save(folder or _arg(self.args, "checkpoint", "checkpoint"))
+
+    def loadTrainExamples(self, folder):
+        """Coach.loadTrainExamples (:175-190): read checkpoint.examples.npz."""
+        self.trainExamplesHistory = ExampleHistory.load(folder, _arg(self.args, "numItersHistory"),
+                                                        device=self.game.engine.device)

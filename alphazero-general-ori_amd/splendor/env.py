@@ -32,6 +32,17 @@ def _stream(device):
 _BIT = None
 
 
+def pack_mask(valid):
+    """bool [...,409] -> [...,7] int64 packed words (bit i of word k = action 64k+i), the
+    engine's mask layout; inverse of unpack_mask."""
+    global _BIT
+    if _BIT is None or _BIT.device != valid.device:
+        _BIT = torch.arange(64, device=valid.device, dtype=torch.int64)
+    pad = torch.zeros((*valid.shape[:-1], MASK_WORDS * 64), dtype=torch.int64, device=valid.device)
+    pad[..., :ACTIONS] = valid.to(torch.int64)
+    return (pad.view(*valid.shape[:-1], MASK_WORDS, 64) << _BIT).sum(-1)
+
+
 def unpack_mask(mask):
     """[...,7] packed words -> bool [...,409] (on the same device)."""
     global _BIT

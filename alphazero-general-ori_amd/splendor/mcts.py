@@ -110,6 +110,26 @@ class BatchedMCTS:
         _lib.check(self.L.spl_mcts_set_roots(self.h, _ptr(roots), int(keep_tree), int(force_full),
                                              self.e._s()), "spl_mcts_set_roots")
 
+    def set_roots_active(self, roots, active, keep_tree=True, force_full=True):
+        """set_roots for the trees with active[t] != 0 (uint8 [B], device); the others keep
+        their tree and run no simulations until re-rooted."""
+        _lib.check(self.L.spl_mcts_set_roots_active(self.h, _ptr(roots), _ptr(active), int(keep_tree),
+                                                    int(force_full), self.e._s()),
+                   "spl_mcts_set_roots_active")
+
+    def pick_best(self, active=None, board_base=0, stream=0, out=None):
+        """getActionProb(temp=0) + argmax (MCTS.py:87-92) for the active trees -> int16 [B]
+        (entries of inactive trees untouched); ties by Philox (seed, board_base + t, stream)."""
+        out = out if out is not None else torch.full((self.B,), -1, dtype=torch.int16, device=self.e.device)
+        _lib.check(self.L.spl_mcts_pick_best(self.h, _ptr(active), int(board_base), int(stream), _ptr(out),
+                                             self.e._s()), "spl_mcts_pick_best")
+        return out
+
+    def search(self):
+        """Run simulations until every tree has spent its budget."""
+        for _ in range(int(self.headers()["budget"].max())):
+            self.simulate()
+
     def simulate(self):
         """One simulation on every tree with budget left: select -> evaluate -> backup."""
         s = self.e._s()

@@ -88,6 +88,34 @@ class SplendorNNet(nn.Module):
         return F.log_softmax(pi, 1), torch.tanh(v), F.log_softmax(sd, 1)
 
 
+LEGACY_ACTIONS = 406
+
+
+def remap_policy_head(state_dict):
+    """SplendorNNet state_dict with a 406-action policy head -> the 409-action layout.
+
+    The shipped checkpoint predates the select-noble actions (SplendorNNet.py:106-109 sizes
+    the head by game.getActionSize(); genbu.pt's head has 406 rows): actions 0-404 are the
+    same moves, row 405 was pass. In the 409 layout pass is 408 and rows 405-407
+    (select-noble, never legal: DESIGN.md §2) get zero weights. The reference's own
+    non-strict loader cannot do this (it copies target -> source for equal shapes and
+    truncates otherwise, GenericNNetWrapper.py:215-232). Returns a new dict; 409-row heads
+    pass through unchanged."""
+    kw, kb = "output_layers_PI.1.weight", "output_layers_PI.1.bias"
+    w, b = state_dict[kw], state_dict[kb]
+    if w.shape[0] == ACTIONS:
+        return dict(state_dict)
+    if w.shape[0] != LEGACY_ACTIONS or b.shape[0] != LEGACY_ACTIONS:
+        raise ValueError(f"policy head has {w.shape[0]} rows; expected {ACTIONS} or {LEGACY_ACTIONS}")
+    nw = w.new_zeros((ACTIONS, w.shape[1]))
+    nb = b.new_zeros(ACTIONS)
+    nw[:405], nb[:405] = w[:405], b[:405]
+    nw[408], nb[408] = w[405], b[405]
+    out = dict(state_dict)
+    out[kw], out[kb] = nw, nb
+    return out
+
+
 def _bn_affine(bn):
     s = bn.weight / torch.sqrt(bn.running_var + bn.eps)
     return s, bn.bias - bn.running_mean * s

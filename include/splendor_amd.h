@@ -161,6 +161,18 @@ long long spl_mcts_device_bytes(const spl_mcts *m);
  * transposition table and keep its subtree (exact GC of unreachable nodes). */
 int spl_mcts_set_roots(spl_mcts *m, const int8_t *roots, int keep_tree, int force_full,
                        void *hip_stream);
+/* same, for the trees with active[t] != 0 only (active: B u8, device; NULL = all). Inactive
+ * trees keep their tree untouched and get no search budget: Arena's per-player MCTS
+ * objects (Arena.py:94-160) search only on their own turns. */
+int spl_mcts_set_roots_active(spl_mcts *m, const int8_t *roots, const uint8_t *active, int keep_tree,
+                              int force_full, void *hip_stream);
+/* Arena move choice (the Arena players of Coach.py:152-153: np.argmax(getActionProb(x, temp=0)[0]),
+ * MCTS.py:87-92): per active tree, the action with the largest (pruned) root count, ties
+ * broken uniformly by Philox (cfg.seed, board_base + t, ST_BEST | stream, draw 0) with
+ * ST_BEST = 6 << 24 and stream < 2^24 (the caller's game id base and ply), written to
+ * action[t] (B i16, device). */
+int spl_mcts_pick_best(spl_mcts *m, const uint8_t *active, uint32_t board_base, uint32_t stream,
+                       int16_t *action, void *hip_stream);
 /* leaf_state: B x S int8, leaf_mask: B x 7 u64, leaf_valid: B u8 (1 = needs the network) */
 int spl_mcts_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
                     void *hip_stream);

@@ -82,3 +82,39 @@ def test_selfplay_with_noise_and_network_sane():
         valid = unpack_mask(ex["valids"])
         assert bool((pi[~valid] == 0).all())
         assert set(np.unique(ex["winner"].cpu().numpy()).tolist()) <= {-1.0, 1.0, np.float32(0.01)}
+
+
+def test_iteration_examples_roundtrip(tmp_path):
+    """Coach.executeIteration -> ExampleSet (columnar, symmetries expanded on device) ->
+    checkpoint.examples.npz -> identical tuples to the reference-format executeEpisodes."""
+    from splendor.SplendorGame import SplendorGame
+    from splendor.coach import Coach
+    from splendor.mcts import HashEvaluator
+    args = dict(numMCTSSims=8, cpuct=1.5, fpu=0.1, prob_fullMCTS=1.0, ratio_fullMCTS=4,
+                forced_playouts=False, dirichletAlpha=0.0, temperature=[1.25, 0.8], tempThreshold=10,
+                numItersHistory=3, checkpoint=str(tmp_path))
+
+    def coach():
+        g = SplendorGame(2)
+        c = Coach(g, None, args, batch=32, seed=5)
+        c.sp.evaluator = HashEvaluator(g.engine)
+        return c
+
+    a = coach()
+    exset = a.executeIteration(4)
+    assert len(exset) > 0 and len(a.trainExamplesHistory.iters) == 1
+    ref = coach().executeEpisodes(4)                    # reference tuple form, same seeds
+    key = lambda t: (t[0].tobytes(), t[1].tobytes())
+    got = sorted(exset.to_tuples(), key=key)
+    ref = sorted(ref, key=key)
+    assert len(got) == len(ref)
+    for x, y in zip(got, ref):
+        for u, v in zip(x, y):
+            np.testing.assert_array_equal(u, v)
+    path = a.saveTrainExamples()
+    b = coach()
+    b.loadTrainExamples(str(tmp_path))
+    back = b.trainExamplesHistory.merged()
+    for k in ("board", "pi", "winner", "scdiff", "valids", "surprise"):
+        assert torch.equal(getattr(back, k).cpu(), getattr(exset, k).cpu()), k
+    assert path.endswith("checkpoint.examples.npz")
