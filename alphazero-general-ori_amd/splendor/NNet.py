@@ -1,35 +1,148 @@
-"""NeuralNet plug-in for Splendor (NNet.py:1-9 + GenericNNetWrapper.predict/checkpoints).
+"""NeuralNet plug-in for Splendor (NNet.py:1-9 + GenericNNetWrapper: predict, train,
+checkpoints).
 
-Inference only: training (GenericNNetWrapper.train, losses, optimiser) is outside the
-self-play hot path. Checkpoints are read with torch.load(weights_only=True);
-files that pickle whole model objects (like the reference's genbu.pt) are refused by that
-loader and are reported, never unpickled.
+`predict` is the reference's batch-1 call; self-play and arenas evaluate leaves in batches
+through splendor.nnet.LeafEvaluator instead (fused HIP kernel). `train` is
+GenericNNetWrapper.train (:43-139) fed straight from columnar device examples
+(splendor.examples.ExampleSet: no per-sample unpickling, targets built on device), with the
+same losses (:171-183), Adam + OneCycleLR schedule and batch sampling; under
+torch.distributed the gradients are averaged across ranks in one flat bucket (RCCL
+all-reduce) so every rank keeps identical weights. Checkpoints are read with
+torch.load(weights_only=True); files that pickle whole model objects (like the reference's
+genbu.pt) are refused by that loader and are reported, never unpickled.
 """
 import os
 
 import numpy as np
 import torch
+import torch.optim as optim
 
+from .env import unpack_mask
+from .examples import ExampleSet
 from .nnet import SplendorNNet, remap_policy_head
+
+DEFAULT_NN_ARGS = dict(learn_rate=0.0003, dropout=0.3, epochs=2, batch_size=32, vl_weight=10.0,
+                       surprise_weight=False)          # main.py:24-33, 121-127
+
+
+# ---------------------------------------------------------------- losses (:171-183)
+def loss_pi(targets, outputs):
+    return -torch.sum(targets * outputs) / targets.size()[0]
+
+
+def loss_v(targets, outputs):
+    return torch.sum((targets - outputs) ** 2) / (targets.size()[0] * targets.size()[-1])
+
+
+def loss_scdiff_cdf(targets, outputs):
+    l2_diff = torch.square(torch.cumsum(targets, axis=1) - torch.cumsum(torch.exp(outputs), axis=1))
+    return 0.02 * torch.sum(l2_diff) / (targets.size()[0] * targets.size()[-1])
+
+
+def loss_scdiff_pdf(targets, outputs):
+    cross_entropy = -torch.sum(torch.mul(targets, outputs))
+    return 0.02 * cross_entropy / (targets.size()[0] * targets.size()[-1])
+
+
+def scdiff_targets(scdiff, max_diff):
+    """One-hot score-difference targets [B, 2*max_diff+1, n] (:76-80), built on device."""
+    B, n = scdiff.shape
+    idx = (scdiff.long() + max_diff).clamp(0, 2 * max_diff)
+    t = torch.zeros((B, 2 * max_diff + 1, n), dtype=torch.float32, device=scdiff.device)
+    t.scatter_(1, idx.unsqueeze(1), 1.0)
+    return t
+
+
+def _allreduce_grads(params):
+    """Average gradients over ranks in one flat bucket (the model is ~1.25 MB of fp32)."""
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat)
+    flat /= dist.get_world_size()
+    off = 0
+    for g in grads:
+        g.copy_(flat[off:off + g.numel()].view_as(g))
+        off += g.numel()
 
 
 class NNetWrapper:
     def __init__(self, game, nn_args=None, use_exchange=True, device=None, seed=0):
-        self.args = nn_args or {}
+        self.args = dict(DEFAULT_NN_ARGS, **(nn_args or {}))
         self.device = torch.device(device) if device else game.engine.device
         torch.manual_seed(seed)
-        self.nnet = SplendorNNet(game.num_players).to(self.device).eval()
+        self.nnet = SplendorNNet(game.num_players, dropout=self.args["dropout"]).to(self.device).eval()
         self.action_size = game.getActionSize()
         self.rows = game.getBoardSize()[0]
+        self.max_diff = game.getMaxScoreDiff()
+        self.num_players = game.num_players
+        self.optimizer = None
 
     @torch.no_grad()
     def predict(self, board, valid_actions):
         """GenericNNetWrapper.predict (:141-168): (exp(log_pi)[409], tanh(v)[n]) as numpy."""
+        self.nnet.eval()
         b = torch.as_tensor(np.asarray(board, dtype=np.float32), device=self.device).reshape(1, self.rows, 7)
         va = torch.as_tensor(np.asarray(valid_actions, dtype=bool), device=self.device).reshape(1, -1)
         log_pi, v, _ = self.nnet(b, va)
         return torch.exp(log_pi)[0].cpu().numpy(), v[0].cpu().numpy()
 
+    # ------------------------------------------------------------ training (:43-139)
+    def losses(self, boards, pis, vs, scdiffs, valids):
+        """(l_pi, l_v, l_scdiff_cdf, l_scdiff_pdf) of one batch of device tensors."""
+        out_pi, out_v, out_sd = self.nnet(boards, valids)
+        t_sd = scdiff_targets(scdiffs, self.max_diff)
+        return (loss_pi(pis, out_pi), loss_v(vs, out_v), loss_scdiff_cdf(t_sd, out_sd),
+                loss_scdiff_pdf(t_sd, out_sd))
+
+    def train(self, examples, generator=None):
+        """One GenericNNetWrapper.train call over `examples` (ExampleSet, or the reference's
+        list of tuples): epochs x (len // batch_size) Adam steps on batches sampled without
+        replacement, total loss l_pi + vl_weight * l_v + l_cdf + l_pdf. Returns the mean of
+        each loss over the last epoch."""
+        if not isinstance(examples, ExampleSet):
+            examples = ExampleSet.from_tuples(list(examples))
+        if self.args["surprise_weight"]:
+            # the reference's weights are [E, n] (one per player) and np.random.choice
+            # rejects a 2-D p, so surprise weighting cannot run there either
+            raise ValueError("surprise_weight: per-example surprise is a vector (reference raises)")
+        ex = examples.to(self.device)
+        E, bs, epochs = len(ex), int(self.args["batch_size"]), int(self.args["epochs"])
+        batch_count = E // bs
+        if batch_count == 0:
+            return None
+        params = list(self.nnet.parameters())
+        if self.optimizer is None:
+            self.optimizer = optim.Adam(params, lr=self.args["learn_rate"])
+        scheduler = optim.lr_scheduler.OneCycleLR(self.optimizer, max_lr=self.args["learn_rate"],
+                                                  steps_per_epoch=batch_count, epochs=epochs)
+        gen = generator or torch.Generator(device=self.device)
+        means = None
+        for _ in range(epochs):
+            self.nnet.train()
+            acc = torch.zeros(3, dtype=torch.float64, device=self.device)
+            for _ in range(batch_count):
+                ids = torch.randperm(E, generator=gen, device=self.device)[:bs]
+                boards = ex.board.index_select(0, ids).float()
+                valids = unpack_mask(ex.valids.index_select(0, ids))
+                pis = ex.pi.index_select(0, ids)
+                vs = ex.winner.index_select(0, ids)
+                sds = ex.scdiff.index_select(0, ids)
+                self.optimizer.zero_grad(set_to_none=True)
+                l_pi, l_v, l_c, l_p = self.losses(boards, pis, vs, sds, valids)
+                total = l_pi + self.args["vl_weight"] * l_v + l_c + l_p
+                total.backward()
+                _allreduce_grads(params)
+                self.optimizer.step()
+                scheduler.step()
+                acc += torch.stack([l_pi.detach(), l_v.detach(), (l_c + l_p).detach()]).double()
+            means = (acc / batch_count).tolist()
+        self.nnet.eval()
+        return {"pi": means[0], "v": means[1], "scdiff": means[2]}
+
+    # ------------------------------------------------------------ checkpoints
     def save_checkpoint(self, folder="checkpoint", filename="checkpoint.pt", additional_keys=None):
         os.makedirs(folder, exist_ok=True)
         data = {"state_dict": self.nnet.state_dict()}

@@ -53,9 +53,10 @@ def _col_pool(x, length=64, chans=5):
 
 
 class SplendorNNet(nn.Module):
-    def __init__(self, n_players=2, action_size=ACTIONS, max_score_diff=15):
+    def __init__(self, n_players=2, action_size=ACTIONS, max_score_diff=15, dropout=0.0):
         super().__init__()
         self.n = n_players
+        self.dropout = float(dropout)                       # nn_args['dropout'] (main.py:26)
         self.rows = 32 + 10 * n_players + n_players * n_players
         self.action_size = action_size
         self.scdiff = 2 * max_score_diff + 1
@@ -73,11 +74,14 @@ class SplendorNNet(nn.Module):
         self.register_buffer("lowvalue", torch.FloatTensor([-1e8]))
 
     def trunk(self, board):
+        """SplendorNNet.forward up to the heads (SplendorNNet.py:127-138), dropout where the
+        reference applies it (training mode only)."""
+        d = lambda t: F.dropout(t, p=self.dropout, training=self.training)  # noqa: E731
         x = board.transpose(-1, -2).reshape(-1, 7, self.rows)
-        x = self.partialgpool_1(self.dense2d_1(x))
-        x = _col_pool(self.dense2d_3(x))
-        x = self.partialgpool_4(self.dense1d_4(x))
-        return self.partialgpool_5(self.dense1d_5(x))
+        x = d(self.partialgpool_1(self.dense2d_1(x)))
+        x = _col_pool(d(self.dense2d_3(x)))
+        x = d(self.partialgpool_4(d(self.dense1d_4(x))))
+        return d(self.partialgpool_5(d(self.dense1d_5(x))))
 
     def forward(self, board, valid):
         """Reference signature: (log_pi, tanh(v), log_softmax(scdiff))."""

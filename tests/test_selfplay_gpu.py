@@ -118,3 +118,25 @@ def test_iteration_examples_roundtrip(tmp_path):
     for k in ("board", "pi", "winner", "scdiff", "valids", "surprise"):
         assert torch.equal(getattr(back, k).cpu(), getattr(exset, k).cpu()), k
     assert path.endswith("checkpoint.examples.npz")
+
+
+def test_train_on_device_examples():
+    """Self-play examples stay on the device into NNetWrapper.train (GenericNNetWrapper
+    .train with columnar inputs), and the trained weights drive the next search."""
+    from splendor.NNet import NNetWrapper
+    from splendor.SplendorGame import SplendorGame
+    from splendor.coach import Coach
+    g = SplendorGame(2)
+    nn = NNetWrapper(g, dict(epochs=1, batch_size=32))
+    args = dict(numMCTSSims=8, cpuct=2.5, fpu=0.3, prob_fullMCTS=1.0, ratio_fullMCTS=4,
+                forced_playouts=False, dirichletAlpha=0.3, temperature=[1.25, 0.8], tempThreshold=10)
+    c = Coach(g, nn, args, batch=64, seed=2)
+    exset = c.executeIteration(8)
+    assert exset.board.is_cuda and len(exset) >= 32
+    before = [p.detach().clone() for p in nn.nnet.parameters()]
+    out = nn.train(exset)
+    assert all(np.isfinite(v) for v in out.values())
+    assert any(not torch.equal(a, b) for a, b in zip(before, nn.nnet.parameters()))
+    c2 = Coach(g, nn, args, batch=16, seed=3)          # evaluator packs the trained weights
+    c2.run_iterations(4)
+    assert c2.sp.stats()["overflow"] == 0

@@ -1,0 +1,151 @@
+"""Training consumer on CPU: GenericNNetWrapper.train's losses and
+score-difference targets (:76-80, :171-183) restated independently in numpy, a training run
+over a columnar ExampleSet, and the 2-rank gradient all-reduce (gloo) keeping ranks in
+lockstep."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from splendor.env import ACTIONS, pack_mask
+from splendor.examples import ExampleSet
+from splendor.NNet import (NNetWrapper, loss_pi, loss_scdiff_cdf, loss_scdiff_pdf, loss_v,
+                           scdiff_targets)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class StubGame:
+    """The Game surface NNetWrapper reads (no device engine needed on CPU)."""
+    def __init__(self, n=2):
+        self.num_players = n
+
+    def getActionSize(self):
+        return ACTIONS
+
+    def getBoardSize(self):
+        return (32 + 10 * self.num_players + self.num_players ** 2, 7)
+
+    def getMaxScoreDiff(self):
+        return 15
+
+
+def synthetic(E, n=2, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    R = 32 + 10 * n + n * n
+    board = torch.randint(-2, 8, (E, R, 7), generator=g, dtype=torch.int8)
+    valid = torch.rand(E, ACTIONS, generator=g) < 0.05
+    valid[:, 408] = True
+    pi = torch.where(valid, torch.rand(E, ACTIONS, generator=g), torch.zeros(()))
+    pi = pi / pi.sum(1, keepdim=True)
+    w = (torch.rand(E, generator=g) < 0.5).float() * 2 - 1
+    winner = torch.stack([w, -w], 1) if n == 2 else torch.rand(E, n, generator=g)
+    scdiff = torch.randint(-20, 21, (E, n), generator=g, dtype=torch.int32)
+    surprise = torch.rand(E, n, generator=g)
+    return ExampleSet(board, pi, winner, scdiff, pack_mask(valid), surprise)
+
+
+def test_loss_functions_match_numpy():
+    rng = np.random.default_rng(0)
+    B, n, D = 5, 2, 31
+    t_pi = rng.random((B, ACTIONS)).astype(np.float32)
+    o_pi = np.log(rng.random((B, ACTIONS))).astype(np.float32)
+    t_v, o_v = rng.random((B, n)).astype(np.float32), rng.random((B, n)).astype(np.float32)
+    t_sd = np.zeros((B, D, n), np.float32)
+    t_sd[np.arange(B), rng.integers(0, D, B), 0] = 1
+    t_sd[np.arange(B), rng.integers(0, D, B), 1] = 1
+    o_sd = np.log(rng.dirichlet(np.ones(D), size=(B, n)).transpose(0, 2, 1)).astype(np.float32)
+    T = torch.from_numpy
+    np.testing.assert_allclose(float(loss_pi(T(t_pi), T(o_pi))), -(t_pi * o_pi).sum() / B, rtol=1e-5)
+    np.testing.assert_allclose(float(loss_v(T(t_v), T(o_v))), ((t_v - o_v) ** 2).sum() / (B * n), rtol=1e-5)
+    cdf = ((np.cumsum(t_sd, 1) - np.cumsum(np.exp(o_sd), 1)) ** 2).sum() * 0.02 / (B * n)
+    np.testing.assert_allclose(float(loss_scdiff_cdf(T(t_sd), T(o_sd))), cdf, rtol=1e-5)
+    pdf = -(t_sd * o_sd).sum() * 0.02 / (B * n)
+    np.testing.assert_allclose(float(loss_scdiff_pdf(T(t_sd), T(o_sd))), pdf, rtol=1e-5)
+
+
+def test_scdiff_targets_match_loop():
+    sd = torch.tensor([[-20, 3], [15, -15], [0, 16]], dtype=torch.int32)
+    got = scdiff_targets(sd, 15).numpy()
+    ref = np.zeros((3, 31, 2), np.float32)                 # GenericNNetWrapper.py:76-80
+    for i in range(3):
+        score_diff = (sd[i].numpy() + 15).clip(0, 30)
+        for p in range(2):
+            ref[i, score_diff[p], p] = 1
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_train_reduces_loss_on_columnar_examples():
+    torch.manual_seed(0)
+    ex = synthetic(256)
+    w = NNetWrapper(StubGame(), dict(epochs=6, batch_size=32, dropout=0.0, learn_rate=3e-3), device="cpu")
+
+    def full_loss():
+        with torch.no_grad():
+            w.nnet.eval()
+            from splendor.env import unpack_mask
+            l = w.losses(ex.board.float(), ex.pi, ex.winner, ex.scdiff, unpack_mask(ex.valids))
+            return float(l[0] + 10 * l[1] + l[2] + l[3])
+
+    before = full_loss()
+    out = w.train(ex, generator=torch.Generator().manual_seed(1))
+    after = full_loss()
+    assert set(out) == {"pi", "v", "scdiff"}
+    assert after < 0.8 * before, (before, after)
+    assert not w.nnet.training
+
+
+def test_train_accepts_reference_tuples_and_rejects_surprise_weight():
+    ex = synthetic(40)
+    w = NNetWrapper(StubGame(), dict(epochs=1, batch_size=16), device="cpu")
+    assert w.train(ex.to_tuples(), generator=torch.Generator().manual_seed(0)) is not None
+    w2 = NNetWrapper(StubGame(), dict(surprise_weight=True), device="cpu")
+    with pytest.raises(ValueError):
+        w2.train(ex)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "alphazero-general-ori_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from test_train import StubGame, synthetic
+    from splendor.NNet import NNetWrapper
+    w = NNetWrapper(StubGame(), dict(epochs=1, batch_size=16, dropout=0.0), device="cpu", seed=0)
+    w.train(synthetic(64, seed=10 + rank), generator=torch.Generator().manual_seed(rank))
+    flat = torch.cat([p.detach().reshape(-1) for p in w.nnet.parameters()])
+    parts = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(parts, flat)
+    if rank == 0:
+        q.put([p.numpy() for p in parts])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gradient_allreduce_keeps_ranks_identical():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(parts[0], parts[1])
+    init = torch.cat([p.detach().reshape(-1) for p in
+                      NNetWrapper(StubGame(), {}, device="cpu", seed=0).nnet.parameters()]).numpy()
+    assert not np.array_equal(parts[0], init)          # the ranks did train
