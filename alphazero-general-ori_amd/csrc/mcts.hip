@@ -76,6 +76,10 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         c[j] = in ? P.echild[e0 + i] : -1;
         r[j] = in ? P.ecr[e0 + i] : make_int2(0, 0);
     }
+#if MCTS_TIMING
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // split load wait / compute
+    SPL_PROBE(8)
+#endif
     int bi = -1;
     if (forced) {                               // MCTS.py:208-213: first under-visited edge
 #pragma unroll
@@ -96,18 +100,29 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
     if (bi < 0) {                               // pick_highest_UCB (MCTS.py:199-219)
         const double fpu_init = C.fpu > 0 ? qs - C.fpu : C.fpu;
         const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
-        double bu = -INFINITY;
+        double bu = -INFINITY, uj[2];
         int bj = 0x7fffffff;
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const int i = 64 * j + l;
+            uj[j] = -INFINITY;
             if (i < ec) {
                 const double u = q[j] != Q_UNSET ? q[j] + C.cpuct * (double)p[j] * sq / (double)(1 + n[j])
                                                  : fpu_init + C.cpuct * (double)p[j] * sq_eps;
+                uj[j] = u;
                 if (u > bu) { bu = u; bj = i; }
             }
         }
-        for (int base = 128; base < ec; base += 64) {
+        if (ec <= 128) {
+            // strict '>' scan in action order = the lowest edge index holding the maximum:
+            // DPP wave max, then the first lane of the first half that holds it
+            const double m = wave_max_f64(bu);
+            const uint64_t b0 = __ballot(uj[0] == m);
+            bi = b0 ? __ffsll((unsigned long long)b0) - 1
+                    : 64 + __ffsll((unsigned long long)__ballot(uj[1] == m)) - 1;
+            bi = uniform(bi);
+        }
+        for (int base = 128; bi < 0 && base < ec; base += 64) {
             const int i = base + l;
             if (i < ec) {
                 const double qq = P.eq[e0 + i], pp = (double)P.ep[e0 + i];
@@ -116,18 +131,21 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
                 if (u > bu) { bu = u; bj = i; }
             }
         }
-        wave_argmax(bu, bj);
-        bi = bj;
+        if (bi < 0) {
+            wave_argmax(bu, bj);
+            bi = bj;
+        }
     }
     const int jb = bi >> 6;
     int av = a[0], cv = c[0], rx = r[0].x, ry = r[0].y;
 #pragma unroll
     for (int j = 1; j < 2; j++)
         if (jb == j) { av = a[j]; cv = c[j]; rx = r[j].x; ry = r[j].y; }
-    av = __shfl(av, bi & 63, 64);
-    cv = __shfl(cv, bi & 63, 64);
-    rx = __shfl(rx, bi & 63, 64);
-    ry = __shfl(ry, bi & 63, 64);
+    bi = uniform(bi);                           // chosen lane -> SGPRs (readlane, no LDS trip)
+    av = __builtin_amdgcn_readlane(av, bi & 63);
+    cv = __builtin_amdgcn_readlane(cv, bi & 63);
+    rx = __builtin_amdgcn_readlane(rx, bi & 63);
+    ry = __builtin_amdgcn_readlane(ry, bi & 63);
     if (bi >= 128) { av = P.ea[e0 + bi]; cv = P.echild[e0 + bi]; const int2 rr = P.ecr[e0 + bi]; rx = rr.x; ry = rr.y; }
     return {bi, av, cv, make_int2(rx, ry)};
 }

@@ -89,6 +89,28 @@ __device__ __forceinline__ void wave_argmax(double &u, int &i) {
     }
 }
 
+// wave maximum of a double, uniform result: butterfly within each 16-lane row on DPP
+// (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror: no LDS round trips), then
+// the four row maxima by readlane. Exact (max returns one of its operands).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, CTRL, 0xF, 0xF, false),
+                            __builtin_amdgcn_update_dpp(lo, lo, CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double wave_max_f64(double v) {
+    v = fmax(v, dpp_f64<0xB1>(v));
+    v = fmax(v, dpp_f64<0x4E>(v));
+    v = fmax(v, dpp_f64<0x141>(v));
+    v = fmax(v, dpp_f64<0x140>(v));
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    double r[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        r[k] = __hiloint2double(__builtin_amdgcn_readlane(hi, 16 * k), __builtin_amdgcn_readlane(lo, 16 * k));
+    return fmax(fmax(r[0], r[1]), fmax(r[2], r[3]));
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

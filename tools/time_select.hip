@@ -39,12 +39,13 @@ int main(int argc, char **argv) {
     float ms; (void)hipEventElapsedTime(&ms, e0, e1);
     unsigned long long h[24];
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_select_timing), sizeof(h));
-    const char *names[] = {"root load", "descend: loop top", "pick_edge + edge loads", "make_move + roll",
-                           "fingerprint + hash", "node checks (to next level)", "leaf: store + mask", "headers"};
+    const char *names[] = {"root load", "descend: loop top", "pick_edge: UCB + argmax", "make_move + roll",
+                           "fingerprint + hash", "node checks (to next level)", "leaf: store + mask", "headers",
+                           "pick_edge: edge loads"};
     const double calls = (double)h[21];
     printf("edge_cap %d, arena %.2f GB\n", cfg.edge_cap, spl_mcts_device_bytes(m) / 1e9);
     printf("%d sims x %d trees: %.1f us per select+hash_eval+backup iteration; %.0f probed waves, %.2f levels/sim\n",
            SIMS, B, ms * 1e3 / SIMS, calls, h[20] / calls);
-    for (int k = 0; k < 8; k++) printf("  %-28s %8.0f cycles per select\n", names[k], h[k] / calls);
+    for (int k = 0; k < 9; k++) printf("  %-28s %8.0f cycles per select\n", names[k], h[k] / calls);
     return 0;
 }
