@@ -774,12 +774,12 @@ __device__ __forceinline__ float wave_np_sum409(const float *a) {
 }
 
 template <int N>
-__global__ __launch_bounds__(THREADS) void k_backup(Pools P, SearchCfg C, int B,
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) void k_backup(Pools P, SearchCfg C, int B,
                                                     const uint64_t *__restrict__ leaf_mask,
                                                     const float *__restrict__ pi,
                                                     const float *__restrict__ v) {
     __shared__ __align__(16) float lpi[WAVES][416];
-    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    const int w = uniform(threadIdx.x >> 6), t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
