@@ -839,9 +839,74 @@ __device__ __forceinline__ int move_kind(int a, const int8_t *act_rsv) {
     return a < 12 ? MK_BUY : (a >= 27 && a < 30 ? MK_BUY_RESERVED : (act_rsv[a] >= 0 ? MK_RESERVE : MK_GEMS));
 }
 
+// make_move for a visible-card buy (KIND == MK_BUY) with every row it touches read up front
+// and kept in registers: the same stages and results as the fixed pipeline below (_buy_card
+// :458-474, _give_nobles_if_earned :763-768, _fill_new_card :445-450, round +1 :287), but
+// one LDS round trip for the reads instead of a chain of write-then-reread steps (the buy
+// wave is the longest move pipeline of the rollout kernel).
+template <int N>
+__device__ __forceinline__ int make_move_buy(int8_t *s, int a, int p, bool det, Chance &ch) {
+    using Lx = Lay<N>;
+    const int r = Lx::TIERS + 2 * a, tier = a >> 2;
+    const uint64_t cost = row(s, r), gain = row(s, r + 1);
+    uint64_t gems = row(s, Lx::GEMS + p), bank = row(s, Lx::BANK);
+    const uint64_t cards = row(s, Lx::CARDS + p);
+    uint64_t nob[Lx::NN];
+#pragma unroll
+    for (int i = 0; i < Lx::NN; i++) nob[i] = row(s, Lx::NOBLES + i);
+    uint64_t cnt = row(s, Lx::DECKS + 2 * tier), bits = row(s, Lx::DECKS + 2 * tier + 1);
+    const bool draw = !det && sum5(cnt) != 0;
+    double u0 = 0.0, u1 = 0.0;
+    if (draw) { u0 = ch.draw(); u1 = ch.draw(); }
+    // _buy_card: coloured gems first, gold for what is missing
+    int miss = 0;
+    uint64_t paid = 0;
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        const int cc = bt(cost, c), gc = bt(gems, c), kc = bt(cards, c);
+        const int d = cc - gc - kc;
+        miss += d > 0 ? d : 0;
+        int need = cc - kc;
+        need = need > 0 ? need : 0;
+        paid |= (uint64_t)(uint8_t)(need < gc ? need : gc) << (8 * c);
+    }
+    gems = bytes_sub(gems, paid);
+    bank = bytes_add(bank, paid);
+    gems = with_bt(gems, 5, bt(gems, 5) - miss);
+    bank = with_bt(bank, 5, bt(bank, 5) + miss);
+    const uint64_t ncards = bytes_add(cards, gain);
+    // _fill_new_card: one deck draw into the bought slot (zeros when the deck is empty)
+    uint64_t ncost = 0, ngain = 0;
+    if (draw) {
+        int color, idx;
+        deck_pick(cnt, bits, u0, u1, ch.tab, color, idx);
+        deck_take(cnt, bits, color, idx);
+        ncost = ch.tab.cards[tier * 40 + color * 8 + idx][0];
+        ngain = ch.tab.cards[tier * 40 + color * 8 + idx][1];
+    }
+    row(s, Lx::CARDS + p) = ncards;
+#pragma unroll
+    for (int i = 0; i < Lx::NN; i++) {
+        if (sum5(nob[i]) > 0 && ge5(ncards, nob[i])) {
+            row(s, Lx::PNOB + Lx::NN * p + i) = nob[i];
+            row(s, Lx::NOBLES + i) = 0;
+        }
+    }
+    if (draw) {
+        row(s, Lx::DECKS + 2 * tier + 1) = bits;
+        row(s, Lx::DECKS + 2 * tier) = cnt;
+    }
+    row(s, r) = ncost;
+    row(s, r + 1) = ngain;
+    row(s, Lx::GEMS + p) = gems;
+    row(s, Lx::BANK) = with_bt(bank, 6, bt(bank, 6) + 1);
+    return (p + 1) % N;
+}
+
 template <int N, int KIND = -1>
 __device__ __forceinline__ int make_move(int8_t *s, int a, int p, bool det, Chance &ch) {
     using Lx = Lay<N>;
+    if constexpr (KIND == MK_BUY) return make_move_buy<N>(s, a, p, det, ch);
     constexpr bool ANY = KIND < 0;
     const int rsv = ANY || KIND == MK_RESERVE ? (int)ch.tab.act_rsv[a] : -1;
     const bool vec = ANY || KIND == MK_GEMS || KIND == MK_RESERVE;

@@ -20,7 +20,7 @@
 #if ROLLOUT_TIMING
 // block-shared cycle accumulators; SPL_PROBE(k) charges the cycles since the previous probe
 // to slot k (thread 0's view; in product builds SPL_PROBE expands to nothing)
-__shared__ uint64_t spl_probe_acc[24];
+__shared__ uint64_t spl_probe_acc[32];
 __shared__ uint64_t spl_probe_last;
 #define SPL_PROBE(k)                                                                       \
     if (threadIdx.x == 0) {                                                                \
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
     int8_t *const gst = state + (size_t)b0 * Lx::S;
 #if ROLLOUT_TIMING
-    if (tid < 24) spl_probe_acc[tid] = 0;
+    if (tid < 32) spl_probe_acc[tid] = 0;
     if (tid == 0) spl_probe_last = clock64();
     const uint64_t wall0 = wall_clock64();
 #endif
@@ -379,6 +379,15 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                 pl[b] = (int8_t)nxt;
             }
             RT_MARK(2)
+#if ROLLOUT_TIMING
+            {   // per wave: move pipeline up to the deals (24+w), games it ended (28+w)
+                const int ne = __popcll(__ballot(ended));
+                if (l == 0) {
+                    atomicAdd((unsigned long long *)&spl_probe_acc[24 + w], (unsigned long long)(clock64() - mv0));
+                    atomicAdd((unsigned long long *)&spl_probe_acc[28 + w], (unsigned long long)ne);
+                }
+            }
+#endif
             for (uint64_t rm = __ballot(ended); rm; rm &= rm - 1) {
                 const int rb = __shfl(b, __ffsll((unsigned long long)rm) - 1);
                 wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)(b0 + rb), step, 3, DEAL_DRAWS);
@@ -409,6 +418,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         for (int k = 0; k < 24; k++) o[k] = spl_probe_acc[k];
         o[24] = wall0;
         o[25] = wall_clock64();
+        for (int k = 24; k < 30; k++) o[k + 2] = spl_probe_acc[k];   // o[26..29] pre-deal, o[30..31] deals w0-1
     }
 #endif
 }

@@ -57,6 +57,19 @@ int main() {
             printf(" %.0f", x / (NB * (double)K));
         }
         printf("\n");
+        printf("  move pipeline before deals per wave, cycles/move:");
+        for (int k = 0; k < 4; k++) {
+            double x = 0;
+            for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 32 + 26 + k];
+            printf(" %.0f", x / (NB * (double)K));
+        }
+        printf("\n  games ended per WG-move by the gems / buy wave:");
+        for (int k = 0; k < 2; k++) {
+            double x = 0;
+            for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 32 + 30 + k];
+            printf(" %.3f", x / (NB * (double)K));
+        }
+        printf("\n");
     }
     return 0;
 }
