@@ -835,6 +835,12 @@ __device__ __forceinline__ void buy_card(int8_t *s, int cost_row, int p) {
 // KIND (move_kind) >= 0 specialises the pipeline to one kind of move when the caller knows
 // it: the stages that kind never uses are compiled out.
 enum { MK_GEMS = 0, MK_BUY = 1, MK_RESERVE = 2, MK_BUY_RESERVED = 3 };
+// same classification without the table: the reserve actions are 12-26 (visible / deck)
+// and 290-364 (reserve-and-give-back), the rows of K_ACT_RSV >= 0 (gen_tables.py)
+__device__ __forceinline__ int move_kind_of(int a) {
+    return a < 12 ? MK_BUY : (a < 27 ? MK_RESERVE : (a < 30 ? MK_BUY_RESERVED :
+                                                     (a >= 290 && a < 365 ? MK_RESERVE : MK_GEMS)));
+}
 __device__ __forceinline__ int move_kind(int a, const int8_t *act_rsv) {
     return a < 12 ? MK_BUY : (a >= 27 && a < 30 ? MK_BUY_RESERVED : (act_rsv[a] >= 0 ? MK_RESERVE : MK_GEMS));
 }

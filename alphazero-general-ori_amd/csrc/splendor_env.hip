@@ -330,7 +330,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                     a = select_bit(m, (int)(ud[b][0] * (double)cnt));
                 }
                 act[b] = (int16_t)a;
-                const int kind = move_kind(a, tabs.act_rsv);
+                const int kind = move_kind_of(a);
                 klist[kind][atomicAdd(&kcount[kind], 1)] = (uint8_t)b;
             }
         }
