@@ -66,15 +66,13 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
     int2 r[2];
     double q[2];
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
+    for (int j = 0; j < 2; j++) {               // two 16-byte records per edge
         const int i = 64 * j + l;
-        const bool in = i < ec;
-        p[j] = in ? P.ep[e0 + i] : 0.f;
-        n[j] = in ? P.en[e0 + i] : 0;
-        q[j] = in ? P.eq[e0 + i] : Q_UNSET;
-        a[j] = in ? (int)P.ea[e0 + i] : 0;
-        c[j] = in ? P.echild[e0 + i] : -1;
-        r[j] = in ? P.ecr[e0 + i] : make_int2(0, 0);
+        EdgeStat st{0.f, 0, Q_UNSET};
+        EdgeLink lk{0, 0, -1, 0, 0};
+        if (i < ec) { st = P.es[e0 + i]; lk = P.el[e0 + i]; }
+        p[j] = st.p; n[j] = st.n; q[j] = st.q;
+        a[j] = lk.a; c[j] = lk.child; r[j] = get_cr(lk);
     }
 #if MCTS_TIMING
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // split load wait / compute
@@ -92,7 +90,7 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         for (int base = 128; bi < 0 && base < ec; base += 64) {
             const int i = base + l;
             bool f = false;
-            if (i < ec) f = (long long)P.en[e0 + i] < (long long)sqrt(0.5 * (double)P.ep[e0 + i] * (double)step);
+            if (i < ec) f = (long long)P.es[e0 + i].n < (long long)sqrt(0.5 * (double)P.es[e0 + i].p * (double)step);
             const uint64_t b = __ballot(f);
             if (b) bi = base + __ffsll((unsigned long long)b) - 1;
         }
@@ -125,8 +123,8 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         for (int base = 128; bi < 0 && base < ec; base += 64) {
             const int i = base + l;
             if (i < ec) {
-                const double qq = P.eq[e0 + i], pp = (double)P.ep[e0 + i];
-                const double u = qq != Q_UNSET ? qq + C.cpuct * pp * sq / (double)(1 + P.en[e0 + i])
+                const double qq = P.es[e0 + i].q, pp = (double)P.es[e0 + i].p;
+                const double u = qq != Q_UNSET ? qq + C.cpuct * pp * sq / (double)(1 + P.es[e0 + i].n)
                                                : fpu_init + C.cpuct * pp * sq_eps;
                 if (u > bu) { bu = u; bj = i; }
             }
@@ -146,7 +144,7 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
     cv = __builtin_amdgcn_readlane(cv, bi & 63);
     rx = __builtin_amdgcn_readlane(rx, bi & 63);
     ry = __builtin_amdgcn_readlane(ry, bi & 63);
-    if (bi >= 128) { av = P.ea[e0 + bi]; cv = P.echild[e0 + bi]; const int2 rr = P.ecr[e0 + bi]; rx = rr.x; ry = rr.y; }
+    if (bi >= 128) { av = P.el[e0 + bi].a; cv = P.el[e0 + bi].child; const int2 rr = get_cr(P.el[e0 + bi]); rx = rr.x; ry = rr.y; }
     return {bi, av, cv, make_int2(rx, ry)};
 }
 
@@ -177,7 +175,7 @@ __device__ __forceinline__ double gamma_sample(double alpha, uint64_t seed, uint
 __device__ __forceinline__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int eb,
                                                  int ec, uint32_t stream) {
     const int l = lane_id();
-    float *ep = P.ep + (size_t)t * P.ecap + eb;
+    EdgeStat *est = P.es + (size_t)t * P.ecap + eb;
     const uint32_t gb = C.board_base + (uint32_t)t;
     const bool tmp = C.dir_temp != 1.0;
     double sp[3], g[3], ssum = 0.0, gsum = 0.0;
@@ -186,7 +184,7 @@ __device__ __forceinline__ void apply_root_noise(const Pools &P, const SearchCfg
         const int i = l + 64 * j;
         sp[j] = 0.0; g[j] = 0.0;
         if (i < ec) {
-            sp[j] = tmp ? pow((double)ep[i], 1.0 / C.dir_temp) : (double)ep[i];
+            sp[j] = tmp ? pow((double)est[i].p, 1.0 / C.dir_temp) : (double)est[i].p;
             uint32_t ctr = (uint32_t)i * 256u;
             g[j] = gamma_sample(C.dir_alpha, C.seed, gb, stream, ctr);
         }
@@ -212,7 +210,7 @@ __device__ __forceinline__ void apply_root_noise(const Pools &P, const SearchCfg
 #pragma unroll
     for (int j = 0; j < 3; j++) {
         const int i = l + 64 * j;
-        if (i < ec) ep[i] = pn[j] / nsum;
+        if (i < ec) est[i].p = pn[j] / nsum;
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
@@ -306,16 +304,16 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round) {
                 int16_t a = 0; float p = 0; int32_t cnt = 0, ch = -1; double qq = 0;
                 int2 cr = make_int2(0, 0);
                 if (in) {
-                    a = P.ea[e0 + jo + q]; p = P.ep[e0 + jo + q]; cnt = P.en[e0 + jo + q];
-                    qq = P.eq[e0 + jo + q]; ch = P.echild[e0 + jo + q]; cr = P.ecr[e0 + jo + q];
+                    a = P.el[e0 + jo + q].a; p = P.es[e0 + jo + q].p; cnt = P.es[e0 + jo + q].n;
+                    qq = P.es[e0 + jo + q].q; ch = P.el[e0 + jo + q].child; cr = get_cr(P.el[e0 + jo + q]);
                 }
                 const int nch = ch >= 0 ? remap[ch] : -1;
                 if (nch >= 0) cr.x = remap_eb[ch];
                 __threadfence_block();
                 __builtin_amdgcn_wave_barrier();
                 if (in) {
-                    P.ea[e0 + jd + q] = a; P.ep[e0 + jd + q] = p; P.en[e0 + jd + q] = cnt;
-                    P.eq[e0 + jd + q] = qq; P.echild[e0 + jd + q] = nch; P.ecr[e0 + jd + q] = cr;
+                    P.el[e0 + jd + q].a = a; P.es[e0 + jd + q].p = p; P.es[e0 + jd + q].n = cnt;
+                    P.es[e0 + jd + q].q = qq; P.el[e0 + jd + q].child = nch; set_cr(P.el[e0 + jd + q], cr.x, cr.y);
                 }
                 __threadfence_block();
                 __builtin_amdgcn_wave_barrier();
@@ -463,11 +461,10 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     const int root = H->root, eb = P.neb[nb + root], ec = P.nec[nb + root];
     const bool forced = H->forced;
     const int sims = H->budget, cm = H->move_no;
-    const int16_t *ea = P.ea + e0 + eb;
-    const int32_t *en = P.en + e0 + eb;
-    const float *ep = P.ep + e0 + eb;
+    const EdgeStat *est = P.es + e0 + eb;
+    const EdgeLink *elk = P.el + e0 + eb;
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, en[i]);
+    for (int i = l; i < ec; i += 64) best = max(best, est[i].n);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
     // policy counts: pruned (MCTS.py:69-74); where the reference would divide 0/0
     // (Coach.py:83 raises) fall back to raw counts, then to uniform
@@ -476,11 +473,11 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     for (; mode < 3; mode++) {
         tot = 0;
         for (int i = l; i < ec; i += 64)
-            tot += mode == 0 ? pruned_count(en[i], best, true, ep[i], sims) : (mode == 1 ? en[i] : 1);
+            tot += mode == 0 ? pruned_count(est[i].n, best, true, est[i].p, sims) : (mode == 1 ? est[i].n : 1);
         for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
         if (tot > 0) break;
     }
-#define POLICY_COUNT(i) (mode == 0 ? pruned_count(en[i], best, true, ep[i], sims) : (mode == 1 ? (long long)en[i] : 1ll))
+#define POLICY_COUNT(i) (mode == 0 ? pruned_count(est[i].n, best, true, est[i].p, sims) : (mode == 1 ? (long long)est[i].n : 1ll))
     const int step = H->episode_step + 1;
     const int player = H->player;
     int8_t *s = lds[w][0], *b = lds[w][1];
@@ -495,7 +492,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         for (int i = l; i < ec; i += 64)   // getSymmetries stores pi as float32 (SplendorGame.py:59-61)
-            pi[ea[i]] = (float)((double)POLICY_COUNT(i) / (double)tot);
+            pi[elk[i].a] = (float)((double)POLICY_COUNT(i) / (double)tot);
         uint64_t m[7];
         wave_valid_moves<N>(s, 0, lim, m);
         store_mask(P.ex_valid + x * 7, m);
@@ -519,10 +516,10 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
             last += temp_pow((double)POLICY_COUNT(i) / (double)tot, T) / sum;
         const double u = philox_u01(C.seed, gb, ST_PICK | (uint32_t)cm, 0);
         double cdf = 0.0;
-        action = ea[ec - 1];
+        action = elk[ec - 1].a;
         for (int i = 0; i < ec; i++) {
             cdf += temp_pow((double)POLICY_COUNT(i) / (double)tot, T) / sum;
-            if (cdf / last > u) { action = ea[i]; break; }
+            if (cdf / last > u) { action = elk[i].a; break; }
         }
     }
     action = __shfl(action, 0, 64);
@@ -681,7 +678,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
                 child = uniform(hash_lookup(P, t, k0, k1));
                 if (child >= 0) {                            // transposition: link + cache
                     cr = make_int2(P.neb[nb + child], P.nterm[nb + child] ? -1 : P.nec[nb + child]);
-                    if (l == 0) { P.echild[e0 + ge] = child; P.ecr[e0 + ge] = cr; }
+                    if (l == 0) { P.el[e0 + ge].child = child; set_cr(P.el[e0 + ge], cr.x, cr.y); }
                 }
             }
             SPL_PROBE(4)
@@ -710,8 +707,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
 #pragma unroll
                     for (int i = 0; i < 4; i++) P.nes[(nb + id) * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
                     hash_insert(P, t, k0, id);
-                    P.echild[e0 + ge] = id;
-                    P.ecr[e0 + ge] = make_int2(0, -1);
+                    P.el[e0 + ge].child = id;
+                    set_cr(P.el[e0 + ge], 0, -1);
                     H->node_count = id + 1;
                 }
                 kind = LEAF_TERMINAL;
@@ -811,11 +808,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             if ((wd >> l) & 1) {
                 const int r = eb + run + __popcll(wd & lanemask_lt());
                 const int a = 64 * k + l;
-                P.ea[e0 + r] = (int16_t)a;
-                P.ep[e0 + r] = pr[a] / sum;
-                P.en[e0 + r] = 0;
-                P.eq[e0 + r] = Q_UNSET;
-                P.echild[e0 + r] = -1;
+                P.el[e0 + r].a = (int16_t)a;
+                P.es[e0 + r].p = pr[a] / sum;
+                P.es[e0 + r].n = 0;
+                P.es[e0 + r].q = Q_UNSET;
+                P.el[e0 + r].child = -1;
             }
             run += __popcll(wd);
         }
@@ -830,8 +827,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             hash_insert(P, t, H->leaf_k0, id);
             if (depth == 0) H->root = id;
             else {
-                P.echild[e0 + path[2 * (depth - 1) + 1]] = id;
-                P.ecr[e0 + path[2 * (depth - 1) + 1]] = make_int2(eb, ec);
+                P.el[e0 + path[2 * (depth - 1) + 1]].child = id;
+                set_cr(P.el[e0 + path[2 * (depth - 1) + 1]], eb, ec);
             }
             H->node_count = id + 1;
             H->edge_count = eb + ec;
@@ -851,11 +848,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         const int rot = (depth - d) % N;
         const double v0 = (double)val[(N - rot) % N];
         const int node = path[2 * d], ge = path[2 * d + 1];
-        const int cnt = P.en[e0 + ge];
-        P.eq[e0 + ge] = ((double)cnt * P.eq[e0 + ge] + v0) / (double)(cnt + 1);
+        const int cnt = P.es[e0 + ge].n;
+        P.es[e0 + ge].q = ((double)cnt * P.es[e0 + ge].q + v0) / (double)(cnt + 1);
         const int ns = P.nns[nb + node];
         P.nqs[nb + node] = ((double)(ns + 1) * P.nqs[nb + node] + v0) / (double)(ns + 2);
-        P.en[e0 + ge] = cnt + 1;
+        P.es[e0 + ge].n = cnt + 1;
         P.nns[nb + node] = ns + 1;
     }
     if (l == 0) {
@@ -891,11 +888,11 @@ __global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int
     const int sims = H->budget;
     const bool forced = H->forced;
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, P.en[e0 + eb + i]);
+    for (int i = l; i < ec; i += 64) best = max(best, P.es[e0 + eb + i].n);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
     long long top = 0;
     for (int i = l; i < ec; i += 64)
-        top = max(top, pruned_count(P.en[e0 + eb + i], best, forced, P.ep[e0 + eb + i], sims));
+        top = max(top, pruned_count(P.es[e0 + eb + i].n, best, forced, P.es[e0 + eb + i].p, sims));
     for (int o = 32; o > 0; o >>= 1) top = max(top, (long long)__shfl_xor(top, o, 64));
     if (top == 0) {
         if (l == 0) action[t] = (int16_t)(int)(u * (double)SPL_ACTIONS);
@@ -904,20 +901,20 @@ __global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int
     int nbest = 0;
     for (int base = 0; base < ec; base += 64) {
         const int i = base + l;
-        const bool hit = i < ec && pruned_count(P.en[e0 + eb + i], best, forced, P.ep[e0 + eb + i], sims) == top;
+        const bool hit = i < ec && pruned_count(P.es[e0 + eb + i].n, best, forced, P.es[e0 + eb + i].p, sims) == top;
         nbest += __popcll(__ballot(hit));
     }
     int k = (int)(u * (double)nbest);                    // k-th best in action order
     for (int base = 0; base < ec; base += 64) {
         const int i = base + l;
-        const bool hit = i < ec && pruned_count(P.en[e0 + eb + i], best, forced, P.ep[e0 + eb + i], sims) == top;
+        const bool hit = i < ec && pruned_count(P.es[e0 + eb + i].n, best, forced, P.es[e0 + eb + i].p, sims) == top;
         const uint64_t b = __ballot(hit);
         const int c = __popcll(b);
         if (k < c) {
             uint64_t x = b;
             for (int j = 0; j < k; j++) x &= x - 1;
             const int pos = __ffsll((unsigned long long)x) - 1;
-            if (l == 0) action[t] = P.ea[e0 + eb + base + pos];
+            if (l == 0) action[t] = P.el[e0 + eb + base + pos].a;
             return;
         }
         k -= c;
@@ -947,23 +944,23 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
     __builtin_amdgcn_wave_barrier();
     const int eb = P.neb[nb + root], ec = P.nec[nb + root];
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, P.en[e0 + eb + i]);
+    for (int i = l; i < ec; i += 64) best = max(best, P.es[e0 + eb + i].n);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
     const int sims = H->budget;
     const bool forced = H->forced;
     long long tot = 0;
     for (int i = l; i < ec; i += 64) {
-        const int a = P.ea[e0 + eb + i];
-        const long long c = pruned_count(P.en[e0 + eb + i], best, forced, P.ep[e0 + eb + i], sims);
-        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = P.en[e0 + eb + i];
+        const int a = P.el[e0 + eb + i].a;
+        const long long c = pruned_count(P.es[e0 + eb + i].n, best, forced, P.es[e0 + eb + i].p, sims);
+        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = P.es[e0 + eb + i].n;
         if (adjusted) adjusted[(size_t)t * SPL_ACTIONS + a] = c;
-        if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = P.eq[e0 + eb + i];
+        if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = P.es[e0 + eb + i].q;
         tot += c;
     }
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
     for (int i = l; i < ec; i += 64) {
-        const int a = P.ea[e0 + eb + i];
-        const long long c = pruned_count(P.en[e0 + eb + i], best, forced, P.ep[e0 + eb + i], sims);
+        const int a = P.el[e0 + eb + i].a;
+        const long long c = pruned_count(P.es[e0 + eb + i].n, best, forced, P.es[e0 + eb + i].p, sims);
         if (probs) probs[(size_t)t * SPL_ACTIONS + a] = (double)c / (double)tot;
     }
     if (q && l == 0) {
@@ -1065,8 +1062,8 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     size_t bytes = 0;
     auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
     acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn); acc(4 * nn);
-    acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(2 * ne); acc(4 * ne); acc(4 * ne);
-    acc(4 * ne); acc(8 * ne); acc(8 * ne); acc(4 * (size_t)B * P.hcap); acc(8 * (size_t)B * P.pcap);
+    acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(sizeof(EdgeStat) * ne); acc(sizeof(EdgeLink) * ne);
+    acc(4 * (size_t)B * P.hcap); acc(8 * (size_t)B * P.pcap);
     acc(4 * nn); acc(4 * nn); acc((size_t)B * m->S);
     const int excap = cfg->selfplay ? 62 * ctx->n + 2 : 0;
     const size_t nx = (size_t)B * excap, no = cfg->selfplay ? (size_t)(cfg->out_cap > 0 ? cfg->out_cap : 4 * B) : 0;
@@ -1083,8 +1080,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.neb = carve<int32_t>(p, nn); P.nec = carve<int32_t>(p, nn); P.nns = carve<int32_t>(p, nn);
     P.nround = carve<int32_t>(p, nn); P.nqs = carve<double>(p, nn); P.nterm = carve<int8_t>(p, nn);
     P.nes = carve<float>(p, 4 * nn);
-    P.ea = carve<int16_t>(p, ne); P.ep = carve<float>(p, ne); P.en = carve<int32_t>(p, ne);
-    P.echild = carve<int32_t>(p, ne); P.eq = carve<double>(p, ne); P.ecr = carve<int2>(p, ne);
+    P.es = carve<EdgeStat>(p, ne); P.el = carve<EdgeLink>(p, ne);
     P.hslot = carve<int32_t>(p, (size_t)B * P.hcap);
     P.path = carve<int32_t>(p, 2 * (size_t)B * P.pcap);
     P.remap = carve<int32_t>(p, nn); P.remap_eb = carve<int32_t>(p, nn);
@@ -1115,7 +1111,7 @@ int spl_mcts_destroy(spl_mcts *m) {
 long long spl_mcts_device_bytes(const spl_mcts *m) {
     if (!m) return SPL_EINVAL;
     const size_t nn = (size_t)m->B * m->P.ncap, ne = (size_t)m->B * m->P.ecap;
-    return (long long)(nn * 57 + ne * 30 + (size_t)m->B * (4 * m->P.hcap + 8 * m->P.pcap + m->S + sizeof(TreeHdr)));
+    return (long long)(nn * 57 + ne * 32 + (size_t)m->B * (4 * m->P.hcap + 8 * m->P.pcap + m->S + sizeof(TreeHdr)));
 }
 
 int spl_mcts_set_roots(spl_mcts *m, const int8_t *roots, int keep_tree, int force_full, void *hs) {

@@ -28,6 +28,23 @@ struct TreeHdr {
 };
 enum { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2 };
 
+// Edge records, two 16-byte halves: what the UCB scan reads for every edge, and what is
+// read only for the chosen one (loaded in the same round trip).
+struct __align__(16) EdgeStat {
+    float p;       // prior Ps[a] (float32)
+    int32_t n;     // Nsa
+    double q;      // Qsa (Q_UNSET = the reference's -42 sentinel)
+};
+struct __align__(16) EdgeLink {
+    int16_t a;     // action
+    int16_t cec;   // cached child CSR count (-1: terminal child); valid when child >= 0
+    int32_t child; // child node (-1: not linked yet)
+    int32_t ceb;   // cached child CSR base
+    int32_t pad;
+};
+__device__ __forceinline__ int2 get_cr(const EdgeLink &e) { return make_int2(e.ceb, e.cec); }
+__device__ __forceinline__ void set_cr(EdgeLink &e, int eb, int ec) { e.ceb = eb; e.cec = (int16_t)ec; }
+
 // per-tree SoA pools; tree t owns [t*ncap, (t+1)*ncap) nodes, [t*ecap, ...) edges
 struct Pools {
     int ncap, ecap, hcap, pcap;          // nodes, edges, hash slots (pow2), path depth
@@ -37,11 +54,8 @@ struct Pools {
     double *nqs;
     int8_t *nterm;
     float *nes;                          // ncap x 4 terminal values
-    int16_t *ea;
-    float *ep;
-    int32_t *en, *echild;
-    int2 *ecr;                           // cached child record {eb, ec} (ec = -1: terminal child)
-    double *eq;
+    EdgeStat *es;                        // UCB inputs of every edge (one 16-byte load)
+    EdgeLink *el;                        // action, child and the child's cached CSR range
     int32_t *hslot;
     int32_t *path;                       // pcap x 2 (node, edge)
     int32_t *remap, *remap_eb;           // ncap scratch for compaction (new index, new CSR base)
