@@ -73,6 +73,13 @@ def nn_flops_per_eval(n):
     return 2 * macs
 
 
+def selfplay_config_name(args):
+    """BASELINE.json config the self-play arguments correspond to (per GPU)."""
+    if args.players == 4:
+        return "config5"
+    return "config4" if args.sims >= 1600 else "config3"
+
+
 def run_selfplay(args, rank, world, dev, dist):
     """BASELINE config 3 (config 4 per GPU at N>1): B concurrent self-play games, one MCTS
     simulation per game per iteration, leaves evaluated by SplendorNNet (fp32, random
@@ -173,8 +180,8 @@ def main():
                 "ms_per_step": r["elapsed"] / K * 1e3, "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "fp32 (network) / int8 (boards) / f64 (tree stats)",
                 "data": "synthetic (Philox-seeded deals), random-init SplendorNNet",
-                "config": {"workload": f"config3: batched self-play, numMCTSSims={args.sims}, genbu args, "
-                                       "SplendorNNet leaf eval, device move commit",
+                "config": {"workload": f"{selfplay_config_name(args)}: batched self-play, numMCTSSims={args.sims}, "
+                                       "genbu args, SplendorNNet leaf eval, device move commit",
                            "players": args.players, "games_per_gpu": B, "global_games": world * B,
                            "parallelism": f"dp{world} (game shards; RCCL all-gather of examples)"},
                 "roofline": {"bound": "mfma", "achieved": flops, "peak": 157.3, "unit": "TFLOP/s",
