@@ -1095,6 +1095,71 @@ __device__ __forceinline__ void wave_philox_uniforms(double *dst, uint64_t seed,
     __builtin_amdgcn_wave_barrier();
 }
 
+// ---- rollout deals keyed by game number (spl_rollout_run): the deal of board b's game g
+// (games counted from the initial deal = 0) takes uniforms 0..DEAL_DRAWS-1 of Philox stream
+// DEAL_STREAM | g, so it can be computed before the game that precedes it ends.
+constexpr uint32_t DEAL_STREAM = 0x80000000u;
+struct DealRec {                      // a dealt board in 72 bytes
+    uint64_t cnt[3], bits[3];         // deck rows after the 12 visible cards are drawn
+    uint64_t perm;                    // noble permutation (nibbles, partial Fisher-Yates)
+    uint8_t card[12];                 // visible cards, tier*40 + colour*8 + index
+    uint32_t pad;
+};
+// lane-per-board: the same draws as deal_tier / deal_nobles_bank, kept as a record
+template <int N>
+__device__ __forceinline__ void lane_deal_record(uint64_t seed, uint32_t board, uint32_t game, const Tabs &tab,
+                                                 DealRec &r) {
+    double u[DEAL_DRAWS + 1];
+#pragma unroll
+    for (int k = 0; k < (DEAL_DRAWS + 1) / 2; k++) philox_pair(seed, board, DEAL_STREAM | game, k, u[2 * k], u[2 * k + 1]);
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+        const uint64_t len = t == 0 ? 8 : (t == 1 ? 6 : 4);
+        uint64_t cnt = len * 0x0000000101010101ull;
+        uint64_t bits = (uint8_t)(0xFFu << (8 - len)) * 0x0000000101010101ull;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            int color, idx;
+            deck_pick(cnt, bits, u[8 * t + 2 * i], u[8 * t + 2 * i + 1], tab, color, idx);
+            deck_take(cnt, bits, color, idx);
+            r.card[4 * t + i] = (uint8_t)(t * 40 + color * 8 + idx);
+        }
+        r.cnt[t] = cnt;
+        r.bits[t] = bits;
+    }
+    uint64_t perm = 0x9876543210ull;
+#pragma unroll
+    for (int i = 0; i < Lay<N>::NN; i++) {
+        const int j = i + (int)floor(u[24 + i] * (double)(10 - i));
+        const uint64_t pi = (perm >> (4 * i)) & 15, pj = (perm >> (4 * j)) & 15;
+        perm &= ~((15ull << (4 * i)) | (15ull << (4 * j)));
+        perm |= (pj << (4 * i)) | (pi << (4 * j));
+    }
+    r.perm = perm;
+}
+// wave-collective: the board a record describes (every row written once; = wave_init_game)
+template <int N>
+__device__ __forceinline__ void wave_apply_deal(int8_t *s, const DealRec &r, const Tabs &tab) {
+    using Lx = Lay<N>;
+    const uint64_t g = N == 2 ? 4 : (N == 3 ? 5 : 7);
+    for (int i = lane_id(); i < Lx::ROWS; i += 64) {
+        uint64_t v = 0;
+        if (i == Lx::BANK) {
+            v = g * 0x0000000101010101ull | (5ull << 40);
+        } else if (i >= Lx::TIERS && i < Lx::TIERS + 24) {
+            const int k = i - Lx::TIERS;
+            v = tab.cards[r.card[4 * (k >> 3) + ((k & 7) >> 1)]][k & 1];
+        } else if (i >= Lx::DECKS && i < Lx::DECKS + 6) {
+            const int k = i - Lx::DECKS;
+            v = (k & 1) ? r.bits[k >> 1] : r.cnt[k >> 1];
+        } else if (i >= Lx::NOBLES && i < Lx::NOBLES + Lx::NN) {
+            v = K_NOBLE_ROWS[(r.perm >> (4 * (i - Lx::NOBLES))) & 15];
+        }
+        row(s, i) = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // wave-collective new game from DEAL_DRAWS uniforms u (LDS or HBM)
 template <int N>
 __device__ __forceinline__ void wave_init_game(int8_t *s, const double *u, const Tabs &tab = Tabs{}) {

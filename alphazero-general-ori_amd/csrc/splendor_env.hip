@@ -224,6 +224,8 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     __shared__ uint64_t pf0[WAVES][RB], pf1[RB];
     __shared__ uint32_t pcond[RB];
     __shared__ uint8_t pbad[WAVES][RB];
+    __shared__ DealRec drec[2][RB];     // deals of games gd0+1, gd0+2 of every board
+    __shared__ int32_t gd0[RB];
     const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
     int8_t *const gst = state + (size_t)b0 * Lx::S;
@@ -243,6 +245,17 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     if (tid < 4) kcount[tid] = 0;
     stage_tabs(tabs, tid, THREADS);
     for (int i = tid; i < 7 * 116; i += THREADS) mfac[i] = (&K_MASK_FACTORS[0][0])[i];
+    // the next two deals of every board, computed up front (lane per board and game, 32
+    // lanes of each wave) so that ending a game costs a row expansion, not the draws;
+    // a third game ending within the launch draws its deal on the spot (same keys)
+    const bool pre = K >= 16;
+    lds_sync();                                            // tables and gdone staged
+    if (tid < nb) gd0[tid] = gdone[tid];
+    if (pre && l < 32) {
+        const int r = w * 32 + l, k = r >> 6, b = r & (RB - 1);
+        if (b < nb) lane_deal_record<N>(seed, bbase + (uint32_t)(b0 + b), (uint32_t)(gdone[b] + 1 + k),
+                                        tabs.view(), drec[k][b]);
+    }
     // every barrier of the move loop orders LDS only: the per-move outputs are write-only
     // HBM streams, and waiting for their stores (__syncthreads) cost ~2K cycles a barrier
     lds_sync();
@@ -390,10 +403,18 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
 #endif
             for (uint64_t rm = __ballot(ended); rm; rm &= rm - 1) {
                 const int rb = __shfl(b, __ffsll((unsigned long long)rm) - 1);
-                wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)(b0 + rb), step, 3, DEAL_DRAWS);
-                RT_MARK(9)
-                wave_init_game<N>(lds + rb * ST, ub[w], tabs.view());
-                RT_MARK(8)
+                const int g = gdone[rb];                      // the new game's number
+                const int slot = g - gd0[rb] - 1;
+                if (pre && slot < 2) {
+                    wave_apply_deal<N>(lds + rb * ST, drec[slot][rb], tabs.view());
+                    RT_MARK(8)
+                } else {
+                    wave_philox_uniforms(ub[w], seed, bbase + (uint32_t)(b0 + rb), DEAL_STREAM | (uint32_t)g, 0,
+                                         DEAL_DRAWS);
+                    RT_MARK(9)
+                    wave_init_game<N>(lds + rb * ST, ub[w], tabs.view());
+                    RT_MARK(8)
+                }
             }
 #if ROLLOUT_TIMING
             if (l == 0) atomicAdd((unsigned long long *)&spl_probe_acc[20 + w], (unsigned long long)(clock64() - mv0));
@@ -633,7 +654,7 @@ int spl_symmetries(const spl_ctx *c, int E, const int8_t *state, const float *pi
 int spl_rollout_run(const spl_ctx *c, int B, int K, int8_t *state, int8_t *player, uint64_t *mask_out,
                     int16_t *action_out, float *ended_out, int32_t *games_done, uint64_t seed,
                     uint32_t step0, uint32_t board_base, void *hs) {
-    if (!ok_ctx(c) || B < 0 || K < 0 || (B && K && (!state || !player || !action_out || !ended_out)))
+    if (!ok_ctx(c) || B < 0 || K < 0 || (B && K && (!state || !player || !action_out || !ended_out || !games_done)))
         return SPL_EINVAL;
     if (!B || !K) return 0;
     SPL_DISPATCH(c->n, hipLaunchKernelGGL(k_rollout<N>, dim3((unsigned)((B + RB - 1) / RB)), dim3(THREADS), 0,

@@ -104,9 +104,11 @@ int spl_symmetries(const spl_ctx *ctx, int E, const int8_t *state, const float *
 /* One fused random-policy self-play step per board (BASELINE config 2; the move loop of
  * Coach.executeEpisode, Coach.py:71-100, with a uniform random policy):
  *   canonical -> valid mask -> action = k-th legal, k = floor(U(seed,b,step,0)*count)
- *   -> make_move(real board, player, chance draws 1,2) -> check_end -> if ended: re-init
- *   (draws 3..) and player=0, games_done[b] += 1.
- * Outputs mask (B x 7), action (B), ended (B x n), all per step. */
+ *   -> make_move(real board, player, chance draws 1,2) -> check_end -> if ended:
+ *   games_done[b] += 1 = g and re-init with the deal of game g: draws 0..28 of stream
+ *   0x80000000 | g (so deals can be drawn ahead of the game end; steps < 2^31), player=0.
+ * games_done is required (it keys the deals). Outputs mask (B x 7), action (B), ended
+ * (B x n), all per step. */
 int spl_rollout_step(const spl_ctx *ctx, int B, int8_t *state, int8_t *player,
                      uint64_t *mask_out, int16_t *action_out, float *ended_out,
                      int32_t *games_done, uint64_t seed, uint32_t step, uint32_t board_base,

@@ -826,6 +826,7 @@ long long or_rollout_run(int n, int B, int steps, uint64_t seed, uint32_t board_
     int S = 7 * or_rows(n);
     int8_t *st = (int8_t *)malloc((size_t)B * S), canon[7 * 88];
     int *pl = (int *)calloc((size_t)B, sizeof(int));
+    uint32_t *gm = (uint32_t *)calloc((size_t)B, sizeof(uint32_t));   /* games ended per board */
     uint8_t mask[409];
     double u[40];
     long long done = 0;
@@ -859,8 +860,9 @@ long long or_rollout_run(int n, int B, int steps, uint64_t seed, uint32_t board_
             for (int i = 0; i < n; i++) any |= e[i] != 0.f;
             if (actions) actions[(size_t)t * B + b] = (int16_t)a;
             if (ended) for (int i = 0; i < n; i++) ended[((size_t)t * B + b) * n + i] = e[i];
-            if (any) {
-                for (int d = 0; d < 29; d++) u[d] = or_uniform(seed, gb, (uint32_t)t, 3u + (uint32_t)d);
+            if (any) {   /* game g's deal: uniforms 0..28 of stream 0x80000000 | g */
+                gm[b] += 1;
+                for (int d = 0; d < 29; d++) u[d] = or_uniform(seed, gb, 0x80000000u | gm[b], (uint32_t)d);
                 or_init(n, s, u, NULL);
                 pl[b] = 0;
                 if (games) games[b] += 1;
@@ -870,7 +872,7 @@ long long or_rollout_run(int n, int B, int steps, uint64_t seed, uint32_t board_
     }
     if (state_out) memcpy(state_out, st, (size_t)B * S);
     if (player_out) for (int b = 0; b < B; b++) player_out[b] = (int8_t)pl[b];
-    free(st); free(pl);
+    free(st); free(pl); free(gm);
     return done;
 }
 

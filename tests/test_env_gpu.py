@@ -177,6 +177,36 @@ def test_rollout_run_matches_oracle(engines, n):
 
 
 @pytest.mark.parametrize("n", NS)
+def test_long_launch_deal_records_and_fallback(engines, n):
+    """One launch of 400 moves: games 1-2 of every board start from the deal records drawn
+    at launch start, later games from deals drawn on the spot — both keyed by game number,
+    so the result equals the oracle's loop."""
+    from splendor.env import RolloutBatch
+    B, T, seed = 256, {2: 400, 3: 800, 4: 1200}[n], 0x5EED + 11 * n
+    ref = O.rollout_run(n, B, T, seed)
+    rb = RolloutBatch(engines[n], B, seed=seed)
+    o = rb.run(T)
+    assert ref["games"].max() >= 3                    # some boards used the fallback path
+    np.testing.assert_array_equal(o["action"].cpu().numpy(), ref["action"])
+    np.testing.assert_array_equal(o["ended"].cpu().numpy(), ref["ended"])
+    np.testing.assert_array_equal(rb.state.cpu().numpy(), ref["state"])
+    np.testing.assert_array_equal(rb.games.cpu().numpy(), ref["games"])
+
+
+def test_rollout_requires_game_counters(engines):
+    from splendor import _lib
+    e = engines[2]
+    B = 64
+    st = e.new_state(B)
+    pl = torch.zeros(B, dtype=torch.int8, device="cuda")
+    mask = torch.zeros((B, 7), dtype=torch.int64, device="cuda")
+    act = torch.zeros(B, dtype=torch.int16, device="cuda")
+    end = torch.zeros((B, 2), dtype=torch.float32, device="cuda")
+    with pytest.raises(_lib.EngineError):
+        e.rollout_step(st, pl, mask, act, end, None, 1, 0)
+
+
+@pytest.mark.parametrize("n", NS)
 def test_rollout_masks_on_perturbed_boards(engines, n):
     """The fused kernel's lane-per-board mask (byte-SAD / lookup fast path and the exact
     path for boards with negative bytes) == the oracle's valid_moves, on golden states whose
@@ -201,7 +231,8 @@ def test_rollout_masks_on_perturbed_boards(engines, n):
     mask = torch.zeros((B, MASK_WORDS), dtype=torch.int64, device="cuda")
     act = torch.zeros(B, dtype=torch.int16, device="cuda")
     end = torch.zeros((B, n), dtype=torch.float32, device="cuda")
-    e.rollout_step(dst, dpl, mask, act, end, None, 0x5EED, 0)
+    games = torch.zeros(B, dtype=torch.int32, device="cuda")
+    e.rollout_step(dst, dpl, mask, act, end, games, 0x5EED, 0)
     np.testing.assert_array_equal(host_mask(mask), want)
 
 
