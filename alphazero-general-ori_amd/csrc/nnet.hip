@@ -255,6 +255,31 @@ __device__ __forceinline__ int acc_col() { return threadIdx.x & 31; }
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
+// wave reductions for the softmax: butterfly inside each 16-lane row on DPP (quad_perm
+// [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the four row results by readlane
+// (uniform result, no LDS round trips)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float rows_f32(float v, int k) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16 * k));
+}
+__device__ __forceinline__ float wave_max_f32(float v) {
+    v = fmaxf(v, dpp_f32<0xB1>(v));
+    v = fmaxf(v, dpp_f32<0x4E>(v));
+    v = fmaxf(v, dpp_f32<0x141>(v));
+    v = fmaxf(v, dpp_f32<0x140>(v));
+    return fmaxf(fmaxf(rows_f32(v, 0), rows_f32(v, 1)), fmaxf(rows_f32(v, 2), rows_f32(v, 3)));
+}
+__device__ __forceinline__ float wave_sum_f32(float v) {
+    v += dpp_f32<0xB1>(v);
+    v += dpp_f32<0x4E>(v);
+    v += dpp_f32<0x141>(v);
+    v += dpp_f32<0x140>(v);
+    return (rows_f32(v, 0) + rows_f32(v, 1)) + (rows_f32(v, 2) + rows_f32(v, 3));
+}
+
 template <int NP>
 // one workgroup per CU (LDS) = 2 waves per SIMD: the register budget is 256, and without
 // saying so the scheduler sinks the prefetched weight loads next to their MFMAs
@@ -267,6 +292,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ __align__(16) float bufA[7 * ML * XS];      // per-column activations / logits
     __shared__ __align__(16) float bufP[ML * PS];          // per-leaf ping
     __shared__ __align__(16) float bufQ[ML * PS];          // per-leaf pong
+    __shared__ uint64_t mskl[ML * 7];                      // legality masks (read at the softmax)
     // wave index in an SGPR: every per-wave choice below is a scalar branch
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, li = lane & 31;
     const int wc = w & 3, wg = w >> 2;                     // column block, wave group
@@ -285,11 +311,36 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     int8_t *x0 = reinterpret_cast<int8_t *>(bufA);
     for (int j = tid; j < 7 * ML * X0S / 4; j += NNT) reinterpret_cast<int32_t *>(x0)[j] = 0;
     lds_barrier();
-    for (int j = tid; j < nb * R; j += NNT) {              // one board row (7 bytes) per thread
-        const int i = j / R, r = j - i * R;
-        const int8_t *src = state + ((size_t)(b0 + i) * R + r) * 7;
+    if (tid < nb * 7) mskl[tid] = mask[(size_t)b0 * 7 + tid];
+    if constexpr ((7 * R) % 4 == 0) {
+        // the workgroup's boards are one contiguous block: dword loads, all in flight at
+        // once, then each byte scattered to its (column, leaf, row) slot
+        const int32_t *src = reinterpret_cast<const int32_t *>(state + (size_t)b0 * R * 7);
+        constexpr int PER = (ML * R * 7 / 4 + NNT - 1) / NNT;
+        int32_t d[PER];
 #pragma unroll
-        for (int c = 0; c < 7; c++) x0[(c * ML + i) * X0S + r] = src[c];
+        for (int k = 0; k < PER; k++) {
+            const int j = tid + k * NNT;
+            d[k] = j < nb * R * 7 / 4 ? src[j] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int j = tid + k * NNT;
+            if (j < nb * R * 7 / 4) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int o = 4 * j + q, i = o / (R * 7), rem = o - i * (R * 7), r = rem / 7, c = rem - 7 * r;
+                    x0[(c * ML + i) * X0S + r] = (int8_t)(d[k] >> (8 * q));
+                }
+            }
+        }
+    } else {
+        for (int j = tid; j < nb * R; j += NNT) {          // one board row (7 bytes) per thread
+            const int i = j / R, r = j - i * R;
+            const int8_t *src = state + ((size_t)(b0 + i) * R + r) * 7;
+#pragma unroll
+            for (int c = 0; c < 7; c++) x0[(c * ML + i) * X0S + r] = src[c];
+        }
     }
     lds_barrier();
 
@@ -526,7 +577,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int q = 0; q < PERW; q++) {
             const int i = w * PERW + q;
-            const uint64_t *mk = mask + (size_t)(b0 + min(i, nb - 1)) * 7;
+            const uint64_t *mk = mskl + min(i, nb - 1) * 7;
             m[q] = -3.0e38f;
 #pragma unroll
             for (int k = 0; k < 7; k++) {
@@ -537,9 +588,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             }
         }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-            for (int q = 0; q < PERW; q++) m[q] = fmaxf(m[q], __shfl_xor(m[q], o, 64));
+        for (int q = 0; q < PERW; q++) m[q] = wave_max_f32(m[q]);
 #pragma unroll
         for (int q = 0; q < PERW; q++) {
             sum[q] = 0.f;
@@ -550,9 +599,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             }
         }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-            for (int q = 0; q < PERW; q++) sum[q] += __shfl_xor(sum[q], o, 64);
+        for (int q = 0; q < PERW; q++) sum[q] = wave_sum_f32(sum[q]);
 #pragma unroll
         for (int q = 0; q < PERW; q++) {
             const int i = w * PERW + q;
