@@ -37,9 +37,7 @@ def bytes_per_board_launch(n, moves):
     return 2 * S + 2 + 8 + moves * (56 + 2 + 4 * n)
 
 
-def cpu_baseline(n, seed, target_s=10.0):
-    """Time the oracle (scalar C port of the reference rules, oracle/) on one host core on
-    a bounded sample of the same workload (same boards, same Philox draws)."""
+def _oracle_lib():
     path = os.path.join(ROOT, "oracle", "liboracle.so")
     if not os.path.exists(path):
         import subprocess
@@ -47,17 +45,102 @@ def cpu_baseline(n, seed, target_s=10.0):
     L = ctypes.CDLL(path)
     L.or_random_rollouts.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int]
     L.or_random_rollouts.restype = ctypes.c_longlong
+    return L
+
+
+def host_threads():
+    """Host cores this process may use (the GPU box grants a 16-core share of a larger
+    machine; os.cpu_count() reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(n, seed, target_s=5.0):
+    """Time the oracle (scalar C port of the reference rules, oracle/) on a bounded sample of
+    the same workload (same boards, same Philox draws): one host core (the reference's
+    Numba path is single-threaded) and every granted core (boards split across threads).
+    `value` is the all-core rate."""
+    L = _oracle_lib()
     B = 32768
-    t = time.perf_counter()
-    L.or_random_rollouts(n, B, 4, seed, 1)
-    probe = time.perf_counter() - t
-    steps = max(4, int(target_s / max(probe / 4, 1e-6)))
-    t = time.perf_counter()
-    done = L.or_random_rollouts(n, B, steps, seed, 1)
-    dt = time.perf_counter() - t
-    return {"value": done / dt, "unit": "rollouts/s", "cores": 1, "kind": "port",
-            "sample": f"{B} boards x {steps} steps (incl. initial deal) on 1 host core, "
-                      f"{dt:.1f} s, oracle/splendor_oracle.c or_random_rollouts"}
+
+    def timed(threads):
+        t = time.perf_counter()
+        L.or_random_rollouts(n, B, 2, seed, threads)
+        probe = time.perf_counter() - t
+        steps = max(2, int(target_s / max(probe / 2, 1e-6)))
+        t = time.perf_counter()
+        done = L.or_random_rollouts(n, B, steps, seed, threads)
+        return done, steps, time.perf_counter() - t
+
+    d1, s1, t1 = timed(1)
+    T = host_threads()
+    dT, sT, tT = timed(T)
+    return {"value": dT / tT, "unit": "rollouts/s", "cores": T, "kind": "port",
+            "sample": f"{B} boards x {sT} steps (incl. initial deal) on {T} host threads, {tT:.1f} s, "
+                      f"oracle/splendor_oracle.c or_random_rollouts",
+            "single_core": {"value": d1 / t1, "cores": 1,
+                            "sample": f"{B} boards x {s1} steps on 1 host core, {t1:.1f} s"}}
+
+
+def cpu_baseline_selfplay(n, seed, args, target_s=4.0):
+    """CPU reference point for config 3 (rollouts = MCTS simulations), one core: the
+    oracle's sequential search + self-play loop (hash-prior network, genbu search args)
+    timed directly, and one SplendorNNet forward at batch 1 on the CPU (PyTorch fp32, as
+    GenericNNetWrapper.predict does per leaf) timed separately; the estimate charges one
+    network call per simulation."""
+    L = _oracle_lib()
+    p8, pf = ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(ctypes.c_float)
+    L.or_selfplay_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                  ctypes.c_int, ctypes.c_int, p8, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
+                                  p8, pf, ctypes.POINTER(ctypes.c_uint64), pf, ctypes.POINTER(ctypes.c_int32), pf,
+                                  ctypes.POINTER(ctypes.c_int32)]
+    L.or_selfplay_run.restype = ctypes.c_int
+    import numpy as np
+    R = 32 + 10 * n + n * n
+    g = dict(GENBU_ARGS, numMCTSSims=args.sims)
+    B = 16
+
+    def run(iters):
+        board = np.zeros((B, R, 7), np.int8)
+        hdr = np.zeros((B, 8), np.int32)
+        t = time.perf_counter()
+        L.or_selfplay_run(n, B, iters, seed, 0, g["numMCTSSims"], g["ratio_fullMCTS"], g["prob_fullMCTS"],
+                          g["cpuct"], g["fpu"], int(g["forced_playouts"]), g["tempThreshold"],
+                          board.ctypes.data_as(p8), hdr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 0,
+                          None, None, None, None, None, None, None)
+        return time.perf_counter() - t
+
+    probe = run(20)
+    iters = max(20, int(20 * target_s / max(probe, 1e-6)))
+    dt = run(iters)
+    tree_rate = B * iters / dt
+    from splendor.nnet import random_net
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        net = random_net(n, seed=0, device="cpu")
+        x = torch.zeros((1, R, 7))
+        va = torch.ones((1, 409), dtype=torch.bool)
+        with torch.no_grad():
+            for _ in range(20):
+                net(x, va)
+            k = 300
+            t = time.perf_counter()
+            for _ in range(k):
+                net(x, va)
+            t_nn = (time.perf_counter() - t) / k
+    finally:
+        torch.set_num_threads(nthreads)
+    return {"value": 1.0 / (1.0 / tree_rate + t_nn), "unit": "rollouts/s (MCTS simulations)", "cores": 1,
+            "kind": "port",
+            "sample": f"oracle self-play {B} games x {iters} simulations ({dt:.1f} s, hash-prior network: "
+                      f"{tree_rate:.0f} sims/s search alone) + SplendorNNet batch-1 CPU forward "
+                      f"{t_nn * 1e6:.0f} us per leaf (PyTorch fp32, 1 thread); value = 1/(1/search + network)",
+            "search_only": tree_rate, "network_us_per_leaf": t_nn * 1e6}
 
 
 # saved args of the reference's only checkpoint, genbu.pt (SURVEY.md §0.7), = BASELINE config 3
@@ -251,6 +334,8 @@ def main():
                      "network_tflops": flops, "network_frac_fp32_peak": flops / 157.3,
                      **r["stats"], "examples_drained": r["examples"], "allgather_s": r["gather_s"],
                      "tree_device_bytes": r["device_bytes"]}
+        if rank == 0 and not args.no_cpu_baseline and world == 1:
+            secondary["cpu_baseline"] = cpu_baseline_selfplay(args.players, args.seed, args)
 
     if rank == 0:
         per = bytes_per_board_launch(args.players, chunk)

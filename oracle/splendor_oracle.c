@@ -11,6 +11,7 @@
 #include "splendor_oracle.h"
 #include <math.h>
 #include <stdlib.h>
+#include <pthread.h>
 #include <string.h>
 
 /* ------------------------------------------------------------------ game tables
@@ -876,7 +877,30 @@ long long or_rollout_run(int n, int B, int steps, uint64_t seed, uint32_t board_
     return done;
 }
 
+/* boards are independent and every draw is keyed by the global board id, so contiguous
+ * board ranges run on separate threads give exactly the single-thread result */
+typedef struct { int n, B, steps; uint64_t seed; uint32_t base; long long done; } rr_job;
+static void *rr_thread(void *p) {
+    rr_job *j = (rr_job *)p;
+    j->done = or_rollout_run(j->n, j->B, j->steps, j->seed, j->base, NULL, NULL, NULL, NULL, NULL, NULL);
+    return NULL;
+}
 long long or_random_rollouts(int n, int B, int steps, uint64_t seed, int threads) {
-    (void)threads;
-    return or_rollout_run(n, B, steps, seed, 0, NULL, NULL, NULL, NULL, NULL, NULL);
+    if (threads <= 1 || B < 2)
+        return or_rollout_run(n, B, steps, seed, 0, NULL, NULL, NULL, NULL, NULL, NULL);
+    if (threads > B) threads = B;
+    build_tables();                              /* shared tables, built before the threads */
+    pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    rr_job *jobs = (rr_job *)malloc(sizeof(rr_job) * (size_t)threads);
+    int start = 0;
+    for (int k = 0; k < threads; k++) {
+        const int cnt = B / threads + (k < B % threads);
+        jobs[k] = (rr_job){n, cnt, steps, seed, (uint32_t)start, 0};
+        start += cnt;
+        pthread_create(&tid[k], NULL, rr_thread, &jobs[k]);
+    }
+    long long done = 0;
+    for (int k = 0; k < threads; k++) { pthread_join(tid[k], NULL); done += jobs[k].done; }
+    free(tid); free(jobs);
+    return done;
 }
