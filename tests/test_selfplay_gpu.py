@@ -140,3 +140,37 @@ def test_train_on_device_examples():
     c2 = Coach(g, nn, args, batch=16, seed=3)          # evaluator packs the trained weights
     c2.run_iterations(4)
     assert c2.sp.stats()["overflow"] == 0
+
+
+def test_full_size_selfplay_invariants():
+    """BASELINE config 3 size (32,768 games, genbu args, SplendorNNet leaves): after every
+    iteration batch, each tree's root visit counts cover its finished simulations, every
+    visited Q lies in [-1, 1] (unvisited = the reference's -42), and moves get committed."""
+    from splendor.env import SplendorEngine
+    from splendor.nnet import LeafEvaluator, random_net
+    from splendor.selfplay import SelfPlay
+    B = 32768
+    args = dict(numMCTSSims=100, cpuct=2.5, fpu=0.3, prob_fullMCTS=0.25, ratio_fullMCTS=5,
+                forced_playouts=False, dirichletAlpha=0.3, temperature=[1.25, 0.8], tempThreshold=10)
+    e = SplendorEngine(2)
+    sp = SelfPlay(e, B, args, evaluator=LeafEvaluator(e, random_net(2, seed=0), B, use_graph=False),
+                  dirichlet_noise=True, seed=17)
+    sp.reset()
+    for rep in range(3):
+        for _ in range(40):
+            sp.step(use_graph=True)
+        torch.cuda.synchronize()
+        h = sp.headers()
+        assert (h["overflow"] == 0).all()
+        counts, qsa, _, _ = sp.root_stats()
+        sims = torch.from_numpy(h["sims_done"].astype(np.int64)).cuda()
+        has_root = torch.from_numpy(h["root"] >= 0).cuda()
+        # every simulation of the current search passes one root edge (except the root's own
+        # expansion when the root is new); a kept root also carries its earlier visits
+        tot = counts.sum(1)
+        assert bool((tot[has_root] >= sims[has_root] - 1).all()), rep
+        visited = counts > 0
+        assert bool(((qsa[visited] >= -1.0) & (qsa[visited] <= 1.0)).all())
+        assert bool((qsa[~visited] == -42.0).all())
+    st = sp.stats()
+    assert st["moves"] > B                              # moves were committed on every tree
