@@ -226,8 +226,8 @@ def load_traffic(path, B, moves):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--boards", type=int, default=32768, help="boards per GPU")
     ap.add_argument("--players", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0x5EED)
