@@ -98,3 +98,21 @@ def gather_examples(examples, group=None):
         dist.all_gather(parts, pad, group=group)
         out[key] = torch.cat([p[:s] for p, s in zip(parts, sizes)])
     return out
+
+
+def broadcast_network(net, src=0, group=None):
+    """Weights of rank `src` to every rank (one broadcast of the
+    SplendorNNet parameters and BatchNorm statistics, repeated only when the network
+    changes), flattened into one buffer so it is a single collective."""
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return net
+    tensors = [t for t in net.state_dict().values() if t.is_floating_point()]
+    flat = torch.cat([t.detach().reshape(-1).float() for t in tensors])
+    dist.broadcast(flat, src=src, group=group)
+    off = 0
+    with torch.no_grad():
+        for t in tensors:
+            t.copy_(flat[off:off + t.numel()].view_as(t).to(t.dtype))
+            off += t.numel()
+    return net

@@ -169,11 +169,14 @@ def run_selfplay(args, rank, world, dev, dist):
     init: the reference's genbu.pt cannot be loaded safely), moves committed on device."""
     from splendor.env import SplendorEngine
     from splendor.nnet import LeafEvaluator, random_net
-    from splendor.selfplay import SelfPlay, gather_examples
+    from splendor.selfplay import SelfPlay, broadcast_network, gather_examples
     B = args.boards
     eng = SplendorEngine(args.players, device=dev)
     sargs = dict(GENBU_ARGS, numMCTSSims=args.sims)
-    ev = LeafEvaluator(eng, random_net(args.players, seed=0, device=dev), B, use_graph=False)
+    net = random_net(args.players, seed=rank, device=dev)
+    if dist:
+        broadcast_network(net)                 # every rank searches with rank 0's network
+    ev = LeafEvaluator(eng, net, B, use_graph=False)
     sp = SelfPlay(eng, B, sargs, evaluator=ev, dirichlet_noise=True, seed=args.seed, board_base=rank * B)
     sp.reset()
     for _ in range(args.warmup):

@@ -1,6 +1,8 @@
 """Multi-rank paths on CPU with the gloo backend (world size 2): board sharding by global
-id is invariant to the number of ranks, and the episode-end example all-gather
-(splendor.selfplay.gather_examples) concatenates every rank's examples in rank order."""
+id is invariant to the number of ranks, the episode-end example all-gather
+(splendor.selfplay.gather_examples) concatenates every rank's examples in rank order, and
+the network broadcast (splendor.selfplay.broadcast_network) leaves every rank with rank
+0's weights."""
 import os
 import socket
 
@@ -37,8 +39,27 @@ def _worker(rank, world, port, B, T, q):
           "pi": torch.arange(k * 409, dtype=torch.float32).reshape(k, 409) + 1000 * rank,
           "winner": torch.full((k, 2), float(rank))}
     got = gather_examples(ex)
+    # 3) network broadcast: differently seeded nets end up equal to rank 0's
+    from splendor.nnet import SplendorNNet
+    from splendor.selfplay import broadcast_network
+    torch.manual_seed(100 + rank)
+    net = SplendorNNet(2)
+    for m in net.modules():
+        if isinstance(m, torch.nn.BatchNorm1d):
+            m.running_mean.fill_(0.1 * (rank + 1))
+    broadcast_network(net)
+    flat = torch.cat([t.reshape(-1).float() for t in net.state_dict().values()])
+    nets = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(nets, flat)
+    torch.manual_seed(100)
+    ref = SplendorNNet(2)
+    for m in ref.modules():
+        if isinstance(m, torch.nn.BatchNorm1d):
+            m.running_mean.fill_(0.1)
+    ref_flat = torch.cat([t.reshape(-1).float() for t in ref.state_dict().values()])
     if rank == 0:
-        q.put((torch.cat(parts).numpy(), {kk: v.numpy() for kk, v in got.items()}))
+        q.put((torch.cat(parts).numpy(), {kk: v.numpy() for kk, v in got.items()},
+               [x.numpy() for x in nets], ref_flat.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -51,7 +72,7 @@ def test_two_rank_sharding_and_example_allgather():
     procs = [ctx.Process(target=_worker, args=(r, world, port, B, T, q)) for r in range(world)]
     for p in procs:
         p.start()
-    states, ex = q.get(timeout=240)
+    states, ex, nets, ref_net = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -63,3 +84,5 @@ def test_two_rank_sharding_and_example_allgather():
     assert ex["board"].shape[0] == 3 + 5
     assert (ex["board"][:3] == 0).all() and (ex["board"][3:] == 1).all()
     np.testing.assert_array_equal(ex["pi"][3:], np.arange(5 * 409, dtype=np.float32).reshape(5, 409) + 1000)
+    np.testing.assert_array_equal(nets[0], ref_net)
+    np.testing.assert_array_equal(nets[1], ref_net)
