@@ -376,6 +376,10 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                     default: nxt = make_move<N, MK_BUY_RESERVED>(s, a, pl[b], false, ch); break;
                 }
                 RT_MARK(6)
+#if ROLLOUT_TIMING
+                // per wave: move pipeline up to make_move's end (slots 28+w, lane 0's board)
+                if (l == 0) atomicAdd((unsigned long long *)&spl_probe_acc[28 + w], (unsigned long long)(clock64() - mv0));
+#endif
                 float e[N];
                 check_end<N>(s, e);
 #pragma unroll
@@ -393,12 +397,8 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
             }
             RT_MARK(2)
 #if ROLLOUT_TIMING
-            {   // per wave: move pipeline up to the deals (24+w), games it ended (28+w)
-                const int ne = __popcll(__ballot(ended));
-                if (l == 0) {
-                    atomicAdd((unsigned long long *)&spl_probe_acc[24 + w], (unsigned long long)(clock64() - mv0));
-                    atomicAdd((unsigned long long *)&spl_probe_acc[28 + w], (unsigned long long)ne);
-                }
+            {   // per wave: move pipeline up to the deals (24+w)
+                if (l == 0) atomicAdd((unsigned long long *)&spl_probe_acc[24 + w], (unsigned long long)(clock64() - mv0));
             }
 #endif
             for (uint64_t rm = __ballot(ended); rm; rm &= rm - 1) {
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         for (int k = 0; k < 24; k++) o[k] = spl_probe_acc[k];
         o[24] = wall0;
         o[25] = wall_clock64();
-        for (int k = 24; k < 30; k++) o[k + 2] = spl_probe_acc[k];   // o[26..29] pre-deal, o[30..31] deals w0-1
+        for (int k = 24; k < 30; k++) o[k + 2] = spl_probe_acc[k];   // o[26..29] pre-deal, o[30..31] make_move done w0-1
     }
 #endif
 }

@@ -63,11 +63,11 @@ int main() {
             for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 32 + 26 + k];
             printf(" %.0f", x / (NB * (double)K));
         }
-        printf("\n  games ended per WG-move by the gems / buy wave:");
+        printf("\n  make_move done (gems / buy wave, lane 0 when it has a board), cycles/move:");
         for (int k = 0; k < 2; k++) {
             double x = 0;
             for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 32 + 30 + k];
-            printf(" %.3f", x / (NB * (double)K));
+            printf(" %.0f", x / (NB * (double)K));
         }
         printf("\n");
     }
