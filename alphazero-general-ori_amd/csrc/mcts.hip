@@ -630,7 +630,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         spl_probe_last = clock64();
     }
 #endif
-    const MaskLane ml = MaskLane::load();                // constant-table operands of the leaf mask
     int8_t *s = lds[w];
     wave_load_board<N>(s, P.root_state + (size_t)t * Lx::S);
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
@@ -721,12 +720,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
     }
     __builtin_amdgcn_wave_barrier();
     SPL_PROBE(5)
-    if (kind == LEAF_NN) {
+    if (kind == LEAF_NN)                                     // its mask: k_leaf_mask
         wave_store_board<N>(leaf_state + (size_t)t * Lx::S, s);
-        uint64_t m[7];
-        wave_valid_moves<N>(s, 0, lim, m, ml);               // MCTS.py:136
-        store_mask(leaf_mask + (size_t)t * 7, m);
-    }
     SPL_PROBE(6)
     if (l == 0) {
         H->depth = depth;
@@ -744,6 +739,90 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         atomicAdd(&g_select_timing[21], 1ull);
     }
 #endif
+}
+
+// ------------------------------------------------------------ leaf masks
+// getValidMoves(leaf, 0) (MCTS.py:136) for every NN leaf of a select, lane per leaf, 64
+// leaves per workgroup: the rollout kernel's factorised predicate and mask-word phases
+// (splendor_device.h lane_predicates_part / lane_mask_word_fast, exact path for boards
+// outside the fast domain), then the pass bit iff nothing else is legal (:263). Replaces
+// the wave-per-board mask of the descent kernel (its lanes are idle for it anyway).
+template <int N>
+__global__ __launch_bounds__(256) void k_leaf_mask(int B, int lim, const int8_t *__restrict__ leaf_state,
+                                                   const uint8_t *__restrict__ leaf_valid,
+                                                   uint64_t *__restrict__ leaf_mask) {
+    using Lx = Lay<N>;
+    using Cv = Conv<N>;
+    constexpr int RB = 64, ST = (Lx::ROWS % 2 ? Lx::ROWS : Lx::ROWS + 1) * 8;
+    __shared__ __align__(16) int8_t lds[RB * ST];
+    __shared__ uint64_t mfac[7 * 116];
+    __shared__ uint64_t pf0[4][RB], pf1[RB];
+    __shared__ uint32_t pcond[RB];
+    __shared__ uint8_t pbad[4][RB];
+    __shared__ uint64_t msk[RB][7];
+    const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
+    const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
+    for (int i = tid; i < nb * Cv::UNITS; i += 256) {
+        const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
+        Cv::load(lds + b * ST, leaf_state + (size_t)(b0 + b) * Lx::S, u);
+    }
+    for (int i = tid; i < 7 * 116; i += 256) mfac[i] = (&K_MASK_FACTORS[0][0])[i];
+    lds_sync();
+    if (l < nb) {                                        // predicates: part w of every leaf
+        uint64_t f0, f1;
+        uint32_t cc;
+        bool bad;
+        const int8_t *st = lds + l * ST;
+        switch (w) {
+            case 0: lane_predicates_part<N, 0>(st, 0, lim, f0, f1, cc, bad); break;
+            case 1: lane_predicates_part<N, 1>(st, 0, lim, f0, f1, cc, bad); break;
+            case 2: lane_predicates_part<N, 2>(st, 0, lim, f0, f1, cc, bad); break;
+            default: lane_predicates_part<N, 3>(st, 0, lim, f0, f1, cc, bad); break;
+        }
+        pf0[w][l] = f0;
+        if (w == 3) pf1[l] = f1;
+        if (w == 2) pcond[l] = cc;
+        pbad[w][l] = bad;
+    }
+    lds_sync();
+    if (l < nb) {                                        // mask words w and w+4
+        const bool bad = pbad[0][l] | pbad[1][l] | pbad[2][l] | pbad[3][l];
+        if (bad) {
+            const LanePred Pr = lane_predicates_exact<N>(lds + l * ST, 0, lim);
+            if (w == 0) { msk[l][0] = lane_mask_word<0>(Pr); msk[l][4] = lane_mask_word<4>(Pr); }
+            else if (w == 1) { msk[l][1] = lane_mask_word<1>(Pr); msk[l][5] = lane_mask_word<5>(Pr); }
+            else if (w == 2) { msk[l][2] = lane_mask_word<2>(Pr); msk[l][6] = lane_mask_word<6>(Pr); }
+            else { msk[l][3] = lane_mask_word<3>(Pr); }
+        } else {
+            const uint64_t F0 = pf0[0][l] | pf0[1][l] | pf0[2][l];
+            const uint32_t Cd = pcond[l], lv = (uint32_t)pf1[l];
+            if (w == 0) {
+                msk[l][0] = lane_mask_word_fast<0>(Cd, F0, lv, mfac);
+                msk[l][4] = lane_mask_word_fast<4>(Cd, F0, lv, mfac);
+            } else if (w == 1) {
+                msk[l][1] = lane_mask_word_fast<1>(Cd, F0, lv, mfac);
+                msk[l][5] = lane_mask_word_fast<5>(Cd, F0, lv, mfac);
+            } else if (w == 2) {
+                msk[l][2] = lane_mask_word_fast<2>(Cd, F0, lv, mfac);
+                msk[l][6] = lane_mask_word_fast<6>(Cd, F0, lv, mfac);
+            } else {
+                msk[l][3] = lane_mask_word_fast<3>(Cd, F0, lv, mfac);
+            }
+        }
+    }
+    lds_sync();
+    {                                                    // pass bit, lane l < 16 of wave w
+        const int b = 16 * w + l;
+        if (l < 16 && b < nb) {
+            int cnt = 0;
+#pragma unroll
+            for (int k = 0; k < 7; k++) cnt += __popcll(msk[b][k]);
+            if (!cnt) msk[b][6] |= 1ull << (408 - 384);
+        }
+    }
+    lds_sync();
+    for (int i = tid; i < nb * 7; i += 256)
+        if (leaf_valid[b0 + i / 7]) leaf_mask[(size_t)b0 * 7 + i] = (&msk[0][0])[i];
 }
 
 // ------------------------------------------------------------ expand + backup
@@ -1141,6 +1220,9 @@ int spl_mcts_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select<N>, wave_grid(m->B), dim3(THREADS), 0,
                                           (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
                                           leaf_state, leaf_mask, leaf_valid));
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_leaf_mask<N>, dim3((unsigned)((m->B + 63) / 64)), dim3(256), 0,
+                                          (hipStream_t)hs, m->B, m->token_limit, leaf_state, leaf_valid,
+                                          leaf_mask));
     return check_launch();
 }
 
