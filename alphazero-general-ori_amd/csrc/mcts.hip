@@ -864,6 +864,20 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const int depth = H->depth;
     const int32_t *path = P.path + (size_t)t * P.pcap * 2;
+    // this simulation's path (lane per level) and the statistics its backup updates are
+    // requested before the expansion, so their round trips overlap it (the expansion never
+    // touches them: the new node is not on its own path)
+    int pnode = 0, pge = 0, pcnt = 0, pns = 0;
+    double pq = 0.0, pqs = 0.0;
+    if (l < depth) {
+        pnode = path[2 * l];
+        pge = path[2 * l + 1];
+        const EdgeStat st = P.es[e0 + pge];
+        pcnt = st.n;
+        pq = st.q;
+        pns = P.nns[nb + pnode];
+        pqs = P.nqs[nb + pnode];
+    }
     float val[4] = {0, 0, 0, 0};
     if (kind == LEAF_NN) {
         const uint64_t *m = leaf_mask + (size_t)t * 7;
@@ -926,11 +940,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
     for (int d = l; d < depth; d += 64) {
         const int rot = (depth - d) % N;
         const double v0 = (double)val[(N - rot) % N];
-        const int node = path[2 * d], ge = path[2 * d + 1];
-        const int cnt = P.es[e0 + ge].n;
-        P.es[e0 + ge].q = ((double)cnt * P.es[e0 + ge].q + v0) / (double)(cnt + 1);
-        const int ns = P.nns[nb + node];
-        P.nqs[nb + node] = ((double)(ns + 1) * P.nqs[nb + node] + v0) / (double)(ns + 2);
+        int node = pnode, ge = pge, cnt = pcnt, ns = pns;
+        double q = pq, qs = pqs;
+        if (d >= 64) {                                   // levels beyond the prefetched 64
+            node = path[2 * d]; ge = path[2 * d + 1];
+            cnt = P.es[e0 + ge].n; q = P.es[e0 + ge].q;
+            ns = P.nns[nb + node]; qs = P.nqs[nb + node];
+        }
+        P.es[e0 + ge].q = ((double)cnt * q + v0) / (double)(cnt + 1);
+        P.nqs[nb + node] = ((double)(ns + 1) * qs + v0) / (double)(ns + 2);
         P.es[e0 + ge].n = cnt + 1;
         P.nns[nb + node] = ns + 1;
     }
