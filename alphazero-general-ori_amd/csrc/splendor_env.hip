@@ -435,11 +435,11 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     __syncthreads();
     RT_MARK(4)
     if (threadIdx.x == 0) {
-        uint64_t *o = g_rollout_timing + (size_t)blockIdx.x * 32;
+        uint64_t *o = g_rollout_timing + (size_t)blockIdx.x * 40;   // tools/time_rollout.hip row
         for (int k = 0; k < 24; k++) o[k] = spl_probe_acc[k];
         o[24] = wall0;
         o[25] = wall_clock64();
-        for (int k = 24; k < 30; k++) o[k + 2] = spl_probe_acc[k];   // o[26..29] pre-deal, o[30..31] make_move done w0-1
+        for (int k = 24; k < 32; k++) o[k + 2] = spl_probe_acc[k];   // o[26..29] pre-deal, o[30..33] make_move done
     }
 #endif
 }

@@ -12,13 +12,13 @@ int main() {
     int8_t *st, *pl; uint64_t *mk; int16_t *ac; float *en; int32_t *gd; uint64_t *tm;
     (void)hipMalloc(&st, (size_t)B * 392); (void)hipMalloc(&pl, B); (void)hipMalloc(&mk, (size_t)K * B * 56);
     (void)hipMalloc(&ac, (size_t)K * 2 * B); (void)hipMalloc(&en, (size_t)K * 8 * B); (void)hipMalloc(&gd, 4 * B);
-    (void)hipMalloc(&tm, (size_t)NB * 32 * 8);
+    (void)hipMalloc(&tm, (size_t)NB * 40 * 8);
     (void)hipMemset(gd, 0, 4 * B);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rollout_timing), &tm, sizeof(tm));
     spl_init(c, B, st, pl, nullptr, 0, 0x5EED, 0xFFFFFFFFu, 0, nullptr);
     for (int k = 0; k < 5; k++) spl_rollout_run(c, B, K, st, pl, mk, ac, en, gd, 0x5EED, K * k, 0, nullptr);
     (void)hipDeviceSynchronize();
-    std::vector<uint64_t> h((size_t)NB * 32);
+    std::vector<uint64_t> h((size_t)NB * 40);
     // probe slots (splendor_env.hip / splendor_device.h SPL_PROBE)
     // (thread 0 = lane 0 of wave 0: its move-phase slots see the gem-move pipeline)
     const int slots[] = {0, 16, 17, 1, 5, 6, 7, 2, 9, 8, 3, 4};
@@ -34,7 +34,7 @@ int main() {
         uint64_t w0 = ~0ull, w1 = 0;
         std::vector<double> ph[NS], life;
         for (int b = 0; b < NB; b++) {
-            const uint64_t *r = &h[(size_t)b * 32];
+            const uint64_t *r = &h[(size_t)b * 40];
             w0 = std::min(w0, r[24]); w1 = std::max(w1, r[25]);
             for (int k = 0; k < NS; k++) ph[k].push_back((double)r[slots[k]] / (per_move[k] ? K : 1));
             life.push_back((double)(r[25] - r[24]) / 100.0);
@@ -48,25 +48,25 @@ int main() {
         std::sort(life.begin(), life.end());
         printf("  block life us p10 %.2f p50 %.2f p90 %.2f max %.2f\n", life[NB / 10], life[NB / 2], life[NB * 9 / 10], life[NB - 1]);
         double xw = 0, xl = 0;
-        for (int b = 0; b < NB; b++) { xw += (double)h[(size_t)b * 32 + 18]; xl += (double)h[(size_t)b * 32 + 19]; }
+        for (int b = 0; b < NB; b++) { xw += (double)h[(size_t)b * 40 + 18]; xl += (double)h[(size_t)b * 40 + 19]; }
         printf("  exact-path waves per wave-move %.4f, lanes per board-move %.5f\n", xw / (NB * 4.0 * K), xl / (NB * 64.0 * K));
         printf("  move phase per wave (gems / buy / reserve / buy reserved), cycles/move:");
         for (int k = 0; k < 4; k++) {
             double x = 0;
-            for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 32 + 20 + k];
+            for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 40 + 20 + k];
             printf(" %.0f", x / (NB * (double)K));
         }
         printf("\n");
         printf("  move pipeline before deals per wave, cycles/move:");
         for (int k = 0; k < 4; k++) {
             double x = 0;
-            for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 32 + 26 + k];
+            for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 40 + 26 + k];
             printf(" %.0f", x / (NB * (double)K));
         }
-        printf("\n  make_move done (gems / buy wave, lane 0 when it has a board), cycles/move:");
-        for (int k = 0; k < 2; k++) {
+        printf("\n  make_move done per wave (lane 0 when it has a board; summed over moves / K):");
+        for (int k = 0; k < 4; k++) {
             double x = 0;
-            for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 32 + 30 + k];
+            for (int b = 0; b < NB; b++) x += (double)h[(size_t)b * 40 + 30 + k];
             printf(" %.0f", x / (NB * (double)K));
         }
         printf("\n");
