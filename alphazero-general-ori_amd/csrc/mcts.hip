@@ -222,7 +222,11 @@ __device__ __forceinline__ void apply_root_noise(const Pools &P, const SearchCfg
 // this root or any later one — an exact subset of the reference's table (which only
 // evicts rounds < R-5, MCTS.py:80-85). Compacts nodes + CSR edges in place, remaps child
 // links, rebuilds the hash table. Wave-collective; returns the root's new index.
-__device__ int compact_tree(const Pools &P, int t, int root, int root_round) {
+// scr: optional LDS scratch of 2 * (ncap + 1) ints for this wave (ncap <= SCR_NODES): the
+// edges then move in batches of 256 new positions (each lane finds its edge's owner by a
+// binary search over the kept nodes' new bases) instead of one kept node at a time.
+constexpr int SCR_NODES = 512;
+__device__ int compact_tree(const Pools &P, int t, int root, int root_round, int *scr = nullptr) {
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
@@ -292,7 +296,9 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round) {
             P.nqs[nb + ni] = qs; P.nterm[nb + ni] = term;
 #pragma unroll
             for (int j = 0; j < 4; j++) P.nes[(nb + ni) * 4 + j] = es[j];
+            if (scr) { scr[ni] = neb; scr[SCR_NODES + 1 + ni] = oeb; }
         }
+        if (scr) { edges += total; continue; }              // edges move in batches below
         // move each kept node's edge block down (increasing order: never overlaps unread data)
         for (int j = 0; j < 64; j++) {
             const int jn = __shfl(ni, j, 64);
@@ -321,6 +327,58 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round) {
         }
         edges += total;
     }
+    if (scr) {
+        // new position k of batch [k0, k0 + 256) comes from old position oeb(j) + k - neb(j),
+        // j = the kept node whose new range holds k. Every old position is >= its new one
+        // and batches run in increasing k with all reads before the writes, so no write
+        // reaches an edge that is still to be read.
+        if (l == 0) scr[kept] = edges;
+        __builtin_amdgcn_wave_barrier();
+        constexpr int R = 4;
+        for (int k0 = 0; k0 < edges; k0 += 64 * R) {
+            EdgeStat st[R];
+            EdgeLink lk[R];
+            int nch[R], ceb[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int k = k0 + 64 * r + l;
+                nch[r] = -1; ceb[r] = 0;
+                if (k < edges) {
+                    int lo = 0, hi = kept - 1;                 // last j with scr[j] <= k
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (scr[mid] <= k) lo = mid; else hi = mid - 1;
+                    }
+                    const int src = scr[SCR_NODES + 1 + lo] + (k - scr[lo]);
+                    st[r] = P.es[e0 + src];
+                    lk[r] = P.el[e0 + src];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int k = k0 + 64 * r + l;
+                if (k < edges && lk[r].child >= 0) {
+                    nch[r] = remap[lk[r].child];
+                    ceb[r] = remap_eb[lk[r].child];
+                }
+            }
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int k = k0 + 64 * r + l;
+                if (k < edges) {
+                    EdgeLink o = lk[r];
+                    o.child = nch[r];
+                    if (nch[r] >= 0) o.ceb = ceb[r];
+                    P.es[e0 + k] = st[r];
+                    P.el[e0 + k] = o;
+                }
+            }
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
     // rebuild the transposition table
     int32_t *hs = P.hslot + (size_t)t * P.hcap;
     for (int i = l; i < P.hcap; i += 64) hs[i] = -1;
@@ -345,7 +403,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round) {
 // empty; draw the full/fast search decision (ST_FULL) and arm root noise. Wave-collective.
 template <int N>
 __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const int8_t *s, bool keep,
-                             bool force_full) {
+                             bool force_full, int *scr = nullptr) {
     using Lx = Lay<N>;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
@@ -355,7 +413,7 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         uint64_t k0, k1;
         wave_fingerprint<N>(s, k0, k1);
         root = hash_lookup(P, t, k0, k1);
-        root = compact_tree(P, t, root, (uint8_t)bt(row(s, 0), 6));
+        root = compact_tree(P, t, root, (uint8_t)bt(row(s, 0), 6), P.ncap <= SCR_NODES ? scr : nullptr);
     } else {
         int32_t *hs = P.hslot + (size_t)t * P.hcap;
         for (int i = l; i < P.hcap; i += 64) hs[i] = -1;
@@ -389,6 +447,7 @@ __global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int
                                                        int force_full) {
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
+    __shared__ int cscr[WAVES][2 * (SCR_NODES + 1)];     // compaction scratch
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     if (active && !active[t]) {
@@ -400,7 +459,7 @@ __global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int
     }
     int8_t *s = lds[w];
     wave_load_board<N>(s, roots + (size_t)t * Lx::S);
-    begin_search<N>(P, C, t, s, keep != 0, force_full != 0);
+    begin_search<N>(P, C, t, s, keep != 0, force_full != 0, cscr[w]);
 }
 
 // ------------------------------------------------------------ self-play
@@ -451,6 +510,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][2][Lx::LS];
     __shared__ double ub[WAVES][DEAL_DRAWS];
+    __shared__ int cscr[WAVES][2 * (SCR_NODES + 1)];     // compaction scratch
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
@@ -577,7 +637,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     __builtin_amdgcn_wave_barrier();
     wave_store_board<N>(P.board + (size_t)t * Lx::S, b);
     wave_roll_players<N>(s, b, nxt);                            // getCanonicalForm (:73)
-    begin_search<N>(P, C, t, s, !ended, false);
+    begin_search<N>(P, C, t, s, !ended, false, cscr[w]);
 }
 
 __global__ void k_drain_copy(Pools P, int S, int max, int8_t *st, float *pi, uint64_t *valid,
