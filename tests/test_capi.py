@@ -80,3 +80,26 @@ def test_mcts_config_struct_layout(tmp_path):
     assert ctypes.sizeof(M) == size
     assert M.seed.offset == off_seed and M.node_cap.offset == off_cap and M.dirichlet_temp.offset == off_temp
     assert M.out_cap.offset == off_out
+
+
+def test_search_and_arena_entry_points_reject_bad_arguments():
+    """Null handles / buffers and out-of-range streams are rejected before any launch
+    (no device needed)."""
+    lib = ctypes.CDLL(LIB)
+    vp = ctypes.c_void_p
+    lib.spl_mcts_set_roots_active.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]
+    lib.spl_mcts_pick_best.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
+    lib.spl_mcts_select.argtypes = [vp] * 5
+    lib.spl_rollout_run.argtypes = [vp, ctypes.c_int, ctypes.c_int] + [vp] * 6 + [ctypes.c_uint64, ctypes.c_uint32,
+                                                                               ctypes.c_uint32, vp]
+    assert lib.spl_mcts_set_roots_active(None, None, None, 1, 1, None) == -1
+    assert lib.spl_mcts_pick_best(None, None, 0, 0, None, None) == -1
+    assert lib.spl_mcts_select(None, None, None, None, None) == -1
+    h = ctypes.c_void_p()
+    assert lib.spl_ctx_create(2, 10, ctypes.byref(h)) == 0
+    # rollouts need the per-board game counters (they key the deals)
+    dummy = ctypes.c_void_p(1)
+    assert lib.spl_rollout_run(h, 4, 1, dummy, dummy, None, dummy, dummy, None, 0, 0, 0, None) == -1
+    assert lib.spl_rollout_run(h, 0, 1, None, None, None, None, None, None, 0, 0, 0, None) == 0
+    lib.spl_ctx_destroy.argtypes = [vp]
+    lib.spl_ctx_destroy(h)
