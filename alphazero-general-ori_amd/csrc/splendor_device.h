@@ -841,9 +841,6 @@ __device__ __forceinline__ int move_kind_of(int a) {
     return a < 12 ? MK_BUY : (a < 27 ? MK_RESERVE : (a < 30 ? MK_BUY_RESERVED :
                                                      (a >= 290 && a < 365 ? MK_RESERVE : MK_GEMS)));
 }
-__device__ __forceinline__ int move_kind(int a, const int8_t *act_rsv) {
-    return a < 12 ? MK_BUY : (a >= 27 && a < 30 ? MK_BUY_RESERVED : (act_rsv[a] >= 0 ? MK_RESERVE : MK_GEMS));
-}
 
 // make_move for a visible-card buy (KIND == MK_BUY) with every row it touches read up front
 // and kept in registers: the same stages and results as the fixed pipeline below (_buy_card
