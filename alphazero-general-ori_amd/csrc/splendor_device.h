@@ -832,7 +832,7 @@ __device__ __forceinline__ void buy_card(int8_t *s, int cost_row, int p) {
 // Actions 405..408 are a no-op + round increment (the reference's select-noble stub does
 // not parse and pass reads give_ids3 out of bounds; DESIGN.md "Defined deviations").
 // Returns the next player.
-// KIND (move_kind) >= 0 specialises the pipeline to one kind of move when the caller knows
+// KIND (move_kind_of) >= 0 specialises the pipeline to one kind of move when the caller knows
 // it: the stages that kind never uses are compiled out.
 enum { MK_GEMS = 0, MK_BUY = 1, MK_RESERVE = 2, MK_BUY_RESERVED = 3 };
 // same classification without the table: the reserve actions are 12-26 (visible / deck)
