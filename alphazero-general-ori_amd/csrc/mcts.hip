@@ -727,7 +727,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             int2 cr = make_int2(uniform(pk.cr.x), uniform(pk.cr.y));
             SPL_PROBE(2)
             Chance ch{nullptr, 0, 0, 0, 0};
-            const int nxt = make_move<N>(s, pk.a, 0, true, ch);   // MCTS.py:227-235
+            int nxt;                                         // MCTS.py:227-235, per kind
+            switch (move_kind_of(pk.a)) {                    // (uniform: a scalar branch)
+                case MK_GEMS: nxt = make_move<N, MK_GEMS>(s, pk.a, 0, true, ch); break;
+                case MK_BUY: nxt = make_move<N, MK_BUY>(s, pk.a, 0, true, ch); break;
+                case MK_RESERVE: nxt = make_move<N, MK_RESERVE>(s, pk.a, 0, true, ch); break;
+                default: nxt = make_move<N, MK_BUY_RESERVED>(s, pk.a, 0, true, ch); break;
+            }
             __builtin_amdgcn_wave_barrier();
             if (nxt) wave_roll_players<N>(s, s, nxt);
             SPL_PROBE(3)
