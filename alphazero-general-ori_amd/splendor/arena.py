@@ -1,5 +1,12 @@
-"""Batched Arena gate: Arena.playGames (Arena.py:175-227) for many games at once on the
-device MCTS, as Coach.learn uses it to accept or reject a new network (Coach.py:150-159).
+"""Arena (Arena.py:15-227) on the engine, in two forms.
+
+`Arena(player1, player2, player3, game, args)` keeps the reference's constructor and
+playGame / playGames: one game at a time through the Game API with arbitrary player
+callables (board -> action), as pit.py and Coach.learn use it.
+
+`BatchedArena(game, nnet1, nnet2, args, batch=B)` is the batched gate: playGames for many
+games at once on the device MCTS, as Coach.learn uses it to accept or reject a new network
+(Coach.py:150-159).
 
 Reference semantics kept:
 * two players, each an MCTS over its own network with a search tree that persists through
@@ -43,7 +50,7 @@ def one_vs_two(i):
     return (i % 4 == 0) or (i % 4 == 3)
 
 
-class Arena:
+class BatchedArena:
     def __init__(self, game, nnet1, nnet2, args, batch=None, seed=0x5EED, game_base=0,
                  evaluators=None, check_valid=True):
         self.game, self.args = game, args
@@ -139,6 +146,53 @@ class Arena:
         two = int(np.sum(np.where(ovt, r0 == -1.0, r0 == 1.0)))
         self.last = last
         return one, two, int(len(r0) - one - two)
+
+
+class Arena:
+    """The reference's sequential Arena (Arena.py:15-227) over the engine-backed Game API:
+    player callables take a canonical board and return an action; the tqdm progress bar,
+    colours, board records and handicap statistics are console features left out."""
+
+    def __init__(self, player1, player2, player3, game, args=None, display=None, no_record=True):
+        self.player1, self.player2, self.player3 = player1, player2, player3
+        self.game, self.display = game, display
+
+    def playGame(self, verbose=False, other_way=False, cur_player=None, board=None):
+        """Arena.playGame (:66-173): (player 0's result, score of player 0, of player 1)."""
+        g = self.game
+        if not other_way:
+            players = [self.player1, self.player2] if self.player3 is None else \
+                [self.player1, self.player2, self.player3]
+        else:
+            players = [self.player2] + [self.player1] * (g.getNumberOfPlayers() - 1)
+        if cur_player is None:
+            cur, board = 0, g.getInitBoard()
+        else:
+            cur = cur_player
+        while not g.getGameEnded(board, cur).any():
+            canonical = g.getCanonicalForm(board, cur)
+            action = players[cur](canonical)
+            valids = g.getValidMoves(canonical, 0)
+            if valids[action] == 0:                          # Arena.py:158-159
+                raise AssertionError(f"player {cur} chose an invalid action {action}")
+            board, cur = g.getNextState(board, cur, action)
+        from .search import MCTS
+        MCTS.reset_all_search_trees()
+        return g.getGameEnded(board, cur)[0], g.getScore(board, 0), g.getScore(board, 1)
+
+    def playGames(self, num, verbose=False, cur_player=None, board=None):
+        """Arena.playGames (:175-227): player1 moves first in games i % 4 in (0, 3)."""
+        one, two, draws = 0, 0, 0
+        for i in range(num):
+            ovt = one_vs_two(i)
+            r, _, _ = self.playGame(verbose=verbose, other_way=not ovt, cur_player=cur_player)
+            if r == (1. if ovt else -1.):
+                one += 1
+            elif r == (-1. if ovt else 1.):
+                two += 1
+            else:
+                draws += 1
+        return one, two, draws
 
 
 def accept_new_network(nwins, pwins, update_threshold):

@@ -50,12 +50,12 @@ def oracle_arena(n, G, sims, cpuct, fpu, seed):
 @pytest.mark.parametrize("n,G,sims", [(2, 12, 6), (4, 6, 4)])
 def test_arena_matches_oracle(n, G, sims):
     from splendor.SplendorGame import SplendorGame
-    from splendor.arena import Arena, one_vs_two
+    from splendor.arena import BatchedArena, one_vs_two
     from splendor.mcts import HashEvaluator
     seed, cpuct, fpu = 21, 1.5, 0.1
     g = SplendorGame(n)
     args = dict(numMCTSSims=sims, cpuct=cpuct, fpu=fpu, arenaCompare=G)
-    ar = Arena(g, None, None, args, batch=G, seed=seed,
+    ar = BatchedArena(g, None, None, args, batch=G, seed=seed,
                evaluators=(HashEvaluator(g.engine), HashEvaluator(g.engine)))
     one, two, draws = ar.playGames(G)
     ref = oracle_arena(n, G, sims, cpuct, fpu, seed)
@@ -75,16 +75,33 @@ def test_arena_batches_and_gate():
     """Games split over several batches give the same per-game records as one batch with
     the same game ids; the Coach.learn acceptance rule."""
     from splendor.SplendorGame import SplendorGame
-    from splendor.arena import Arena, accept_new_network
+    from splendor.arena import BatchedArena, accept_new_network
     from splendor.mcts import HashEvaluator
     g = SplendorGame(2)
     args = dict(numMCTSSims=4, cpuct=1.0, fpu=0.0)
     ev = (HashEvaluator(g.engine), HashEvaluator(g.engine))
-    a = Arena(g, None, None, args, batch=8, seed=5, evaluators=ev)
+    a = BatchedArena(g, None, None, args, batch=8, seed=5, evaluators=ev)
     a.playGames(8)
-    b = Arena(g, None, None, args, batch=3, seed=5, evaluators=ev)
+    b = BatchedArena(g, None, None, args, batch=3, seed=5, evaluators=ev)
     b.playGames(8)
     for k in ("result", "plies", "score", "one_vs_two", "game"):
         np.testing.assert_array_equal(a.last[k], b.last[k], err_msg=k)
     assert accept_new_network(6, 4, 0.55) and not accept_new_network(5, 5, 0.55)
     assert not accept_new_network(0, 0, 0.55)
+
+
+def test_reference_arena_with_player_callables():
+    """Arena(player1, player2, None, game, args).playGames with plain callables (the pit.py
+    form): first-legal vs last-legal players; every game ends, counts add up, and game i is
+    the same game as a direct Game-API loop with the seats of Arena.py:200-203."""
+    from splendor.SplendorGame import SplendorGame
+    from splendor.arena import Arena, one_vs_two
+    g = SplendorGame(2)
+    first = lambda b: int(np.flatnonzero(g.getValidMoves(b, 0))[0])      # noqa: E731
+    last = lambda b: int(np.flatnonzero(g.getValidMoves(b, 0))[-1])      # noqa: E731
+    ar = Arena(first, last, None, g, None)
+    results = [ar.playGame(other_way=not one_vs_two(i))[0] for i in range(4)]
+    one, two, draws = Arena(first, last, None, g, None).playGames(4)
+    assert one + two + draws == 4
+    exp_one = sum(1 for i, r in enumerate(results) if r == (1. if one_vs_two(i) else -1.))
+    assert one == exp_one
