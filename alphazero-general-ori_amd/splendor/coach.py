@@ -6,13 +6,15 @@ recorded position with getSymmetries (Coach.py:77-80, device kernel spl_symmetri
 returns the reference's example records (board, pi, winner, scdiff, valids, surprise)
 (Coach.py:91-98). `executeEpisode()` is the one-game form. `executeIteration(k)` returns
 the same examples as a columnar `ExampleSet` and appends it to `trainExamplesHistory`
-(an `ExampleHistory`, saved as .npz by `saveTrainExamples`, Coach.py:167-190). Training
-(`learn`) is out of scope.
+(an `ExampleHistory`, saved as .npz by `saveTrainExamples`, Coach.py:167-190). `learn()`
+is Coach.learn (Coach.py:102-164): self-play iterations, training on the example history,
+the new-vs-previous BatchedArena gate and checkpoints.
 """
 import numpy as np
 import torch
 
 from .env import unpack_mask
+from .arena import BatchedArena, accept_new_network
 from .examples import ExampleHistory, ExampleSet
 from .search import evaluator_for
 from .selfplay import SelfPlay, gather_examples
@@ -43,6 +45,7 @@ class Coach:
         self.game, self.nnet, self.args = game, nnet, args
         B = int(batch or _arg(args, "numEps", 1))
         self.B = B
+        self.seed = seed
         self.sp = SelfPlay(game.engine, B, args, evaluator=evaluator_for(game.engine, nnet, B),
                            dirichlet_noise=float(_arg(args, "dirichletAlpha", 0.0)) > 0, seed=seed,
                            board_base=board_base)
@@ -55,12 +58,13 @@ class Coach:
 
     def executeEpisodes(self, num_games, with_symmetries=True, as_tuples=True, gather=False):
         collected, done = [], 0
+        start = self.sp.stats()["games_done"]
         while done < num_games:
             self.run_iterations(32)
             ex = self.sp.drain()
             if ex["board"].shape[0]:
                 collected.append(ex)
-            done = self.sp.stats()["games_done"]
+            done = self.sp.stats()["games_done"] - start
         ex = {k: torch.cat([c[k] for c in collected]) for k in collected[0]} if collected else self.sp.drain()
         if gather:
             ex = gather_examples(ex)
@@ -94,3 +98,45 @@ class Coach:
         """Coach.loadTrainExamples (:175-190): read checkpoint.examples.npz."""
         self.trainExamplesHistory = ExampleHistory.load(folder, _arg(self.args, "numItersHistory"),
                                                         device=self.game.engine.device)
+
+    def refresh_network(self):
+        """Re-pack the leaf evaluator after the network's weights changed (the fused kernel
+        reads a packed copy)."""
+        self.sp.evaluator = evaluator_for(self.game.engine, self.nnet, self.B)
+
+    def learn(self, pnet=None, log=None):
+        """Coach.learn (Coach.py:102-164): for numIters iterations, numEps self-play games
+        (fresh games and trees, as the reference's executeEpisode + reset_all_search_trees),
+        the example history saved, the network trained on it, then pitted against the
+        previous weights over arenaCompare games (BatchedArena, temp 0, full searches) and
+        kept iff it wins >= updateThreshold of the decisive games; checkpoints as
+        checkpoint_<i>.pt / best.pt / temp.pt in args.checkpoint. Returns per-iteration
+        (nwins, pwins, draws, accepted)."""
+        from .NNet import NNetWrapper
+        folder = _arg(self.args, "checkpoint", "checkpoint")
+        pnet = pnet or NNetWrapper(self.game, dict(self.nnet.args), device=self.nnet.device)
+        history = []
+        for i in range(1, int(_arg(self.args, "numIters", 1)) + 1):
+            if not _arg(self.args, "skipFirstSelfPlay", False) or i > 1:
+                self.sp.reset()
+                self.executeIteration(int(_arg(self.args, "numEps", self.B)))
+            self.saveTrainExamples(folder)
+            self.nnet.save_checkpoint(folder=folder, filename="temp.pt")
+            pnet.load_checkpoint(folder=folder, filename="temp.pt")
+            self.nnet.train(self.trainExamplesHistory.merged())
+            games = int(_arg(self.args, "arenaCompare", 2))
+            arena = BatchedArena(self.game, self.nnet, pnet, self.args, batch=min(games, self.B),
+                                 seed=self.seed + i)
+            nwins, pwins, draws = arena.playGames(games)
+            ok = accept_new_network(nwins, pwins, float(_arg(self.args, "updateThreshold", 0.55)))
+            if ok:
+                self.nnet.save_checkpoint(folder=folder, filename=f"checkpoint_{i}.pt")
+                self.nnet.save_checkpoint(folder=folder, filename="best.pt")
+            else:
+                self.nnet.load_checkpoint(folder=folder, filename="temp.pt")
+            self.refresh_network()
+            history.append((nwins, pwins, draws, ok))
+            if log:
+                log(f"iter {i}: new vs previous {nwins}-{pwins} ({draws} draws) -> "
+                    f"{'ACCEPTED' if ok else 'REJECTED'}")
+        return history

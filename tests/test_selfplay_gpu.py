@@ -174,3 +174,27 @@ def test_full_size_selfplay_invariants():
         assert bool((qsa[~visited] == -42.0).all())
     st = sp.stats()
     assert st["moves"] > B                              # moves were committed on every tree
+
+
+def test_coach_learn_iteration(tmp_path):
+    """Coach.learn (Coach.py:102-164) end to end on the engine, tiny: self-play games,
+    example history file, one training pass, the BatchedArena gate and checkpoints."""
+    import os
+    from splendor.NNet import NNetWrapper
+    from splendor.SplendorGame import SplendorGame
+    from splendor.coach import Coach
+    g = SplendorGame(2)
+    nn = NNetWrapper(g, dict(epochs=1, batch_size=32))
+    args = dict(numMCTSSims=6, cpuct=2.5, fpu=0.3, prob_fullMCTS=1.0, ratio_fullMCTS=3,
+                forced_playouts=False, dirichletAlpha=0.3, temperature=[1.25, 0.8], tempThreshold=10,
+                numIters=1, numEps=4, numItersHistory=2, arenaCompare=4, updateThreshold=0.55,
+                checkpoint=str(tmp_path))
+    c = Coach(g, nn, args, batch=32, seed=4)
+    hist = c.learn()
+    assert len(hist) == 1
+    nwins, pwins, draws, ok = hist[0]
+    assert nwins + pwins + draws == 4
+    files = set(os.listdir(tmp_path))
+    assert {"temp.pt", "checkpoint.examples.npz"} <= files
+    assert ("best.pt" in files) == ok
+    assert len(c.trainExamplesHistory.iters) == 1 and len(c.trainExamplesHistory) > 0
