@@ -906,10 +906,65 @@ __device__ __forceinline__ int make_move_buy(int8_t *s, int a, int p, bool det, 
     return (p + 1) % N;
 }
 
+// make_move for a reserve (KIND == MK_RESERVE) in the same register-resident form: the
+// player's reserve slots, the reserved visible card, the tier's deck, gems and bank read in
+// one LDS round trip, then the same stages as the fixed pipeline below (_reserve
+// :517-536: first free slot, visible card or a deck draw, the gold, the action's take /
+// give-back vectors, round +1), all writes at the end (every row written is distinct).
+template <int N>
+__device__ __forceinline__ int make_move_reserve(int8_t *s, int a, int p, bool det, Chance &ch) {
+    using Lx = Lay<N>;
+    const int rsv = (int)ch.tab.act_rsv[a];
+    const uint64_t take = ch.tab.act_take[a], give = ch.tab.act_give[a];
+    const bool vis = rsv < 12;
+    const int tier = vis ? rsv >> 2 : rsv - 12, R = Lx::RSV + 6 * p;
+    const int vr = Lx::TIERS + 2 * (vis ? rsv : 0);
+    const uint64_t c0 = row(s, R), c1 = row(s, R + 2), c2 = row(s, R + 4);
+    const uint64_t vcost = row(s, vr), vgain = row(s, vr + 1);
+    uint64_t cnt = row(s, Lx::DECKS + 2 * tier), bits = row(s, Lx::DECKS + 2 * tier + 1);
+    uint64_t gems = row(s, Lx::GEMS + p), bank = row(s, Lx::BANK);
+    const int slot = sum5(c0) == 0 ? R : (sum5(c1) == 0 ? R + 2 : (sum5(c2) == 0 ? R + 4 : -1));
+    const bool draw = !det && sum5(cnt) != 0;
+    uint64_t cost = 0, gain = 0;
+    if (draw) {
+        const double u0 = ch.draw(), u1 = ch.draw();
+        int color, idx;
+        deck_pick(cnt, bits, u0, u1, ch.tab, color, idx);
+        deck_take(cnt, bits, color, idx);
+        cost = ch.tab.cards[tier * 40 + color * 8 + idx][0];
+        gain = ch.tab.cards[tier * 40 + color * 8 + idx][1];
+    }
+    if (bt(bank, 5) > 0) {
+        gems = with_bt(gems, 5, bt(gems, 5) + 1);
+        bank = with_bt(bank, 5, bt(bank, 5) - 1);
+    }
+    gems = bytes_sub(bytes_add(gems, take), give);
+    bank = bytes_add(bytes_sub(bank, take), give);
+    if (vis) {
+        if (slot >= 0) {
+            row(s, slot) = vcost;
+            row(s, slot + 1) = vgain;
+        }
+        row(s, vr) = cost;
+        row(s, vr + 1) = gain;
+    } else if (draw && slot >= 0) {
+        row(s, slot) = cost;
+        row(s, slot + 1) = gain;
+    }
+    if (draw) {
+        row(s, Lx::DECKS + 2 * tier + 1) = bits;
+        row(s, Lx::DECKS + 2 * tier) = cnt;
+    }
+    row(s, Lx::GEMS + p) = gems;
+    row(s, Lx::BANK) = with_bt(bank, 6, bt(bank, 6) + 1);
+    return (p + 1) % N;
+}
+
 template <int N, int KIND = -1>
 __device__ __forceinline__ int make_move(int8_t *s, int a, int p, bool det, Chance &ch) {
     using Lx = Lay<N>;
     if constexpr (KIND == MK_BUY) return make_move_buy<N>(s, a, p, det, ch);
+    if constexpr (KIND == MK_RESERVE) return make_move_reserve<N>(s, a, p, det, ch);
     constexpr bool ANY = KIND < 0;
     const int rsv = ANY || KIND == MK_RESERVE ? (int)ch.tab.act_rsv[a] : -1;
     const bool vec = ANY || KIND == MK_GEMS || KIND == MK_RESERVE;
@@ -1024,6 +1079,18 @@ __device__ __forceinline__ void check_end_rows(const V &rows, float out[N]) {
 }
 template <int N>
 __device__ __forceinline__ void check_end(const int8_t *lds, float out[N]) { check_end_rows<N>(LdsRows{lds}, out); }
+
+// check_end with the round counter after the move given (r, uint8: the caller read it
+// before the move), so the common no-end case reads no row the move wrote
+template <int N>
+__device__ __forceinline__ void check_end_round(const int8_t *lds, int r, float out[N]) {
+    if (r % N != 0) {
+#pragma unroll
+        for (int i = 0; i < N; i++) out[i] = 0.f;
+        return;
+    }
+    check_end<N>(lds, out);
+}
 template <int N>
 __device__ __forceinline__ int get_score(const int8_t *lds, int p) { return score_rows<N>(LdsRows{lds}, p); }
 

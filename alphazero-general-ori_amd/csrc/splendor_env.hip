@@ -367,6 +367,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                 b = klist[w][l];
                 const int a = act[b];
                 int8_t *s = lds + b * ST;
+                const int r = (uint8_t)(bt(row(s, Lx::BANK), 6) + 1);   // the round after the move
                 Chance ch{&ud[b][0], 0, 0, 0, 1, 0.0, false, tabs.view()};
                 int nxt;
                 switch (w) {
@@ -381,7 +382,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                 if (l == 0) atomicAdd((unsigned long long *)&spl_probe_acc[28 + w], (unsigned long long)(clock64() - mv0));
 #endif
                 float e[N];
-                check_end<N>(s, e);
+                check_end_round<N>(s, r, e);
 #pragma unroll
                 for (int i = 0; i < N; i++) {
                     ended |= e[i] != 0.f;
