@@ -193,6 +193,11 @@ __global__ __launch_bounds__(THREADS) void k_tree_step(int B, const int8_t *__re
 #endif
 constexpr int RB = ROLLOUT_RB;   // boards per workgroup (<= 64: lane per board)
 #define RT_MARK(k) SPL_PROBE(k)
+// v of lane I of this lane's quad (DPP quad_perm broadcast; every lane must be active)
+template <int I>
+__device__ __forceinline__ int quad_bcast(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, I | I << 2 | I << 4 | I << 6, 0xF, 0xF, false);
+}
 template <int N>
 struct RolloutLds {
     static constexpr int STRIDE = (Lay<N>::ROWS % 2 ? Lay<N>::ROWS : Lay<N>::ROWS + 1) * 8;
@@ -210,6 +215,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     using Cv = Conv<N>;
     constexpr int ST = RolloutLds<N>::STRIDE;
     constexpr int PER = RB / WAVES;
+    static_assert(PER * 4 == 64, "select: four lanes per board, one wave per PER boards");
     __shared__ __align__(16) int8_t lds[RB * ST];
     __shared__ uint64_t msk[RB][7];    // legality masks (odd qword stride: conflict-free)
     __shared__ int8_t pl[RB];
@@ -327,21 +333,40 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         }
         lds_sync();
         RT_MARK(1)
-        // select: lane l < 16 of wave w: pass bit (:263), uniform pick, filed by move kind
+        // select: four lanes per board (board w*16 + l/4; lane q = l%4 holds mask words 2q,
+        // 2q+1): quad-wide counts by DPP, then the lane whose words hold the drawn index
+        // finds its bit, so no lane walks all seven words. Pass bit (:263) when nothing is
+        // legal; the board is filed by move kind.
         {
-            const int b = w * PER + l;
-            if (ROLLOUT_ABLATE != 2 && l < PER && b < nb) {
-                int a;
+            const int b = w * PER + (l >> 2), q = l & 3;
+            const bool on = ROLLOUT_ABLATE != 2 && b < nb;
+            uint64_t x0 = 0, x1 = 0;
+            if (on) {
+                x0 = msk[b][2 * q];
+                if (q < 3) x1 = msk[b][2 * q + 1];
+            }
+            const int c0 = __popcll(x0), c = c0 + __popcll(x1);
+            const int k0 = quad_bcast<0>(c), k1 = quad_bcast<1>(c), k2 = quad_bcast<2>(c), k3 = quad_bcast<3>(c);
+            const int cnt = k0 + k1 + k2 + k3;
+            const int pre = (q > 0 ? k0 : 0) + (q > 1 ? k1 : 0) + (q > 2 ? k2 : 0);
+            int a = -1;
+            if (on) {
                 if (ROLLOUT_ABLATE == 1) {
-                    a = 30 + (int)((step + b) % 5);
+                    if (q == 0) a = 30 + (int)((step + b) % 5);
+                } else if (cnt == 0) {
+                    if (q == 3) {
+                        a = 408;
+                        msk[b][6] = x0 | 1ull << (408 - 384);
+                    }
                 } else {
-                    uint64_t m[7];
-                    int cnt = 0;
-#pragma unroll
-                    for (int k = 0; k < 7; k++) { m[k] = msk[b][k]; cnt += __popcll(m[k]); }
-                    if (!cnt) { m[6] |= 1ull << (408 - 384); msk[b][6] = m[6]; cnt = 1; }
-                    a = select_bit(m, (int)(ud[b][0] * (double)cnt));
+                    const int r = (int)(ud[b][0] * (double)cnt) - pre;
+                    if (r >= 0 && r < c) {
+                        const bool hi = r >= c0;
+                        a = 128 * q + (hi ? 64 : 0) + kth_bit64(hi ? x1 : x0, hi ? r - c0 : r);
+                    }
                 }
+            }
+            if (a >= 0) {
                 act[b] = (int16_t)a;
                 const int kind = move_kind_of(a);
                 klist[kind][atomicAdd(&kcount[kind], 1)] = (uint8_t)b;
