@@ -224,8 +224,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     __shared__ double ub[WAVES][DEAL_DRAWS];
     __shared__ TabsLds tabs;
     __shared__ uint64_t mfac[7 * 116];  // K_MASK_FACTORS (lane_mask_word_fast)
-    __shared__ int16_t act[RB];
-    __shared__ uint8_t klist[4][RB];
+    __shared__ uint32_t klist[4][RB];  // per move kind: board | action << 8 | player << 20
     __shared__ int kcount[4];
     __shared__ uint64_t pf0[WAVES][RB], pf1[RB];
     __shared__ uint32_t pcond[RB];
@@ -367,9 +366,8 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                 }
             }
             if (a >= 0) {
-                act[b] = (int16_t)a;
                 const int kind = move_kind_of(a);
-                klist[kind][atomicAdd(&kcount[kind], 1)] = (uint8_t)b;
+                klist[kind][atomicAdd(&kcount[kind], 1)] = (uint32_t)b | (uint32_t)a << 8 | (uint32_t)pl[b] << 20;
             }
         }
         lds_sync();
@@ -388,18 +386,20 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         {
             int b = 0;
             bool ended = false;
-            if (ROLLOUT_ABLATE != 2 && l < kcount[w]) {
-                b = klist[w][l];
-                const int a = act[b];
+            const int kc = kcount[w];
+            const uint32_t ke = klist[w][l];                 // (read before the count is known)
+            if (ROLLOUT_ABLATE != 2 && l < kc) {
+                b = ke & 0xFF;
+                const int a = (ke >> 8) & 0xFFF, p = ke >> 20;
                 int8_t *s = lds + b * ST;
                 const int r = (uint8_t)(bt(row(s, Lx::BANK), 6) + 1);   // the round after the move
                 Chance ch{&ud[b][0], 0, 0, 0, 1, 0.0, false, tabs.view()};
                 int nxt;
                 switch (w) {
-                    case MK_GEMS: nxt = make_move<N, MK_GEMS>(s, a, pl[b], false, ch); break;
-                    case MK_BUY: nxt = make_move<N, MK_BUY>(s, a, pl[b], false, ch); break;
-                    case MK_RESERVE: nxt = make_move<N, MK_RESERVE>(s, a, pl[b], false, ch); break;
-                    default: nxt = make_move<N, MK_BUY_RESERVED>(s, a, pl[b], false, ch); break;
+                    case MK_GEMS: nxt = make_move<N, MK_GEMS>(s, a, p, false, ch); break;
+                    case MK_BUY: nxt = make_move<N, MK_BUY>(s, a, p, false, ch); break;
+                    case MK_RESERVE: nxt = make_move<N, MK_RESERVE>(s, a, p, false, ch); break;
+                    default: nxt = make_move<N, MK_BUY_RESERVED>(s, a, p, false, ch); break;
                 }
                 RT_MARK(6)
 #if ROLLOUT_TIMING
