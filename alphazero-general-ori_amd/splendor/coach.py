@@ -53,8 +53,7 @@ class Coach:
         self.trainExamplesHistory = ExampleHistory(_arg(args, "numItersHistory"))
 
     def run_iterations(self, k, use_graph=False):
-        for _ in range(k):
-            self.sp.step(use_graph=use_graph)
+        self.sp.run(k, use_graph=use_graph)
 
     def executeEpisodes(self, num_games, with_symmetries=True, as_tuples=True, gather=False):
         collected, done = [], 0

@@ -179,8 +179,7 @@ def run_selfplay(args, rank, world, dev, dist):
     ev = LeafEvaluator(eng, net, B, use_graph=False)
     sp = SelfPlay(eng, B, sargs, evaluator=ev, dirichlet_noise=True, seed=args.seed, board_base=rank * B)
     sp.reset()
-    for _ in range(args.warmup):
-        sp.step(use_graph=True)
+    sp.run(args.warmup, use_graph=True)      # (captures both graphs)
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
@@ -188,8 +187,7 @@ def run_selfplay(args, rank, world, dev, dist):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record()
-    for _ in range(args.steps):
-        sp.step(use_graph=True)
+    sp.run(args.steps, use_graph=True)
     ev1.record()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0

@@ -31,8 +31,13 @@ def sort_examples(ex, meta):
 def test_selfplay_matches_oracle(n, forced, graph):
     B, iters, sims, ratio, pf, seed = 96, 1200, 8, 4, 0.25, 9
     e, sp = make(n, B, sims, ratio, pf, forced, seed=seed, out_cap=20000)
-    for _ in range(iters):
-        sp.step(use_graph=graph)
+    if graph:
+        sp.run(iters - 3, use_graph=True)     # 8-iteration graph replays + single replays
+        for _ in range(3):
+            sp.step(use_graph=True)
+    else:
+        for _ in range(iters):
+            sp.step(use_graph=False)
     torch.cuda.synchronize()
     hdr = sp.headers()
     assert hdr["overflow"].max() == 0
