@@ -355,7 +355,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                 } else if (cnt == 0) {
                     if (q == 3) {
                         a = 408;
-                        msk[b][6] = x0 | 1ull << (408 - 384);
+                        x0 |= 1ull << (408 - 384);
                     }
                 } else {
                     const int r = (int)(ud[b][0] * (double)cnt) - pre;
@@ -365,6 +365,12 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                     }
                 }
             }
+            // the move's final mask goes to HBM from these registers (no LDS re-read)
+            if (mask_out && on && ROLLOUT_ABLATE != 1) {
+                uint64_t *mo = mask_out + (ob + b) * 7 + 2 * q;
+                mo[0] = x0;
+                if (q < 3) mo[1] = x1;
+            }
             if (a >= 0) {
                 const int kind = move_kind_of(a);
                 klist[kind][atomicAdd(&kcount[kind], 1)] = (uint32_t)b | (uint32_t)a << 8 | (uint32_t)pl[b] << 20;
@@ -372,7 +378,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         }
         lds_sync();
         RT_MARK(5)
-        // move phase. The move's masks (final since select) go to HBM. Wave w makes every move
+        // move phase. Wave w makes every move
         // of kind w (one pipeline specialisation per wave, so no wave carries the stages of
         // other kinds): chance draws 1-2, end check, outputs. Then the wave re-deals the games
         // its own moves finished (wave-collective; draws 3.. of the step stream) — mostly the
@@ -381,8 +387,6 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
 #if ROLLOUT_TIMING
         const uint64_t mv0 = clock64();
 #endif
-        if (mask_out && ROLLOUT_ABLATE != 1)
-            for (int i = tid; i < nb * 7; i += THREADS) mask_out[ob * 7 + i] = (&msk[0][0])[i];
         {
             int b = 0;
             bool ended = false;
