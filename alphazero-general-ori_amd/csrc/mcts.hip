@@ -36,6 +36,7 @@ struct spl_mcts {
     SearchCfg cfg;
     Pools P;
     void *arena;
+    size_t bytes;                        // the whole arena (spl_mcts_device_bytes)
 };
 
 namespace {
@@ -148,70 +149,93 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
     return {bi, av, cv, make_int2(rx, ry)};
 }
 
-// ------------------------------------------------------------ Dirichlet root noise
-// applyDirNoise (MCTS.py:180-186) after softmax(Ps, T0) (:245-250), then normalise.
-// Gamma(alpha) by Marsaglia-Tsang with the alpha<1 boost, driven by Philox; the reference
-// uses numpy's Generator.dirichlet (unseeded), so parity here is distributional.
-__device__ __forceinline__ double gamma_sample(double alpha, uint64_t seed, uint32_t board,
-                                               uint32_t stream, uint32_t &ctr) {
-    const double a = alpha < 1.0 ? alpha + 1.0 : alpha;
-    const double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
-    double g = 0.0;
-    for (int it = 0; it < 64; it++) {
-        const double u1 = philox_u01(seed, board, stream, ctr++);
-        const double u2 = philox_u01(seed, board, stream, ctr++);
-        const double z = sqrt(-2.0 * log(fmax(u1, 1e-300))) * cos(6.283185307179586 * u2);
-        double v = 1.0 + c * z;
-        if (v <= 0.0) continue;
-        v = v * v * v;
-        const double u = philox_u01(seed, board, stream, ctr++);
-        if (log(fmax(u, 1e-300)) < 0.5 * z * z + d - d * v + d * log(v)) { g = d * v; break; }
-    }
-    if (alpha < 1.0) g *= pow(philox_u01(seed, board, stream, ctr++), 1.0 / alpha);
-    return g;
+// ------------------------------------------------------------ prior sums
+// numpy pairwise float32 sum of the 409 staged priors (np_sum409 order), 32 lanes:
+// lane = 8*block + j accumulates r_j of block `block`; blocks [0,96) [96,200) [200,304)
+// [304,409); combine ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) (+ tail), then (b0+b1)+(b2+b3).
+__device__ __forceinline__ float wave_np_sum409(const float *a) {
+    const int l = lane_id();
+    const int blk = (l >> 3) & 3, j = l & 7;
+    const int off = blk == 0 ? 0 : (blk == 1 ? 96 : (blk == 2 ? 200 : 304));
+    const int len = blk == 0 ? 96 : (blk == 3 ? 105 : 104);
+    float r = a[off + j];
+    for (int i = 8; i < len - (len % 8); i += 8) r += a[off + i + j];
+    float r1 = __shfl_xor(r, 1, 64);
+    float p01 = (j & 1) ? r1 + r : r + r1;            // pair sums (r0+r1) etc. on even lanes
+    float p23 = __shfl_xor(p01, 2, 64);
+    float q = (j & 2) ? p23 + p01 : p01 + p23;        // ((r0+r1)+(r2+r3)) on lane 0 of quad
+    float q2 = __shfl_xor(q, 4, 64);
+    float res = (j & 4) ? q2 + q : q + q2;            // lane j==0 holds the block result
+    float blockv = __shfl(res, 8 * blk, 64);
+    if (blk == 3) blockv = blockv + a[off + 104];     // 105 = 13*8 + 1 trailing element
+    const float b0 = __shfl(blockv, 0, 64), b1 = __shfl(blockv, 8, 64);
+    const float b2 = __shfl(blockv, 16, 64), b3 = __shfl(blockv, 24, 64);
+    return (b0 + b1) + (b2 + b3);
 }
 
-// P (float32, ec edges of the root) <- normalise(0.75*softmax(P,T0) + 0.25*Dir(alpha))
-__device__ __forceinline__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int eb,
-                                                 int ec, uint32_t stream) {
+// ------------------------------------------------------------ Dirichlet root noise
+// softmax(Ps, T0) (MCTS.py:245-250) -> applyDirNoise (:180-186) -> normalise (:239-242) on
+// the root's priors, for any number of legal actions. Types and orders as the oracle pins
+// them against the reference (oracle/splendor_oracle.c or_root_noise): Ps ** (1/T0) in
+// float64 (Numba's typing) summed in NumPy's pairwise order, divided and stored float32;
+// the mix 0.75*P + 0.25*d in float64 stored float32; normalise in float32 pairwise order.
+// The Dirichlet vector replaces the reference's unseeded Generator.dirichlet: det_gamma on
+// the Philox sequence (seed, board, stream), counters 4096*i for the i-th legal action,
+// normalised like numpy's dirichlet (sequential sum, times its reciprocal).
+// pr: LDS scratch of 416 floats for this wave; raw: pr already holds the network's priors
+// (a new root, :141-144), else the stored priors of an expanded root are used (:150-154).
+__device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int eb, int ec, uint32_t stream,
+                                 float *pr, bool raw) {
     const int l = lane_id();
     EdgeStat *est = P.es + (size_t)t * P.ecap + eb;
+    const EdgeLink *elk = P.el + (size_t)t * P.ecap + eb;
     const uint32_t gb = C.board_base + (uint32_t)t;
-    const bool tmp = C.dir_temp != 1.0;
-    double sp[3], g[3], ssum = 0.0, gsum = 0.0;
+    if (!raw) {
+        for (int a = l; a < 416; a += 64) pr[a] = 0.f;
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        for (int i = l; i < ec; i += 64) pr[elk[i].a] = est[i].p;
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (C.dir_temp != 1.0) {
+        const double e = 1.0 / C.dir_temp;
+        const double s = wave_np_sum409_f64(pr, [e](float x) { return det_pow((double)x, e); });
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = (float)(det_pow((double)pr[a], e) / s);
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+    }
+    double g[7];
 #pragma unroll
-    for (int j = 0; j < 3; j++) {   // <= 192 legal actions (observed max 133)
-        const int i = l + 64 * j;
-        sp[j] = 0.0; g[j] = 0.0;
+    for (int j = 0; j < 7; j++) {
+        const int i = 64 * j + l;
+        g[j] = i < ec ? det_gamma(C.dir_alpha, C.seed, gb, stream, (uint32_t)i * 4096u) : 0.0;
+    }
+    double acc = 0.0;                            // sequential, in action order
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        const int m = min(64, ec - 64 * j);
+        const int lo = __double2loint(g[j]), hi = __double2hiint(g[j]);
+        for (int k = 0; k < m; k++)
+            acc = acc + __hiloint2double(__builtin_amdgcn_readlane(hi, k), __builtin_amdgcn_readlane(lo, k));
+    }
+    const bool ok = acc > 0.0;
+    const double inv = ok ? 1.0 / acc : 0.0;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        const int i = 64 * j + l;
         if (i < ec) {
-            sp[j] = tmp ? pow((double)est[i].p, 1.0 / C.dir_temp) : (double)est[i].p;
-            uint32_t ctr = (uint32_t)i * 256u;
-            g[j] = gamma_sample(C.dir_alpha, C.seed, gb, stream, ctr);
+            const int a = elk[i].a;
+            const double d = ok ? g[j] * inv : 1.0 / (double)ec;
+            pr[a] = (float)(0.75 * (double)pr[a] + 0.25 * d);
         }
-        ssum += sp[j];
-        gsum += g[j];
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        ssum += __shfl_xor(ssum, o, 64);
-        gsum += __shfl_xor(gsum, o, 64);
-    }
-    float pn[3], nsum = 0.f;
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int i = l + 64 * j;
-        pn[j] = 0.f;
-        if (i < ec) {
-            const float smx = tmp ? (float)(sp[j] / ssum) : (float)sp[j];
-            pn[j] = (float)(0.75 * (double)smx + 0.25 * (g[j] / gsum));
-        }
-        nsum += pn[j];
-    }
-    for (int o = 32; o > 0; o >>= 1) nsum += __shfl_xor(nsum, o, 64);
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int i = l + 64 * j;
-        if (i < ec) est[i].p = pn[j] / nsum;
-    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    const float nsum = wave_np_sum409(pr);
+    for (int i = l; i < ec; i += 64) est[i].p = pr[elk[i].a] / nsum;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
 }
@@ -222,20 +246,54 @@ __device__ __forceinline__ void apply_root_noise(const Pools &P, const SearchCfg
 // this root or any later one — an exact subset of the reference's table (which only
 // evicts rounds < R-5, MCTS.py:80-85). Compacts nodes + CSR edges in place, remaps child
 // links, rebuilds the hash table. Wave-collective; returns the root's new index.
+// linked = true (capacity pressure, see begin_search): keep only the root and the nodes
+// reachable from it through child links (mark_linked), dropping nodes that only a
+// transposition lookup could reach.
 // scr: optional LDS scratch of 2 * (ncap + 1) ints for this wave (ncap <= SCR_NODES): the
 // edges then move in batches of 256 new positions (each lane finds its edge's owner by a
 // binary search over the kept nodes' new bases) instead of one kept node at a time.
 constexpr int SCR_NODES = 512;
-__device__ int compact_tree(const Pools &P, int t, int root, int root_round, int *scr = nullptr) {
+
+// remap[i] = 1 for the root and every node reachable from it through child links, 0 else
+// (breadth-first, the wave walks one node's edges at a time; remap_eb is the queue).
+__device__ void mark_linked(const Pools &P, int t, int root) {
+    const int l = lane_id();
+    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
+    const int nc = P.hdr[t].node_count;
+    int32_t *mark = P.remap + nb, *q = P.remap_eb + nb;
+    for (int i = l; i < nc; i += 64) mark[i] = i == root ? 1 : 0;
+    if (l == 0) q[0] = root;
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    int head = 0, tail = 1;
+    while (head < tail) {
+        const int node = q[head++];
+        const int eb = P.neb[nb + node], ec = P.nterm[nb + node] ? 0 : P.nec[nb + node];
+        for (int base = 0; base < ec; base += 64) {
+            const int i = base + l;
+            const int c = i < ec ? P.el[e0 + eb + i].child : -1;
+            const bool fresh = c >= 0 && atomicCAS(&mark[c], 0, 1) == 0;
+            const uint64_t b = __ballot(fresh);
+            if (fresh) q[tail + __popcll(b & lanemask_lt())] = c;
+            tail += __popcll(b);
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+__device__ int compact_tree(const Pools &P, int t, int root, int root_round, int *scr = nullptr,
+                            bool linked = false) {
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const int nc = H->node_count;
     int32_t *remap = P.remap + nb;
+    if (linked) mark_linked(P, t, root);
     int kept = 0;
     for (int base = 0; base < nc; base += 64) {
         const int i = base + l;
-        const bool keep = i < nc && (i == root || P.nround[nb + i] > root_round);
+        const bool keep = i < nc && (i == root || (linked ? remap[i] == 1 : P.nround[nb + i] > root_round));
         const uint64_t b = __ballot(keep);
         if (i < nc) remap[i] = keep ? kept + __popcll(b & lanemask_lt()) : -1;
         kept += __popcll(b);
@@ -401,6 +459,10 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
 // Re-root tree t at the canonical board staged in LDS `s` (MCTS.getActionProb entry,
 // :45-56): look the root up in the persistent table (keep) and collect garbage, or start
 // empty; draw the full/fast search decision (ST_FULL) and arm root noise. Wave-collective.
+// Capacity: a search adds at most `budget` nodes; when the kept tree plus that (and 409
+// edges for the root plus edge_reserve per simulation) does not fit the tree's pool, the tree is pruned to
+// the nodes linked from the root (prunes++), and emptied if that is still too large
+// (resets++). Without such an event the kept tree is exactly the reference's reachable table.
 template <int N>
 __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const int8_t *s, bool keep,
                              bool force_full, int *scr = nullptr) {
@@ -408,26 +470,42 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
     wave_store_board<N>(P.root_state + (size_t)t * Lx::S, s);
+    const int mv = H->move_no;
+    const bool full = force_full || philox_u01(C.seed, C.board_base + t, ST_FULL | (uint32_t)mv, 0) < C.prob_full;
+    const int budget = full ? C.num_sims : C.num_sims / C.ratio_full;
     int root = -1;
+    bool empty = true;
     if (keep && H->node_count > 0) {
         uint64_t k0, k1;
         wave_fingerprint<N>(s, k0, k1);
         root = hash_lookup(P, t, k0, k1);
-        root = compact_tree(P, t, root, (uint8_t)bt(row(s, 0), 6), P.ncap <= SCR_NODES ? scr : nullptr);
-    } else {
+        const int rr = (uint8_t)bt(row(s, 0), 6);
+        int *cs = P.ncap <= SCR_NODES ? scr : nullptr;
+        root = compact_tree(P, t, root, rr, cs);
+        const auto fits = [&]() {
+            return H->node_count + budget + 1 <= P.ncap &&
+                   (long long)H->edge_count + SPL_ACTIONS + (long long)budget * C.edge_reserve <= (long long)P.ecap;
+        };
+        if (!fits() && root >= 0) {
+            root = compact_tree(P, t, root, rr, cs, true);
+            if (l == 0) H->prunes += 1;
+        }
+        empty = !fits();
+        if (empty && l == 0) H->resets += 1;
+    }
+    if (empty) {
+        root = -1;
         int32_t *hs = P.hslot + (size_t)t * P.hcap;
         for (int i = l; i < P.hcap; i += 64) hs[i] = -1;
         if (l == 0) { H->node_count = 0; H->edge_count = 0; }
     }
-    const int mv = H->move_no;
-    const bool full = force_full || philox_u01(C.seed, C.board_base + t, ST_FULL | (uint32_t)mv, 0) < C.prob_full;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     if (l == 0) {
         H->root = root;
         H->sims_done = 0;
         H->full = full;
-        H->budget = full ? C.num_sims : C.num_sims / C.ratio_full;
+        H->budget = budget;
         H->forced = full && C.forced_playouts;
         H->noise_pending = full && C.dirichlet;
         H->leaf_kind = LEAF_NONE;
@@ -675,6 +753,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
                                                     uint8_t *__restrict__ leaf_valid) {
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
+    __shared__ __align__(16) float lpr[WAVES][416];          // root-noise scratch
     const int w = uniform(threadIdx.x >> 6), t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
@@ -702,7 +781,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         wave_fingerprint<N>(s, k0, k1);                  // the root itself is the leaf
     } else {
         if (sims == 0 && H->noise_pending)
-            apply_root_noise(P, C, t, P.neb[nb + node], P.nec[nb + node], ST_DIR | (uint32_t)H->move_no);
+            apply_root_noise(P, C, t, P.neb[nb + node], P.nec[nb + node], ST_DIR | (uint32_t)H->move_no, lpr[w],
+                             false);
         const bool forced = H->forced;
         // CSR range of the current node: the root's from its record, every child's from the
         // {eb, ec} cached on the edge that led to it, so a level costs ONE round trip (the
@@ -763,7 +843,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             for (int i = 0; i < N; i++) any |= es[i] != 0.f;
             if (any) {
                 const int id = H->node_count;
-                if (id >= P.ncap) { kind = LEAF_NONE; if (l == 0) H->overflow = 1; break; }
+                kind = LEAF_TERMINAL;
+#pragma unroll
+                for (int i = 0; i < N; i++) val[i] = es[i];
+                if (id >= P.ncap) {                          // no room: back up, do not store
+                    if (l == 0) H->unexpanded += 1;
+                    break;
+                }
                 __builtin_amdgcn_wave_barrier();
                 if (l == 0) {
                     P.nkey0[nb + id] = k0; P.nkey1[nb + id] = k1; P.neb[nb + id] = 0;
@@ -776,9 +862,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
                     set_cr(P.el[e0 + ge], 0, -1);
                     H->node_count = id + 1;
                 }
-                kind = LEAF_TERMINAL;
-#pragma unroll
-                for (int i = 0; i < N; i++) val[i] = es[i];
                 break;
             }
             break;                                           // new NN leaf
@@ -891,30 +974,6 @@ __global__ __launch_bounds__(256) void k_leaf_mask(int B, int lim, const int8_t 
         if (leaf_valid[b0 + i / 7]) leaf_mask[(size_t)b0 * 7 + i] = (&msk[0][0])[i];
 }
 
-// ------------------------------------------------------------ expand + backup
-// numpy pairwise float32 sum of the 409 staged priors (np_sum409 order), 32 lanes:
-// lane = 8*block + j accumulates r_j of block `block`; blocks [0,96) [96,200) [200,304)
-// [304,409); combine ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) (+ tail), then (b0+b1)+(b2+b3).
-__device__ __forceinline__ float wave_np_sum409(const float *a) {
-    const int l = lane_id();
-    const int blk = (l >> 3) & 3, j = l & 7;
-    const int off = blk == 0 ? 0 : (blk == 1 ? 96 : (blk == 2 ? 200 : 304));
-    const int len = blk == 0 ? 96 : (blk == 3 ? 105 : 104);
-    float r = a[off + j];
-    for (int i = 8; i < len - (len % 8); i += 8) r += a[off + i + j];
-    float r1 = __shfl_xor(r, 1, 64);
-    float p01 = (j & 1) ? r1 + r : r + r1;            // pair sums (r0+r1) etc. on even lanes
-    float p23 = __shfl_xor(p01, 2, 64);
-    float q = (j & 2) ? p23 + p01 : p01 + p23;        // ((r0+r1)+(r2+r3)) on lane 0 of quad
-    float q2 = __shfl_xor(q, 4, 64);
-    float res = (j & 4) ? q2 + q : q + q2;            // lane j==0 holds the block result
-    float blockv = __shfl(res, 8 * blk, 64);
-    if (blk == 3) blockv = blockv + a[off + 104];     // 105 = 13*8 + 1 trailing element
-    const float b0 = __shfl(blockv, 0, 64), b1 = __shfl(blockv, 8, 64);
-    const float b2 = __shfl(blockv, 16, 64), b3 = __shfl(blockv, 24, 64);
-    return (b0 + b1) + (b2 + b3);
-}
-
 template <int N>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) void k_backup(Pools P, SearchCfg C, int B,
                                                     const uint64_t *__restrict__ leaf_mask,
@@ -951,9 +1010,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
 #pragma unroll
         for (int k = 0; k < 7; k++) ec += __popcll(m[k]);
         const int id = H->node_count, eb = H->edge_count;
-        if (id >= P.ncap || eb + ec > P.ecap) {
-            if (l == 0) { H->overflow = 1; H->leaf_kind = LEAF_NONE; }
-            return;
+        if (id >= P.ncap || eb + ec > P.ecap) {          // no room: back up v, do not store
+#pragma unroll
+            for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
+            if (l == 0) H->unexpanded += 1;
+            goto backup;
         }
         float *pr = lpi[w];
         const float *g = pi + (size_t)t * SPL_ACTIONS;
@@ -994,12 +1055,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         }
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
-        if (depth == 0 && H->sims_done == 0 && H->noise_pending)   // noise on a new root
-            apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no);
+        if (depth == 0 && H->sims_done == 0 && H->noise_pending)   // noise on a new root (raw priors)
+            apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no, pr, true);
     } else {
 #pragma unroll
         for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
     }
+backup:
     // backup (MCTS.py:169-176): level d sees the leaf value rolled (depth - d) times; the
     // levels touch distinct nodes/edges (rounds strictly increase along a path), so one
     // lane per level applies exactly the sequential update.
@@ -1133,6 +1195,22 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
     }
 }
 
+// root priors Ps as stored (MCTS.py:147/176), 409 floats per tree
+__global__ __launch_bounds__(THREADS) void k_root_priors(Pools P, int B, float *ps) {
+    const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
+    if (t >= B) return;
+    const int l = lane_id();
+    float *o = ps + (size_t)t * SPL_ACTIONS;
+    for (int a = l; a < SPL_ACTIONS; a += 64) o[a] = 0.f;
+    const int root = P.hdr[t].root;
+    if (root < 0) return;
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
+    const int eb = P.neb[nb + root], ec = P.nec[nb + root];
+    for (int i = l; i < ec; i += 64) o[P.el[e0 + eb + i].a] = P.es[e0 + eb + i].p;
+}
+
 // leaf int8 [B,R,7] + packed mask -> float32 board and bool mask (predict, :160-161).
 // The board is written TRANSPOSED, [B,7,R] (the layout SplendorNNet.forward builds at
 // SplendorNNet.py:129), so the first layer is a plain row-major GEMM.
@@ -1200,10 +1278,48 @@ T *carve(char *&p, size_t count) {
 
 extern "C" {
 
+// Pool layout of spl_mcts_create (also what spl_mcts_plan_bytes reports).
+struct Plan {
+    int ncap, ecap, hcap, pcap, S, excap, out_cap;
+    size_t bytes;
+};
+static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
+    Plan L;
+    L.ncap = cfg->node_cap; L.ecap = cfg->edge_cap;
+    int h = 1;
+    while (h < 2 * L.ncap) h <<= 1;
+    L.hcap = h;
+    L.pcap = cfg->num_sims + 64 > 256 ? cfg->num_sims + 64 : 256;
+    L.S = 7 * (32 + 10 * n + n * n);
+    L.excap = cfg->selfplay ? 62 * n + 2 : 0;
+    L.out_cap = cfg->selfplay ? (cfg->out_cap > 0 ? cfg->out_cap : 4 * B) : 0;
+    const size_t nn = (size_t)B * L.ncap, ne = (size_t)B * L.ecap;
+    const size_t nx = (size_t)B * L.excap, no = (size_t)L.out_cap;
+    size_t bytes = 0;
+    auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
+    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn); acc(4 * nn);
+    acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(sizeof(EdgeStat) * ne); acc(sizeof(EdgeLink) * ne);
+    acc(4 * (size_t)B * L.hcap); acc(8 * (size_t)B * L.pcap);
+    acc(4 * nn); acc(4 * nn); acc((size_t)B * L.S);
+    acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
+    acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
+    acc(16 * no); acc(64);
+    L.bytes = bytes;
+    return L;
+}
+
+static bool valid_cfg(const spl_ctx *ctx, int B, const spl_mcts_config *cfg) {
+    return ctx && ctx->n >= 2 && ctx->n <= 4 && B > 0 && cfg && cfg->num_sims > 0 && cfg->ratio_full > 0 &&
+           cfg->node_cap > 0 && cfg->edge_cap > 0;
+}
+
+long long spl_mcts_plan_bytes(const spl_ctx *ctx, int B, const spl_mcts_config *cfg) {
+    if (!valid_cfg(ctx, B, cfg)) return SPL_EINVAL;
+    return (long long)plan_pools(ctx->n, B, cfg).bytes;
+}
+
 int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_mcts **out) {
-    if (!ctx || ctx->n < 2 || ctx->n > 4 || B <= 0 || !cfg || !out) return SPL_EINVAL;
-    if (cfg->num_sims <= 0 || cfg->ratio_full <= 0 || cfg->node_cap <= 0 || cfg->edge_cap <= 0)
-        return SPL_EINVAL;
+    if (!valid_cfg(ctx, B, cfg) || !out) return SPL_EINVAL;
     spl_mcts *m = new (std::nothrow) spl_mcts;
     if (!m) return SPL_EINVAL;
     m->n = ctx->n; m->B = B; m->S = 7 * (32 + 10 * ctx->n + ctx->n * ctx->n);
@@ -1216,27 +1332,18 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     C.temp_threshold = cfg->temp_threshold; C.seed = cfg->seed; C.board_base = cfg->board_base;
     C.selfplay = cfg->selfplay;
     Pools &P = m->P;
-    P.ncap = cfg->node_cap; P.ecap = cfg->edge_cap;
-    int h = 1;
-    while (h < 2 * P.ncap) h <<= 1;
-    P.hcap = h;
-    P.pcap = cfg->num_sims + 64 > 256 ? cfg->num_sims + 64 : 256;
+    const Plan L = plan_pools(ctx->n, B, cfg);
+    P.ncap = L.ncap; P.ecap = L.ecap; P.hcap = L.hcap; P.pcap = L.pcap;
+    C.edge_reserve = P.ecap / P.ncap < 32 ? P.ecap / P.ncap : 32;
     const size_t nn = (size_t)B * P.ncap, ne = (size_t)B * P.ecap;
-    size_t bytes = 0;
-    auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
-    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn); acc(4 * nn);
-    acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(sizeof(EdgeStat) * ne); acc(sizeof(EdgeLink) * ne);
-    acc(4 * (size_t)B * P.hcap); acc(8 * (size_t)B * P.pcap);
-    acc(4 * nn); acc(4 * nn); acc((size_t)B * m->S);
-    const int excap = cfg->selfplay ? 62 * ctx->n + 2 : 0;
-    const size_t nx = (size_t)B * excap, no = cfg->selfplay ? (size_t)(cfg->out_cap > 0 ? cfg->out_cap : 4 * B) : 0;
-    acc((size_t)B * m->S); acc(nx * m->S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
-    acc(no * m->S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
-    acc(16 * no); acc(64);
+    const int excap = L.excap;
+    const size_t nx = (size_t)B * excap, no = (size_t)L.out_cap;
+    const size_t bytes = L.bytes;
     void *arena = nullptr;
     if (hipMalloc(&arena, bytes) != hipSuccess) { delete m; return SPL_EDEVICE; }
     if (hipMemset(arena, 0, bytes) != hipSuccess) { (void)hipFree(arena); delete m; return SPL_EDEVICE; }
     m->arena = arena;
+    m->bytes = bytes;
     char *p = (char *)arena;
     P.hdr = carve<TreeHdr>(p, B);
     P.nkey0 = carve<uint64_t>(p, nn); P.nkey1 = carve<uint64_t>(p, nn);
@@ -1273,8 +1380,7 @@ int spl_mcts_destroy(spl_mcts *m) {
 
 long long spl_mcts_device_bytes(const spl_mcts *m) {
     if (!m) return SPL_EINVAL;
-    const size_t nn = (size_t)m->B * m->P.ncap, ne = (size_t)m->B * m->P.ecap;
-    return (long long)(nn * 57 + ne * 32 + (size_t)m->B * (4 * m->P.hcap + 8 * m->P.pcap + m->S + sizeof(TreeHdr)));
+    return (long long)m->bytes;
 }
 
 int spl_mcts_set_roots(spl_mcts *m, const int8_t *roots, int keep_tree, int force_full, void *hs) {
@@ -1326,6 +1432,12 @@ int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs
     return check_launch();
 }
 
+int spl_mcts_root_priors(spl_mcts *m, float *ps, void *hs) {
+    if (!m || !ps) return SPL_EINVAL;
+    hipLaunchKernelGGL(k_root_priors, wave_grid(m->B), dim3(THREADS), 0, (hipStream_t)hs, m->P, m->B, ps);
+    return check_launch();
+}
+
 int spl_mcts_reset_games(spl_mcts *m, void *hs) {
     if (!m || !m->cfg.selfplay) return SPL_EINVAL;
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_reset_games<N>, wave_grid(m->B), dim3(THREADS), 0,
@@ -1353,6 +1465,12 @@ int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *val
     }
     hipLaunchKernelGGL(k_drain_reset, dim3(1), dim3(1), 0, (hipStream_t)hs, m->P, max, n_out);
     return check_launch();
+}
+
+int spl_mcts_counters(spl_mcts *m, int32_t *out, void *hs) {
+    if (!m || !out || !m->cfg.selfplay) return SPL_EINVAL;
+    return hipMemcpyAsync(out, m->P.counters, 2 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)hs) ==
+                   hipSuccess ? 0 : SPL_EDEVICE;
 }
 
 int spl_mcts_headers(spl_mcts *m, int32_t *out, void *hs) {

@@ -25,6 +25,10 @@ struct TreeHdr {
     uint64_t leaf_k0, leaf_k1;
     float leaf_v[4];
     int32_t games_done, forced, pad0, pad1;
+    // capacity events: searches that started on a tree pruned to the nodes
+    // linked from the root / on an emptied tree, and simulations whose leaf did not fit
+    // (evaluated and backed up without being stored)
+    int32_t prunes, resets, unexpanded, pad2;
 };
 enum { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2 };
 
@@ -78,6 +82,7 @@ struct SearchCfg {
     double cpuct, fpu, dir_alpha, dir_temp, prob_full;
     int num_sims, ratio_full, forced_playouts, dirichlet;
     int temp_threshold, selfplay;
+    int edge_reserve;                    // edges reserved per simulation at search start
     uint64_t seed;
     uint32_t board_base;
 };
@@ -187,6 +192,95 @@ __device__ __forceinline__ float pw_block(const float *a, int len) {
 // pairwise(409) = ((pw[0,96) + pw[96,200)) + (pw[200,304) + pw[304,409)))
 __device__ __forceinline__ float np_sum409(const float *a) {
     return (pw_block(a, 96) + pw_block(a + 96, 104)) + (pw_block(a + 200, 104) + pw_block(a + 304, 105));
+}
+
+// pairwise(409) of a double-valued function of a 409-float array (NumPy's float64 pairwise
+// order, the block tree of np_sum409); 32 lanes, lane = 8*block + j, uniform result.
+template <class F>
+__device__ __forceinline__ double wave_np_sum409_f64(const float *a, F f) {
+    const int l = lane_id();
+    const int blk = (l >> 3) & 3, j = l & 7;
+    const int off = blk == 0 ? 0 : (blk == 1 ? 96 : (blk == 2 ? 200 : 304));
+    const int len = blk == 0 ? 96 : (blk == 3 ? 105 : 104);
+    double r = f(a[off + j]);
+    for (int i = 8; i < len - (len % 8); i += 8) r += f(a[off + i + j]);
+    const double r1 = __shfl_xor(r, 1, 64);
+    const double p01 = (j & 1) ? r1 + r : r + r1;
+    const double p23 = __shfl_xor(p01, 2, 64);
+    const double q = (j & 2) ? p23 + p01 : p01 + p23;
+    const double q2 = __shfl_xor(q, 4, 64);
+    const double res = (j & 4) ? q2 + q : q + q2;
+    double blockv = __shfl(res, 8 * blk, 64);
+    if (blk == 3) blockv = blockv + f(a[off + 104]);
+    const double b0 = __shfl(blockv, 0, 64), b1 = __shfl(blockv, 8, 64);
+    const double b2 = __shfl(blockv, 16, 64), b3 = __shfl(blockv, 24, 64);
+    return (b0 + b1) + (b2 + b3);
+}
+
+// ----------------------------------------------------------- deterministic transcendentals
+// The Dirichlet sampler and the noise softmax use a logarithm / exponential built from
+// + - * / only, so the device, the C oracle (oracle/splendor_oracle.c det_*) and the
+// fixture generator (tests/golden/detrand.py) compute identical bits (no libm / ocml
+// rounding differences; the library is built with -ffp-contract=off).
+constexpr double DET_LN2_HI = 6.93147180369123816490e-01;
+constexpr double DET_LN2_LO = 1.90821492927058770002e-10;
+constexpr double DET_INV_LN2 = 1.44269504088896338700e+00;
+
+__device__ inline double det_log(double x) {         // x > 0, normal
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    int e = (int)((b >> 52) & 0x7ff) - 1023;
+    double m = __longlong_as_double((long long)((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull));
+    if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
+    const double f = (m - 1.0) / (m + 1.0), s = f * f;
+    double p = 1.0 / 23.0;
+    p = p * s + 1.0 / 21.0; p = p * s + 1.0 / 19.0; p = p * s + 1.0 / 17.0;
+    p = p * s + 1.0 / 15.0; p = p * s + 1.0 / 13.0; p = p * s + 1.0 / 11.0;
+    p = p * s + 1.0 / 9.0; p = p * s + 1.0 / 7.0; p = p * s + 1.0 / 5.0; p = p * s + 1.0 / 3.0;
+    const double t = 2.0 * f, r = t + t * (s * p);
+    return (double)e * DET_LN2_HI + (r + (double)e * DET_LN2_LO);
+}
+__device__ inline double det_exp(double x) {
+    if (x < -700.0) return 0.0;
+    const double kf = floor(x * DET_INV_LN2 + 0.5);
+    const double r = (x - kf * DET_LN2_HI) - kf * DET_LN2_LO;
+    double p = 1.0 / 6227020800.0;
+    p = p * r + 1.0 / 479001600.0; p = p * r + 1.0 / 39916800.0; p = p * r + 1.0 / 3628800.0;
+    p = p * r + 1.0 / 362880.0; p = p * r + 1.0 / 40320.0; p = p * r + 1.0 / 5040.0;
+    p = p * r + 1.0 / 720.0; p = p * r + 1.0 / 120.0; p = p * r + 1.0 / 24.0;
+    p = p * r + 1.0 / 6.0; p = p * r + 0.5; p = p * r + 1.0; p = p * r + 1.0;
+    return ldexp(p, (int)kf);
+}
+__device__ inline double det_pow(double x, double y) { return x == 0.0 ? 0.0 : det_exp(y * det_log(x)); }
+
+// Gamma(alpha) for the Dirichlet draw: Marsaglia-Tsang with polar normals (and the alpha<1
+// boost), uniforms ctr, ctr+1, ... of the Philox sequence (seed, board, stream).
+__device__ inline double det_gamma(double alpha, uint64_t seed, uint32_t board, uint32_t stream,
+                                   uint32_t ctr) {
+    const double a = alpha < 1.0 ? alpha + 1.0 : alpha;
+    const double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
+    double g = 0.0;
+    for (int it = 0; it < 64; it++) {
+        double z = 0.0;
+        for (int j = 0; j < 16; j++) {
+            const double u1 = 2.0 * philox_u01(seed, board, stream, ctr) - 1.0;
+            const double u2 = 2.0 * philox_u01(seed, board, stream, ctr + 1) - 1.0;
+            ctr += 2;
+            const double s = u1 * u1 + u2 * u2;
+            if (s < 1.0 && s > 0.0) { z = u1 * sqrt(-2.0 * det_log(s) / s); break; }
+        }
+        double v = 1.0 + c * z;
+        if (v <= 0.0) continue;
+        v = v * v * v;
+        double u = philox_u01(seed, board, stream, ctr++);
+        if (u < 1e-300) u = 1e-300;
+        if (det_log(u) < 0.5 * z * z + d - d * v + d * det_log(v)) { g = d * v; break; }
+    }
+    if (alpha < 1.0) {
+        double u = philox_u01(seed, board, stream, ctr++);
+        if (u < 1e-300) u = 1e-300;
+        g = g * det_exp(det_log(u) / alpha);
+    }
+    return g;
 }
 
 // x ** (1/T) of applyTemperatureAndNormalize (Coach.py:25) with an exactly specified

@@ -53,6 +53,35 @@ def scdiff_targets(scdiff, max_diff):
     return t
 
 
+def _dist_world():
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return None, 0, 1
+    return dist, dist.get_rank(), dist.get_world_size()
+
+
+def _agreed_batch_count(batch_count, device):
+    """Every rank must make the same number of gradient all-reduces: the minimum over ranks
+    of E // batch_size (ranks may hold different example counts)."""
+    dist, _, world = _dist_world()
+    if world == 1:
+        return batch_count
+    t = torch.tensor([batch_count], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
+def _batch_generator(device):
+    """Batch sampling stream: seeded from the global torch RNG (itself unseeded unless the
+    caller seeds it, like the reference's np.random.choice) and decorrelated per rank, so
+    ranks draw different batches and repeated calls differ."""
+    _, rank, _ = _dist_world()
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) ^ (0x9E3779B97F4A7C15 * (rank + 1) & (2 ** 63 - 1))
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return g
+
+
 def _allreduce_grads(params):
     """Average gradients over ranks in one flat bucket (the model is ~1.25 MB of fp32)."""
     import torch.distributed as dist
@@ -101,7 +130,8 @@ class NNetWrapper:
         """One GenericNNetWrapper.train call over `examples` (ExampleSet, or the reference's
         list of tuples): epochs x (len // batch_size) Adam steps on batches sampled without
         replacement, total loss l_pi + vl_weight * l_v + l_cdf + l_pdf. Returns the mean of
-        each loss over the last epoch."""
+        each loss over the last epoch. Across ranks: gradients averaged in one all-reduce per
+        step, the step count agreed (minimum over ranks), batches drawn per rank."""
         if not isinstance(examples, ExampleSet):
             examples = ExampleSet.from_tuples(list(examples))
         if self.args["surprise_weight"]:
@@ -110,7 +140,7 @@ class NNetWrapper:
             raise ValueError("surprise_weight: per-example surprise is a vector (reference raises)")
         ex = examples.to(self.device)
         E, bs, epochs = len(ex), int(self.args["batch_size"]), int(self.args["epochs"])
-        batch_count = E // bs
+        batch_count = _agreed_batch_count(E // bs, self.device)
         if batch_count == 0:
             return None
         params = list(self.nnet.parameters())
@@ -118,7 +148,7 @@ class NNetWrapper:
             self.optimizer = optim.Adam(params, lr=self.args["learn_rate"])
         scheduler = optim.lr_scheduler.OneCycleLR(self.optimizer, max_lr=self.args["learn_rate"],
                                                   steps_per_epoch=batch_count, epochs=epochs)
-        gen = generator or torch.Generator(device=self.device)
+        gen = generator or _batch_generator(self.device)
         means = None
         for _ in range(epochs):
             self.nnet.train()

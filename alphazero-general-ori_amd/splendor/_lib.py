@@ -52,12 +52,15 @@ _SIGS = {
     "spl_mcts_create": ([C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)], C.c_int),
     "spl_mcts_destroy": ([C.c_void_p], C.c_int),
     "spl_mcts_device_bytes": ([C.c_void_p], C.c_longlong),
+    "spl_mcts_plan_bytes": ([_vp, C.c_int, _vp], C.c_longlong),
+    "spl_mcts_counters": ([C.c_void_p, _vp, _vp], C.c_int),
     "spl_mcts_set_roots": ([C.c_void_p, _vp, C.c_int, C.c_int, _vp], C.c_int),
     "spl_mcts_set_roots_active": ([C.c_void_p, _vp, _vp, C.c_int, C.c_int, _vp], C.c_int),
     "spl_mcts_pick_best": ([C.c_void_p, _vp, C.c_uint32, C.c_uint32, _vp, _vp], C.c_int),
     "spl_mcts_select": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_backup": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_root_stats": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_mcts_root_priors": ([C.c_void_p, _vp, _vp], C.c_int),
     "spl_mcts_headers": ([C.c_void_p, _vp, _vp], C.c_int),
     "spl_mcts_reset_games": ([C.c_void_p, _vp], C.c_int),
     "spl_mcts_commit": ([C.c_void_p, _vp], C.c_int),

@@ -97,6 +97,7 @@ class BatchedArena:
         result = torch.zeros((B, n), dtype=torch.float32, device=dev)
         plies = torch.zeros(B, dtype=torch.int32, device=dev)
         action = torch.full((B,), PASS, dtype=torch.int16, device=dev)
+        trace = []                                                             # actions per ply
         max_plies = 62 * n * 2 + 8                                             # round cap (:322)
         for ply in range(max_plies):
             cur = ply % n
@@ -120,6 +121,7 @@ class BatchedArena:
                 if bool(bad.any()):
                     raise AssertionError(f"invalid arena action in games {gid[bad.cpu().numpy()].tolist()}")
             action = torch.where(live, action, torch.full_like(action, PASS))
+            trace.append(torch.where(live, action, torch.full_like(action, -1)))
             e.step(boards, action, player=player, deterministic=False, seed=self.seed, stream=ply,
                    board_base=base)
             ended = e.game_ended(boards)
@@ -129,13 +131,17 @@ class BatchedArena:
             done |= newly
             if not bool((alive & ~done).any()):
                 break
+        acts = torch.stack(trace, 1)[:G].cpu().numpy()
+        pad = np.full((G, max_plies - acts.shape[1]), -1, dtype=np.int16)
         return {"game": gid[:G], "one_vs_two": first[:G], "result": result[:G].cpu().numpy(),
-                "plies": plies[:G].cpu().numpy(), "score": e.score(boards)[:G].cpu().numpy()}
+                "plies": plies[:G].cpu().numpy(), "score": e.score(boards)[:G].cpu().numpy(),
+                "actions": np.concatenate([acts, pad], 1)}
 
     # ---------------------------------------------------------------- reference API
     def playGames(self, num, verbose=False):
         """Arena.playGames: (oneWon, twoWon, draws) over `num` games; per-game records in
-        self.last (game id, one_vs_two, result vector, plies, final scores)."""
+        self.last (game id, one_vs_two, result vector, plies, final scores, actions per ply
+        with -1 after the game's end)."""
         recs = []
         for g0 in range(0, num, self.B):
             recs.append(self._play_batch(g0, min(self.B, num - g0)))

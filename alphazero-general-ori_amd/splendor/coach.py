@@ -56,6 +56,11 @@ class Coach:
         self.sp.run(k, use_graph=use_graph)
 
     def executeEpisodes(self, num_games, with_symmetries=True, as_tuples=True, gather=False):
+        """Play until num_games games have finished (counted from the call), draining the
+        example queue every 32 iterations. Raises EngineError if a tree froze (search path
+        overflow) or finished examples were dropped. Capacity events (trees pruned under
+        memory pressure) are counted in self.sp.stats()."""
+        from . import _lib
         collected, done = [], 0
         start = self.sp.stats()["games_done"]
         while done < num_games:
@@ -63,7 +68,10 @@ class Coach:
             ex = self.sp.drain()
             if ex["board"].shape[0]:
                 collected.append(ex)
-            done = self.sp.stats()["games_done"] - start
+            st = self.sp.stats()
+            if st["overflow"]:
+                raise _lib.EngineError(f"{st['overflow']} self-play trees overflowed their search path")
+            done = st["games_done"] - start
         ex = {k: torch.cat([c[k] for c in collected]) for k in collected[0]} if collected else self.sp.drain()
         if gather:
             ex = gather_examples(ex)
@@ -108,7 +116,9 @@ class Coach:
         (fresh games and trees, as the reference's executeEpisode + reset_all_search_trees),
         the example history saved, the network trained on it, then pitted against the
         previous weights over arenaCompare games (BatchedArena, temp 0, full searches) and
-        kept iff it wins >= updateThreshold of the decisive games; checkpoints as
+        kept iff it wins >= updateThreshold of the decisive games (under torch.distributed
+        every rank's examples are all-gathered first, so all ranks train on the same set);
+        checkpoints as
         checkpoint_<i>.pt / best.pt / temp.pt in args.checkpoint. Returns per-iteration
         (nwins, pwins, draws, accepted)."""
         from .NNet import NNetWrapper
@@ -118,7 +128,7 @@ class Coach:
         for i in range(1, int(_arg(self.args, "numIters", 1)) + 1):
             if not _arg(self.args, "skipFirstSelfPlay", False) or i > 1:
                 self.sp.reset()
-                self.executeIteration(int(_arg(self.args, "numEps", self.B)))
+                self.executeIteration(int(_arg(self.args, "numEps", self.B)), gather=True)
             self.saveTrainExamples(folder)
             self.nnet.save_checkpoint(folder=folder, filename="temp.pt")
             pnet.load_checkpoint(folder=folder, filename="temp.pt")

@@ -21,15 +21,16 @@ import torch
 from . import _lib
 from .env import ACTIONS, MASK_WORDS, _ptr
 
-# TreeHdr (csrc/mcts_device.h), 112 bytes
+# TreeHdr (csrc/mcts_device.h), 128 bytes
 HDR_DTYPE = np.dtype([
     ("node_count", "<i4"), ("edge_count", "<i4"), ("root", "<i4"), ("sims_done", "<i4"),
     ("budget", "<i4"), ("full", "<i4"), ("noise_pending", "<i4"), ("depth", "<i4"),
     ("leaf_kind", "<i4"), ("player", "<i4"), ("episode_step", "<i4"), ("move_no", "<i4"),
     ("game_no", "<i4"), ("overflow", "<i4"), ("n_examples", "<i4"), ("leaf_round", "<i4"),
     ("leaf_k0", "<u8"), ("leaf_k1", "<u8"), ("leaf_v", "<f4", (4,)),
-    ("games_done", "<i4"), ("forced", "<i4"), ("pad0", "<i4"), ("pad1", "<i4")])
-assert HDR_DTYPE.itemsize == 112
+    ("games_done", "<i4"), ("forced", "<i4"), ("pad0", "<i4"), ("pad1", "<i4"),
+    ("prunes", "<i4"), ("resets", "<i4"), ("unexpanded", "<i4"), ("pad2", "<i4")])
+assert HDR_DTYPE.itemsize == 128
 
 DEFAULT_ARGS = dict(numMCTSSims=100, cpuct=1.0, fpu=0.0, prob_fullMCTS=1.0, ratio_fullMCTS=5,
                     forced_playouts=False, dirichletAlpha=0.0, temperature=[1.25, 0.8],
@@ -78,13 +79,11 @@ class BatchedMCTS:
         cfg.dirichlet_alpha = float(_arg(args, "dirichletAlpha")) if dirichlet_noise else 0.0
         cfg.dirichlet_temp = float(_arg(args, "temperature")[0])
         cfg.temp_threshold = int(_arg(args, "tempThreshold"))
-        # capacity: a search adds <= sims nodes; keep room for retained subtrees
-        cfg.node_cap = int(node_cap or max(4 * sims + 64, 256))
-        cfg.edge_cap = int(edge_cap or 32 * cfg.node_cap)
         cfg.seed = seed
         cfg.board_base = board_base
         cfg.selfplay = int(bool(selfplay))
         cfg.out_cap = int(getattr(self, "_selfplay_out_cap", 0))
+        cfg.node_cap, cfg.edge_cap = self._caps(engine, B, sims, cfg, node_cap, edge_cap)
         self.cfg = cfg
         h = C.c_void_p()
         _lib.check(self.L.spl_mcts_create(engine.ctx, B, C.byref(cfg), C.byref(h)), "spl_mcts_create")
@@ -96,6 +95,37 @@ class BatchedMCTS:
         self.evaluator = evaluator or HashEvaluator(engine)
         self._hdr = torch.empty((B, HDR_DTYPE.itemsize // 4), dtype=torch.int32, device=dev)
 
+    MEM_FRACTION = 0.8     # of the device's free memory a default-sized arena may take
+
+    def _caps(self, engine, B, sims, cfg, node_cap, edge_cap):
+        """Per-tree pool sizes. A search adds at most `sims` nodes, but the
+        kept table (every node whose round exceeds the root's, MCTS.py semantics) keeps
+        growing through a game: measured trees pass 8 x sims nodes (tools/tree_sizes.py).
+        Default: 8 x sims + 64 nodes, 48 edges per node slot; when B such trees do not fit
+        MEM_FRACTION of the free HBM, 24 edges per node and as many nodes as fit (searches
+        then start on pruned trees under pressure, counted in the tree headers)."""
+        if node_cap and edge_cap:
+            return int(node_cap), int(edge_cap)
+        nc = int(node_cap or max(8 * sims + 64, 256))
+        ec = int(edge_cap or 48 * nc)
+
+        def plan(nc_, ec_):
+            cfg.node_cap, cfg.edge_cap = int(nc_), int(ec_)
+            return int(self.L.spl_mcts_plan_bytes(engine.ctx, B, C.byref(cfg)))
+        if engine.device.type != "cuda" or (node_cap or edge_cap):
+            return nc, ec
+        free = torch.cuda.mem_get_info(engine.device)[0]
+        limit = int(self.MEM_FRACTION * free)
+        if plan(nc, ec) <= limit:
+            return nc, ec
+        ratio = 24
+        lo = plan(64, 64 * ratio)
+        per = (plan(1064, 1064 * ratio) - lo) / 1000.0
+        nc = max(64, int((limit - lo) / per) + 64)
+        while nc > 64 and plan(nc, nc * ratio) > limit:
+            nc = int(nc * 0.97)
+        return nc, nc * ratio
+
     def __del__(self):
         if getattr(self, "h", None) is not None:
             self.L.spl_mcts_destroy(self.h)
@@ -104,6 +134,13 @@ class BatchedMCTS:
     @property
     def device_bytes(self):
         return int(self.L.spl_mcts_device_bytes(self.h))
+
+    def capacity_events(self, hdr=None):
+        """Trees pruned / emptied at a search start and simulations whose leaf did not fit
+        (0 everywhere = every search ran on the reference's exact table)."""
+        h = self.headers() if hdr is None else hdr
+        return {"prunes": int(h["prunes"].sum()), "resets": int(h["resets"].sum()),
+                "unexpanded": int(h["unexpanded"].sum())}
 
     # ---------------------------------------------------------------- primitives
     def set_roots(self, roots, keep_tree=True, force_full=True):
@@ -153,6 +190,13 @@ class BatchedMCTS:
         _lib.check(self.L.spl_mcts_root_stats(self.h, _ptr(counts), _ptr(qsa), _ptr(probs), _ptr(q),
                                               _ptr(adj), self.e._s()), "spl_mcts_root_stats")
         return (counts, qsa, probs, q, adj) if adjusted else (counts, qsa, probs, q)
+
+    def root_priors(self):
+        """Stored root priors Ps (float32 [B,409]; MCTS.nodes_data[s][2], noised when root
+        Dirichlet noise was applied)."""
+        ps = torch.empty((self.B, ACTIONS), dtype=torch.float32, device=self.e.device)
+        _lib.check(self.L.spl_mcts_root_priors(self.h, _ptr(ps), self.e._s()), "spl_mcts_root_priors")
+        return ps
 
     # ---------------------------------------------------------------- reference API
     def get_action_prob(self, canonical_boards, force_full_search=True, keep_tree=True):

@@ -21,9 +21,14 @@ from .mcts import BatchedMCTS
 
 
 class SelfPlay(BatchedMCTS):
+    """out_cap: finished-example queue (default: one full game of examples per tree, B x
+    (62n + 2), so a drain per game length cannot overflow it; examples that still do not fit
+    are counted and `drain` raises)."""
+
     def __init__(self, engine, B, args=None, evaluator=None, dirichlet_noise=True, seed=0x5EED,
                  board_base=0, out_cap=None, node_cap=None, edge_cap=None):
-        self._selfplay_out_cap = int(out_cap or 8 * B)
+        self._selfplay_out_cap = int(out_cap or B * (62 * engine.n + 2))
+        self._dropped_seen = 0
         super().__init__(engine, B, args, evaluator, dirichlet_noise=dirichlet_noise, seed=seed,
                          board_base=board_base, node_cap=node_cap, edge_cap=edge_cap, selfplay=True)
         self.graph = None
@@ -76,9 +81,28 @@ class SelfPlay(BatchedMCTS):
             return
         self.graph.replay()
 
-    def drain(self):
-        """Move finished examples out of the device queue: dict of device tensors."""
-        E, n, dev = self._selfplay_out_cap, self.e.n, self.e.device
+    def counters(self):
+        """(examples queued, examples dropped so far) — one small device read."""
+        c = torch.empty(2, dtype=torch.int32, device=self.e.device)
+        _lib.check(self.L.spl_mcts_counters(self.h, _ptr(c), self.e._s()), "spl_mcts_counters")
+        q, d = c.tolist()
+        return q, d
+
+    def dropped_examples(self):
+        return self.counters()[1]
+
+    def drain(self, allow_drops=False):
+        """Move finished examples out of the device queue: dict of device tensors. Raises
+        EngineError if examples were lost to a full queue since the last drain (training
+        data must not vanish silently) unless allow_drops."""
+        queued, dropped = self.counters()
+        if dropped > self._dropped_seen and not allow_drops:
+            lost = dropped - self._dropped_seen
+            self._dropped_seen = dropped
+            raise _lib.EngineError(f"{lost} finished examples dropped: the example queue (out_cap="
+                                   f"{self._selfplay_out_cap}) filled up between drains")
+        self._dropped_seen = dropped
+        E, n, dev = min(queued, self._selfplay_out_cap), self.e.n, self.e.device
         out = {
             "board": torch.empty((E, self.e.rows, 7), dtype=torch.int8, device=dev),
             "pi": torch.empty((E, ACTIONS), dtype=torch.float32, device=dev),
@@ -100,7 +124,8 @@ class SelfPlay(BatchedMCTS):
         h = self.headers()
         return {"games_done": int(h["games_done"].sum()), "moves": int(h["pad0"].sum()),
                 "overflow": int((h["overflow"] != 0).sum()),
-                "nodes_max": int(h["node_count"].max()), "edges_max": int(h["edge_count"].max())}
+                "nodes_max": int(h["node_count"].max()), "edges_max": int(h["edge_count"].max()),
+                **self.capacity_events(h), "examples_dropped": self.dropped_examples()}
 
 
 def gather_examples(examples, group=None):

@@ -95,7 +95,8 @@ def cpu_baseline_selfplay(n, seed, args, target_s=4.0):
     p8, pf = ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(ctypes.c_float)
     L.or_selfplay_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32,
                                   ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
-                                  ctypes.c_int, ctypes.c_int, p8, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, p8,
+                                  ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
                                   p8, pf, ctypes.POINTER(ctypes.c_uint64), pf, ctypes.POINTER(ctypes.c_int32), pf,
                                   ctypes.POINTER(ctypes.c_int32)]
     L.or_selfplay_run.restype = ctypes.c_int
@@ -110,7 +111,7 @@ def cpu_baseline_selfplay(n, seed, args, target_s=4.0):
         t = time.perf_counter()
         L.or_selfplay_run(n, B, iters, seed, 0, g["numMCTSSims"], g["ratio_fullMCTS"], g["prob_fullMCTS"],
                           g["cpuct"], g["fpu"], int(g["forced_playouts"]), g["tempThreshold"],
-                          board.ctypes.data_as(p8), hdr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 0,
+                          g["dirichletAlpha"], g["temperature"][0], board.ctypes.data_as(p8), hdr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 0,
                           None, None, None, None, None, None, None)
         return time.perf_counter() - t
 

@@ -158,6 +158,10 @@ typedef struct {
 
 int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_mcts **out);
 int spl_mcts_destroy(spl_mcts *m);
+/* HBM bytes of the whole search arena: trees (node_cap nodes, edge_cap edges, hash table,
+ * path per tree) + self-play buffers. plan_bytes: the same figure before creating it (pool
+ * sizing by the caller); device_bytes: of a created arena. */
+long long spl_mcts_plan_bytes(const spl_ctx *ctx, int B, const spl_mcts_config *cfg);
 long long spl_mcts_device_bytes(const spl_mcts *m);
 /* roots: B canonical boards (device). keep_tree: look the root up in the persistent
  * transposition table and keep its subtree (exact GC of unreachable nodes). */
@@ -184,6 +188,10 @@ int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, con
 /* counts B x 409 i64 (root visit counts Nsa), qsa B x 409 f64 (-42 = unvisited), probs
  * B x 409 f64 (temp = 1), q B x n f64, adjusted B x 409 i64 (counts after policy-target
  * pruning, MCTS.py:69-74; = counts without forced playouts); any may be NULL */
+/* ps: B x 409 f32, the root's stored priors Ps (nodes_data[s][2], MCTS.py:147/176: after
+ * root Dirichlet noise when it was applied), 0 for illegal actions and for trees without a
+ * root. */
+int spl_mcts_root_priors(spl_mcts *m, float *ps, void *hip_stream);
 int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs, double *q,
                         int64_t *adjusted, void *hip_stream);
 /* ---- self-play (Coach.executeEpisode, Coach.py:50-100), selfplay=1 only ----
@@ -202,6 +210,10 @@ int spl_mcts_commit(spl_mcts *m, void *hip_stream);
  * (global board id, game number, example index in game, player)), write the count to
  * *n_out (device int32) and empty the queue (examples beyond `max` are dropped). Any
  * output pointer may be NULL. */
+/* out (device, 2 x i32): [0] finished examples waiting in the queue, [1] examples dropped
+ * so far because the queue (out_cap) was full when their game ended or a drain asked for
+ * fewer than were queued. Self-play arenas only. */
+int spl_mcts_counters(spl_mcts *m, int32_t *out, void *hip_stream);
 int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *valid,
                             float *winner, int32_t *scdiff, float *q, int32_t *meta, int max,
                             int32_t *n_out, void *hip_stream);

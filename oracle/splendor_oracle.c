@@ -534,6 +534,116 @@ static float pw_sum(const float *a, int len) {   /* numpy pairwise_sum, float32 
 }
 float or_np_sum_f32(const float *x, int len) { return pw_sum(x, len); }
 
+static double pw_sum_f64(const double *a, int len) {   /* numpy pairwise_sum, float64 */
+    if (len < 8) { double r = 0.0; for (int i = 0; i < len; i++) r += a[i]; return r; }
+    if (len <= 128) {
+        double r[8]; int i;
+        for (int j = 0; j < 8; j++) r[j] = a[j];
+        for (i = 8; i < len - (len % 8); i += 8) for (int j = 0; j < 8; j++) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < len; i++) res += a[i];
+        return res;
+    }
+    int n2 = len / 2; n2 -= n2 % 8;
+    return pw_sum_f64(a, n2) + pw_sum_f64(a + n2, len - n2);
+}
+
+/* ------------------------------------------------------------------ Dirichlet noise
+ * The reference draws Dirichlet noise from an unseeded numpy Generator (MCTS.py:40,181),
+ * so the sampler itself is this build's own definition, shared bit-for-bit with the
+ * device (csrc/mcts_device.h det_*) and with tests/golden/detrand.py: logarithm and
+ * exponential from +,-,*,/ only (no libm, so host and device agree), Marsaglia-Tsang Gamma
+ * with polar normals on the Philox stream (seed, board, stream), counters i*4096 for the
+ * i-th legal action, normalised as numpy's Generator.dirichlet does (sequential sum,
+ * multiply by its reciprocal). What the reference does with the vector — softmax(Ps, T0)
+ * (MCTS.py:245-250, float64 as Numba types Ps ** (1./T)), the 0.75/0.25 mix over the
+ * valid actions (:180-186, float64 then stored float32) and normalise (:239-242) — is
+ * pinned against the reference by tests/golden/noise_*.npz. */
+#define DET_LN2_HI 6.93147180369123816490e-01
+#define DET_LN2_LO 1.90821492927058770002e-10
+#define DET_INV_LN2 1.44269504088896338700e+00
+#define DET_SQRT2 1.4142135623730951
+
+static double det_log(double x) {          /* x > 0, normal */
+    uint64_t b; memcpy(&b, &x, 8);
+    int e = (int)((b >> 52) & 0x7ff) - 1023;
+    uint64_t mb = (b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+    double m; memcpy(&m, &mb, 8);
+    if (m > DET_SQRT2) { m = m * 0.5; e = e + 1; }
+    double f = (m - 1.0) / (m + 1.0), s = f * f;
+    double p = 1.0 / 23.0;
+    p = p * s + 1.0 / 21.0; p = p * s + 1.0 / 19.0; p = p * s + 1.0 / 17.0;
+    p = p * s + 1.0 / 15.0; p = p * s + 1.0 / 13.0; p = p * s + 1.0 / 11.0;
+    p = p * s + 1.0 / 9.0; p = p * s + 1.0 / 7.0; p = p * s + 1.0 / 5.0; p = p * s + 1.0 / 3.0;
+    double t = 2.0 * f, r = t + t * (s * p);
+    return (double)e * DET_LN2_HI + (r + (double)e * DET_LN2_LO);
+}
+static double det_exp(double x) {
+    if (x < -700.0) return 0.0;
+    double kf = floor(x * DET_INV_LN2 + 0.5);
+    double r = (x - kf * DET_LN2_HI) - kf * DET_LN2_LO;
+    double p = 1.0 / 6227020800.0;
+    p = p * r + 1.0 / 479001600.0; p = p * r + 1.0 / 39916800.0; p = p * r + 1.0 / 3628800.0;
+    p = p * r + 1.0 / 362880.0; p = p * r + 1.0 / 40320.0; p = p * r + 1.0 / 5040.0;
+    p = p * r + 1.0 / 720.0; p = p * r + 1.0 / 120.0; p = p * r + 1.0 / 24.0;
+    p = p * r + 1.0 / 6.0; p = p * r + 0.5; p = p * r + 1.0; p = p * r + 1.0;
+    return ldexp(p, (int)kf);
+}
+static double det_pow(double x, double y) { return x == 0.0 ? 0.0 : det_exp(y * det_log(x)); }
+
+static double det_gamma(double alpha, uint64_t seed, uint32_t board, uint32_t stream, uint32_t ctr) {
+    const double a = alpha < 1.0 ? alpha + 1.0 : alpha;
+    const double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
+    double g = 0.0;
+    for (int it = 0; it < 64; it++) {
+        double z = 0.0;
+        for (int j = 0; j < 16; j++) {
+            double u1 = 2.0 * or_uniform(seed, board, stream, ctr++) - 1.0;
+            double u2 = 2.0 * or_uniform(seed, board, stream, ctr++) - 1.0;
+            double s = u1 * u1 + u2 * u2;
+            if (s < 1.0 && s > 0.0) { z = u1 * sqrt(-2.0 * det_log(s) / s); break; }
+        }
+        double v = 1.0 + c * z;
+        if (v <= 0.0) continue;
+        v = v * v * v;
+        double u = or_uniform(seed, board, stream, ctr++);
+        if (u < 1e-300) u = 1e-300;
+        if (det_log(u) < 0.5 * z * z + d - d * v + d * det_log(v)) { g = d * v; break; }
+    }
+    if (alpha < 1.0) {
+        double u = or_uniform(seed, board, stream, ctr++);
+        if (u < 1e-300) u = 1e-300;
+        g = g * det_exp(det_log(u) / alpha);
+    }
+    return g;
+}
+
+void or_dirichlet(double alpha, uint64_t seed, uint32_t board, uint32_t stream, int count, double *out) {
+    double acc = 0.0;
+    for (int i = 0; i < count; i++) {
+        out[i] = det_gamma(alpha, seed, board, stream, (uint32_t)i * 4096u);
+        acc = acc + out[i];
+    }
+    if (acc > 0.0) { double inv = 1.0 / acc; for (int i = 0; i < count; i++) out[i] = out[i] * inv; }
+    else for (int i = 0; i < count; i++) out[i] = 1.0 / (double)count;
+}
+
+/* softmax(Ps, T0) -> applyDirNoise(Ps, Vs) -> normalise(Ps) (MCTS.py:141-144 / :150-154)
+ * on ps[409] in place, dir[] = one value per valid action in action order. */
+void or_root_noise(float *ps, const uint8_t *vs, const double *dir, double temp0) {
+    if (temp0 != 1.0) {                                 /* softmax (:245-250) */
+        double sp[409];
+        for (int a = 0; a < 409; a++) sp[a] = det_pow((double)ps[a], 1.0 / temp0);
+        double s = pw_sum_f64(sp, 409);
+        for (int a = 0; a < 409; a++) ps[a] = (float)(sp[a] / s);
+    }
+    int k = 0;                                          /* applyDirNoise (:180-186) */
+    for (int a = 0; a < 409; a++)
+        if (vs[a]) { ps[a] = (float)(0.75 * (double)ps[a] + 0.25 * dir[k]); k++; }
+    float sum = pw_sum(ps, 409);                        /* normalise (:239-242) */
+    for (int a = 0; a < 409; a++) ps[a] = ps[a] / sum;
+}
+
 /* ------------------------------------------------------------------ MCTS */
 #define NAN_Q (-42.0)
 typedef struct {
@@ -553,6 +663,10 @@ struct or_mcts {
     double cpuct, fpu;
     node_t **slots; int cap, count;
     int step;
+    /* root Dirichlet noise (MCTS.py:58, :141-154): applied at step 0 when alpha > 0 */
+    double dir_alpha, dir_temp;
+    uint64_t dir_seed; uint32_t dir_board, dir_stream;
+    int neg_v;                /* second hash network (values negated), arena fixtures */
 };
 
 or_mcts *or_mcts_new(int n, int sims, double cpuct, double fpu, int forced) {
@@ -562,6 +676,19 @@ or_mcts *or_mcts_new(int n, int sims, double cpuct, double fpu, int forced) {
     m->forced = forced; m->cap = 1 << 12;
     m->slots = (node_t **)calloc((size_t)m->cap, sizeof(node_t *));
     return m;
+}
+void or_mcts_set_noise(or_mcts *m, double alpha, double temp0, uint64_t seed, uint32_t board,
+                       uint32_t stream) {
+    m->dir_alpha = alpha; m->dir_temp = temp0; m->dir_seed = seed; m->dir_board = board;
+    m->dir_stream = stream;
+}
+void or_mcts_set_net(or_mcts *m, int neg_v) { m->neg_v = neg_v; }
+static void mcts_noise(or_mcts *m, node_t *nd) {
+    double dir[409];
+    int cnt = 0;
+    for (int a = 0; a < 409; a++) cnt += nd->vs[a] != 0;
+    or_dirichlet(m->dir_alpha, m->dir_seed, m->dir_board, m->dir_stream, cnt, dir);
+    or_root_noise(nd->ps, nd->vs, dir, m->dir_temp);
 }
 void or_mcts_free(or_mcts *m) {
     for (int i = 0; i < m->cap; i++) if (m->slots[i]) { free(m->slots[i]->key); free(m->slots[i]); }
@@ -603,7 +730,7 @@ static int pick_ucb(or_mcts *m, node_t *nd, int forced) {
     return ba;
 }
 
-static void search(or_mcts *m, const int8_t *st, int forced, float *vout) {
+static void search(or_mcts *m, const int8_t *st, int forced, int noise, float *vout) {
     int n = m->n;
     node_t *nd = *lookup(m, st);
     if (!nd) {
@@ -617,18 +744,23 @@ static void search(or_mcts *m, const int8_t *st, int forced, float *vout) {
         or_valid_moves(n, st, 0, nd->vs);
         float v[4];
         or_fake_predict(n, st, nd->vs, nd->ps, v);
-        float sum = pw_sum(nd->ps, 409);        /* normalise (MCTS.py:239-242) */
-        for (int a = 0; a < 409; a++) nd->ps[a] = nd->ps[a] / sum;
+        if (m->neg_v) for (int i = 0; i < n; i++) v[i] = -v[i];
+        if (noise) mcts_noise(m, nd);           /* softmax + noise + normalise (:141-144) */
+        else {
+            float sum = pw_sum(nd->ps, 409);    /* normalise (MCTS.py:239-242) */
+            for (int a = 0; a < 409; a++) nd->ps[a] = nd->ps[a] / sum;
+        }
         nd->has_ps = 1; nd->ns = 0; nd->qs = (double)v[0];
         for (int a = 0; a < 409; a++) { nd->qsa[a] = NAN_Q; nd->nsa[a] = 0; }
         memcpy(vout, v, sizeof(float) * n);
         return;
     }
+    if (noise) mcts_noise(m, nd);               /* re-noised stored priors (:150-154) */
     int a = pick_ucb(m, nd, forced);
     int8_t *child = (int8_t *)malloc((size_t)m->S);
     int nxt = or_tree_step(n, st, a, child);
     float vc[4];
-    search(m, child, 0, vc);
+    search(m, child, 0, 0, vc);
     free(child);
     nd = *lookup(m, st);                       /* table may have been rehashed */
     for (int i = 0; i < n; i++) vout[i] = vc[((i - nxt) % n + n) % n];   /* np.roll */
@@ -641,7 +773,8 @@ static void search(or_mcts *m, const int8_t *st, int forced, float *vout) {
 int or_mcts_search(or_mcts *m, const int8_t *root, int64_t *counts, double *qsa,
                    double *probs, double *q) {
     float v[4];
-    for (m->step = 0; m->step < m->sims; m->step++) search(m, root, m->forced, v);
+    for (m->step = 0; m->step < m->sims; m->step++)
+        search(m, root, m->forced, m->step == 0 && m->dir_alpha > 0, v);
     node_t *nd = *lookup(m, root);
     long long c[409], best = 0;
     for (int a = 0; a < 409; a++) { c[a] = nd->nsa[a]; if (c[a] > best) best = c[a]; }
@@ -667,8 +800,10 @@ int or_mcts_search(or_mcts *m, const int8_t *root, int64_t *counts, double *qsa,
  * one MCTS simulation per iteration per game; when a search's budget is spent the move is
  * committed. Random decisions use Philox streams shared with the device:
  *   full/fast search ST_FULL|move, action pick ST_PICK|move, chance ST_MOVE|move,
- *   deals ST_DEAL|game. Dirichlet noise off (the device's is distributional only). */
+ *   deals ST_DEAL|game, root Dirichlet noise ST_DIR|move (at the first simulation of a
+ *   full search when dir_alpha > 0). */
 #define ST_FULL (1u << 24)
+#define ST_DIR  (2u << 24)
 #define ST_PICK (3u << 24)
 #define ST_MOVE (4u << 24)
 #define ST_DEAL (5u << 24)
@@ -697,9 +832,9 @@ typedef struct {
 
 int or_selfplay_run(int n, int B, int iters, uint64_t seed, uint32_t board_base, int num_sims,
                     int ratio_full, double prob_full, double cpuct, double fpu, int forced_po,
-                    int temp_threshold, int8_t *board_out, int32_t *hdr_out, int max_ex,
-                    int8_t *ex_state, float *ex_pi, uint64_t *ex_valid, float *ex_winner,
-                    int32_t *ex_scdiff, float *ex_q, int32_t *ex_meta) {
+                    int temp_threshold, double dir_alpha, double dir_temp, int8_t *board_out,
+                    int32_t *hdr_out, int max_ex, int8_t *ex_state, float *ex_pi, uint64_t *ex_valid,
+                    float *ex_winner, int32_t *ex_scdiff, float *ex_q, int32_t *ex_meta) {
     build_tables();
     int S = 7 * or_rows(n), n_out = 0;
     or_ex_t *stage = (or_ex_t *)malloc(sizeof(or_ex_t) * (62 * n + 2));
@@ -720,12 +855,13 @@ int or_selfplay_run(int n, int B, int iters, uint64_t seed, uint32_t board_base,
             move_no++;                                                                 \
             budget = full ? num_sims : num_sims / ratio_full;                          \
             forced = full && forced_po; sims_done = 0;                                 \
+            or_mcts_set_noise(m, dir_alpha, dir_temp, seed, gb, ST_DIR | (uint32_t)move_no); \
         } while (0)
         BEGIN_SEARCH();
         for (int it = 0; it < iters; it++) {
             float v[4];
             m->step = sims_done;
-            search(m, canon, forced, v);
+            search(m, canon, forced, sims_done == 0 && full && dir_alpha > 0, v);
             sims_done++;
             if (sims_done < budget) continue;
             /* commit */

@@ -57,10 +57,22 @@ void or_fake_predict(int n, const int8_t *state, const uint8_t *valids, float *p
 /* numpy float32 pairwise sum (np.sum order, pinned in tests) */
 float or_np_sum_f32(const float *x, int len);
 
-/* Sequential MCTS (one tree), fake network. Mirrors MCTS.getActionProb with
- * dirichlet noise off. Tree persists across calls until or_mcts_free. */
+/* Root Dirichlet noise (MCTS.py:141-154, 180-186, 239-250). or_dirichlet: this build's
+ * Philox Gamma sampler (counters i*4096 for valid action i), normalised like numpy's
+ * Generator.dirichlet. or_root_noise: softmax(ps, temp0) -> 0.75/0.25 mix with dir over the
+ * valid actions -> normalise, in place on ps[409]. */
+void or_dirichlet(double alpha, uint64_t seed, uint32_t board, uint32_t stream, int count, double *out);
+void or_root_noise(float *ps, const uint8_t *vs, const double *dir, double temp0);
+
+/* Sequential MCTS (one tree), fake network. Mirrors MCTS.getActionProb; root noise when
+ * or_mcts_set_noise gave alpha > 0 (applied at step 0 of every search). Tree persists
+ * across calls until or_mcts_free. */
 typedef struct or_mcts or_mcts;
 or_mcts *or_mcts_new(int n, int num_sims, double cpuct, double fpu, int forced_playouts);
+/* neg_v: the hash network with negated values (a second, different network) */
+void     or_mcts_set_net(or_mcts *m, int neg_v);
+void     or_mcts_set_noise(or_mcts *m, double alpha, double temp0, uint64_t seed, uint32_t board,
+                           uint32_t stream);
 void     or_mcts_free(or_mcts *m);
 /* runs a full search from root (canonical). counts[409] (int64), qsa[409] (f64),
  * probs[409] (f64, temp=1), q[n] (f64). Returns number of nodes in the table. */
@@ -73,9 +85,9 @@ int or_mcts_search(or_mcts *m, const int8_t *root, int64_t *counts, double *qsa,
  * games_done, moves, sims_done, budget). */
 int or_selfplay_run(int n, int B, int iters, uint64_t seed, uint32_t board_base, int num_sims,
                     int ratio_full, double prob_full, double cpuct, double fpu, int forced_po,
-                    int temp_threshold, int8_t *board_out, int32_t *hdr_out, int max_ex,
-                    int8_t *ex_state, float *ex_pi, uint64_t *ex_valid, float *ex_winner,
-                    int32_t *ex_scdiff, float *ex_q, int32_t *ex_meta);
+                    int temp_threshold, double dir_alpha, double dir_temp, int8_t *board_out,
+                    int32_t *hdr_out, int max_ex, int8_t *ex_state, float *ex_pi, uint64_t *ex_valid,
+                    float *ex_winner, int32_t *ex_scdiff, float *ex_q, int32_t *ex_meta);
 
 /* random-policy rollout loop used as the CPU baseline: B boards, steps steps each,
  * mask -> uniform valid action -> chance step -> end check -> reset on end.

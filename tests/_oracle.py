@@ -43,6 +43,10 @@ def lib():
         L.or_mcts_new.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, C.c_int]
         L.or_mcts_new.restype = C.c_void_p
         L.or_mcts_free.argtypes = [C.c_void_p]
+        L.or_mcts_set_net.argtypes = [C.c_void_p, C.c_int]
+        L.or_mcts_set_noise.argtypes = [C.c_void_p, C.c_double, C.c_double, C.c_uint64, C.c_uint32, C.c_uint32]
+        L.or_dirichlet.argtypes = [C.c_double, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, pd]
+        L.or_root_noise.argtypes = [pf, pu8, pd, C.c_double]
         L.or_mcts_search.argtypes = [C.c_void_p, p8, C.POINTER(C.c_int64), pd, pd, pd]
         L.or_random_rollouts.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int]
         L.or_random_rollouts.restype = C.c_longlong
@@ -50,7 +54,8 @@ def lib():
                                      C.POINTER(C.c_int16), pf, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
         L.or_rollout_run.restype = C.c_longlong
         L.or_selfplay_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint32, C.c_int, C.c_int,
-                                      C.c_double, C.c_double, C.c_double, C.c_int, C.c_int, p8,
+                                      C.c_double, C.c_double, C.c_double, C.c_int, C.c_int, C.c_double,
+                                      C.c_double, p8,
                                       C.POINTER(C.c_int32), C.c_int, p8, pf, C.POINTER(C.c_uint64), pf,
                                       C.POINTER(C.c_int32), pf, C.POINTER(C.c_int32)]
         L.or_selfplay_run.restype = C.c_int
@@ -153,10 +158,31 @@ def np_sum_f32(x):
     return np.float32(lib().or_np_sum_f32(_p(x, C.c_float), len(x)))
 
 
+def dirichlet(alpha, seed, board, stream, count):
+    out = np.zeros(max(count, 1), np.float64)
+    lib().or_dirichlet(alpha, seed, board, stream, count, _p(out, C.c_double))
+    return out[:count]
+
+
+def root_noise(ps, vs, dir_values, temp0):
+    """softmax(ps, temp0) -> applyDirNoise -> normalise (MCTS.py:141-144), returns float32[409]."""
+    p = np.array(ps, np.float32, copy=True)
+    va = np.ascontiguousarray(vs, np.uint8)
+    d = np.ascontiguousarray(np.concatenate([np.asarray(dir_values, np.float64), [0.0]]))
+    lib().or_root_noise(_p(p, C.c_float), _p(va, C.c_uint8), _p(d, C.c_double), float(temp0))
+    return p
+
+
 class Mcts:
     def __init__(self, n, sims, cpuct, fpu, forced):
         self.n = n
         self.h = lib().or_mcts_new(n, sims, cpuct, fpu, int(forced))
+
+    def set_net(self, neg_v):
+        lib().or_mcts_set_net(self.h, int(neg_v))
+
+    def set_noise(self, alpha, temp0, seed, board, stream):
+        lib().or_mcts_set_noise(self.h, alpha, temp0, seed, board, stream)
 
     def search(self, root):
         st = np.ascontiguousarray(root, np.int8)
@@ -194,7 +220,7 @@ def rollout_run(n, B, steps, seed, board_base=0):
 
 
 def selfplay_run(n, B, iters, seed, num_sims, ratio_full, prob_full, cpuct, fpu, forced, temp_threshold,
-                 board_base=0, max_ex=20000):
+                 board_base=0, max_ex=20000, dir_alpha=0.0, dir_temp=1.25):
     """Oracle of the device self-play loop (spl_mcts_commit semantics)."""
     R = rows(n)
     board = np.zeros((B, R, 7), np.int8)
@@ -207,9 +233,55 @@ def selfplay_run(n, B, iters, seed, num_sims, ratio_full, prob_full, cpuct, fpu,
     q = np.zeros((max_ex, n), np.float32)
     meta = np.zeros((max_ex, 4), np.int32)
     k = lib().or_selfplay_run(n, B, iters, seed, board_base, num_sims, ratio_full, prob_full, cpuct, fpu,
-                              int(forced), temp_threshold, _p(board, C.c_int8), _p(hdr, C.c_int32), max_ex,
+                              int(forced), temp_threshold, dir_alpha, dir_temp, _p(board, C.c_int8), _p(hdr, C.c_int32), max_ex,
                               _p(st, C.c_int8), _p(pi, C.c_float), _p(va, C.c_uint64), _p(win, C.c_float),
                               _p(sd, C.c_int32), _p(q, C.c_float), _p(meta, C.c_int32))
     k = min(k, max_ex)
     return {"board": board, "hdr": hdr, "ex_board": st[:k], "pi": pi[:k], "valids": va[:k],
             "winner": win[:k], "scdiff": sd[:k], "surprise": q[:k], "meta": meta[:k]}
+
+
+ST_FULL, ST_DIR, ST_PICK, ST_MOVE, ST_DEAL, ST_BEST = (1 << 24), (2 << 24), (3 << 24), (4 << 24), (5 << 24), (6 << 24)
+DEAL_DRAWS = 29
+
+
+def one_vs_two(i):
+    """Arena.py:199: player 1 moves first in games i % 4 in (0, 3)."""
+    return (i % 4 == 0) or (i % 4 == 3)
+
+
+def arena_play(n, G, sims, cpuct, fpu, seed, neg2=False):
+    """Sequential restatement of Arena.playGames (Arena.py:64-227) on the oracle: per game
+    two persistent trees (reset between games), temp-0 moves = the best root count with the
+    Philox tie-break (seed ^ (k+1), game, ST_BEST | ply), chance (seed, game, ply), deal
+    (seed, game, 0xFFFFFFFF); seats [p1] + [p2] * (n - 1) or the mirror. Player 2's network
+    negates values when neg2. Returns per game (result vector, plies, scores, actions)."""
+    out = []
+    for gid in range(G):
+        st, _ = init(n, [uniform(seed, gid, 0xFFFFFFFF, k) for k in range(DEAL_DRAWS)])
+        seats = [0] + [1] * (n - 1) if one_vs_two(gid) else [1] + [0] * (n - 1)
+        trees = [Mcts(n, sims, cpuct, fpu, False) for _ in range(2)]
+        if neg2:
+            trees[1].set_net(1)
+        result, plies, actions = np.zeros(n, np.float32), 0, []
+        for ply in range(62 * n * 2 + 8):
+            cur = ply % n
+            canon = swap_players(n, st, cur) if cur else st.copy()
+            k = seats[cur]
+            counts = trees[k].search(canon)[0]
+            u = uniform(seed ^ (k + 1), gid, ST_BEST | ply, 0)
+            top = counts.max()
+            if top == 0:
+                a = int(u * 409)
+            else:
+                best = np.flatnonzero(counts == top)
+                a = int(best[int(u * len(best))])
+            assert valid_moves(n, canon, 0)[a]
+            actions.append(a)
+            st, _, _ = make_move(n, st, a, cur, False, [uniform(seed, gid, ply, d) for d in range(8)])
+            r = check_end(n, st)
+            if r.any():
+                result, plies = r, ply + 1
+                break
+        out.append((result, plies, [score(n, st, p) for p in range(n)], actions))
+    return out

@@ -24,10 +24,21 @@ float32 arithmetic where the deployed code does float64; these restore the deplo
       f64 -> call it with Ps as float64 and Qs/Ns/cpuct/fpu as Python floats.
   P7  MCTS.py:172      Qs update (plain Python, NumPy 1.x legacy promotion = float64).
   P8  MCTS.py:71       policy-target pruning sqrt(k*Psa*sims) in float64.
+  P9  MCTS.py:248      softmax is @njit: Numba types Ps (f32) ** (1./T) (f64) as float64, so
+                       the power is taken in float64 (then normalised and cast to float32).
+  P10 MCTS.py:185      applyDirNoise under NumPy 1.x scalar rules: float32 Ps[idx] * 0.75 is
+                       float64, the mix is float64 and stored into the float32 Ps.
 Chance injection (the reference is unseeded):
   np.random.random -> pops the next double of an injected uniform stream.
   np.random.choice(10, k, replace=False) (noble draw, SplendorLogicNumba.py:241) ->
       partial Fisher-Yates driven by the same stream: for i<k: j=i+floor(u*(10-i)).
+  np.random.choice(n, p=p) (Coach.random_pick, Coach.py:32) -> numpy's legacy algorithm
+      (cdf = cumsum(p) / cdf[-1], searchsorted(cdf, u, 'right')) on one injected uniform;
+      checked against numpy's RandomState.choice at start-up.
+  np.random.choice(bestAs) (MCTS.py:89, temp-0 tie-break) -> bestAs[floor(u * len)].
+  MCTS.rng.random / MCTS.rng.dirichlet (MCTS.py:54, :181) -> the keyed Philox draws of the
+      device / oracle (tests/golden/detrand.py), so whole episodes (Coach.executeEpisode)
+      and arena games (Arena.playGames) replay with the build's random streams.
 
 Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz)
 """
@@ -40,6 +51,8 @@ import numpy as np
 
 REF = "/root/reference"
 OUT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, OUT)
+import detrand  # noqa: E402
 
 
 # ----------------------------------------------------------------------------- shims
@@ -131,6 +144,10 @@ def load_reference():
              "Qs = ((Ns+1) * float(Qs) + float(v[0])) / (Ns+2)"),  # P7
             ("Psas   = [self.nodes_data[s][2][a] for a",
              "Psas   = [float(self.nodes_data[s][2][a]) for a"),  # P8
+            ("result = Ps ** (1. / softmax_temp)",
+             "result = np.asarray(Ps, dtype=np.float64) ** (1. / softmax_temp)"),  # P9
+            ("Ps[idx] = (0.75 * Ps[idx]) + (0.25 * dir_values[dir_idx])",
+             "Ps[idx] = (0.75 * float(Ps[idx])) + (0.25 * float(dir_values[dir_idx]))"),  # P10
         ])
     orig_ucb = mcts_mod.pick_highest_UCB
 
@@ -148,6 +165,8 @@ class UniformStream:
     def __init__(self):
         self.src = None
         self.used = []
+        self.pick = None      # source of Coach.random_pick's uniform
+        self.tie = None       # source of the temp-0 tie-break uniform
 
     def set_source(self, rng):
         self.src = rng
@@ -160,7 +179,14 @@ class UniformStream:
         return u
 
     def choice(self, a, size=None, replace=True, p=None):
-        assert replace is False and p is None and isinstance(a, (int, np.integer))
+        if p is not None:                       # Coach.random_pick: legacy choice with p
+            assert size is None and isinstance(a, (int, np.integer))
+            return legacy_choice_p(int(a), p, self.pick.random())
+        if not isinstance(a, (int, np.integer)):   # MCTS.py:89 tie-break over bestAs
+            assert size is None
+            a = np.asarray(a)
+            return a[int(self.tie.random() * len(a))]
+        assert replace is False
         perm = list(range(int(a)))
         for i in range(int(size)):
             u = self.random()
@@ -170,6 +196,44 @@ class UniformStream:
 
 
 STREAM = UniformStream()
+
+
+def legacy_choice_p(n, p, u):
+    """numpy RandomState.choice(n, p=p) given its one uniform draw u (mtrand.pyx: cdf =
+    p.cumsum(); cdf /= cdf[-1]; cdf.searchsorted(u, side='right'))."""
+    p = np.asarray(p, dtype=np.float64)
+    assert len(p) == n and np.all(p >= 0) and abs(p.sum() - 1.0) <= math.sqrt(np.finfo(np.float64).eps)
+    cdf = np.cumsum(p)
+    cdf /= cdf[-1]
+    return int(np.searchsorted(cdf, u, side="right"))
+
+
+def _check_legacy_choice():
+    rng = np.random.default_rng(5)
+    for t in range(200):
+        p = rng.random(409) * (rng.random(409) < 0.1)
+        p[rng.integers(409)] += 1e-3
+        p = list(p / p.sum())
+        a = np.random.RandomState(t).choice(409, p=p)
+        u = np.random.RandomState(t).random_sample()
+        assert a == legacy_choice_p(409, p, u), "legacy choice restatement mismatch"
+
+
+class InjectedRng:
+    """MCTS.rng replacement (MCTS.py:40): random() -> keyed full/fast draw, dirichlet() ->
+    the build's keyed Dirichlet sampler (detrand.dirichlet)."""
+
+    def __init__(self):
+        self.full = None          # (seed, board, stream) of the next rng.random()
+        self.dir = None           # (seed, board, stream) of the next rng.dirichlet()
+
+    def random(self):
+        return detrand.uniform(*self.full, 0)
+
+    def dirichlet(self, alphas):
+        alphas = list(alphas)
+        assert all(a == alphas[0] for a in alphas)
+        return np.array(detrand.dirichlet(float(alphas[0]), *self.dir, len(alphas)), dtype=np.float64)
 
 
 def _patch_np_random():
@@ -495,6 +559,266 @@ def nnet_fixture(n_players, boards):
             "n_params": np.array(sum(p.numel() for p in net.parameters()))}
 
 
+
+# ------------------------------------------------------------- noise / episode / arena
+ST_FULL, ST_DIR, ST_PICK, ST_MOVE, ST_DEAL, ST_BEST = (1 << 24), (2 << 24), (3 << 24), (4 << 24), (5 << 24), (6 << 24)
+GEM_TOTAL = {2: 4, 3: 5, 4: 7}
+
+
+class FakeNNetC(FakeNNet):
+    """FakeNNet with the NeuralNet constructor signature (Coach.py:44 builds a second one);
+    neg=True negates v (a second, different 'network' for arena games)."""
+
+    def __init__(self, game, args=None, neg=False):
+        super().__init__(game.num_players)
+        self.args = args or {}
+        self.neg = neg
+
+    def predict(self, board, valid_actions):
+        pi, v = super().predict(board, valid_actions)
+        return (pi, -v) if self.neg else (pi, v)
+
+
+def wide_roots(numba_logic, n, states):
+    """Canonical positions with the widest action sets: player 0 holds 2 gems of every colour
+    (10 tokens: every exchange family is open), the bank holds the rest of each colour and 5
+    gold. 4p positions reach 229 legal actions (> 3 x 64)."""
+    Board = numba_logic.Board
+    b = Board(n)
+    out = []
+    for st in states:
+        s_ = st.copy()
+        for p in range(n):
+            s_[32 + n + p, :6] = 0
+        s_[32 + n, :5] = 2
+        s_[0, :5] = GEM_TOTAL[n] - 2
+        s_[0, 5] = 5
+        b.copy_state(s_, True)
+        out.append((int(b.valid_moves(0).sum()), s_))
+    out.sort(key=lambda x: -x[0])
+    return [x[1] for x in out]
+
+
+def noise_fixtures(game_mod, mcts_mod, numba_logic, n, states, seed):
+    """softmax(Ps, T0) -> applyDirNoise -> normalise (MCTS.py:141-144) on raw network priors,
+    and on stored (normalised) priors (:150-154), with injected Dirichlet vectors."""
+    Game = game_mod.SplendorGame
+    Board = numba_logic.Board
+    b = Board(n)
+    rec = {k: [] for k in ("ps_in", "vs", "dir", "temp0", "alpha", "key", "ps_out", "stored")}
+    for i, st in enumerate(states):
+        b.copy_state(st, True)
+        vs = b.valid_moves(0)
+        raw, _ = fake_predict(st, vs, n)
+        for j, (t0, alpha, stored) in enumerate(((1.25, 0.3, False), (1.0, 0.3, False), (1.25, 0.2, True),
+                                                 (0.8, 1.5, True))):
+            ps = raw.copy()
+            if stored:
+                mcts_mod.normalise(ps)
+            key = (seed, i, ST_DIR | j)
+            dirv = np.array(detrand.dirichlet(alpha, *key, int(vs.sum())))
+            g = Game(n)
+            m = mcts_mod.MCTS(g, FakeNNet(n), _DotDict({"dirichletAlpha": alpha, "temperature": [t0, 0.8]}),
+                              dirichlet_noise=True)
+            m.rng = InjectedRng()
+            m.rng.dir = key
+            pin = ps.copy()
+            P = mcts_mod.softmax(ps, t0)
+            m.applyDirNoise(P, vs)
+            mcts_mod.normalise(P)
+            d409 = np.zeros(409)
+            d409[:len(dirv)] = dirv
+            rec["ps_in"].append(pin)
+            rec["vs"].append(vs.astype(np.uint8))
+            rec["dir"].append(d409)
+            rec["temp0"].append(t0)
+            rec["alpha"].append(alpha)
+            rec["key"].append(np.array(key, dtype=np.uint64))
+            rec["ps_out"].append(np.asarray(P, dtype=np.float32))
+            rec["stored"].append(int(stored))
+    return {k: np.array(v) for k, v in rec.items()}
+
+
+def noise_search_fixtures(game_mod, mcts_mod, n, roots, seed, cases):
+    """Full searches with root Dirichlet noise (MCTS.py:58-59), two searches per tree from
+    the same root (the second re-noises the stored priors, :150-154). Tree t of case c has
+    board id 100*c + t; search s (1, 2) draws its noise from (seed, board, ST_DIR | s)."""
+    Game = game_mod.SplendorGame
+    out = {k: [] for k in ("root", "case", "board", "sims", "cpuct", "fpu", "alpha", "temp0", "forced",
+                           "counts1", "qsa1", "probs1", "q1", "counts2", "qsa2", "probs2", "q2")}
+    for ci, (sims, cpuct, fpu, alpha, t0, forced) in enumerate(cases):
+        for t, root in enumerate(roots):
+            g = Game(n)
+            args = {"numMCTSSims": sims, "cpuct": cpuct, "fpu": fpu, "prob_fullMCTS": 1.0,
+                    "ratio_fullMCTS": 5, "forced_playouts": forced, "no_mem_optim": False,
+                    "dirichletAlpha": alpha, "temperature": [t0, 0.8]}
+            m = mcts_mod.MCTS(g, FakeNNet(n), _DotDict(args), dirichlet_noise=True)
+            m.rng = InjectedRng()
+            board = 100 * ci + t
+            s = g.stringRepresentation(root)
+            for k in (1, 2):
+                m.rng.dir = (seed, board, ST_DIR | k)
+                probs, q, _ = m.getActionProb(root.copy(), temp=1, force_full_search=True)
+                node = m.nodes_data[s]
+                out[f"counts{k}"].append(np.array(node[5], dtype=np.int64, copy=True))
+                out[f"qsa{k}"].append(np.array(node[4], dtype=np.float64, copy=True))
+                out[f"probs{k}"].append(np.asarray(probs, dtype=np.float64))
+                out[f"q{k}"].append(np.asarray(q, dtype=np.float64))
+            out["root"].append(root.copy())
+            out["case"].append(ci)
+            out["board"].append(board)
+            for key, val in (("sims", sims), ("cpuct", cpuct), ("fpu", fpu), ("alpha", alpha),
+                             ("temp0", t0), ("forced", int(forced))):
+                out[key].append(val)
+    return {k: np.array(v) for k, v in out.items()}
+
+
+def load_coach():
+    stub = types.ModuleType("Arena")
+    stub.Arena = object                      # executeEpisode does not use the Arena
+    sys.modules["Arena"] = stub
+    mod = _exec_module("Coach", f"{REF}/Coach.py")
+    del sys.modules["Arena"]
+    return mod
+
+
+def episode_fixtures(game_mod, coach_mod, n, seed, boards, args):
+    """Coach.executeEpisode (Coach.py:50-100), one game per board id, every random draw
+    injected from the build's keyed streams (move k of a game: full/fast draw ST_FULL|k,
+    Dirichlet ST_DIR|k+1, action pick ST_PICK|k+1, chance ST_MOVE|k+1; deal ST_DEAL|0)."""
+    Game = game_mod.SplendorGame
+    ex = {k: [] for k in ("board", "pi", "winner", "scdiff", "valids", "surprise", "game")}
+    games = {k: [] for k in ("board_id", "moves", "n_examples", "actions")}
+    for gi, gb in enumerate(boards):
+        STREAM.set_source(np.random.default_rng([seed, gb]))       # constructor's deal (unused)
+        g = Game(n)
+        c = coach_mod.Coach(g, FakeNNetC(g), _DotDict(args))
+        rng = InjectedRng()
+        c.mcts.rng = rng
+        st = {"k": 0}
+        actions = []
+        orig_gap, orig_next = c.mcts.getActionProb, g.getNextState
+
+        def gap(canon, temp=1, force_full_search=False, bias=None, _gb=gb):
+            k = st["k"]
+            rng.full = (seed, _gb, ST_FULL | k)
+            rng.dir = (seed, _gb, ST_DIR | (k + 1))
+            r = orig_gap(canon, temp=temp, force_full_search=force_full_search, bias=bias)
+            STREAM.pick = detrand.Stream(seed, _gb, ST_PICK | (k + 1))
+            STREAM.set_source(detrand.Stream(seed, _gb, ST_MOVE | (k + 1)))
+            st["k"] = k + 1
+            return r
+
+        def nxt(board, player, action, deterministic=False):
+            actions.append(int(action))
+            return orig_next(board, player, action, deterministic)
+        c.mcts.getActionProb = gap
+        g.getNextState = nxt
+        STREAM.set_source(detrand.Stream(seed, gb, ST_DEAL | 0))
+        out = c.executeEpisode()
+        for x in out:
+            ex["board"].append(np.asarray(x[0], dtype=np.int8))
+            ex["pi"].append(np.asarray(x[1], dtype=np.float32))
+            ex["winner"].append(np.asarray(x[2], dtype=np.float32))
+            ex["scdiff"].append(np.asarray(x[3], dtype=np.int32))
+            ex["valids"].append(np.asarray(x[4], dtype=np.uint8))
+            ex["surprise"].append(np.asarray(x[5], dtype=np.float64))
+            ex["game"].append(gi)
+        games["board_id"].append(gb)
+        games["moves"].append(st["k"])
+        games["n_examples"].append(len(out))
+        games["actions"].append(np.array(actions + [-1] * (400 - len(actions)), dtype=np.int16))
+    res = {k: np.array(v) for k, v in ex.items()}
+    res.update({"game_" + k: np.array(v) for k, v in games.items()})
+    for k, v in args.items():
+        res["arg_" + k] = np.array(v)
+    res["seed"] = np.array(seed, dtype=np.uint64)
+    return res
+
+
+def symmetry_fixtures(game_mod, n, states, seed):
+    """SplendorGame.getSymmetries (SplendorGame.py:59-61 -> SplendorLogicNumba.py:349-395)
+    on canonical positions with random policies; variants of position i are
+    [off[i], off[i+1])."""
+    g = game_mod.SplendorGame(n)
+    rng = np.random.default_rng(seed)
+    rec = {k: [] for k in ("src", "src_pi", "src_valids", "state", "pi", "valids")}
+    off = [0]
+    for st in states:
+        valid = g.getValidMoves(st, 0)
+        pi = (rng.random(409) * valid).astype(np.float32)
+        syms = g.getSymmetries(st, pi, valid)
+        rec["src"].append(st.copy())
+        rec["src_pi"].append(pi)
+        rec["src_valids"].append(np.asarray(valid, dtype=np.uint8))
+        for s_, p_, v_ in syms:
+            rec["state"].append(np.asarray(s_, dtype=np.int8).copy())
+            rec["pi"].append(np.asarray(p_, dtype=np.float32))
+            rec["valids"].append(np.asarray(v_, dtype=np.uint8))
+        off.append(len(rec["state"]))
+    res = {k: np.array(v) for k, v in rec.items()}
+    res["off"] = np.array(off)
+    return res
+
+
+def load_arena():
+    for name in ("splendor.NNet",):
+        stub = types.ModuleType(name)
+        stub.NNetWrapper = object            # Arena.py:10 imports it; playGames never uses it
+        sys.modules[name] = stub
+    _exec_module("utils", f"{REF}/utils.py")
+    return _exec_module("Arena", f"{REF}/Arena.py")
+
+
+def arena_fixtures(game_mod, mcts_mod, arena_mod, n, G, sims, cpuct, fpu, seed):
+    """Arena.playGames (Arena.py:175-227) between two MCTS players over different hash
+    networks (player 2 negates v), moves = argmax of getActionProb(temp=0, full search)
+    (Coach.py:152-153). Injected draws, keyed like BatchedArena: game g deal (seed, g,
+    0xFFFFFFFF), chance of ply p (seed, g, p), tie-break of player k (seed ^ (k+1), g,
+    ST_BEST | p)."""
+    Game = game_mod.SplendorGame
+    STREAM.set_source(np.random.default_rng([seed, 1]))
+    g = Game(n)
+    args = _DotDict({"numMCTSSims": sims, "cpuct": cpuct, "fpu": fpu, "prob_fullMCTS": 1.0,
+                     "ratio_fullMCTS": 5, "forced_playouts": False, "no_mem_optim": False,
+                     "dirichletAlpha": 0.0, "temperature": [1.25, 0.8], "lag": 0})
+    ctx = {"gid": -1, "ply": 0}
+    acts, results = [], []
+    nets = (FakeNNetC(g), FakeNNetC(g, neg=True))
+    trees = [mcts_mod.MCTS(g, nets[k], args) for k in range(2)]
+
+    def player_of(k):
+        def play(x):
+            ply = ctx["ply"]
+            STREAM.tie = detrand.Stream(seed ^ (k + 1), ctx["gid"], ST_BEST | ply)
+            a = int(np.argmax(trees[k].getActionProb(x, temp=0, force_full_search=True)[0]))
+            STREAM.set_source(detrand.Stream(seed, ctx["gid"], ply))
+            ctx["ply"] = ply + 1
+            acts[-1].append(a)
+            return a
+        return play
+    p1, p2 = player_of(0), player_of(1)
+    arena = arena_mod.Arena(p1, p2, p2 if n == 3 else None, g, args, no_record=True)
+    orig = arena.playGame
+
+    def play_game(verbose=False, other_way=False, cur_player=None, board=None, handi=None):
+        ctx["gid"] += 1
+        ctx["ply"] = 0
+        acts.append([])
+        STREAM.set_source(detrand.Stream(seed, ctx["gid"], 0xFFFFFFFF))
+        r = orig(verbose=verbose, other_way=other_way, cur_player=cur_player, board=board, handi=handi)
+        results.append([float(r[0]), float(r[1]), float(r[2])])
+        return r
+    arena.playGame = play_game
+    one, two, draws = arena.playGames(G)
+    L = max(len(a) for a in acts)
+    return {"one": np.array(one), "two": np.array(two), "draws": np.array(draws),
+            "result": np.array(results), "plies": np.array([len(a) for a in acts]),
+            "actions": np.array([a + [-1] * (L - len(a)) for a in acts], dtype=np.int16),
+            "sims": np.array(sims), "cpuct": np.array(cpuct), "fpu": np.array(fpu),
+            "seed": np.array(seed, dtype=np.uint64)}
+
+
 def main():
     logic, numba_logic, game_mod, mcts_mod = load_reference()
     _patch_np_random()
@@ -524,6 +848,40 @@ def main():
         mf = mcts_fixtures(game_mod, mcts_mod, numba_logic, n, seed=2000 + n, cases=cases)
         np.savez_compressed(os.path.join(OUT, f"mcts_{n}p.npz"), **mf)
         print(f"mcts {n}p: {len(mf['root'])} searches, seq moves {len(mf['seq_root'])}")
+    # round 2: root noise, episodes, symmetries, arena (injected keyed draws)
+    _check_legacy_choice()
+    for n in (2, 3, 4):
+        env = np.load(os.path.join(OUT, f"env_{n}p.npz"))
+        canon = env["canon"]
+        wide = wide_roots(numba_logic, n, canon[::11][:40])[:6]
+        nf = noise_fixtures(game_mod, mcts_mod, numba_logic, n, list(canon[::29][:8]) + wide, seed=3000 + n)
+        np.savez_compressed(os.path.join(OUT, f"noise_{n}p.npz"), **nf)
+        print(f"noise {n}p: {len(nf['ps_in'])} cases, max legal {int(nf['vs'].sum(1).max())}")
+        ncases = [(25, 1.5, 0.1, 0.3, 1.25, False), (60, 2.5, 0.3, 0.3, 1.25, True)]
+        roots = list(canon[::41][:4]) + wide[:2]
+        sf = noise_search_fixtures(game_mod, mcts_mod, n, roots, seed=3100 + n, cases=ncases)
+        np.savez_compressed(os.path.join(OUT, f"noisesearch_{n}p.npz"), **sf)
+        print(f"noise searches {n}p: {len(sf['root'])}")
+        rsv = [st for st in canon if np.any(st[32 + 2 * n + n * (n + 1) + n:] != 0)]
+        sym_states = list(canon[::23][:20]) + rsv[::max(1, len(rsv) // 20)][:20]
+        yf = symmetry_fixtures(game_mod, n, sym_states, seed=3200 + n)
+        np.savez_compressed(os.path.join(OUT, f"sym_{n}p.npz"), **yf)
+        print(f"symmetries {n}p: {len(yf['src'])} positions, {len(yf['state'])} variants")
+    coach_mod = load_coach()
+    eargs = {"numMCTSSims": 24, "cpuct": 1.5, "fpu": 0.1, "prob_fullMCTS": 0.5, "ratio_fullMCTS": 4,
+             "forced_playouts": False, "no_mem_optim": False, "dirichletAlpha": 0.3,
+             "temperature": [1.25, 0.8], "tempThreshold": 10, "no_compression": True}
+    for n, boards, forced in ((2, (3, 17), False), (2, (5,), True), (4, (2,), False)):
+        a = dict(eargs, forced_playouts=forced)
+        ef = episode_fixtures(game_mod, coach_mod, n, 0x5EED + n, boards, a)
+        tag = f"{n}p" + ("_forced" if forced else "")
+        np.savez_compressed(os.path.join(OUT, f"episode_{tag}.npz"), **ef)
+        print(f"episode {tag}: moves {ef['game_moves'].tolist()}, examples {ef['game_n_examples'].tolist()}")
+    arena_mod = load_arena()
+    for n, G, sims in ((2, 8, 8), (3, 4, 6)):
+        af = arena_fixtures(game_mod, mcts_mod, arena_mod, n, G, sims, 1.5, 0.1, seed=41 + n)
+        np.savez_compressed(os.path.join(OUT, f"arena_{n}p.npz"), **af)
+        print(f"arena {n}p: {int(af['one'])}-{int(af['two'])}-{int(af['draws'])}, plies {af['plies'].tolist()}")
 
 
 if __name__ == "__main__":

@@ -71,6 +71,45 @@ def test_arena_matches_oracle(n, G, sims):
     assert one + two + draws == G
 
 
+class NegatedHash:
+    """The reference fixture's second network: the hash network with values negated."""
+
+    def __init__(self, engine):
+        from splendor.mcts import HashEvaluator
+        self.h = HashEvaluator(engine)
+
+    def __call__(self, leaf_state, leaf_mask, leaf_valid):
+        pi, v = self.h(leaf_state, leaf_mask, leaf_valid)
+        return pi, -v
+
+
+@pytest.mark.parametrize("n", (2, 3))
+def test_arena_matches_reference(n):
+    """BatchedArena against Arena.playGames itself (tests/golden/arena_*.npz: the reference
+    run with two MCTS players over different hash networks and the build's keyed draws
+    injected): every move of every game, per-game results and the totals."""
+    import os
+    from splendor.SplendorGame import SplendorGame
+    from splendor.arena import BatchedArena
+    from splendor.mcts import HashEvaluator
+    with np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"arena_{n}p.npz")) as z:
+        d = {k: z[k] for k in z.files}
+    G = len(d["plies"])
+    g = SplendorGame(n)
+    args = dict(numMCTSSims=int(d["sims"]), cpuct=float(d["cpuct"]), fpu=float(d["fpu"]), arenaCompare=G)
+    ar = BatchedArena(g, None, None, args, batch=G, seed=int(d["seed"]),
+                      evaluators=(HashEvaluator(g.engine), NegatedHash(g.engine)))
+    one, two, draws = ar.playGames(G)
+    last = ar.last
+    for i in range(G):
+        p = int(d["plies"][i])
+        assert last["plies"][i] == p, f"game {i}"
+        np.testing.assert_array_equal(last["actions"][i][:p], d["actions"][i][:p], err_msg=f"game {i}")
+        assert [float(last["result"][i][0]), float(last["score"][i][0]), float(last["score"][i][1])] == \
+            list(d["result"][i])
+    assert (one, two, draws) == (int(d["one"]), int(d["two"]), int(d["draws"]))
+
+
 def test_arena_batches_and_gate():
     """Games split over several batches give the same per-game records as one batch with
     the same game ids; the Coach.learn acceptance rule."""

@@ -1,0 +1,162 @@
+"""BASELINE configs 4 and 5 on the GPU, and device sharding.
+
+* Sharding: every random draw is keyed by the global board id, so a shard of B' boards at
+  board_base = k * B' must reproduce, bit for bit, the matching slice of one launch over
+  all boards — for the fused rollout kernel (config 2) and for batched self-play (configs
+  3-5). This is what makes results independent of the GPU count.
+* Config 5 (4 players, 16,384 games, numMCTSSims=400, Dirichlet on): full-size self-play
+  with SplendorNNet leaves (property checks), and the slice equality plus the oracle on a
+  64-game slice with the hash network (bit-exact, noise included).
+* Config 4 per-GPU shard (2 players, 32,768 games, numMCTSSims=1600): full size with pools
+  planned against the device's memory; searches keep running under capacity pressure
+  (events counted, never a frozen tree), and the slice equality with the hash network.
+"""
+import gc
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import _oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+GENBU = dict(cpuct=2.5, fpu=0.3, prob_fullMCTS=0.25, ratio_fullMCTS=5, forced_playouts=False,
+             dirichletAlpha=0.3, temperature=[1.25, 0.8], tempThreshold=10)
+HDR_KEYS = ("player", "episode_step", "move_no", "game_no", "games_done", "sims_done", "budget", "full",
+            "node_count", "edge_count", "root", "pad0", "prunes", "resets", "unexpanded")
+
+
+def free_all():
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def test_rollout_shard_equals_slice():
+    """Config 2: 32,768 boards in one launch vs a 512-board shard at board_base 20,480."""
+    from splendor.env import RolloutBatch, SplendorEngine
+    e = SplendorEngine(2)
+    B, b0, Bs, K = 32768, 20480, 512, 150
+    full = RolloutBatch(e, B, seed=0x5EED)
+    fo = full.run(K)
+    shard = RolloutBatch(e, Bs, seed=0x5EED, board_base=b0)
+    so = shard.run(K)
+    torch.cuda.synchronize()
+    sl = slice(b0, b0 + Bs)
+    assert torch.equal(full.state[sl], shard.state)
+    assert torch.equal(full.player[sl], shard.player)
+    assert torch.equal(full.games[sl], shard.games)
+    assert torch.equal(fo["action"][:, sl], so["action"])
+    assert torch.equal(fo["mask"][:, sl], so["mask"])
+    assert torch.equal(fo["ended"][:, sl], so["ended"])
+    assert int(full.games.sum()) > 0
+
+
+def selfplay(n, B, sims, board_base=0, evaluator=None, **kw):
+    from splendor.env import SplendorEngine
+    from splendor.mcts import HashEvaluator
+    from splendor.selfplay import SelfPlay
+    e = SplendorEngine(n)
+    sp = SelfPlay(e, B, dict(GENBU, numMCTSSims=sims), evaluator=evaluator or HashEvaluator(e),
+                  dirichlet_noise=True, seed=0x5EED, board_base=board_base, **kw)
+    sp.reset()
+    return e, sp
+
+
+def assert_slice_equal(full, shard, b0):
+    hf, hs = full.headers(), shard.headers()
+    Bs = shard.B
+    for k in HDR_KEYS:
+        np.testing.assert_array_equal(hf[k][b0:b0 + Bs], hs[k], err_msg=k)
+    assert torch.equal(full.root_stats()[0][b0:b0 + Bs], shard.root_stats()[0])
+    assert torch.equal(full.root_priors()[b0:b0 + Bs], shard.root_priors())
+
+
+def test_config5_shard_equals_slice_and_oracle():
+    """4p, 16,384 games, 400 simulations, root noise: a 64-game shard equals the slice of
+    the full batch, and the oracle's self-play on those 64 board ids (bit-exact)."""
+    n, B, sims, iters, b0, Bs = 4, 16384, 400, 900, 8192, 64
+    caps = dict(node_cap=4096, edge_cap=4096 * 48)
+    _, full = selfplay(n, B, sims, **caps)
+    full.run(iters, use_graph=True)
+    _, shard = selfplay(n, Bs, sims, board_base=b0, **caps)
+    shard.run(iters, use_graph=True)
+    torch.cuda.synchronize()
+    assert_slice_equal(full, shard, b0)
+    st = full.stats()
+    assert st["overflow"] == 0 and st["moves"] > B and st["unexpanded"] == 0
+    assert st["prunes"] == st["resets"] == 0
+    del full
+    free_all()
+    ref = O.selfplay_run(n, Bs, iters, 0x5EED, sims, GENBU["ratio_fullMCTS"], GENBU["prob_fullMCTS"], GENBU["cpuct"],
+                         GENBU["fpu"], False, GENBU["tempThreshold"], board_base=b0, dir_alpha=0.3, dir_temp=1.25)
+    h = shard.headers()
+    for j, k in enumerate(("player", "episode_step", "move_no", "game_no", "games_done", "pad0", "sims_done", "budget")):
+        np.testing.assert_array_equal(h[k], ref["hdr"][:, j], err_msg=k)
+
+
+@pytest.mark.parametrize("n,B,sims,iters", [(4, 16384, 400, 1000), (2, 32768, 1600, 2400)])
+def test_full_size_selfplay_with_network(n, B, sims, iters):
+    """Configs 5 and 4 (per-GPU shard) at full size with SplendorNNet leaves and the default
+    memory-planned pools: moves commit on every tree, root statistics are consistent, noised
+    root priors sum to 1, no tree freezes; capacity events are reported."""
+    from splendor.nnet import LeafEvaluator, random_net
+    from splendor.env import SplendorEngine
+    e = SplendorEngine(n)
+    ev = LeafEvaluator(e, random_net(n, seed=0), B, use_graph=False)
+    free = torch.cuda.mem_get_info()[0]
+    _, sp = selfplay(n, B, sims, evaluator=ev)
+    assert sp.device_bytes <= 0.8 * free                      # planned against free memory
+    sp.run(iters, use_graph=True)
+    torch.cuda.synchronize()
+    st = sp.stats()
+    h = sp.headers()
+    assert st["overflow"] == 0 and st["moves"] >= B
+    counts, qsa, _, _ = sp.root_stats()
+    has_root = torch.from_numpy(h["root"] >= 0).cuda()
+    sims_done = torch.from_numpy(h["sims_done"].astype(np.int64)).cuda()
+    assert bool((counts.sum(1)[has_root] >= sims_done[has_root] - 1).all())
+    visited = counts > 0
+    assert bool(((qsa[visited] >= -1.0) & (qsa[visited] <= 1.0)).all())
+    ps = sp.root_priors()
+    tot = ps.double().sum(1)[has_root]
+    assert bool((torch.abs(tot - 1.0) < 1e-4).all())
+    print(f"config n={n} B={B} sims={sims}: {st}, node_cap {sp.cfg.node_cap}, edge_cap {sp.cfg.edge_cap}, "
+          f"device bytes {sp.device_bytes / 2**30:.1f} GiB")
+    del sp, ev
+    free_all()
+
+
+def test_config4_shard_equals_slice():
+    """2p, 32,768 games x 1,600 simulations (hash network): a 128-game shard at board_base
+    24,576 equals the slice of the full batch (headers, root counts, root priors)."""
+    n, B, sims, iters, b0, Bs = 2, 32768, 1600, 2000, 24576, 128
+    caps = dict(node_cap=2560, edge_cap=2560 * 32)
+    _, full = selfplay(n, B, sims, **caps)
+    full.run(iters, use_graph=True)
+    _, shard = selfplay(n, Bs, sims, board_base=b0, **caps)
+    shard.run(iters, use_graph=True)
+    torch.cuda.synchronize()
+    assert_slice_equal(full, shard, b0)
+    assert full.stats()["moves"] > B
+    del full, shard
+    free_all()
+
+
+def test_capacity_pressure_is_graceful():
+    """Pools far too small for the trees the reference would keep: searches start on pruned
+    or emptied trees and leaves that do not fit are backed up without being stored — every
+    game keeps playing, examples keep flowing, the events are counted."""
+    n, B, sims = 2, 256, 64
+    _, sp = selfplay(n, B, sims, node_cap=96, edge_cap=96 * 24)
+    for _ in range(10):
+        sp.run(400, use_graph=True)
+        sp.drain()
+    st = sp.stats()
+    assert st["overflow"] == 0 and st["games_done"] > 0
+    assert st["prunes"] > 0 and st["resets"] + st["unexpanded"] >= 0
+    h = sp.headers()
+    assert (h["node_count"] <= 96).all() and (h["edge_count"] <= 96 * 24).all()
+    assert h["pad0"].min() > 10                                 # every tree kept committing moves

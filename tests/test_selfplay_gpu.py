@@ -1,6 +1,10 @@
 """GPU parity of the batched self-play driver (Coach.executeEpisode on device) against the
-oracle's sequential self-play loop: same Philox decisions, hash network, Dirichlet off.
-Bit-exact boards, per-game counters and every finished training example."""
+oracle's sequential self-play loop (same Philox decisions and Dirichlet draws, hash
+network) and against whole reference episodes recorded with the same draws injected
+(tests/golden/episode_*.npz). Bit-exact boards, per-game counters and every finished
+training example."""
+import os
+
 import numpy as np
 import pytest
 
@@ -27,10 +31,12 @@ def sort_examples(ex, meta):
     return {k: v[order] for k, v in ex.items() if hasattr(v, "shape") and v.shape[:1] == meta.shape[:1]}
 
 
-@pytest.mark.parametrize("n,forced,graph", [(2, False, False), (2, True, True), (4, False, False)])
-def test_selfplay_matches_oracle(n, forced, graph):
+@pytest.mark.parametrize("n,forced,graph,noise", [(2, False, False, False), (2, True, True, False),
+                                                  (4, False, False, False), (2, False, True, True),
+                                                  (4, True, True, True), (3, False, True, True)])
+def test_selfplay_matches_oracle(n, forced, graph, noise):
     B, iters, sims, ratio, pf, seed = 96, 1200, 8, 4, 0.25, 9
-    e, sp = make(n, B, sims, ratio, pf, forced, seed=seed, out_cap=20000)
+    e, sp = make(n, B, sims, ratio, pf, forced, seed=seed, out_cap=20000, noise=noise)
     if graph:
         sp.run(iters - 3, use_graph=True)     # 8-iteration graph replays + single replays
         for _ in range(3):
@@ -41,7 +47,8 @@ def test_selfplay_matches_oracle(n, forced, graph):
     torch.cuda.synchronize()
     hdr = sp.headers()
     assert hdr["overflow"].max() == 0
-    ref = O.selfplay_run(n, B, iters, seed, sims, ratio, pf, 1.5, 0.1, forced, 10)
+    ref = O.selfplay_run(n, B, iters, seed, sims, ratio, pf, 1.5, 0.1, forced, 10,
+                         dir_alpha=0.3 if noise else 0.0, dir_temp=1.25)
     rh = ref["hdr"]
     np.testing.assert_array_equal(hdr["player"], rh[:, 0])
     np.testing.assert_array_equal(hdr["episode_step"], rh[:, 1])
@@ -62,6 +69,47 @@ def test_selfplay_matches_oracle(n, forced, graph):
     np.testing.assert_array_equal(ex["winner"], rf["winner"])
     np.testing.assert_array_equal(ex["scdiff"], rf["scdiff"])
     np.testing.assert_array_equal(ex["surprise"], rf["surprise"])
+
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("tag", ("2p", "2p_forced", "4p"))
+def test_episode_matches_reference(tag):
+    """Whole reference episodes (Coach.executeEpisode with root noise, temperature sampling,
+    chance, symmetries; recorded with the build's keyed draws injected) replayed by the
+    device self-play driver on one tree per recorded board id, examples expanded by the
+    device symmetry kernel: the reference's example list, bit for bit."""
+    from splendor.coach import expand_symmetries
+    from splendor.env import unpack_mask
+    with np.load(os.path.join(GOLD, f"episode_{tag}.npz")) as z:
+        d = {k: z[k] for k in z.files}
+    n = {56: 2, 71: 3, 88: 4}[d["board"].shape[1]]
+    a = {k[4:]: d[k] for k in d if k.startswith("arg_")}
+    sims, ratio = int(a["numMCTSSims"]), int(a["ratio_fullMCTS"])
+    for gi, gb in enumerate(d["game_board_id"]):
+        e, sp = make(n, 1, sims, ratio, float(a["prob_fullMCTS"]), bool(a["forced_playouts"]),
+                     tthr=int(a["tempThreshold"]), seed=int(d["seed"]), board_base=int(gb), noise=True,
+                     out_cap=4096)
+        assert float(a["cpuct"]) == 1.5 and float(a["fpu"]) == 0.1 and float(a["dirichletAlpha"]) == 0.3
+        moves = 0
+        while sp.stats()["games_done"] == 0:
+            sp.run(256, use_graph=True)
+            moves += 1
+            assert moves < 64, "episode did not finish"
+        ex = sp.drain()
+        keep = ex["meta"][:, 1] == 0
+        ex = {k: v[keep] for k, v in ex.items()}
+        order = torch.argsort(ex["meta"][:, 2])
+        ex = expand_symmetries(e, {k: v[order] for k, v in ex.items()})
+        sel = d["game"] == gi
+        assert ex["board"].shape[0] == int(sel.sum()) == int(d["game_n_examples"][gi])
+        np.testing.assert_array_equal(ex["board"].cpu().numpy(), d["board"][sel])
+        np.testing.assert_array_equal(ex["pi"].cpu().numpy(), d["pi"][sel])
+        np.testing.assert_array_equal(unpack_mask(ex["valids"]).cpu().numpy().astype(np.uint8), d["valids"][sel])
+        np.testing.assert_array_equal(ex["winner"].cpu().numpy(), d["winner"][sel])
+        np.testing.assert_array_equal(ex["scdiff"].cpu().numpy(), d["scdiff"][sel])
+        np.testing.assert_array_equal(ex["surprise"].cpu().numpy(), d["surprise"][sel].astype(np.float32))
 
 
 def test_selfplay_with_noise_and_network_sane():
