@@ -249,7 +249,7 @@ __device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int 
 // linked = true (capacity pressure, see begin_search): keep only the root and the nodes
 // reachable from it through child links (mark_linked), dropping nodes that only a
 // transposition lookup could reach.
-// scr: optional LDS scratch of 2 * (ncap + 1) ints for this wave (ncap <= SCR_NODES): the
+// scr: scratch of 2 x sstride ints (sstride >= ncap + 1; LDS when ncap <= SCR_NODES): the
 // edges then move in batches of 256 new positions (each lane finds its edge's owner by a
 // binary search over the kept nodes' new bases) instead of one kept node at a time.
 constexpr int SCR_NODES = 512;
@@ -282,7 +282,7 @@ __device__ void mark_linked(const Pools &P, int t, int root) {
     }
 }
 
-__device__ int compact_tree(const Pools &P, int t, int root, int root_round, int *scr = nullptr,
+__device__ int compact_tree(const Pools &P, int t, int root, int root_round, int *scr, int sstride,
                             bool linked = false) {
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
@@ -354,7 +354,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
             P.nqs[nb + ni] = qs; P.nterm[nb + ni] = term;
 #pragma unroll
             for (int j = 0; j < 4; j++) P.nes[(nb + ni) * 4 + j] = es[j];
-            if (scr) { scr[ni] = neb; scr[SCR_NODES + 1 + ni] = oeb; }
+            if (scr) { scr[ni] = neb; scr[sstride + ni] = oeb; }
         }
         if (scr) { edges += total; continue; }              // edges move in batches below
         // move each kept node's edge block down (increasing order: never overlaps unread data)
@@ -407,7 +407,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
                         const int mid = (lo + hi + 1) >> 1;
                         if (scr[mid] <= k) lo = mid; else hi = mid - 1;
                     }
-                    const int src = scr[SCR_NODES + 1 + lo] + (k - scr[lo]);
+                    const int src = scr[sstride + lo] + (k - scr[lo]);
                     st[r] = P.es[e0 + src];
                     lk[r] = P.el[e0 + src];
                 }
@@ -479,16 +479,23 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         uint64_t k0, k1;
         wave_fingerprint<N>(s, k0, k1);
         root = hash_lookup(P, t, k0, k1);
-        const int rr = (uint8_t)bt(row(s, 0), 6);
-        int *cs = P.ncap <= SCR_NODES ? scr : nullptr;
-        root = compact_tree(P, t, root, rr, cs);
         const auto fits = [&]() {
             return H->node_count + budget + 1 <= P.ncap &&
                    (long long)H->edge_count + SPL_ACTIONS + (long long)budget * C.edge_reserve <= (long long)P.ecap;
         };
-        if (!fits() && root >= 0) {
-            root = compact_tree(P, t, root, rr, cs, true);
-            if (l == 0) H->prunes += 1;
+        // lazy garbage collection: nodes with rounds <= the root's are unreachable (and no
+        // lookup can match them), so they are only compacted away when the search would
+        // not fit otherwise — the search sees the same reachable table either way
+        if (!fits()) {
+            const int rr = (uint8_t)bt(row(s, 0), 6);
+            // edge-move scratch: LDS for small trees, the tree's global scratch otherwise
+            int *cs = P.ncap <= SCR_NODES && scr ? scr : P.cscr + (size_t)t * 2 * (P.ncap + 1);
+            const int cstride = P.ncap <= SCR_NODES && scr ? SCR_NODES + 1 : P.ncap + 1;
+            root = compact_tree(P, t, root, rr, cs, cstride);
+            if (!fits() && root >= 0) {
+                root = compact_tree(P, t, root, rr, cs, cstride, true);
+                if (l == 0) H->prunes += 1;
+            }
         }
         empty = !fits();
         if (empty && l == 0) H->resets += 1;
@@ -501,8 +508,12 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
+    const int reb = root >= 0 ? P.neb[(size_t)t * P.ncap + root] : 0;
+    const int rec = root >= 0 ? P.nec[(size_t)t * P.ncap + root] : 0;
     if (l == 0) {
         H->root = root;
+        H->root_eb = reb;
+        H->root_ec = rec;
         H->sims_done = 0;
         H->full = full;
         H->budget = budget;
@@ -718,22 +729,35 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     begin_search<N>(P, C, t, s, !ended, false, cscr[w]);
 }
 
+// flat copy of `bytes` bytes (16-byte vectors when both ends allow it), grid-stride
+__device__ __forceinline__ void grid_copy(void *dst, const void *src, size_t bytes) {
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    if (((uintptr_t)dst | (uintptr_t)src) % 16 == 0) {
+        const size_t nv = bytes / 16;
+        uint4 *d = (uint4 *)dst;
+        const uint4 *s = (const uint4 *)src;
+        for (size_t i = tid; i < nv; i += nth) d[i] = s[i];
+        for (size_t i = nv * 16 + tid; i < bytes; i += nth) ((uint8_t *)dst)[i] = ((const uint8_t *)src)[i];
+    } else {
+        for (size_t i = tid; i < bytes; i += nth) ((uint8_t *)dst)[i] = ((const uint8_t *)src)[i];
+    }
+}
+
+// the queue's first k examples into caller buffers: board / pi / valid rows are contiguous
+// in both layouts (flat copies), the per-player columns go from 4 to n
 __global__ void k_drain_copy(Pools P, int S, int max, int8_t *st, float *pi, uint64_t *valid,
                              float *winner, int32_t *scdiff, float *q, int32_t *meta, int n) {
     const int k = min(P.counters[0], min(max, P.out_cap));
-    const size_t W = S > SPL_ACTIONS ? (size_t)S : (size_t)SPL_ACTIONS;   // per-example span
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)k * W;
-         i += (size_t)gridDim.x * blockDim.x) {
-        const size_t e = i / W, j = i % W;
-        if (pi && j < SPL_ACTIONS) pi[e * SPL_ACTIONS + j] = P.out_pi[e * SPL_ACTIONS + j];
-        if (st && j < (size_t)S) st[e * S + j] = P.out_state[e * S + j];
-        if (j < 7 && valid) valid[e * 7 + j] = P.out_valid[e * 7 + j];
-        if (j < 4 && meta) meta[e * 4 + j] = P.out_meta[e * 4 + j];
-        if (j < (size_t)n) {
-            if (winner) winner[e * n + j] = P.out_winner[e * 4 + j];
-            if (scdiff) scdiff[e * n + j] = P.out_scdiff[e * 4 + j];
-            if (q) q[e * n + j] = P.out_q[e * 4 + j];
-        }
+    if (pi) grid_copy(pi, P.out_pi, (size_t)k * SPL_ACTIONS * 4);
+    if (st) grid_copy(st, P.out_state, (size_t)k * S);
+    if (valid) grid_copy(valid, P.out_valid, (size_t)k * 7 * 8);
+    if (meta) grid_copy(meta, P.out_meta, (size_t)k * 4 * 4);
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = tid; i < (size_t)k * n; i += nth) {
+        const size_t e = i / (size_t)n, j = i - e * (size_t)n;
+        if (winner) winner[i] = P.out_winner[e * 4 + j];
+        if (scdiff) scdiff[i] = P.out_scdiff[e * 4 + j];
+        if (q) q[i] = P.out_q[e * 4 + j];
     }
 }
 
@@ -758,6 +782,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
     if (t >= B) return;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
+    int8_t *s = lds[w];
+    // the root board is requested together with the header (no dependency between them)
+    wave_load_board<N>(s, P.root_state + (size_t)t * Lx::S);
     const int sims = H->sims_done;
     if (sims >= H->budget || H->overflow) {
         if (l == 0) { leaf_valid[t] = 0; H->leaf_kind = LEAF_NONE; }
@@ -769,8 +796,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         spl_probe_last = clock64();
     }
 #endif
-    int8_t *s = lds[w];
-    wave_load_board<N>(s, P.root_state + (size_t)t * Lx::S);
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     int32_t *path = P.path + (size_t)t * P.pcap * 2;
     SPL_PROBE(0)
@@ -780,14 +805,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
     if (node < 0) {
         wave_fingerprint<N>(s, k0, k1);                  // the root itself is the leaf
     } else {
-        if (sims == 0 && H->noise_pending)
-            apply_root_noise(P, C, t, P.neb[nb + node], P.nec[nb + node], ST_DIR | (uint32_t)H->move_no, lpr[w],
-                             false);
-        const bool forced = H->forced;
-        // CSR range of the current node: the root's from its record, every child's from the
+        // CSR range of the current node: the root's from the header, every child's from the
         // {eb, ec} cached on the edge that led to it, so a level costs ONE round trip (the
         // node's visit stats travel with its edges); ec < 0 marks a terminal child
-        int eb = P.neb[nb + node], ec = P.nec[nb + node];
+        int eb = H->root_eb, ec = H->root_ec;
+        if (sims == 0 && H->noise_pending)
+            apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no, lpr[w], false);
+        const bool forced = H->forced;
         for (;;) {
             SPL_PROBE(1)
             if (depth > 0 && ec < 0) {
@@ -1045,7 +1069,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             P.neb[nb + id] = eb; P.nec[nb + id] = ec; P.nns[nb + id] = 0;
             P.nqs[nb + id] = (double)val[0]; P.nround[nb + id] = H->leaf_round; P.nterm[nb + id] = 0;
             hash_insert(P, t, H->leaf_k0, id);
-            if (depth == 0) H->root = id;
+            if (depth == 0) { H->root = id; H->root_eb = eb; H->root_ec = ec; }
             else {
                 P.el[e0 + path[2 * (depth - 1) + 1]].child = id;
                 set_cr(P.el[e0 + path[2 * (depth - 1) + 1]], eb, ec);
@@ -1300,7 +1324,7 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn); acc(4 * nn);
     acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(sizeof(EdgeStat) * ne); acc(sizeof(EdgeLink) * ne);
     acc(4 * (size_t)B * L.hcap); acc(8 * (size_t)B * L.pcap);
-    acc(4 * nn); acc(4 * nn); acc((size_t)B * L.S);
+    acc(4 * nn); acc(4 * nn); acc(8 * ((size_t)B * (L.ncap + 1))); acc((size_t)B * L.S);
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
     acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
     acc(16 * no); acc(64);
@@ -1354,6 +1378,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.hslot = carve<int32_t>(p, (size_t)B * P.hcap);
     P.path = carve<int32_t>(p, 2 * (size_t)B * P.pcap);
     P.remap = carve<int32_t>(p, nn); P.remap_eb = carve<int32_t>(p, nn);
+    P.cscr = carve<int32_t>(p, 2 * ((size_t)B * (P.ncap + 1)));
     P.root_state = carve<int8_t>(p, (size_t)B * m->S);
     P.excap = excap; P.out_cap = (int)no;
     P.board = carve<int8_t>(p, (size_t)B * m->S);
@@ -1456,10 +1481,9 @@ int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *val
                             int32_t *scdiff, float *q, int32_t *meta, int max, int32_t *n_out,
                             void *hs) {
     if (!m || !m->cfg.selfplay || max < 0) return SPL_EINVAL;
-    const size_t work = (size_t)(max < m->P.out_cap ? max : m->P.out_cap) *
-                        (size_t)(m->S > SPL_ACTIONS ? m->S : SPL_ACTIONS);
+    const size_t work = (size_t)(max < m->P.out_cap ? max : m->P.out_cap) * SPL_ACTIONS / 4;   // 16-byte pi vectors
     if (work) {
-        const unsigned grid = (unsigned)((work + 255) / 256 > 4096 ? 4096 : (work + 255) / 256);
+        const unsigned grid = (unsigned)((work + 255) / 256 > 8192 ? 8192 : (work + 255) / 256);
         hipLaunchKernelGGL(k_drain_copy, dim3(grid), dim3(256), 0, (hipStream_t)hs, m->P, m->S, max,
                            state, pi, valid, winner, scdiff, q, meta, m->n);
     }

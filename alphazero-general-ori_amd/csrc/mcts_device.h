@@ -24,11 +24,12 @@ struct TreeHdr {
     int32_t game_no, overflow, n_examples, leaf_round;
     uint64_t leaf_k0, leaf_k1;
     float leaf_v[4];
-    int32_t games_done, forced, pad0, pad1;
+    int32_t games_done, forced, pad0, root_eb;
     // capacity events: searches that started on a tree pruned to the nodes
     // linked from the root / on an emptied tree, and simulations whose leaf did not fit
-    // (evaluated and backed up without being stored)
-    int32_t prunes, resets, unexpanded, pad2;
+    // (evaluated and backed up without being stored); root_eb / root_ec: the root's CSR
+    // range (so the descent's first level needs no node load)
+    int32_t prunes, resets, unexpanded, root_ec;
 };
 enum { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2 };
 
@@ -63,6 +64,7 @@ struct Pools {
     int32_t *hslot;
     int32_t *path;                       // pcap x 2 (node, edge)
     int32_t *remap, *remap_eb;           // ncap scratch for compaction (new index, new CSR base)
+    int32_t *cscr;                       // 2 x (ncap + 1) per tree: edge-move scratch of large trees
     int8_t *root_state;                  // B x S (canonical root)
     // self-play (Coach.executeEpisode) state
     int excap, out_cap;                  // staged examples per tree, finished-example queue

@@ -28,8 +28,8 @@ HDR_DTYPE = np.dtype([
     ("leaf_kind", "<i4"), ("player", "<i4"), ("episode_step", "<i4"), ("move_no", "<i4"),
     ("game_no", "<i4"), ("overflow", "<i4"), ("n_examples", "<i4"), ("leaf_round", "<i4"),
     ("leaf_k0", "<u8"), ("leaf_k1", "<u8"), ("leaf_v", "<f4", (4,)),
-    ("games_done", "<i4"), ("forced", "<i4"), ("pad0", "<i4"), ("pad1", "<i4"),
-    ("prunes", "<i4"), ("resets", "<i4"), ("unexpanded", "<i4"), ("pad2", "<i4")])
+    ("games_done", "<i4"), ("forced", "<i4"), ("pad0", "<i4"), ("root_eb", "<i4"),
+    ("prunes", "<i4"), ("resets", "<i4"), ("unexpanded", "<i4"), ("root_ec", "<i4")])
 assert HDR_DTYPE.itemsize == 128
 
 DEFAULT_ARGS = dict(numMCTSSims=100, cpuct=1.0, fpu=0.0, prob_fullMCTS=1.0, ratio_fullMCTS=5,
@@ -100,14 +100,17 @@ class BatchedMCTS:
     def _caps(self, engine, B, sims, cfg, node_cap, edge_cap):
         """Per-tree pool sizes. A search adds at most `sims` nodes, but the
         kept table (every node whose round exceeds the root's, MCTS.py semantics) keeps
-        growing through a game: measured trees pass 8 x sims nodes (tools/tree_sizes.py).
-        Default: 8 x sims + 64 nodes, 48 edges per node slot; when B such trees do not fit
-        MEM_FRACTION of the free HBM, 24 edges per node and as many nodes as fit (searches
-        then start on pruned trees under pressure, counted in the tree headers)."""
+        growing through a game: at genbu's arguments and 100 simulations, steady-state
+        trees reach ~1,850 nodes / 50 K edges (tools/tree_sizes.py, 15-19 edges per node on
+        average). Default: 16 x sims + 256 node slots, 32 edges per slot (garbage is only
+        collected when a search would not fit, so the slots also hold dead nodes); when B
+        such trees do not fit MEM_FRACTION of the free HBM, 24 edges per slot and as many
+        slots as fit (searches then start on pruned trees under pressure, counted in the
+        tree headers)."""
         if node_cap and edge_cap:
             return int(node_cap), int(edge_cap)
-        nc = int(node_cap or max(8 * sims + 64, 256))
-        ec = int(edge_cap or 48 * nc)
+        nc = int(node_cap or 16 * sims + 256)
+        ec = int(edge_cap or 32 * nc)
 
         def plan(nc_, ec_):
             cfg.node_cap, cfg.edge_cap = int(nc_), int(ec_)

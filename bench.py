@@ -4,9 +4,10 @@
 Default workload = BASELINE config 2: 2-player Splendor, 32,768 concurrent boards per GPU,
 random-policy self-play by the fused HIP rollout kernel (canonical form -> 409-action
 legality mask -> action -> chance transition -> end check -> auto-reset). One bench "step"
-is one move of every board; a launch runs --chunk moves with the boards kept on chip and
-writes every move's mask, action and end result to HBM. A "rollout" is one board-move
-(BASELINE.md units). Data are synthetic: boards start from Philox-seeded deals (seed
+is one move of every board (a board-step); a launch runs --chunk moves
+with the boards kept on chip and writes every move's mask, action and end result to HBM.
+The line's unit is board-steps/s; the config-3 self-play object reports rollouts = MCTS
+simulations. Data are synthetic: boards start from Philox-seeded deals (seed
 0x5EED, board id) and reset on game end.
 
 Contract: `python bench.py --gpus N --steps K --warmup W`; for N>1 launched by
@@ -27,12 +28,20 @@ import torch  # noqa: E402
 
 METRIC = "self-play rollouts/sec (32k boards, 2p Splendor) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+FP32_MFMA_PEAK = 157.3    # TFLOP/s, dense fp32 MFMA (MI355X_MICROARCH.md)
+
+
+def bytes_per_board_step(n):
+    """SURVEY.md §8(d) algorithmic bytes of one board-step: state read + write (2S), packed
+    mask (52 = ceil(409/8)), action (2), end result (4n): 846 B for 2 players."""
+    S = 7 * (32 + 10 * n + n * n)
+    return 2 * S + 52 + 2 + 4 * n
 
 
 def bytes_per_board_launch(n, moves):
-    """Algorithmic HBM bytes of one rollout launch for one board: state read +
-    write (2S), player read + write (2), game counter read + write (8), and per move the
-    packed mask (56), action (2) and end result (4n)."""
+    """Bytes one rollout launch actually moves across HBM per board: boards
+    stay on chip for the launch, so state read + write (2S), player (2) and game counter (8)
+    once, and per move the packed mask (56), action (2) and end result (4n)."""
     S = 7 * (32 + 10 * n + n * n)
     return 2 * S + 2 + 8 + moves * (56 + 2 + 4 * n)
 
@@ -164,14 +173,21 @@ def selfplay_config_name(args):
     return "config4" if args.sims >= 1600 else "config3"
 
 
-def run_selfplay(args, rank, world, dev, dist):
-    """BASELINE config 3 (config 4 per GPU at N>1): B concurrent self-play games, one MCTS
-    simulation per game per iteration, leaves evaluated by SplendorNNet (fp32, random
-    init: the reference's genbu.pt cannot be loaded safely), moves committed on device."""
+def run_selfplay(args, rank, world, dev, dist, steps=None, warmup=None):
+    """BASELINE config 3 (config 4 per GPU at N>1, config 5 with --players 4): B concurrent
+    self-play games, one MCTS simulation per game per iteration, leaves evaluated by the
+    fused SplendorNNet kernel (fp32, random init: the reference's genbu.pt cannot be loaded
+    safely), moves committed on device. Warm-up first (the games desynchronise and trees
+    reach their steady size), then a timed window of `steps` iterations (default ~3 full
+    games per board) that ends with draining the finished examples and the
+    RCCL all-gather of them; symmetry expansion is timed separately."""
+    from splendor.coach import expand_symmetries
     from splendor.env import SplendorEngine
     from splendor.nnet import LeafEvaluator, random_net
     from splendor.selfplay import SelfPlay, broadcast_network, gather_examples
     B = args.boards
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
     eng = SplendorEngine(args.players, device=dev)
     sargs = dict(GENBU_ARGS, numMCTSSims=args.sims)
     net = random_net(args.players, seed=rank, device=dev)
@@ -180,49 +196,91 @@ def run_selfplay(args, rank, world, dev, dist):
     ev = LeafEvaluator(eng, net, B, use_graph=False)
     sp = SelfPlay(eng, B, sargs, evaluator=ev, dirichlet_noise=True, seed=args.seed, board_base=rank * B)
     sp.reset()
-    sp.run(args.warmup, use_graph=True)      # (captures both graphs)
+    sp.run(max(warmup, 9), use_graph=True)     # (captures both graphs)
+    sp.drain()
     torch.cuda.synchronize(dev)
+    st0 = sp.stats()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record()
-    sp.run(args.steps, use_graph=True)
+    sp.run(steps, use_graph=True)
     ev1.record()
+    torch.cuda.synchronize(dev)              # (the graph replays run asynchronously)
+    tg = time.perf_counter()
+    ex = sp.drain()
+    ex_local = int(ex["board"].shape[0])
+    if dist:
+        ex = gather_examples(ex)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    st = sp.stats()
-    # episode-end exchange of finished examples (RCCL all-gather), timed separately
-    tg = time.perf_counter()
-    ex = gather_examples(sp.drain()) if dist else sp.drain()
-    torch.cuda.synchronize(dev)
     gather_s = time.perf_counter() - tg
+    st = sp.stats()
     if dist:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return {"elapsed": elapsed, "iter_ms": ev0.elapsed_time(ev1) / args.steps, "stats": st,
-            "examples": int(next(iter(ex.values())).shape[0]), "gather_s": gather_s,
-            "device_bytes": sp.device_bytes}
+    # symmetry expansion of the window's examples (Board.get_symmetries), outside the window
+    nsym = min(ex_local, 200000)
+    ts = time.perf_counter()
+    sym = expand_symmetries(eng, {k: v[:nsym] for k, v in ex.items()}) if nsym else None
+    torch.cuda.synchronize(dev)
+    sym_s = time.perf_counter() - ts
+    # the network kernel on its own: k_nn_forward over B leaves, HIP events on its stream
+    nk = 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev(sp.leaf_state, sp.leaf_mask)
+    e0.record()
+    for _ in range(nk):
+        ev(sp.leaf_state, sp.leaf_mask)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    nn_us = e0.elapsed_time(e1) / nk * 1e3
+    delta = {k: st[k] - st0[k] for k in ("games_done", "moves", "prunes", "resets", "unexpanded")}
+    return {"elapsed": elapsed, "iter_ms": ev0.elapsed_time(ev1) / steps, "stats": st, "window": delta,
+            "examples": ex_local, "examples_gathered": int(ex["board"].shape[0]), "gather_s": gather_s,
+            "symmetry": {"examples": nsym, "variants": int(sym["board"].shape[0]) if sym else 0, "s": sym_s},
+            "device_bytes": sp.device_bytes, "node_cap": int(sp.cfg.node_cap), "edge_cap": int(sp.cfg.edge_cap),
+            "nn_kernel_us": nn_us}
+
+
+def selfplay_record(args, r, world, steps, warmup):
+    """Secondary object of the bench line for the self-play workload."""
+    B = args.boards
+    fl = nn_flops_per_eval(args.players) * B
+    return {"workload": f"{selfplay_config_name(args)}: batched self-play, numMCTSSims={args.sims}, genbu args, "
+                        "SplendorNNet fp32 leaf eval (random init), device move commit",
+            "value": world * B * steps / r["elapsed"], "unit": "rollouts/s (MCTS simulations)",
+            "ms_per_iteration": r["elapsed"] / steps * 1e3, "steps": steps, "warmup": warmup,
+            "window": {**r["window"], "examples_drained": r["examples"], "examples_gathered": r["examples_gathered"],
+                       "drain_allgather_s": r["gather_s"]},
+            "tree": {k: r["stats"][k] for k in ("nodes_max", "edges_max", "overflow", "examples_dropped")}
+                    | {"node_cap": r["node_cap"], "edge_cap": r["edge_cap"], "device_bytes": r["device_bytes"]},
+            "symmetry_expansion": r["symmetry"],
+            "network_kernel": {"kernel": f"k_nn_forward<{args.players}>", "avg_us": r["nn_kernel_us"],
+                               "tflops": fl / (r["nn_kernel_us"] * 1e-6) / 1e12,
+                               "frac_fp32_mfma_peak": fl / (r["nn_kernel_us"] * 1e-6) / 1e12 / FP32_MFMA_PEAK,
+                               "note": "k_nn_forward alone over B leaves (HIP events, 20 launches)"}}
 
 
 def load_traffic(path, B, moves):
     """The newest committed rocprofv3 --pmc summary of this workload (profiles/
     rNN_rollout_pmc.json, tools/pmc_rollout.sh; HBM bytes corrected as DESIGN.md §6
     describes), if it was taken at this board count and launch size."""
-    if not path:
-        import glob
-        found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_rollout_pmc.json")))
-        path = found[-1] if found else None
-    if not path or not os.path.exists(path):
-        return None
-    with open(path) as f:
-        d = json.load(f)
-    if d.get("boards") != B or d.get("moves_per_launch", 1) != moves:
-        return None
-    return d
+    import glob
+    paths = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_rollout_pmc*.json")))
+    best = None
+    for p in paths:
+        if not os.path.exists(p):
+            continue
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("boards") == B and d.get("moves_per_launch", 1) == moves:
+            best = dict(d, file=os.path.relpath(p, ROOT))        # newest round wins (sorted names)
+    return best
 
 
 def main():
@@ -239,7 +297,10 @@ def main():
     ap.add_argument("--sims", type=int, default=100, help="selfplay: numMCTSSims")
     ap.add_argument("--no-selfplay", action="store_true",
                     help="env workload: skip the secondary config-3 self-play measurement")
-    ap.add_argument("--selfplay-steps", type=int, default=100)
+    ap.add_argument("--selfplay-steps", type=int, default=10000,
+                    help="env workload: timed self-play iterations (~3 full games per board)")
+    ap.add_argument("--selfplay-warmup", type=int, default=3000,
+                    help="env workload: untimed self-play iterations first (games finish, trees grow)")
     ap.add_argument("--chunk", type=int, default=100, help="env: moves per rollout launch")
     args = ap.parse_args()
 
@@ -258,23 +319,21 @@ def main():
         r = run_selfplay(args, rank, world, dev, dist)
         if rank == 0:
             B, K = args.boards, args.steps
-            flops = nn_flops_per_eval(args.players) * B / (r["iter_ms"] * 1e-3) / 1e12
+            rec = selfplay_record(args, r, world, K, args.warmup)
+            nk = rec["network_kernel"]
             print(json.dumps({
-                "metric": METRIC, "value": world * B * K / r["elapsed"], "unit": "rollouts/s",
+                "metric": METRIC, "value": rec["value"], "unit": "rollouts/s (MCTS simulations)",
                 "n_gpus": world, "steps": K, "warmup": args.warmup,
-                "ms_per_step": r["elapsed"] / K * 1e3, "higher_is_better": True, "scaling": "weak",
+                "ms_per_step": rec["ms_per_iteration"], "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "fp32 (network) / int8 (boards) / f64 (tree stats)",
                 "data": "synthetic (Philox-seeded deals), random-init SplendorNNet",
-                "config": {"workload": f"{selfplay_config_name(args)}: batched self-play, numMCTSSims={args.sims}, "
-                                       "genbu args, SplendorNNet leaf eval, device move commit",
-                           "players": args.players, "games_per_gpu": B, "global_games": world * B,
+                "config": {"workload": rec["workload"], "players": args.players, "games_per_gpu": B,
+                           "global_games": world * B,
                            "parallelism": f"dp{world} (game shards; RCCL all-gather of examples)"},
-                "roofline": {"bound": "mfma", "achieved": flops, "peak": 157.3, "unit": "TFLOP/s",
-                             "frac": flops / 157.3, "traffic": None,
-                             "note": "network FLOPs per iteration / iteration time (fp32 MFMA peak)"},
-                "selfplay": {**r["stats"], "examples": r["examples"], "allgather_s": r["gather_s"],
-                             "tree_device_bytes": r["device_bytes"], "iter_ms": r["iter_ms"]},
-                "cpu_baseline": None}))
+                "roofline": {"bound": "mfma", "achieved": nk["tflops"], "peak": FP32_MFMA_PEAK, "unit": "TFLOP/s",
+                             "frac": nk["frac_fp32_mfma_peak"], "traffic": None, "kernel": nk["kernel"],
+                             "kernel_avg_us": nk["avg_us"]},
+                "selfplay": rec, "cpu_baseline": None}))
         if dist:
             dist.destroy_process_group()
         return
@@ -323,33 +382,27 @@ def main():
 
     secondary = None
     if not args.no_selfplay:
-        del rb
+        del rb, outs
         torch.cuda.empty_cache()
-        sp_args = argparse.Namespace(**vars(args))
-        sp_args.steps, sp_args.warmup = args.selfplay_steps, 20
-        r = run_selfplay(sp_args, rank, world, dev, dist)
-        flops = nn_flops_per_eval(args.players) * B / (r["iter_ms"] * 1e-3) / 1e12
-        secondary = {"workload": f"config3: batched self-play, numMCTSSims={args.sims}, genbu args, "
-                                 "SplendorNNet fp32 leaf eval (random init), device move commit",
-                     "value": world * B * sp_args.steps / r["elapsed"], "unit": "rollouts/s (MCTS simulations)",
-                     "ms_per_iteration": r["elapsed"] / sp_args.steps * 1e3, "steps": sp_args.steps,
-                     "network_tflops": flops, "network_frac_fp32_peak": flops / 157.3,
-                     **r["stats"], "examples_drained": r["examples"], "allgather_s": r["gather_s"],
-                     "tree_device_bytes": r["device_bytes"]}
+        r = run_selfplay(args, rank, world, dev, dist, steps=args.selfplay_steps, warmup=args.selfplay_warmup)
+        secondary = selfplay_record(args, r, world, args.selfplay_steps, args.selfplay_warmup)
         if rank == 0 and not args.no_cpu_baseline and world == 1:
             secondary["cpu_baseline"] = cpu_baseline_selfplay(args.players, args.seed, args)
 
     if rank == 0:
-        per = bytes_per_board_launch(args.players, chunk)
-        achieved = per * B / (kernel_ms * 1e-3) / 1e9
+        step_b = bytes_per_board_step(args.players)
+        achieved = step_b * B * chunk / (kernel_ms * 1e-3) / 1e9
+        moved = bytes_per_board_launch(args.players, chunk)
+        moved_gbs = moved * B / (kernel_ms * 1e-3) / 1e9
         prof = load_traffic(args.traffic_json, B, chunk)
         traffic = prof.get("hbm_bytes_per_launch") if prof else None
-        issue = ({k: prof.get(k) for k in ("valu_insts_per_board_move", "valu_issue_frac", "effective_clock_ghz")}
+        issue = ({k: prof.get(k) for k in ("valu_insts_per_board_move", "valu_issue_frac", "effective_clock_ghz",
+                                            "kernel_avg_us_rocprof", "file")}
                  if prof else None)
         out = {
             "metric": METRIC,
             "value": world * B * K / elapsed,
-            "unit": "rollouts/s",
+            "unit": "board-steps/s",
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,
@@ -367,9 +420,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"k_rollout<{args.players}>", "kernel_avg_us": kernel_ms * 1e3,
-                         "moves_per_launch": chunk, "bytes_per_board_launch": per,
-                         "valu_issue": issue,
-                         "note": "VALU-issue bound, not HBM bound: see DESIGN.md §5"},
+                         "moves_per_launch": chunk, "algorithmic_bytes_per_board_step": step_b,
+                         "algorithmic_bytes_per_launch": step_b * B * chunk,
+                         "moved_bytes_per_launch": moved * B, "moved_gbs": moved_gbs,
+                         "moved_frac": moved_gbs / HBM_PEAK_GBS,
+                         "limiter": "VALU issue + dependency latency, not HBM (boards stay on chip for the "
+                                    "launch; traffic = the measured bytes of the launch size, PMC)",
+                         "pmc": issue},
             "cpu_baseline": cpu,
             "games_completed": games,
             "config3_selfplay": secondary,

@@ -35,6 +35,7 @@ def avg(disp, name, skip=2):
 
 def main():
     root, rnd = sys.argv[1], sys.argv[2]
+    moves = int(sys.argv[3]) if len(sys.argv) > 3 else 100
     fe, wr, sq = counters(os.path.join(root, "fetch")), counters(os.path.join(root, "write")), counters(os.path.join(root, "sq"))
     fetch_kb, n1 = avg(fe, "FETCH_SIZE")
     write_kb, n2 = avg(wr, "WRITE_SIZE")
@@ -44,12 +45,12 @@ def main():
         for r in csv.DictReader(open(f)):
             if KERNEL in r["Name"]:
                 avg_ns = float(r["AverageNs"])
-    B, moves, n = 32768, 100, 2
+    B, n = 32768, 2
     S = 7 * (32 + 10 * n + n * n)
     alg = B * (2 * S + 2 + 8 + moves * (56 + 2 + 4 * n))
     res = {"kernel": KERNEL, "boards": B, "moves_per_launch": moves, "round": rnd,
            "command": "tools/pmc_rollout.sh: rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE | --pmc SQ_* "
-                      "(separate passes) -- python3 bench.py --steps 200 --warmup 100 --chunk 100",
+                      f"(separate passes) -- python3 bench.py --steps {2 * moves} --warmup {moves} --chunk {moves}",
            "dispatches_used": [n1, n2], "kernel_avg_us_rocprof": avg_ns / 1e3 if avg_ns else None,
            "FETCH_SIZE_KB_avg": fetch_kb, "WRITE_SIZE_KB_avg": write_kb}
     if fetch_kb is not None and write_kb is not None:

@@ -9,31 +9,35 @@
 #include <vector>
 #include <cstdlib>
 int main(int argc, char **argv) {
-    const int B = 32768, SIMS = 100, MOVES = 3;
-    const int emul = argc > 1 ? atoi(argv[1]) : 32;   // edge_cap = emul x node_cap
+    // argv: [sims=100] [warm iterations=3000] [timed iterations=1000] [node_cap=2048]
+    // self-play steady state (spl_mcts_commit), genbu args, hash-prior network
+    const int B = 32768;
+    const int SIMS = argc > 1 ? atoi(argv[1]) : 100;
+    const int WARM = argc > 2 ? atoi(argv[2]) : 3000, ITERS = argc > 3 ? atoi(argv[3]) : 1000;
     spl_ctx *c; spl_ctx_create(2, 10, &c);
     spl_mcts_config cfg{};
-    cfg.num_sims = SIMS; cfg.ratio_full = 1; cfg.prob_full = 1.0; cfg.cpuct = 2.5; cfg.fpu = 0.3;
-    cfg.node_cap = 4 * SIMS + 64; cfg.edge_cap = emul * cfg.node_cap; cfg.seed = 0x5EED; cfg.temp_threshold = 10;
-    cfg.dirichlet_temp = 1.0;
+    cfg.num_sims = SIMS; cfg.ratio_full = 5; cfg.prob_full = 0.25; cfg.cpuct = 2.5; cfg.fpu = 0.3;
+    cfg.node_cap = argc > 4 ? atoi(argv[4]) : 2048; cfg.edge_cap = 32 * cfg.node_cap; cfg.seed = 0x5EED;
+    cfg.temp_threshold = 10; cfg.dirichlet_alpha = 0.3; cfg.dirichlet_temp = 1.25; cfg.selfplay = 1;
+    cfg.out_cap = 64 * B;
     spl_mcts *m; if (spl_mcts_create(c, B, &cfg, &m)) { printf("create failed\n"); return 1; }
-    int8_t *st, *leaf; uint64_t *mk; uint8_t *lv; float *pi, *v;
-    (void)hipMalloc(&st, (size_t)B * 392); (void)hipMalloc(&leaf, (size_t)B * 392); (void)hipMalloc(&mk, (size_t)B * 56);
+    int8_t *leaf; uint64_t *mk; uint8_t *lv; float *pi, *v; int32_t *cnt;
+    (void)hipMalloc(&leaf, (size_t)B * 392); (void)hipMalloc(&mk, (size_t)B * 56);
     (void)hipMalloc(&lv, B); (void)hipMalloc(&pi, (size_t)B * 409 * 4); (void)hipMalloc(&v, (size_t)B * 8);
-    spl_init(c, B, st, nullptr, nullptr, 0, 0x5EED, 0xFFFFFFFFu, 0, nullptr);
+    (void)hipMalloc(&cnt, 4);
+    spl_mcts_reset_games(m, nullptr);
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
-    for (int mv = 0; mv < MOVES; mv++) {
-        spl_mcts_set_roots(m, st, mv > 0, 1, nullptr);
-        if (mv == MOVES - 1) {
+    for (int it = 0; it < WARM + ITERS; it++) {
+        if (it == WARM) {
             unsigned long long z[24] = {0};
             (void)hipMemcpyToSymbol(HIP_SYMBOL(g_select_timing), z, sizeof(z));
             (void)hipEventRecord(e0);
         }
-        for (int s = 0; s < SIMS; s++) {
-            spl_mcts_select(m, leaf, mk, lv, nullptr);
-            spl_hash_eval(c, B, leaf, mk, pi, v, nullptr);
-            spl_mcts_backup(m, mk, pi, v, nullptr);
-        }
+        spl_mcts_select(m, leaf, mk, lv, nullptr);
+        spl_hash_eval(c, B, leaf, mk, pi, v, nullptr);
+        spl_mcts_backup(m, mk, pi, v, nullptr);
+        spl_mcts_commit(m, nullptr);
+        if (it % 500 == 499) spl_mcts_drain_examples(m, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, cnt, nullptr);
     }
     (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
     float ms; (void)hipEventElapsedTime(&ms, e0, e1);
@@ -43,9 +47,9 @@ int main(int argc, char **argv) {
                            "fingerprint + hash", "node checks (to next level)", "leaf: store + mask", "headers",
                            "pick_edge: edge loads"};
     const double calls = (double)h[21];
-    printf("edge_cap %d, arena %.2f GB\n", cfg.edge_cap, spl_mcts_device_bytes(m) / 1e9);
-    printf("%d sims x %d trees: %.1f us per select+hash_eval+backup iteration; %.0f probed waves, %.2f levels/sim\n",
-           SIMS, B, ms * 1e3 / SIMS, calls, h[20] / calls);
+    printf("node_cap %d edge_cap %d, arena %.2f GB\n", cfg.node_cap, cfg.edge_cap, spl_mcts_device_bytes(m) / 1e9);
+    printf("%d sims, %d trees, steady state after %d iterations: %.1f us per select+hash_eval+backup+commit iteration; "
+           "%.0f probed waves, %.2f levels/sim\n", SIMS, B, WARM, ms * 1e3 / ITERS, calls, h[20] / calls);
     for (int k = 0; k < 9; k++) printf("  %-28s %8.0f cycles per select\n", names[k], h[k] / calls);
     return 0;
 }
