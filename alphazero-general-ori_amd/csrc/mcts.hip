@@ -24,6 +24,10 @@ __device__ unsigned long long g_select_timing[24];
 #endif
 #include "mcts_device.h"
 
+#ifndef SELECT_WAVES
+#define SELECT_WAVES 7     // k_select waves per SIMD (SGPR budget: 6 at 106 SGPRs, 7 at <= 96)
+#endif
+
 using namespace spl;
 
 struct spl_ctx {  // must match splendor_env.hip
@@ -391,6 +395,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
         // and batches run in increasing k with all reads before the writes, so no write
         // reaches an edge that is still to be read.
         if (l == 0) scr[kept] = edges;
+        __threadfence_block();                          // (scr may be global memory)
         __builtin_amdgcn_wave_barrier();
         constexpr int R = 4;
         for (int k0 = 0; k0 < edges; k0 += 64 * R) {
@@ -483,10 +488,13 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
             return H->node_count + budget + 1 <= P.ncap &&
                    (long long)H->edge_count + SPL_ACTIONS + (long long)budget * C.edge_reserve <= (long long)P.ecap;
         };
-        // lazy garbage collection: nodes with rounds <= the root's are unreachable (and no
-        // lookup can match them), so they are only compacted away when the search would
-        // not fit otherwise — the search sees the same reachable table either way
-        if (!fits()) {
+        // lazy garbage collection (self-play): nodes with rounds <= the root's are
+        // unreachable (and no lookup can match them), so they are only compacted away when
+        // the search would not fit otherwise, or when a leaf does not fit mid-search
+        // (k_backup withdraws the simulation, k_commit collects) — the search sees the same
+        // reachable table either way. Without k_commit (search-only arenas) every search
+        // starts on a compacted tree.
+        if (!C.selfplay || !fits()) {
             const int rr = (uint8_t)bt(row(s, 0), 6);
             // edge-move scratch: LDS for small trees, the tree's global scratch otherwise
             int *cs = P.ncap <= SCR_NODES && scr ? scr : P.cscr + (size_t)t * 2 * (P.ncap + 1);
@@ -521,6 +529,7 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         H->noise_pending = full && C.dirichlet;
         H->leaf_kind = LEAF_NONE;
         H->overflow = 0;
+        H->gc_state = 0;
         H->move_no = mv + 1;
     }
     __threadfence_block();
@@ -604,6 +613,18 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     if (t >= B) return;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
+    if (H->gc_state == 1) {                              // requested by k_backup (lazy GC)
+        const int root = H->root;
+        const size_t nbr = (size_t)t * P.ncap;
+        int *cs = P.ncap <= SCR_NODES ? cscr[w] : P.cscr + (size_t)t * 2 * (P.ncap + 1);
+        const int nroot = compact_tree(P, t, root, P.nround[nbr + root], cs,
+                                       P.ncap <= SCR_NODES ? SCR_NODES + 1 : P.ncap + 1);
+        if (l == 0) {
+            H->root = nroot; H->root_eb = P.neb[nbr + nroot]; H->root_ec = P.nec[nbr + nroot];
+            H->gc_state = 2;                             // once per search
+        }
+        return;
+    }
     if (H->sims_done < H->budget || H->overflow || H->root < 0) return;
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const uint32_t gb = C.board_base + (uint32_t)t;
@@ -771,7 +792,7 @@ __global__ void k_drain_reset(Pools P, int max, int32_t *n_out) {
 
 // ------------------------------------------------------------ select
 template <int N>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) void k_select(Pools P, SearchCfg C, int B, int lim,
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_WAVES))) void k_select(Pools P, SearchCfg C, int B, int lim,
                                                     int8_t *__restrict__ leaf_state,
                                                     uint64_t *__restrict__ leaf_mask,
                                                     uint8_t *__restrict__ leaf_valid) {
@@ -1033,7 +1054,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         int ec = 0;
 #pragma unroll
         for (int k = 0; k < 7; k++) ec += __popcll(m[k]);
-        const int id = H->node_count, eb = H->edge_count;
+        int id = H->node_count, eb = H->edge_count;
+        if (eb + ec > P.ecap && depth > 0 && H->gc_state == 0) {
+            // garbage is collected lazily (begin_search), so a search may run out of edge
+            // room with dead nodes still in the pool: this simulation is withdrawn (no
+            // backup, not counted), k_commit collects the garbage (exact: nodes with rounds
+            // <= the root's) and the next select repeats the same descent
+            if (l == 0) { H->gc_state = 1; H->leaf_kind = LEAF_NONE; }
+            return;
+        }
         if (id >= P.ncap || eb + ec > P.ecap) {          // no room: back up v, do not store
 #pragma unroll
             for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];

@@ -30,6 +30,7 @@ struct TreeHdr {
     // (evaluated and backed up without being stored); root_eb / root_ec: the root's CSR
     // range (so the descent's first level needs no node load)
     int32_t prunes, resets, unexpanded, root_ec;
+    int32_t gc_state, pad1, pad2, pad3;  // 1: a leaf did not fit, k_commit collects garbage; 2: done
 };
 enum { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2 };
 

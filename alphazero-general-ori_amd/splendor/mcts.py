@@ -21,7 +21,7 @@ import torch
 from . import _lib
 from .env import ACTIONS, MASK_WORDS, _ptr
 
-# TreeHdr (csrc/mcts_device.h), 128 bytes
+# TreeHdr (csrc/mcts_device.h), 144 bytes
 HDR_DTYPE = np.dtype([
     ("node_count", "<i4"), ("edge_count", "<i4"), ("root", "<i4"), ("sims_done", "<i4"),
     ("budget", "<i4"), ("full", "<i4"), ("noise_pending", "<i4"), ("depth", "<i4"),
@@ -29,8 +29,9 @@ HDR_DTYPE = np.dtype([
     ("game_no", "<i4"), ("overflow", "<i4"), ("n_examples", "<i4"), ("leaf_round", "<i4"),
     ("leaf_k0", "<u8"), ("leaf_k1", "<u8"), ("leaf_v", "<f4", (4,)),
     ("games_done", "<i4"), ("forced", "<i4"), ("pad0", "<i4"), ("root_eb", "<i4"),
-    ("prunes", "<i4"), ("resets", "<i4"), ("unexpanded", "<i4"), ("root_ec", "<i4")])
-assert HDR_DTYPE.itemsize == 128
+    ("prunes", "<i4"), ("resets", "<i4"), ("unexpanded", "<i4"), ("root_ec", "<i4"),
+    ("gc_state", "<i4"), ("pad1", "<i4"), ("pad2", "<i4"), ("pad3", "<i4")])
+assert HDR_DTYPE.itemsize == 144
 
 DEFAULT_ARGS = dict(numMCTSSims=100, cpuct=1.0, fpu=0.0, prob_fullMCTS=1.0, ratio_fullMCTS=5,
                     forced_playouts=False, dirichletAlpha=0.0, temperature=[1.25, 0.8],

@@ -217,7 +217,7 @@ int spl_mcts_counters(spl_mcts *m, int32_t *out, void *hip_stream);
 int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *valid,
                             float *winner, int32_t *scdiff, float *q, int32_t *meta, int max,
                             int32_t *n_out, void *hip_stream);
-/* copies the B per-tree headers (112 bytes each, layout in splendor/mcts.py) to `out` */
+/* copies the B per-tree headers (144 bytes each, layout in splendor/mcts.py) to `out` */
 int spl_mcts_headers(spl_mcts *m, int32_t *out, void *hip_stream);
 
 /* predict input conversion (GenericNNetWrapper.py:160-161): int8 boards [B][R][7] -> f32
