@@ -211,28 +211,27 @@ __device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int 
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
     }
-    double g[7];
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
+    // Dirichlet: gammas lane-parallel, their sum sequential in action order; the gammas
+    // are drawn again for the mix (deterministic) instead of being kept in registers
+    double acc = 0.0;
+#pragma unroll 1
+    for (int j = 0; j < (ec + 63) / 64; j++) {
         const int i = 64 * j + l;
-        g[j] = i < ec ? det_gamma(C.dir_alpha, C.seed, gb, stream, (uint32_t)i * 4096u) : 0.0;
-    }
-    double acc = 0.0;                            // sequential, in action order
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
+        const double g = i < ec ? det_gamma(C.dir_alpha, C.seed, gb, stream, (uint32_t)i * 4096u) : 0.0;
         const int m = min(64, ec - 64 * j);
-        const int lo = __double2loint(g[j]), hi = __double2hiint(g[j]);
+        const int lo = __double2loint(g), hi = __double2hiint(g);
         for (int k = 0; k < m; k++)
             acc = acc + __hiloint2double(__builtin_amdgcn_readlane(hi, k), __builtin_amdgcn_readlane(lo, k));
     }
     const bool ok = acc > 0.0;
     const double inv = ok ? 1.0 / acc : 0.0;
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
+#pragma unroll 1
+    for (int j = 0; j < (ec + 63) / 64; j++) {
         const int i = 64 * j + l;
         if (i < ec) {
             const int a = elk[i].a;
-            const double d = ok ? g[j] * inv : 1.0 / (double)ec;
+            const double d = ok ? det_gamma(C.dir_alpha, C.seed, gb, stream, (uint32_t)i * 4096u) * inv
+                                : 1.0 / (double)ec;
             pr[a] = (float)(0.75 * (double)pr[a] + 0.25 * d);
         }
     }
@@ -830,8 +829,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         // {eb, ec} cached on the edge that led to it, so a level costs ONE round trip (the
         // node's visit stats travel with its edges); ec < 0 marks a terminal child
         int eb = H->root_eb, ec = H->root_ec;
-        if (sims == 0 && H->noise_pending)
+        if (sims == 0 && H->noise_pending) {
             apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no, lpr[w], false);
+            if (l == 0) H->noise_pending = 0;           // (a withdrawn simulation must not re-noise)
+        }
         const bool forced = H->forced;
         for (;;) {
             SPL_PROBE(1)

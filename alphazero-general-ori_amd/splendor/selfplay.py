@@ -125,6 +125,7 @@ class SelfPlay(BatchedMCTS):
         return {"games_done": int(h["games_done"].sum()), "moves": int(h["pad0"].sum()),
                 "overflow": int((h["overflow"] != 0).sum()),
                 "nodes_max": int(h["node_count"].max()), "edges_max": int(h["edge_count"].max()),
+                "leaf_depth_mean": float(h["depth"].mean()), "leaf_depth_max": int(h["depth"].max()),
                 **self.capacity_events(h), "examples_dropped": self.dropped_examples()}
 
 

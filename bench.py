@@ -257,7 +257,8 @@ def selfplay_record(args, r, world, steps, warmup):
             "ms_per_iteration": r["elapsed"] / steps * 1e3, "steps": steps, "warmup": warmup,
             "window": {**r["window"], "examples_drained": r["examples"], "examples_gathered": r["examples_gathered"],
                        "drain_allgather_s": r["gather_s"]},
-            "tree": {k: r["stats"][k] for k in ("nodes_max", "edges_max", "overflow", "examples_dropped")}
+            "tree": {k: r["stats"][k] for k in ("nodes_max", "edges_max", "leaf_depth_mean", "leaf_depth_max",
+                                                 "overflow", "examples_dropped")}
                     | {"node_cap": r["node_cap"], "edge_cap": r["edge_cap"], "device_bytes": r["device_bytes"]},
             "symmetry_expansion": r["symmetry"],
             "network_kernel": {"kernel": f"k_nn_forward<{args.players}>", "avg_us": r["nn_kernel_us"],

@@ -14,7 +14,8 @@ import sys
 KERNELS = ("k_select", "k_leaf_mask", "k_nn_forward", "k_backup", "k_commit")
 
 
-def per_kernel(d):
+def per_kernel(d, last=None):
+    """Counter averages per dispatch of each kernel, over its last `last` dispatches."""
     acc = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -27,8 +28,9 @@ def per_kernel(d):
             acc[k][disp][c] = acc[k][disp].get(c, 0.0) + float(r["Counter_Value"])
     out = {}
     for k, disps in acc.items():
-        names = {c for v in disps.values() for c in v}
-        out[k] = {c: sum(v.get(c, 0.0) for v in disps.values()) / len(disps) for c in names}
+        ids = sorted(disps)[-last:] if last else sorted(disps)
+        names = {c for i in ids for c in disps[i]}
+        out[k] = {c: sum(disps[i].get(c, 0.0) for i in ids) / len(ids) for c in names}
     return out
 
 
@@ -44,12 +46,16 @@ def durations(d):
 
 def main():
     root, rnd = sys.argv[1], sys.argv[2]
-    fe, wr, sq, du = (per_kernel(os.path.join(root, "fetch")), per_kernel(os.path.join(root, "write")),
-                      per_kernel(os.path.join(root, "sq")), durations(os.path.join(root, "trace")))
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else None
+    warm = int(sys.argv[4]) if len(sys.argv) > 4 else None
+    fe, wr, sq, sq2, mem = (per_kernel(os.path.join(root, x), steps) for x in ("fetch", "write", "sq", "sq2", "mem"))
+    du = durations(os.path.join(root, "trace"))
     res = {"round": rnd, "workload": "config 3: 32768 self-play games, numMCTSSims=100 (genbu args), "
-           "one select/network/backup/commit per iteration",
-           "command": "tools/pmc_selfplay.sh (separate --pmc passes; python3 bench.py --workload selfplay "
-                      "--steps 40 --warmup 10)", "kernels": {}}
+           "one select/network/backup/commit per iteration, steady state",
+           "command": f"tools/pmc_selfplay.sh (separate --pmc passes; python3 bench.py --workload selfplay "
+                      f"--steps {steps} --warmup {warm}); counters averaged over each kernel's last {steps} "
+                      f"dispatches; durations: kernel trace over the whole run",
+           "kernels": {}}
     for k in KERNELS:
         e = {}
         if k in du:
@@ -58,15 +64,31 @@ def main():
             e["hbm_bytes_per_launch"] = fe[k]["FETCH_SIZE"] * 1024 * 2 + wr[k]["WRITE_SIZE"] * 1024
             if "avg_us" in e:
                 e["hbm_GBps"] = e["hbm_bytes_per_launch"] / (e["avg_us"] * 1e3)
-        if k in sq:
-            s = sq[k]
+        s = {**sq.get(k, {}), **sq2.get(k, {}), **mem.get(k, {})}
+        if s:
             w = max(s.get("SQ_WAVES", 1.0), 1.0)
             e["waves"] = s.get("SQ_WAVES")
-            for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "SQ_INSTS_MFMA"):
+            for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+                      "SQ_INSTS_LDS", "SQ_INSTS_MFMA"):
                 if c in s:
                     e[c.lower().replace("sq_insts_", "") + "_per_wave"] = s[c] / w
-            if "SQ_WAVE_CYCLES" in s and s["SQ_WAVE_CYCLES"]:
-                e["wait_frac"] = s.get("SQ_WAIT_ANY", 0.0) / s["SQ_WAVE_CYCLES"]
+            wc = s.get("SQ_WAVE_CYCLES")
+            if wc:
+                e["wait_frac"] = s.get("SQ_WAIT_ANY", 0.0) / wc
+                e["wait_inst_frac"] = s.get("SQ_WAIT_INST_ANY", 0.0) / wc
+                e["active_inst_frac"] = s.get("SQ_ACTIVE_INST_ANY", 0.0) / wc
+                e["wave_cycles_per_wave"] = wc / w
+            if s.get("SQ_INSTS_VMEM_RD") and "SQ_INST_LEVEL_VMEM" in s:
+                e["vmem_latency_cycles"] = s["SQ_INST_LEVEL_VMEM"] / (s["SQ_INSTS_VMEM_RD"] + s.get("SQ_INSTS_VMEM_WR", 0.0))
+            if s.get("TCP_TCC_READ_REQ_sum"):
+                e["l2_read_latency_cycles"] = s.get("TCP_TCC_READ_REQ_LATENCY_sum", 0.0) / s["TCP_TCC_READ_REQ_sum"]
+                e["l2_read_requests"] = s["TCP_TCC_READ_REQ_sum"]
+            if s.get("TCC_HIT_sum") is not None and s.get("TCC_MISS_sum") is not None:
+                e["l2_hit_rate"] = s["TCC_HIT_sum"] / max(s["TCC_HIT_sum"] + s["TCC_MISS_sum"], 1.0)
+            tm, th = s.get("TCP_UTCL1_TRANSLATION_MISS_sum"), s.get("TCP_UTCL1_TRANSLATION_HIT_sum")
+            if tm is not None and th is not None:
+                e["utcl1_miss_rate"] = tm / max(tm + th, 1.0)
+            e["raw"] = s
         res["kernels"][k] = e
     print(json.dumps(res, indent=1))
 
