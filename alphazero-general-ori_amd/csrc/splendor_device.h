@@ -1201,6 +1201,44 @@ __device__ __forceinline__ void lane_deal_record(uint64_t seed, uint32_t board, 
     }
     r.perm = perm;
 }
+// one quarter of lane_deal_record: part t < 3 deals tier t (draws 8t .. 8t+7: Philox
+// blocks 4t .. 4t+3), part 3 the nobles (draws 24 .. 28: blocks 12 .. 14). The parts write
+// disjoint fields, so four lanes build a record together at a quarter of the latency.
+template <int N>
+__device__ __forceinline__ void lane_deal_part(uint64_t seed, uint32_t board, uint32_t game, int part,
+                                               const Tabs &tab, DealRec &r) {
+    if (part < 3) {
+        const int t = part;
+        double u[8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) philox_pair(seed, board, DEAL_STREAM | game, 4 * t + k, u[2 * k], u[2 * k + 1]);
+        const uint64_t len = t == 0 ? 8 : (t == 1 ? 6 : 4);
+        uint64_t cnt = len * 0x0000000101010101ull;
+        uint64_t bits = (uint8_t)(0xFFu << (8 - len)) * 0x0000000101010101ull;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            int color, idx;
+            deck_pick(cnt, bits, u[2 * i], u[2 * i + 1], tab, color, idx);
+            deck_take(cnt, bits, color, idx);
+            r.card[4 * t + i] = (uint8_t)(t * 40 + color * 8 + idx);
+        }
+        r.cnt[t] = cnt;
+        r.bits[t] = bits;
+    } else {
+        double u[6];
+#pragma unroll
+        for (int k = 0; k < 3; k++) philox_pair(seed, board, DEAL_STREAM | game, 12 + k, u[2 * k], u[2 * k + 1]);
+        uint64_t perm = 0x9876543210ull;
+#pragma unroll
+        for (int i = 0; i < Lay<N>::NN; i++) {
+            const int j = i + (int)floor(u[i] * (double)(10 - i));
+            const uint64_t pi = (perm >> (4 * i)) & 15, pj = (perm >> (4 * j)) & 15;
+            perm &= ~((15ull << (4 * i)) | (15ull << (4 * j)));
+            perm |= (pj << (4 * i)) | (pi << (4 * j));
+        }
+        r.perm = perm;
+    }
+}
 // wave-collective: the board a record describes (every row written once; = wave_init_game)
 template <int N>
 __device__ __forceinline__ void wave_apply_deal(int8_t *s, const DealRec &r, const Tabs &tab) {

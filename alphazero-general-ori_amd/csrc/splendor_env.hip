@@ -253,16 +253,17 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     if (tid < 4) kcount[tid] = 0;
     stage_tabs(tabs, tid, THREADS);
     for (int i = tid; i < 7 * 116; i += THREADS) mfac[i] = (&K_MASK_FACTORS[0][0])[i];
-    // the next two deals of every board, computed up front (lane per board and game, 32
-    // lanes of each wave) so that ending a game costs a row expansion, not the draws;
-    // a third game ending within the launch draws its deal on the spot (same keys)
-    const bool pre = K >= 16;
+    // the next deals of every board (one for launches of 4-47 moves, two beyond),
+    // computed up front by four lanes per deal (3 tiers + nobles, lane_deal_part) so that
+    // ending a game costs a row expansion, not the draws; a game ending beyond them draws
+    // its deal on the spot (same keys)
+    const int pre = K >= 48 ? 2 : (K >= 4 ? 1 : 0);
     lds_sync();                                            // tables and gdone staged
     if (tid < nb) gd0[tid] = gdone[tid];
-    if (pre && l < 32) {
-        const int r = w * 32 + l, k = r >> 6, b = r & (RB - 1);
-        if (b < nb) lane_deal_record<N>(seed, bbase + (uint32_t)(b0 + b), (uint32_t)(gdone[b] + 1 + k),
-                                        tabs.view(), drec[k][b]);
+    for (int task = tid; task < pre * RB * 4; task += THREADS) {
+        const int part = task & 3, rec = task >> 2, k = rec / RB, b = rec - k * RB;
+        if (b < nb) lane_deal_part<N>(seed, bbase + (uint32_t)(b0 + b), (uint32_t)(gdone[b] + 1 + k), part,
+                                      tabs.view(), drec[k][b]);
     }
     // every barrier of the move loop orders LDS only: the per-move outputs are write-only
     // HBM streams, and waiting for their stores (__syncthreads) cost ~2K cycles a barrier
@@ -444,7 +445,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
                 const int rb = __shfl(b, __ffsll((unsigned long long)rm) - 1);
                 const int g = gdone[rb];                      // the new game's number
                 const int slot = g - gd0[rb] - 1;
-                if (pre && slot < 2) {
+                if (slot < pre) {
                     wave_apply_deal<N>(lds + rb * ST, drec[slot][rb], tabs.view());
                     RT_MARK(8)
                 } else {

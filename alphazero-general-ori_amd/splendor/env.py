@@ -196,6 +196,22 @@ class RolloutBatch:
                             self.seed, self.t, self.board_base)
         self.t += 1
 
+    def launcher(self, K, out):
+        """A prebuilt launch of `run(K, out=out)`: every argument but the step counter is
+        converted once, so a timed region pays one ctypes call per launch (bench.py)."""
+        e = self.e
+        fn = e.L.spl_rollout_run
+        head = (e.ctx, self.B, int(K), _ptr(self.state), _ptr(self.player), _ptr(out["mask"]),
+                _ptr(out["action"]), _ptr(out["ended"]), _ptr(self.games), self.seed)
+        tail = (self.board_base, e._s())
+
+        def launch():
+            rc = fn(*head, self.t, *tail)
+            if rc:
+                _lib.check(rc, "spl_rollout_run")
+            self.t += K
+        return launch
+
     def run(self, K, masks=True, out=None):
         """K moves in one launch (boards stay on chip); returns the stacked per-move outputs
         {"mask": [K,B,7] or None, "action": [K,B], "ended": [K,B,n]} (reused if `out`)."""

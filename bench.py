@@ -29,6 +29,7 @@ import torch  # noqa: E402
 METRIC = "self-play rollouts/sec (32k boards, 2p Splendor) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP32_MFMA_PEAK = 157.3    # TFLOP/s, dense fp32 MFMA (MI355X_MICROARCH.md)
+RAMP_S = 0.05             # untimed launches before the env window (GPU clock ramp)
 
 
 def bytes_per_board_step(n):
@@ -201,6 +202,8 @@ def run_selfplay(args, rank, world, dev, dist, steps=None, warmup=None):
     torch.cuda.synchronize(dev)
     st0 = sp.stats()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    ev1.record()
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -339,10 +342,6 @@ def main():
             dist.destroy_process_group()
         return
 
-    cpu = None
-    if rank == 0 and world == 1 and args.gpus == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.players, args.seed)
-
     from splendor.env import RolloutBatch, SplendorEngine
     eng = SplendorEngine(args.players, device=dev)
     B = args.boards
@@ -358,18 +357,33 @@ def main():
         w -= chunk
     for k in set(launches):
         run(k)                                 # output buffers of every launch size exist
+    launchers = {k: rb.launcher(k, outs[k]) for k in set(launches)}
+    # clock ramp: an idle GPU starts the timed launches at a low clock; untimed launches of
+    # the timed size for ~RAMP_S seconds first (the boards just play on)
+    ramp = 0
+    t_r = time.perf_counter()
+    while time.perf_counter() - t_r < RAMP_S:
+        launchers[chunk]()
+        ramp += 1
+        if ramp % 16 == 0:
+            torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
 
     # HIP events on the stream the kernel is launched on (torch's current stream): one
-    # pair around the back-to-back launches -> average launch duration
+    # pair around the back-to-back launches -> average launch duration (recorded once before:
+    # torch creates the HIP event at its first record, which must not land in the window)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    ev1.record()
+    torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    seq = [launchers[k] for k in launches]
     t0 = time.perf_counter()
     ev0.record()
-    for k in launches:
-        run(k)
+    for fn in seq:
+        fn()
     ev1.record()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -380,6 +394,10 @@ def main():
         elapsed = float(t.item())
     kernel_ms = ev0.elapsed_time(ev1) / len(launches)
     games = int(rb.games.sum().item())
+
+    cpu = None                                 # (after the GPU window: the CPU sample runs for seconds)
+    if rank == 0 and world == 1 and args.gpus == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.players, args.seed)
 
     secondary = None
     if not args.no_selfplay:
@@ -430,6 +448,7 @@ def main():
                          "pmc": issue},
             "cpu_baseline": cpu,
             "games_completed": games,
+            "untimed_ramp_launches": ramp,
             "config3_selfplay": secondary,
         }
         print(json.dumps(out))
