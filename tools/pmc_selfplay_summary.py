@@ -48,7 +48,8 @@ def main():
     root, rnd = sys.argv[1], sys.argv[2]
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else None
     warm = int(sys.argv[4]) if len(sys.argv) > 4 else None
-    fe, wr, sq, sq2, mem = (per_kernel(os.path.join(root, x), steps) for x in ("fetch", "write", "sq", "sq2", "mem"))
+    fe, wr, sq, sq2, mem, ea = (per_kernel(os.path.join(root, x), steps)
+                                for x in ("fetch", "write", "sq", "sq2", "mem", "ea"))
     du = durations(os.path.join(root, "trace"))
     res = {"round": rnd, "workload": "config 3: 32768 self-play games, numMCTSSims=100 (genbu args), "
            "one select/network/backup/commit per iteration, steady state",
@@ -64,7 +65,14 @@ def main():
             e["hbm_bytes_per_launch"] = fe[k]["FETCH_SIZE"] * 1024 * 2 + wr[k]["WRITE_SIZE"] * 1024
             if "avg_us" in e:
                 e["hbm_GBps"] = e["hbm_bytes_per_launch"] / (e["avg_us"] * 1e3)
-        s = {**sq.get(k, {}), **sq2.get(k, {}), **mem.get(k, {})}
+        s = {**sq.get(k, {}), **sq2.get(k, {}), **mem.get(k, {}), **ea.get(k, {})}
+        if "TCC_EA0_RDREQ_sum" in s:
+            # memory-side read requests by size (MI355X_MICROARCH.md: FETCH_SIZE = RDREQ x 64 B,
+            # exact only for 128-B streaming reads); random small reads are sized per request
+            n, n32, n128 = s["TCC_EA0_RDREQ_sum"], s.get("TCC_EA0_RDREQ_32B_sum", 0.0), s.get("TCC_EA0_RDREQ_128B_sum", 0.0)
+            e["read_bytes_by_request_size"] = 32 * n32 + 64 * max(n - n32 - n128, 0.0) + 128 * n128
+            if k in wr:
+                e["hbm_bytes_per_launch_by_request_size"] = e["read_bytes_by_request_size"] + wr[k]["WRITE_SIZE"] * 1024
         if s:
             w = max(s.get("SQ_WAVES", 1.0), 1.0)
             e["waves"] = s.get("SQ_WAVES")
