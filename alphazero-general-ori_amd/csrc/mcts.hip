@@ -45,7 +45,10 @@ struct spl_mcts {
 
 namespace {
 
-constexpr int WAVES = 4;
+#ifndef TREE_WG
+#define TREE_WG 1          // waves (trees) per workgroup of the per-tree kernels: trees finish
+#endif                     // at different depths, and a 1-wave workgroup frees its slot at once
+constexpr int WAVES = TREE_WG;
 constexpr int THREADS = 64 * WAVES;
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
@@ -75,7 +78,7 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         const int i = 64 * j + l;
         EdgeStat st{0.f, 0, Q_UNSET};
         EdgeLink lk{0, 0, -1, 0, 0};
-        if (i < ec) { st = P.es[e0 + i]; lk = P.el[e0 + i]; }
+        if (i < ec) { st = P.ed[e0 + i].s; lk = P.ed[e0 + i].k; }
         p[j] = st.p; n[j] = st.n; q[j] = st.q;
         a[j] = lk.a; c[j] = lk.child; r[j] = get_cr(lk);
     }
@@ -95,13 +98,40 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         for (int base = 128; bi < 0 && base < ec; base += 64) {
             const int i = base + l;
             bool f = false;
-            if (i < ec) f = (long long)P.es[e0 + i].n < (long long)sqrt(0.5 * (double)P.es[e0 + i].p * (double)step);
+            if (i < ec) f = (long long)P.ed[e0 + i].s.n < (long long)sqrt(0.5 * (double)P.ed[e0 + i].s.p * (double)step);
             const uint64_t b = __ballot(f);
             if (b) bi = base + __ffsll((unsigned long long)b) - 1;
         }
     }
+    const double fpu_init = C.fpu > 0 ? qs - C.fpu : C.fpu;
+    if (bi < 0 && ec <= 128) {
+        // pick_highest_UCB screened in float32: each edge's UCB u (the float64 value the
+        // reference computes) lies in [uf - e, uf + e] for its float32 estimate uf (relative
+        // error of the estimate <= 7e-7 of |uf| + |q|; e is 3x that). With L = max(uf - e),
+        // every edge that can hold the maximum has uf + e >= L; when that is one edge, it is
+        // the strict-'>' arg-max and the exact float64 evaluation is skipped. Ties and near
+        // ties (several candidates) fall through to the exact path below.
+        const float cf = (float)C.cpuct, sqf = sqrtf((float)ns), sqef = sqrtf((float)ns + 1e-8f);
+        const float ff = (float)fpu_init;
+        float lo[2], hi[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            lo[j] = -INFINITY; hi[j] = -INFINITY;
+            if (64 * j + l < ec) {
+                const bool vis = q[j] != Q_UNSET;
+                const float qf = vis ? (float)q[j] : ff;
+                const float tf = vis ? cf * p[j] * sqf * __builtin_amdgcn_rcpf(1.f + (float)n[j]) : cf * p[j] * sqef;
+                const float uf = qf + tf;
+                const float e = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
+                lo[j] = uf - e; hi[j] = uf + e;
+            }
+        }
+        const float L = wave_max_f32(fmaxf(lo[0], lo[1]));
+        const uint64_t c0 = __ballot(hi[0] >= L), c1 = __ballot(hi[1] >= L);
+        if (__popcll(c0) + __popcll(c1) == 1)
+            bi = uniform(c0 ? __ffsll((unsigned long long)c0) - 1 : 64 + __ffsll((unsigned long long)c1) - 1);
+    }
     if (bi < 0) {                               // pick_highest_UCB (MCTS.py:199-219)
-        const double fpu_init = C.fpu > 0 ? qs - C.fpu : C.fpu;
         const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
         double bu = -INFINITY, uj[2];
         int bj = 0x7fffffff;
@@ -128,8 +158,8 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         for (int base = 128; bi < 0 && base < ec; base += 64) {
             const int i = base + l;
             if (i < ec) {
-                const double qq = P.es[e0 + i].q, pp = (double)P.es[e0 + i].p;
-                const double u = qq != Q_UNSET ? qq + C.cpuct * pp * sq / (double)(1 + P.es[e0 + i].n)
+                const double qq = P.ed[e0 + i].s.q, pp = (double)P.ed[e0 + i].s.p;
+                const double u = qq != Q_UNSET ? qq + C.cpuct * pp * sq / (double)(1 + P.ed[e0 + i].s.n)
                                                : fpu_init + C.cpuct * pp * sq_eps;
                 if (u > bu) { bu = u; bj = i; }
             }
@@ -149,7 +179,7 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
     cv = __builtin_amdgcn_readlane(cv, bi & 63);
     rx = __builtin_amdgcn_readlane(rx, bi & 63);
     ry = __builtin_amdgcn_readlane(ry, bi & 63);
-    if (bi >= 128) { av = P.el[e0 + bi].a; cv = P.el[e0 + bi].child; const int2 rr = get_cr(P.el[e0 + bi]); rx = rr.x; ry = rr.y; }
+    if (bi >= 128) { av = P.ed[e0 + bi].k.a; cv = P.ed[e0 + bi].k.child; const int2 rr = get_cr(P.ed[e0 + bi].k); rx = rr.x; ry = rr.y; }
     return {bi, av, cv, make_int2(rx, ry)};
 }
 
@@ -191,14 +221,13 @@ __device__ __forceinline__ float wave_np_sum409(const float *a) {
 __device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int eb, int ec, uint32_t stream,
                                  float *pr, bool raw) {
     const int l = lane_id();
-    EdgeStat *est = P.es + (size_t)t * P.ecap + eb;
-    const EdgeLink *elk = P.el + (size_t)t * P.ecap + eb;
+    Edge *ede = P.ed + (size_t)t * P.ecap + eb;
     const uint32_t gb = C.board_base + (uint32_t)t;
     if (!raw) {
         for (int a = l; a < 416; a += 64) pr[a] = 0.f;
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
-        for (int i = l; i < ec; i += 64) pr[elk[i].a] = est[i].p;
+        for (int i = l; i < ec; i += 64) pr[ede[i].k.a] = ede[i].s.p;
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
     }
@@ -229,7 +258,7 @@ __device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int 
     for (int j = 0; j < (ec + 63) / 64; j++) {
         const int i = 64 * j + l;
         if (i < ec) {
-            const int a = elk[i].a;
+            const int a = ede[i].k.a;
             const double d = ok ? det_gamma(C.dir_alpha, C.seed, gb, stream, (uint32_t)i * 4096u) * inv
                                 : 1.0 / (double)ec;
             pr[a] = (float)(0.75 * (double)pr[a] + 0.25 * d);
@@ -238,7 +267,7 @@ __device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int 
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     const float nsum = wave_np_sum409(pr);
-    for (int i = l; i < ec; i += 64) est[i].p = pr[elk[i].a] / nsum;
+    for (int i = l; i < ec; i += 64) ede[i].s.p = pr[ede[i].k.a] / nsum;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
 }
@@ -274,7 +303,7 @@ __device__ void mark_linked(const Pools &P, int t, int root) {
         const int eb = P.neb[nb + node], ec = P.nterm[nb + node] ? 0 : P.nec[nb + node];
         for (int base = 0; base < ec; base += 64) {
             const int i = base + l;
-            const int c = i < ec ? P.el[e0 + eb + i].child : -1;
+            const int c = i < ec ? P.ed[e0 + eb + i].k.child : -1;
             const bool fresh = c >= 0 && atomicCAS(&mark[c], 0, 1) == 0;
             const uint64_t b = __ballot(fresh);
             if (fresh) q[tail + __popcll(b & lanemask_lt())] = c;
@@ -286,7 +315,7 @@ __device__ void mark_linked(const Pools &P, int t, int root) {
 }
 
 __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int *scr, int sstride,
-                            bool linked = false) {
+                            int bunits, bool linked = false) {
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
@@ -357,38 +386,11 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
             P.nqs[nb + ni] = qs; P.nterm[nb + ni] = term;
 #pragma unroll
             for (int j = 0; j < 4; j++) P.nes[(nb + ni) * 4 + j] = es[j];
-            if (scr) { scr[ni] = neb; scr[sstride + ni] = oeb; }
+            scr[ni] = neb; scr[sstride + ni] = oeb;
         }
-        if (scr) { edges += total; continue; }              // edges move in batches below
-        // move each kept node's edge block down (increasing order: never overlaps unread data)
-        for (int j = 0; j < 64; j++) {
-            const int jn = __shfl(ni, j, 64);
-            if (jn < 0) continue;
-            const int jo = __shfl(oeb, j, 64), jd = __shfl(neb, j, 64), jc = __shfl(ec, j, 64);
-            for (int base2 = 0; base2 < jc; base2 += 64) {
-                const int q = base2 + l;
-                const bool in = q < jc;
-                int16_t a = 0; float p = 0; int32_t cnt = 0, ch = -1; double qq = 0;
-                int2 cr = make_int2(0, 0);
-                if (in) {
-                    a = P.el[e0 + jo + q].a; p = P.es[e0 + jo + q].p; cnt = P.es[e0 + jo + q].n;
-                    qq = P.es[e0 + jo + q].q; ch = P.el[e0 + jo + q].child; cr = get_cr(P.el[e0 + jo + q]);
-                }
-                const int nch = ch >= 0 ? remap[ch] : -1;
-                if (nch >= 0) cr.x = remap_eb[ch];
-                __threadfence_block();
-                __builtin_amdgcn_wave_barrier();
-                if (in) {
-                    P.el[e0 + jd + q].a = a; P.es[e0 + jd + q].p = p; P.es[e0 + jd + q].n = cnt;
-                    P.es[e0 + jd + q].q = qq; P.el[e0 + jd + q].child = nch; set_cr(P.el[e0 + jd + q], cr.x, cr.y);
-                }
-                __threadfence_block();
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        edges += total;
+        edges += total;                                  // edges move in batches below
     }
-    if (scr) {
+    {
         // new position k of batch [k0, k0 + 256) comes from old position oeb(j) + k - neb(j),
         // j = the kept node whose new range holds k. Every old position is >= its new one
         // and batches run in increasing k with all reads before the writes, so no write
@@ -412,8 +414,8 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
                         if (scr[mid] <= k) lo = mid; else hi = mid - 1;
                     }
                     const int src = scr[sstride + lo] + (k - scr[lo]);
-                    st[r] = P.es[e0 + src];
-                    lk[r] = P.el[e0 + src];
+                    st[r] = P.ed[e0 + src].s;
+                    lk[r] = P.ed[e0 + src].k;
                 }
             }
 #pragma unroll
@@ -433,9 +435,44 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
                     EdgeLink o = lk[r];
                     o.child = nch[r];
                     if (nch[r] >= 0) o.ceb = ceb[r];
-                    P.es[e0 + k] = st[r];
-                    P.el[e0 + k] = o;
+                    P.ed[e0 + k].s = st[r];
+                    P.ed[e0 + k].k = o;
                 }
+            }
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (P.nbrd) {
+        // node boards (bunits 16-byte units each) move the same way: unit k of the kept
+        // boards comes from unit k + bunits * (old - new), old = scr[new] >= new,
+        // batches run in increasing k with all reads before the writes
+        for (int i = l; i < nc; i += 64)
+            if (remap[i] >= 0) scr[remap[i]] = i;
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        uint4 *bb = reinterpret_cast<uint4 *>(P.nbrd) + nb * bunits;
+        const int units = kept * bunits;
+        constexpr int R = 8;
+        for (int k0 = 0; k0 < units; k0 += 64 * R) {
+            uint4 d[R];
+            int src[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int k = k0 + 64 * r + l;
+                src[r] = k;
+                if (k < units) {
+                    const int nn = k / bunits;
+                    src[r] = k + bunits * (scr[nn] - nn);
+                    if (src[r] != k) d[r] = bb[src[r]];
+                }
+            }
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int k = k0 + 64 * r + l;
+                if (k < units && src[r] != k) bb[k] = d[r];
             }
             __threadfence_block();
             __builtin_amdgcn_wave_barrier();
@@ -498,9 +535,9 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
             // edge-move scratch: LDS for small trees, the tree's global scratch otherwise
             int *cs = P.ncap <= SCR_NODES && scr ? scr : P.cscr + (size_t)t * 2 * (P.ncap + 1);
             const int cstride = P.ncap <= SCR_NODES && scr ? SCR_NODES + 1 : P.ncap + 1;
-            root = compact_tree(P, t, root, rr, cs, cstride);
+            root = compact_tree(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS);
             if (!fits() && root >= 0) {
-                root = compact_tree(P, t, root, rr, cs, cstride, true);
+                root = compact_tree(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS, true);
                 if (l == 0) H->prunes += 1;
             }
         }
@@ -617,7 +654,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         const size_t nbr = (size_t)t * P.ncap;
         int *cs = P.ncap <= SCR_NODES ? cscr[w] : P.cscr + (size_t)t * 2 * (P.ncap + 1);
         const int nroot = compact_tree(P, t, root, P.nround[nbr + root], cs,
-                                       P.ncap <= SCR_NODES ? SCR_NODES + 1 : P.ncap + 1);
+                                       P.ncap <= SCR_NODES ? SCR_NODES + 1 : P.ncap + 1, NodeBoard<N>::UNITS);
         if (l == 0) {
             H->root = nroot; H->root_eb = P.neb[nbr + nroot]; H->root_ec = P.nec[nbr + nroot];
             H->gc_state = 2;                             // once per search
@@ -630,10 +667,9 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     const int root = H->root, eb = P.neb[nb + root], ec = P.nec[nb + root];
     const bool forced = H->forced;
     const int sims = H->budget, cm = H->move_no;
-    const EdgeStat *est = P.es + e0 + eb;
-    const EdgeLink *elk = P.el + e0 + eb;
+    const Edge *ede = P.ed + e0 + eb;
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, est[i].n);
+    for (int i = l; i < ec; i += 64) best = max(best, ede[i].s.n);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
     // policy counts: pruned (MCTS.py:69-74); where the reference would divide 0/0
     // (Coach.py:83 raises) fall back to raw counts, then to uniform
@@ -642,11 +678,11 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     for (; mode < 3; mode++) {
         tot = 0;
         for (int i = l; i < ec; i += 64)
-            tot += mode == 0 ? pruned_count(est[i].n, best, true, est[i].p, sims) : (mode == 1 ? est[i].n : 1);
+            tot += mode == 0 ? pruned_count(ede[i].s.n, best, true, ede[i].s.p, sims) : (mode == 1 ? ede[i].s.n : 1);
         for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
         if (tot > 0) break;
     }
-#define POLICY_COUNT(i) (mode == 0 ? pruned_count(est[i].n, best, true, est[i].p, sims) : (mode == 1 ? (long long)est[i].n : 1ll))
+#define POLICY_COUNT(i) (mode == 0 ? pruned_count(ede[i].s.n, best, true, ede[i].s.p, sims) : (mode == 1 ? (long long)ede[i].s.n : 1ll))
     const int step = H->episode_step + 1;
     const int player = H->player;
     int8_t *s = lds[w][0], *b = lds[w][1];
@@ -661,7 +697,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         for (int i = l; i < ec; i += 64)   // getSymmetries stores pi as float32 (SplendorGame.py:59-61)
-            pi[elk[i].a] = (float)((double)POLICY_COUNT(i) / (double)tot);
+            pi[ede[i].k.a] = (float)((double)POLICY_COUNT(i) / (double)tot);
         uint64_t m[7];
         wave_valid_moves<N>(s, 0, lim, m);
         store_mask(P.ex_valid + x * 7, m);
@@ -685,10 +721,10 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
             last += temp_pow((double)POLICY_COUNT(i) / (double)tot, T) / sum;
         const double u = philox_u01(C.seed, gb, ST_PICK | (uint32_t)cm, 0);
         double cdf = 0.0;
-        action = elk[ec - 1].a;
+        action = ede[ec - 1].k.a;
         for (int i = 0; i < ec; i++) {
             cdf += temp_pow((double)POLICY_COUNT(i) / (double)tot, T) / sum;
-            if (cdf / last > u) { action = elk[i].a; break; }
+            if (cdf / last > u) { action = ede[i].k.a; break; }
         }
     }
     action = __shfl(action, 0, 64);
@@ -797,7 +833,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                                                     uint8_t *__restrict__ leaf_valid) {
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
-    __shared__ __align__(16) float lpr[WAVES][416];          // root-noise scratch
+    __shared__ __align__(16) float lpr[WAVES][416];         // root-noise scratch
     const int w = uniform(threadIdx.x >> 6), t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
@@ -834,6 +870,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             if (l == 0) H->noise_pending = 0;           // (a withdrawn simulation must not re-noise)
         }
         const bool forced = H->forced;
+        // node_boards: a linked child's board is stored, so the descent follows links without
+        // the in-tree transition and stages a board only where it needs one (the edge to
+        // expand); `bnode` is the node whose board is in LDS (the root's, from root_state)
+        const uint64_t *nbrd = P.nbrd ? reinterpret_cast<const uint64_t *>(P.nbrd + nb * NodeBoard<N>::BYTES) : nullptr;
+        int bnode = node;
         for (;;) {
             SPL_PROBE(1)
             if (depth > 0 && ec < 0) {
@@ -852,6 +893,18 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             int child = uniform(pk.child);
             int2 cr = make_int2(uniform(pk.cr.x), uniform(pk.cr.y));
             SPL_PROBE(2)
+            if (child >= 0 && nbrd) {                        // linked: no transition needed
+                node = child;
+                eb = cr.x;
+                ec = cr.y;
+                continue;
+            }
+            if (bnode != node) {                             // stage this node's stored board
+                const uint64_t *src = nbrd + (size_t)node * (NodeBoard<N>::BYTES / 8);
+                for (int r = l; r < Lx::ROWS; r += 64) row(s, r) = src[r];
+                __builtin_amdgcn_wave_barrier();
+                bnode = node;
+            }
             Chance ch{nullptr, 0, 0, 0, 0};
             int nxt;                                         // MCTS.py:227-235, per kind
             switch (move_kind_of(pk.a)) {                    // (uniform: a scalar branch)
@@ -869,7 +922,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                 child = uniform(hash_lookup(P, t, k0, k1));
                 if (child >= 0) {                            // transposition: link + cache
                     cr = make_int2(P.neb[nb + child], P.nterm[nb + child] ? -1 : P.nec[nb + child]);
-                    if (l == 0) { P.el[e0 + ge].child = child; set_cr(P.el[e0 + ge], cr.x, cr.y); }
+                    if (l == 0) { P.ed[e0 + ge].k.child = child; set_cr(P.ed[e0 + ge].k, cr.x, cr.y); }
                 }
             }
             SPL_PROBE(4)
@@ -878,6 +931,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
 #endif
             if (child >= 0) {
                 node = child;
+                bnode = child;
                 eb = cr.x;
                 ec = cr.y;
                 continue;
@@ -904,8 +958,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
 #pragma unroll
                     for (int i = 0; i < 4; i++) P.nes[(nb + id) * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
                     hash_insert(P, t, k0, id);
-                    P.el[e0 + ge].child = id;
-                    set_cr(P.el[e0 + ge], 0, -1);
+                    P.ed[e0 + ge].k.child = id;
+                    set_cr(P.ed[e0 + ge].k, 0, -1);
                     H->node_count = id + 1;
                 }
                 break;
@@ -915,8 +969,14 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
     }
     __builtin_amdgcn_wave_barrier();
     SPL_PROBE(5)
-    if (kind == LEAF_NN)                                     // its mask: k_leaf_mask
+    if (kind == LEAF_NN) {                                   // its mask: k_leaf_mask
         wave_store_board<N>(leaf_state + (size_t)t * Lx::S, s);
+        const int id = H->node_count;                        // the slot k_backup will insert it at
+        if (P.nbrd && id < P.ncap) {
+            uint64_t *dst = reinterpret_cast<uint64_t *>(P.nbrd + (nb + id) * NodeBoard<N>::BYTES);
+            for (int r = l; r < Lx::ROWS; r += 64) dst[r] = row(s, r);
+        }
+    }
     SPL_PROBE(6)
     if (l == 0) {
         H->depth = depth;
@@ -1043,7 +1103,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
     if (l < depth) {
         pnode = path[2 * l];
         pge = path[2 * l + 1];
-        const EdgeStat st = P.es[e0 + pge];
+        const EdgeStat st = P.ed[e0 + pge].s;
         pcnt = st.n;
         pq = st.q;
         pns = P.nns[nb + pnode];
@@ -1082,11 +1142,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             if ((wd >> l) & 1) {
                 const int r = eb + run + __popcll(wd & lanemask_lt());
                 const int a = 64 * k + l;
-                P.el[e0 + r].a = (int16_t)a;
-                P.es[e0 + r].p = pr[a] / sum;
-                P.es[e0 + r].n = 0;
-                P.es[e0 + r].q = Q_UNSET;
-                P.el[e0 + r].child = -1;
+                P.ed[e0 + r].k.a = (int16_t)a;
+                P.ed[e0 + r].s.p = pr[a] / sum;
+                P.ed[e0 + r].s.n = 0;
+                P.ed[e0 + r].s.q = Q_UNSET;
+                P.ed[e0 + r].k.child = -1;
             }
             run += __popcll(wd);
         }
@@ -1101,8 +1161,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             hash_insert(P, t, H->leaf_k0, id);
             if (depth == 0) { H->root = id; H->root_eb = eb; H->root_ec = ec; }
             else {
-                P.el[e0 + path[2 * (depth - 1) + 1]].child = id;
-                set_cr(P.el[e0 + path[2 * (depth - 1) + 1]], eb, ec);
+                P.ed[e0 + path[2 * (depth - 1) + 1]].k.child = id;
+                set_cr(P.ed[e0 + path[2 * (depth - 1) + 1]].k, eb, ec);
             }
             H->node_count = id + 1;
             H->edge_count = eb + ec;
@@ -1126,12 +1186,12 @@ backup:
         double q = pq, qs = pqs;
         if (d >= 64) {                                   // levels beyond the prefetched 64
             node = path[2 * d]; ge = path[2 * d + 1];
-            cnt = P.es[e0 + ge].n; q = P.es[e0 + ge].q;
+            cnt = P.ed[e0 + ge].s.n; q = P.ed[e0 + ge].s.q;
             ns = P.nns[nb + node]; qs = P.nqs[nb + node];
         }
-        P.es[e0 + ge].q = ((double)cnt * q + v0) / (double)(cnt + 1);
+        P.ed[e0 + ge].s.q = ((double)cnt * q + v0) / (double)(cnt + 1);
         P.nqs[nb + node] = ((double)(ns + 1) * qs + v0) / (double)(ns + 2);
-        P.es[e0 + ge].n = cnt + 1;
+        P.ed[e0 + ge].s.n = cnt + 1;
         P.nns[nb + node] = ns + 1;
     }
     if (l == 0) {
@@ -1167,11 +1227,11 @@ __global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int
     const int sims = H->budget;
     const bool forced = H->forced;
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, P.es[e0 + eb + i].n);
+    for (int i = l; i < ec; i += 64) best = max(best, P.ed[e0 + eb + i].s.n);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
     long long top = 0;
     for (int i = l; i < ec; i += 64)
-        top = max(top, pruned_count(P.es[e0 + eb + i].n, best, forced, P.es[e0 + eb + i].p, sims));
+        top = max(top, pruned_count(P.ed[e0 + eb + i].s.n, best, forced, P.ed[e0 + eb + i].s.p, sims));
     for (int o = 32; o > 0; o >>= 1) top = max(top, (long long)__shfl_xor(top, o, 64));
     if (top == 0) {
         if (l == 0) action[t] = (int16_t)(int)(u * (double)SPL_ACTIONS);
@@ -1180,20 +1240,20 @@ __global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int
     int nbest = 0;
     for (int base = 0; base < ec; base += 64) {
         const int i = base + l;
-        const bool hit = i < ec && pruned_count(P.es[e0 + eb + i].n, best, forced, P.es[e0 + eb + i].p, sims) == top;
+        const bool hit = i < ec && pruned_count(P.ed[e0 + eb + i].s.n, best, forced, P.ed[e0 + eb + i].s.p, sims) == top;
         nbest += __popcll(__ballot(hit));
     }
     int k = (int)(u * (double)nbest);                    // k-th best in action order
     for (int base = 0; base < ec; base += 64) {
         const int i = base + l;
-        const bool hit = i < ec && pruned_count(P.es[e0 + eb + i].n, best, forced, P.es[e0 + eb + i].p, sims) == top;
+        const bool hit = i < ec && pruned_count(P.ed[e0 + eb + i].s.n, best, forced, P.ed[e0 + eb + i].s.p, sims) == top;
         const uint64_t b = __ballot(hit);
         const int c = __popcll(b);
         if (k < c) {
             uint64_t x = b;
             for (int j = 0; j < k; j++) x &= x - 1;
             const int pos = __ffsll((unsigned long long)x) - 1;
-            if (l == 0) action[t] = P.el[e0 + eb + base + pos].a;
+            if (l == 0) action[t] = P.ed[e0 + eb + base + pos].k.a;
             return;
         }
         k -= c;
@@ -1223,23 +1283,23 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
     __builtin_amdgcn_wave_barrier();
     const int eb = P.neb[nb + root], ec = P.nec[nb + root];
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, P.es[e0 + eb + i].n);
+    for (int i = l; i < ec; i += 64) best = max(best, P.ed[e0 + eb + i].s.n);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
     const int sims = H->budget;
     const bool forced = H->forced;
     long long tot = 0;
     for (int i = l; i < ec; i += 64) {
-        const int a = P.el[e0 + eb + i].a;
-        const long long c = pruned_count(P.es[e0 + eb + i].n, best, forced, P.es[e0 + eb + i].p, sims);
-        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = P.es[e0 + eb + i].n;
+        const int a = P.ed[e0 + eb + i].k.a;
+        const long long c = pruned_count(P.ed[e0 + eb + i].s.n, best, forced, P.ed[e0 + eb + i].s.p, sims);
+        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = P.ed[e0 + eb + i].s.n;
         if (adjusted) adjusted[(size_t)t * SPL_ACTIONS + a] = c;
-        if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = P.es[e0 + eb + i].q;
+        if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = P.ed[e0 + eb + i].s.q;
         tot += c;
     }
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
     for (int i = l; i < ec; i += 64) {
-        const int a = P.el[e0 + eb + i].a;
-        const long long c = pruned_count(P.es[e0 + eb + i].n, best, forced, P.es[e0 + eb + i].p, sims);
+        const int a = P.ed[e0 + eb + i].k.a;
+        const long long c = pruned_count(P.ed[e0 + eb + i].s.n, best, forced, P.ed[e0 + eb + i].s.p, sims);
         if (probs) probs[(size_t)t * SPL_ACTIONS + a] = (double)c / (double)tot;
     }
     if (q && l == 0) {
@@ -1262,7 +1322,7 @@ __global__ __launch_bounds__(THREADS) void k_root_priors(Pools P, int B, float *
     __builtin_amdgcn_wave_barrier();
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const int eb = P.neb[nb + root], ec = P.nec[nb + root];
-    for (int i = l; i < ec; i += 64) o[P.el[e0 + eb + i].a] = P.es[e0 + eb + i].p;
+    for (int i = l; i < ec; i += 64) o[P.ed[e0 + eb + i].k.a] = P.ed[e0 + eb + i].s.p;
 }
 
 // leaf int8 [B,R,7] + packed mask -> float32 board and bool mask (predict, :160-161).
@@ -1334,7 +1394,7 @@ extern "C" {
 
 // Pool layout of spl_mcts_create (also what spl_mcts_plan_bytes reports).
 struct Plan {
-    int ncap, ecap, hcap, pcap, S, excap, out_cap;
+    int ncap, ecap, hcap, pcap, S, excap, out_cap, nbb;   // nbb: bytes per node board (0: none)
     size_t bytes;
 };
 static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
@@ -1347,17 +1407,18 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     L.S = 7 * (32 + 10 * n + n * n);
     L.excap = cfg->selfplay ? 62 * n + 2 : 0;
     L.out_cap = cfg->selfplay ? (cfg->out_cap > 0 ? cfg->out_cap : 4 * B) : 0;
+    L.nbb = cfg->node_boards ? (8 * (32 + 10 * n + n * n) + 15) & ~15 : 0;
     const size_t nn = (size_t)B * L.ncap, ne = (size_t)B * L.ecap;
     const size_t nx = (size_t)B * L.excap, no = (size_t)L.out_cap;
     size_t bytes = 0;
     auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
     acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn); acc(4 * nn);
-    acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(sizeof(EdgeStat) * ne); acc(sizeof(EdgeLink) * ne);
+    acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(sizeof(Edge) * ne);
     acc(4 * (size_t)B * L.hcap); acc(8 * (size_t)B * L.pcap);
     acc(4 * nn); acc(4 * nn); acc(8 * ((size_t)B * (L.ncap + 1))); acc((size_t)B * L.S);
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
     acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
-    acc(16 * no); acc(64);
+    acc(16 * no); acc(64); acc((size_t)L.nbb * nn);
     L.bytes = bytes;
     return L;
 }
@@ -1404,7 +1465,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.neb = carve<int32_t>(p, nn); P.nec = carve<int32_t>(p, nn); P.nns = carve<int32_t>(p, nn);
     P.nround = carve<int32_t>(p, nn); P.nqs = carve<double>(p, nn); P.nterm = carve<int8_t>(p, nn);
     P.nes = carve<float>(p, 4 * nn);
-    P.es = carve<EdgeStat>(p, ne); P.el = carve<EdgeLink>(p, ne);
+    P.ed = carve<Edge>(p, ne);
     P.hslot = carve<int32_t>(p, (size_t)B * P.hcap);
     P.path = carve<int32_t>(p, 2 * (size_t)B * P.pcap);
     P.remap = carve<int32_t>(p, nn); P.remap_eb = carve<int32_t>(p, nn);
@@ -1419,6 +1480,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.out_winner = carve<float>(p, 4 * no); P.out_q = carve<float>(p, 4 * no);
     P.out_valid = carve<uint64_t>(p, 7 * no); P.out_scdiff = carve<int32_t>(p, 4 * no);
     P.out_meta = carve<int32_t>(p, 4 * no); P.counters = carve<int32_t>(p, 16);
+    P.nbrd = L.nbb ? carve<int8_t>(p, (size_t)L.nbb * nn) : nullptr;
     if (hipMemset(P.hslot, 0xFF, 4 * (size_t)B * P.hcap) != hipSuccess) {
         (void)hipFree(arena); delete m; return SPL_EDEVICE;
     }

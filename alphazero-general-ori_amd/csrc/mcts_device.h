@@ -34,8 +34,8 @@ struct TreeHdr {
 };
 enum { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2 };
 
-// Edge records, two 16-byte halves: what the UCB scan reads for every edge, and what is
-// read only for the chosen one (loaded in the same round trip).
+// Edge records, two 16-byte halves: the UCB inputs and the link (both read by the scan in
+// one round trip).
 struct __align__(16) EdgeStat {
     float p;       // prior Ps[a] (float32)
     int32_t n;     // Nsa
@@ -47,6 +47,11 @@ struct __align__(16) EdgeLink {
     int32_t child; // child node (-1: not linked yet)
     int32_t ceb;   // cached child CSR base
     int32_t pad;
+};
+// one edge = both halves in one 32-byte record (one pool pointer: fewer live SGPRs)
+struct __align__(16) Edge {
+    EdgeStat s;
+    EdgeLink k;
 };
 __device__ __forceinline__ int2 get_cr(const EdgeLink &e) { return make_int2(e.ceb, e.cec); }
 __device__ __forceinline__ void set_cr(EdgeLink &e, int eb, int ec) { e.ceb = eb; e.cec = (int16_t)ec; }
@@ -60,12 +65,13 @@ struct Pools {
     double *nqs;
     int8_t *nterm;
     float *nes;                          // ncap x 4 terminal values
-    EdgeStat *es;                        // UCB inputs of every edge (one 16-byte load)
-    EdgeLink *el;                        // action, child and the child's cached CSR range
+    Edge *ed;                            // edges: UCB inputs + action, child, child's CSR range
     int32_t *hslot;
     int32_t *path;                       // pcap x 2 (node, edge)
     int32_t *remap, *remap_eb;           // ncap scratch for compaction (new index, new CSR base)
     int32_t *cscr;                       // 2 x (ncap + 1) per tree: edge-move scratch of large trees
+    int8_t *nbrd;                        // ncap x LS canonical board per node (LDS row format), or
+                                         // nullptr (node_boards = 0: the descent re-applies moves)
     int8_t *root_state;                  // B x S (canonical root)
     // self-play (Coach.executeEpisode) state
     int excap, out_cap;                  // staged examples per tree, finished-example queue
@@ -79,6 +85,13 @@ struct Pools {
     uint64_t *out_valid;                 // out_cap x 7
     int32_t *out_scdiff, *out_meta;      // out_cap x 4, out_cap x 4 (board id, game, index, player)
     int32_t *counters;                   // [0] queued examples [1] dropped
+};
+
+// per-node board slot (Pools::nbrd): the LDS row format padded to 16 bytes
+template <int N>
+struct NodeBoard {
+    static constexpr int BYTES = (Lay<N>::LS + 15) & ~15;
+    static constexpr int UNITS = BYTES / 16;
 };
 
 struct SearchCfg {
@@ -131,6 +144,24 @@ __device__ __forceinline__ double wave_max_f64(double v) {
     for (int k = 0; k < 4; k++)
         r[k] = __hiloint2double(__builtin_amdgcn_readlane(hi, 16 * k), __builtin_amdgcn_readlane(lo, 16 * k));
     return fmax(fmax(r[0], r[1]), fmax(r[2], r[3]));
+}
+
+// wave maximum of a float through order-preserving int keys (v_max_i32 folds the DPP row
+// moves; no canonicalisation), uniform result. No NaNs; -0 < +0 here (callers compare the
+// result back in float).
+__device__ __forceinline__ int fkey(float x) {
+    const int b = __float_as_int(x);
+    return b ^ ((b >> 31) & 0x7fffffff);
+}
+__device__ __forceinline__ float wave_max_f32(float x) {
+    int k = fkey(x);
+    k = max(k, __builtin_amdgcn_update_dpp(k, k, 0xB1, 0xF, 0xF, false));
+    k = max(k, __builtin_amdgcn_update_dpp(k, k, 0x4E, 0xF, 0xF, false));
+    k = max(k, __builtin_amdgcn_update_dpp(k, k, 0x141, 0xF, 0xF, false));
+    k = max(k, __builtin_amdgcn_update_dpp(k, k, 0x140, 0xF, 0xF, false));
+    const int m = max(max(__builtin_amdgcn_readlane(k, 0), __builtin_amdgcn_readlane(k, 16)),
+                      max(__builtin_amdgcn_readlane(k, 32), __builtin_amdgcn_readlane(k, 48)));
+    return __int_as_float(m ^ ((m >> 31) & 0x7fffffff));
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {

@@ -10,7 +10,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("SPLENDOR_AMD_LIB") or os.path.join(PKG_ROOT, "libsplendor_amd.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 EINVAL, EDEVICE = -1, -2
 
 
@@ -77,7 +77,7 @@ class MctsConfig(C.Structure):
                 ("dirichlet_alpha", C.c_double), ("dirichlet_temp", C.c_double),
                 ("temp_threshold", C.c_int), ("node_cap", C.c_int), ("edge_cap", C.c_int),
                 ("seed", C.c_uint64), ("board_base", C.c_uint32), ("selfplay", C.c_int),
-                ("out_cap", C.c_int)]
+                ("out_cap", C.c_int), ("node_boards", C.c_int)]
 
 
 def exported_symbols():

@@ -64,7 +64,7 @@ class HashEvaluator:
 
 class BatchedMCTS:
     def __init__(self, engine, B, args=None, evaluator=None, dirichlet_noise=False, seed=0x5EED,
-                 board_base=0, node_cap=None, edge_cap=None, selfplay=False):
+                 board_base=0, node_cap=None, edge_cap=None, selfplay=False, node_boards=None):
         self.e = engine
         self.L = engine.L
         self.B = B
@@ -84,7 +84,8 @@ class BatchedMCTS:
         cfg.board_base = board_base
         cfg.selfplay = int(bool(selfplay))
         cfg.out_cap = int(getattr(self, "_selfplay_out_cap", 0))
-        cfg.node_cap, cfg.edge_cap = self._caps(engine, B, sims, cfg, node_cap, edge_cap)
+        cfg.node_boards = 1 if node_boards is None else int(bool(node_boards))
+        cfg.node_cap, cfg.edge_cap = self._caps(engine, B, sims, cfg, node_cap, edge_cap, node_boards is None)
         self.cfg = cfg
         h = C.c_void_p()
         _lib.check(self.L.spl_mcts_create(engine.ctx, B, C.byref(cfg), C.byref(h)), "spl_mcts_create")
@@ -98,7 +99,7 @@ class BatchedMCTS:
 
     MEM_FRACTION = 0.8     # of the device's free memory a default-sized arena may take
 
-    def _caps(self, engine, B, sims, cfg, node_cap, edge_cap):
+    def _caps(self, engine, B, sims, cfg, node_cap, edge_cap, auto_boards=False):
         """Per-tree pool sizes. A search adds at most `sims` nodes, but the
         kept table (every node whose round exceeds the root's, MCTS.py semantics) keeps
         growing through a game: at genbu's arguments and 100 simulations, steady-state
@@ -107,7 +108,9 @@ class BatchedMCTS:
         collected when a search would not fit, so the slots also hold dead nodes); when B
         such trees do not fit MEM_FRACTION of the free HBM, 24 edges per slot and as many
         slots as fit (searches then start on pruned trees under pressure, counted in the
-        tree headers)."""
+        tree headers). Node boards (cfg.node_boards, a speed option) are kept unless the
+        caller chose (auto_boards False); under memory pressure they are dropped first, so
+        capacity (the reference's exact table) wins over descent speed."""
         if node_cap and edge_cap:
             return int(node_cap), int(edge_cap)
         nc = int(node_cap or 16 * sims + 256)
@@ -122,6 +125,10 @@ class BatchedMCTS:
         limit = int(self.MEM_FRACTION * free)
         if plan(nc, ec) <= limit:
             return nc, ec
+        if auto_boards and cfg.node_boards:
+            cfg.node_boards = 0
+            if plan(nc, ec) <= limit:
+                return nc, ec
         ratio = 24
         lo = plan(64, 64 * ratio)
         per = (plan(1064, 1064 * ratio) - lo) / 1000.0

@@ -26,11 +26,12 @@ class SelfPlay(BatchedMCTS):
     are counted and `drain` raises)."""
 
     def __init__(self, engine, B, args=None, evaluator=None, dirichlet_noise=True, seed=0x5EED,
-                 board_base=0, out_cap=None, node_cap=None, edge_cap=None):
+                 board_base=0, out_cap=None, node_cap=None, edge_cap=None, node_boards=None):
         self._selfplay_out_cap = int(out_cap or B * (62 * engine.n + 2))
         self._dropped_seen = 0
         super().__init__(engine, B, args, evaluator, dirichlet_noise=dirichlet_noise, seed=seed,
-                         board_base=board_base, node_cap=node_cap, edge_cap=edge_cap, selfplay=True)
+                         board_base=board_base, node_cap=node_cap, edge_cap=edge_cap, selfplay=True,
+                         node_boards=node_boards)
         self.graph = None
         self.graph_k = None
 

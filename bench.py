@@ -195,7 +195,8 @@ def run_selfplay(args, rank, world, dev, dist, steps=None, warmup=None):
     if dist:
         broadcast_network(net)                 # every rank searches with rank 0's network
     ev = LeafEvaluator(eng, net, B, use_graph=False)
-    sp = SelfPlay(eng, B, sargs, evaluator=ev, dirichlet_noise=True, seed=args.seed, board_base=rank * B)
+    sp = SelfPlay(eng, B, sargs, evaluator=ev, dirichlet_noise=True, seed=args.seed, board_base=rank * B,
+                  node_boards=None if args.node_boards < 0 else bool(args.node_boards))
     sp.reset()
     sp.run(max(warmup, 9), use_graph=True)     # (captures both graphs)
     sp.drain()
@@ -246,7 +247,7 @@ def run_selfplay(args, rank, world, dev, dist, steps=None, warmup=None):
     return {"elapsed": elapsed, "iter_ms": ev0.elapsed_time(ev1) / steps, "stats": st, "window": delta,
             "examples": ex_local, "examples_gathered": int(ex["board"].shape[0]), "gather_s": gather_s,
             "symmetry": {"examples": nsym, "variants": int(sym["board"].shape[0]) if sym else 0, "s": sym_s},
-            "device_bytes": sp.device_bytes, "node_cap": int(sp.cfg.node_cap), "edge_cap": int(sp.cfg.edge_cap),
+            "device_bytes": sp.device_bytes, "node_cap": int(sp.cfg.node_cap), "edge_cap": int(sp.cfg.edge_cap), "node_boards": int(sp.cfg.node_boards),
             "nn_kernel_us": nn_us}
 
 
@@ -262,7 +263,7 @@ def selfplay_record(args, r, world, steps, warmup):
                        "drain_allgather_s": r["gather_s"]},
             "tree": {k: r["stats"][k] for k in ("nodes_max", "edges_max", "leaf_depth_mean", "leaf_depth_max",
                                                  "overflow", "examples_dropped")}
-                    | {"node_cap": r["node_cap"], "edge_cap": r["edge_cap"], "device_bytes": r["device_bytes"]},
+                    | {"node_cap": r["node_cap"], "edge_cap": r["edge_cap"], "device_bytes": r["device_bytes"], "node_boards": r["node_boards"]},
             "symmetry_expansion": r["symmetry"],
             "network_kernel": {"kernel": f"k_nn_forward<{args.players}>", "avg_us": r["nn_kernel_us"],
                                "tflops": fl / (r["nn_kernel_us"] * 1e-6) / 1e12,
@@ -306,6 +307,8 @@ def main():
     ap.add_argument("--selfplay-warmup", type=int, default=3000,
                     help="env workload: untimed self-play iterations first (games finish, trees grow)")
     ap.add_argument("--chunk", type=int, default=100, help="env: moves per rollout launch")
+    ap.add_argument("--node-boards", type=int, default=-1, help="selfplay: 1/0 force node boards on/off "
+                    "(default: on unless the pools do not fit)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

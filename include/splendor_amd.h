@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 1
+#define SPL_ABI_VERSION 2
 #define SPL_ACTIONS 409
 #define SPL_MASK_WORDS 7
 #define SPL_EINVAL (-1)
@@ -154,6 +154,10 @@ typedef struct {
     uint32_t board_base;     /* global id of tree 0 (multi-GPU sharding) */
     int selfplay;            /* 1: trees play games (spl_mcts_reset_games / spl_mcts_commit) */
     int out_cap;             /* self-play: finished-example queue capacity (examples) */
+    int node_boards;         /* 1: keep every node's canonical board (8 x rows bytes per node
+                                slot), so a descent through linked edges skips the in-tree
+                                transition (getNextState, MCTS.py:155-157) — the descent then
+                                runs one transition per simulation instead of one per level */
 } spl_mcts_config;
 
 int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_mcts **out);

@@ -78,11 +78,13 @@ def test_batch_searches_match_oracle(engines, n, sims):
         np.testing.assert_array_equal(q[b], oq)
 
 
-def test_persistent_trees_with_gc_match_oracle(engines):
-    """64 games x 12 moves: argmax play, chance via Philox, persistent trees + exact GC."""
+@pytest.mark.parametrize("boards", (True, False))
+def test_persistent_trees_with_gc_match_oracle(engines, boards):
+    """64 games x 12 moves: argmax play, chance via Philox, persistent trees + exact GC
+    (node boards move with their nodes)."""
     n, B, sims, seed = 2, 64, 60, 77
     e = engines[n]
-    m = mcts_for(e, B, sims, 1.5, 0.2, False, node_cap=1024, edge_cap=24576)
+    m = mcts_for(e, B, sims, 1.5, 0.2, False, node_cap=1024, edge_cap=24576, node_boards=boards)
     st = e.new_state(B)
     player = torch.zeros(B, dtype=torch.int8, device="cuda")
     e.init(st, player, seed=seed, stream=0xFFFFFFFF)

@@ -31,12 +31,15 @@ def sort_examples(ex, meta):
     return {k: v[order] for k, v in ex.items() if hasattr(v, "shape") and v.shape[:1] == meta.shape[:1]}
 
 
-@pytest.mark.parametrize("n,forced,graph,noise", [(2, False, False, False), (2, True, True, False),
-                                                  (4, False, False, False), (2, False, True, True),
-                                                  (4, True, True, True), (3, False, True, True)])
-def test_selfplay_matches_oracle(n, forced, graph, noise):
+@pytest.mark.parametrize("n,forced,graph,noise,boards", [(2, False, False, False, True), (2, True, True, False, True),
+                                                         (4, False, False, False, True), (2, False, True, True, True),
+                                                         (4, True, True, True, True), (3, False, True, True, True),
+                                                         (2, True, True, True, False), (3, False, True, True, False)])
+def test_selfplay_matches_oracle(n, forced, graph, noise, boards):
+    """boards: node boards kept (the descent follows linked edges without transitions) or
+    not (the transition at every level) — identical results either way."""
     B, iters, sims, ratio, pf, seed = 96, 1200, 8, 4, 0.25, 9
-    e, sp = make(n, B, sims, ratio, pf, forced, seed=seed, out_cap=20000, noise=noise)
+    e, sp = make(n, B, sims, ratio, pf, forced, seed=seed, out_cap=20000, noise=noise, node_boards=boards)
     if graph:
         sp.run(iters - 3, use_graph=True)     # 8-iteration graph replays + single replays
         for _ in range(3):

@@ -4,7 +4,7 @@
 # counter group (FETCH_SIZE and WRITE_SIZE in passes of their own, <= 8 SQ / 4 TCP / 2 TCC
 # counters per pass), then tools/pmc_selfplay_summary.py -> JSON over the last STEPS
 # dispatches of each kernel.
-# usage: tools/pmc_selfplay.sh OUTDIR ROUND [WARMUP] [STEPS]
+# usage: tools/pmc_selfplay.sh OUTDIR ROUND [WARMUP] [STEPS]   (PASSES="sq sq2 ..." for a subset)
 set -euo pipefail
 OUT=${1:-gpurun_out/pmc_sp}
 ROUND=${2:-r02}
@@ -15,8 +15,10 @@ mkdir -p "$OUT"
 CMD=(python3 bench.py --workload selfplay --steps "$STEPS" --warmup "$WARM" --no-cpu-baseline)
 # counters only for the self-play kernels, dispatches WARM .. WARM+STEPS of each
 FILT=(--kernel-include-regex "k_(select|leaf_mask|nn_forward|backup|commit)" --kernel-iteration-range "[$WARM-$((WARM + STEPS))]")
+PASSES=${PASSES:-fetch write sq sq2 mem ea}
 pass() {
     local name=$1; shift
+    [[ " $PASSES " == *" $name "* ]] || return 0
     echo "$(date +%T) pass $name start" >> "$OUT/progress.log"
     timeout -k 10 170 rocprofv3 --pmc "$@" "${FILT[@]}" --output-format csv -d "$OUT/$name" -o run -- "${CMD[@]}" > "$OUT/$name.log" 2>&1
     echo "$(date +%T) pass $name done" >> "$OUT/progress.log"
