@@ -66,7 +66,7 @@ struct Pick {
     int2 cr;                                    // child's cached {eb, ec} (valid when child >= 0)
 };
 __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &C, int t, int eb, int ec,
-                                               int ns, double qs, bool forced, int step) {
+                                               int ns, double qs, bool forced, int step, const Edge &first) {
     const int l = lane_id();
     const size_t e0 = (size_t)t * P.ecap + eb;
     float p[2];
@@ -74,11 +74,14 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
     int2 r[2];
     double q[2];
 #pragma unroll
-    for (int j = 0; j < 2; j++) {               // two 16-byte records per edge
+    for (int j = 0; j < 2; j++) {               // first: edge l, already requested by the caller
         const int i = 64 * j + l;
         EdgeStat st{0.f, 0, Q_UNSET};
         EdgeLink lk{0, 0, -1, 0, 0};
-        if (i < ec) { st = P.ed[e0 + i].s; lk = P.ed[e0 + i].k; }
+        if (i < ec) {
+            const Edge &ei = j == 0 ? first : P.ed[e0 + i];
+            st = ei.s; lk = ei.k;
+        }
         p[j] = st.p; n[j] = st.n; q[j] = st.q;
         a[j] = lk.a; c[j] = lk.child; r[j] = get_cr(lk);
     }
@@ -181,6 +184,43 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
     ry = __builtin_amdgcn_readlane(ry, bi & 63);
     if (bi >= 128) { av = P.ed[e0 + bi].k.a; cv = P.ed[e0 + bi].k.child; const int2 rr = get_cr(P.ed[e0 + bi].k); rx = rr.x; ry = rr.y; }
     return {bi, av, cv, make_int2(rx, ry)};
+}
+
+// the descent's common case: a node with at most 64 edges and no forced playouts at this
+// level — one edge per lane, straight-line (lanes past the node's range read its first edge
+// and take no part), the float32 screen of pick_edge_desc with the exact float64 arg-max as
+// the fallback. Same result as pick_edge_desc.
+__device__ __forceinline__ Pick pick_edge64(const Edge &e, double cpuct, double fpu, float cf, int ec, int ns,
+                                            double qs) {
+    const int l = lane_id();
+    const bool in = l < ec;
+    const double fpu_init = fpu > 0 ? qs - fpu : fpu;
+    const bool vis = e.s.q != Q_UNSET;
+    int bi;
+    {
+        // branch-free estimate; v_sqrt_f32 / v_rcp_f32 (1 ulp) are inside the error bound
+        const float nf = (float)ns;
+        const float sq = vis ? __builtin_amdgcn_sqrtf(nf) : __builtin_amdgcn_sqrtf(nf + 1e-8f);
+        const float rc = vis ? __builtin_amdgcn_rcpf(1.f + (float)e.s.n) : 1.f;
+        const float qf = vis ? (float)e.s.q : (float)fpu_init;
+        const float uf = qf + cf * e.s.p * sq * rc;
+        const float er = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
+        const float L = wave_max_f32(in ? uf - er : -INFINITY);
+        const uint64_t c = __ballot(in && uf + er >= L);
+        bi = __popcll(c) == 1 ? __ffsll((unsigned long long)c) - 1 : -1;
+    }
+    if (bi < 0) {
+        const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
+        double u = -INFINITY;
+        if (in)
+            u = vis ? e.s.q + cpuct * (double)e.s.p * sq / (double)(1 + e.s.n)
+                    : fpu_init + cpuct * (double)e.s.p * sq_eps;
+        const double m = wave_max_f64(u);
+        bi = __ffsll((unsigned long long)__ballot(u == m)) - 1;
+    }
+    bi = uniform(bi);
+    return {bi, __builtin_amdgcn_readlane((int)e.k.a, bi), __builtin_amdgcn_readlane(e.k.child, bi),
+            make_int2(__builtin_amdgcn_readlane(e.k.ceb, bi), __builtin_amdgcn_readlane((int)e.k.cec, bi))};
 }
 
 // ------------------------------------------------------------ prior sums
@@ -364,8 +404,8 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
         float es[4] = {0, 0, 0, 0};
         if (ni >= 0) {
             k0 = P.nkey0[nb + i]; k1 = P.nkey1[nb + i];
-            oeb = P.neb[nb + i]; ec = P.nec[nb + i]; ns = P.nns[nb + i]; rd = P.nround[nb + i];
-            qs = P.nqs[nb + i]; term = P.nterm[nb + i];
+            oeb = P.neb[nb + i]; ec = P.nec[nb + i]; ns = P.nst[nb + i].ns; rd = P.nround[nb + i];
+            qs = P.nst[nb + i].qs; term = P.nterm[nb + i];
 #pragma unroll
             for (int j = 0; j < 4; j++) es[j] = P.nes[(nb + i) * 4 + j];
         }
@@ -382,8 +422,8 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
         __builtin_amdgcn_wave_barrier();
         if (ni >= 0) {
             P.nkey0[nb + ni] = k0; P.nkey1[nb + ni] = k1;
-            P.neb[nb + ni] = neb; P.nec[nb + ni] = ec; P.nns[nb + ni] = ns; P.nround[nb + ni] = rd;
-            P.nqs[nb + ni] = qs; P.nterm[nb + ni] = term;
+            P.neb[nb + ni] = neb; P.nec[nb + ni] = ec; P.nst[nb + ni].ns = ns; P.nround[nb + ni] = rd;
+            P.nst[nb + ni].qs = qs; P.nterm[nb + ni] = term;
 #pragma unroll
             for (int j = 0; j < 4; j++) P.nes[(nb + ni) * 4 + j] = es[j];
             scr[ni] = neb; scr[sstride + ni] = oeb;
@@ -702,7 +742,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         wave_valid_moves<N>(s, 0, lim, m);
         store_mask(P.ex_valid + x * 7, m);
         if (l == 0) {
-            const double q0 = P.nqs[nb + root];
+            const double q0 = P.nst[nb + root].qs;
             P.ex_player[x] = player;
             for (int i = 0; i < 4; i++)
                 P.ex_q[x * 4 + i] = i == 0 ? (float)q0 : (i < N ? (float)(-q0 / (double)(N - 1)) : 0.f);
@@ -875,6 +915,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         // expand); `bnode` is the node whose board is in LDS (the root's, from root_state)
         const uint64_t *nbrd = P.nbrd ? reinterpret_cast<const uint64_t *>(P.nbrd + nb * NodeBoard<N>::BYTES) : nullptr;
         int bnode = node;
+        // per-tree bases and search constants of the hot loop, set up once
+        const Edge *ed_t = P.ed + e0;
+        const NodeStat *nst_t = P.nst + nb;
+        const double cpuct = C.cpuct, fpu = C.fpu;
+        const float cf = (float)C.cpuct;
         for (;;) {
             SPL_PROBE(1)
             if (depth > 0 && ec < 0) {
@@ -884,9 +929,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                 break;
             }
             if (depth >= P.pcap) { kind = LEAF_NONE; if (l == 0) H->overflow = 2; break; }
-            const int ns = P.nns[nb + node];
-            const double qs = P.nqs[nb + node];
-            const Pick pk = pick_edge_desc(P, C, t, eb, ec, ns, qs, forced && depth == 0, sims);
+            // the level's edges (first 64; lanes past the range read the first edge) and the
+            // node's visit stats are requested together: one round trip per level
+            const NodeStat nsq = nst_t[node];
+            const Edge e64 = ed_t[eb + (l < ec ? l : 0)];
+            const int ns = nsq.ns;
+            const double qs = nsq.qs;
+            const Pick pk = ec <= 64 && !(forced && depth == 0)
+                                ? pick_edge64(e64, cpuct, fpu, cf, ec, ns, qs)
+                                : pick_edge_desc(P, C, t, eb, ec, ns, qs, forced && depth == 0, sims, e64);
             const int ge = eb + pk.e;
             if (l == 0) { path[2 * depth] = node; path[2 * depth + 1] = ge; }
             depth++;
@@ -953,7 +1004,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                 __builtin_amdgcn_wave_barrier();
                 if (l == 0) {
                     P.nkey0[nb + id] = k0; P.nkey1[nb + id] = k1; P.neb[nb + id] = 0;
-                    P.nec[nb + id] = 0; P.nns[nb + id] = 0; P.nqs[nb + id] = 0;
+                    P.nec[nb + id] = 0; P.nst[nb + id].ns = 0; P.nst[nb + id].qs = 0;
                     P.nround[nb + id] = (uint8_t)bt(row(s, 0), 6); P.nterm[nb + id] = 1;
 #pragma unroll
                     for (int i = 0; i < 4; i++) P.nes[(nb + id) * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
@@ -1106,8 +1157,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         const EdgeStat st = P.ed[e0 + pge].s;
         pcnt = st.n;
         pq = st.q;
-        pns = P.nns[nb + pnode];
-        pqs = P.nqs[nb + pnode];
+        pns = P.nst[nb + pnode].ns;
+        pqs = P.nst[nb + pnode].qs;
     }
     float val[4] = {0, 0, 0, 0};
     if (kind == LEAF_NN) {
@@ -1156,8 +1207,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         __builtin_amdgcn_wave_barrier();
         if (l == 0) {
             P.nkey0[nb + id] = H->leaf_k0; P.nkey1[nb + id] = H->leaf_k1;
-            P.neb[nb + id] = eb; P.nec[nb + id] = ec; P.nns[nb + id] = 0;
-            P.nqs[nb + id] = (double)val[0]; P.nround[nb + id] = H->leaf_round; P.nterm[nb + id] = 0;
+            P.neb[nb + id] = eb; P.nec[nb + id] = ec; P.nst[nb + id].ns = 0;
+            P.nst[nb + id].qs = (double)val[0]; P.nround[nb + id] = H->leaf_round; P.nterm[nb + id] = 0;
             hash_insert(P, t, H->leaf_k0, id);
             if (depth == 0) { H->root = id; H->root_eb = eb; H->root_ec = ec; }
             else {
@@ -1187,12 +1238,12 @@ backup:
         if (d >= 64) {                                   // levels beyond the prefetched 64
             node = path[2 * d]; ge = path[2 * d + 1];
             cnt = P.ed[e0 + ge].s.n; q = P.ed[e0 + ge].s.q;
-            ns = P.nns[nb + node]; qs = P.nqs[nb + node];
+            ns = P.nst[nb + node].ns; qs = P.nst[nb + node].qs;
         }
         P.ed[e0 + ge].s.q = ((double)cnt * q + v0) / (double)(cnt + 1);
-        P.nqs[nb + node] = ((double)(ns + 1) * qs + v0) / (double)(ns + 2);
+        P.nst[nb + node].qs = ((double)(ns + 1) * qs + v0) / (double)(ns + 2);
         P.ed[e0 + ge].s.n = cnt + 1;
-        P.nns[nb + node] = ns + 1;
+        P.nst[nb + node].ns = ns + 1;
     }
     if (l == 0) {
         H->sims_done += 1;
@@ -1303,7 +1354,7 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
         if (probs) probs[(size_t)t * SPL_ACTIONS + a] = (double)c / (double)tot;
     }
     if (q && l == 0) {
-        const double q0 = P.nqs[nb + root];
+        const double q0 = P.nst[nb + root].qs;
         q[(size_t)t * n] = q0;
         for (int i = 1; i < n; i++) q[(size_t)t * n + i] = -q0 / (double)(n - 1);
     }
@@ -1412,8 +1463,8 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     const size_t nx = (size_t)B * L.excap, no = (size_t)L.out_cap;
     size_t bytes = 0;
     auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
-    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn); acc(4 * nn);
-    acc(4 * nn); acc(8 * nn); acc(nn); acc(16 * nn); acc(sizeof(Edge) * ne);
+    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn); acc(sizeof(NodeStat) * nn);
+    acc(4 * nn); acc(nn); acc(16 * nn); acc(sizeof(Edge) * ne);
     acc(4 * (size_t)B * L.hcap); acc(8 * (size_t)B * L.pcap);
     acc(4 * nn); acc(4 * nn); acc(8 * ((size_t)B * (L.ncap + 1))); acc((size_t)B * L.S);
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
@@ -1462,8 +1513,8 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     char *p = (char *)arena;
     P.hdr = carve<TreeHdr>(p, B);
     P.nkey0 = carve<uint64_t>(p, nn); P.nkey1 = carve<uint64_t>(p, nn);
-    P.neb = carve<int32_t>(p, nn); P.nec = carve<int32_t>(p, nn); P.nns = carve<int32_t>(p, nn);
-    P.nround = carve<int32_t>(p, nn); P.nqs = carve<double>(p, nn); P.nterm = carve<int8_t>(p, nn);
+    P.neb = carve<int32_t>(p, nn); P.nec = carve<int32_t>(p, nn); P.nst = carve<NodeStat>(p, nn);
+    P.nround = carve<int32_t>(p, nn); P.nterm = carve<int8_t>(p, nn);
     P.nes = carve<float>(p, 4 * nn);
     P.ed = carve<Edge>(p, ne);
     P.hslot = carve<int32_t>(p, (size_t)B * P.hcap);

@@ -56,13 +56,20 @@ struct __align__(16) Edge {
 __device__ __forceinline__ int2 get_cr(const EdgeLink &e) { return make_int2(e.ceb, e.cec); }
 __device__ __forceinline__ void set_cr(EdgeLink &e, int eb, int ec) { e.ceb = eb; e.cec = (int16_t)ec; }
 
+// a node's visit statistics (Ns, Qs), read together by the descent
+struct __align__(16) NodeStat {
+    double qs;     // Qs
+    int32_t ns;    // Ns
+    int32_t pad;
+};
+
 // per-tree SoA pools; tree t owns [t*ncap, (t+1)*ncap) nodes, [t*ecap, ...) edges
 struct Pools {
     int ncap, ecap, hcap, pcap;          // nodes, edges, hash slots (pow2), path depth
     TreeHdr *hdr;
     uint64_t *nkey0, *nkey1;
-    int32_t *neb, *nec, *nns, *nround;
-    double *nqs;
+    int32_t *neb, *nec, *nround;
+    NodeStat *nst;                       // visit count and value of every node (one 16-byte load)
     int8_t *nterm;
     float *nes;                          // ncap x 4 terminal values
     Edge *ed;                            // edges: UCB inputs + action, child, child's CSR range
