@@ -162,10 +162,10 @@ __device__ __forceinline__ int fkey(float x) {
 }
 __device__ __forceinline__ float wave_max_f32(float x) {
     int k = fkey(x);
-    k = max(k, __builtin_amdgcn_update_dpp(k, k, 0xB1, 0xF, 0xF, false));
-    k = max(k, __builtin_amdgcn_update_dpp(k, k, 0x4E, 0xF, 0xF, false));
-    k = max(k, __builtin_amdgcn_update_dpp(k, k, 0x141, 0xF, 0xF, false));
-    k = max(k, __builtin_amdgcn_update_dpp(k, k, 0x140, 0xF, 0xF, false));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, 0xB1, 0xF, 0xF, true));   // bound_ctrl: foldable
+    k = max(k, __builtin_amdgcn_mov_dpp(k, 0x4E, 0xF, 0xF, true));    // into v_max_i32_dpp
+    k = max(k, __builtin_amdgcn_mov_dpp(k, 0x141, 0xF, 0xF, true));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, 0x140, 0xF, 0xF, true));
     const int m = max(max(__builtin_amdgcn_readlane(k, 0), __builtin_amdgcn_readlane(k, 16)),
                       max(__builtin_amdgcn_readlane(k, 32), __builtin_amdgcn_readlane(k, 48)));
     return __int_as_float(m ^ ((m >> 31) & 0x7fffffff));
