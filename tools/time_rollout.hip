@@ -6,8 +6,10 @@
 #include <algorithm>
 #include <cstdio>
 #include <vector>
-int main() {
-    const int B = 32768, NB = B / 64, K = 100;
+#include <cstdlib>
+int main(int argc, char **argv) {
+    // argv: [K = moves per launch, 100]
+    const int B = 32768, NB = B / 64, K = argc > 1 ? atoi(argv[1]) : 100;
     spl_ctx *c; spl_ctx_create(2, 10, &c);
     int8_t *st, *pl; uint64_t *mk; int16_t *ac; float *en; int32_t *gd; uint64_t *tm;
     (void)hipMalloc(&st, (size_t)B * 392); (void)hipMalloc(&pl, B); (void)hipMalloc(&mk, (size_t)K * B * 56);
