@@ -328,44 +328,69 @@ constexpr int SCR_NODES = 512;
 
 // remap[i] = 1 for the root and every node reachable from it through child links, 0 else
 // (breadth-first, the wave walks one node's edges at a time; remap_eb is the queue).
-__device__ void mark_linked(const Pools &P, int t, int root) {
+__device__ void mark_linked(const Pools &P, int t, int root, int32_t *mark, int32_t *q) {
     const int l = lane_id();
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const int nc = P.hdr[t].node_count;
-    int32_t *mark = P.remap + nb, *q = P.remap_eb + nb;
     for (int i = l; i < nc; i += 64) mark[i] = i == root ? 1 : 0;
     if (l == 0) q[0] = root;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
+    // breadth-first in batches of up to 64 queued nodes (lane per node), their edges 64 at a
+    // time (lane per edge, owner found by a binary search over the batch's edge offsets):
+    // a round trip per batch and per 64 edges, not per node
     int head = 0, tail = 1;
     while (head < tail) {
-        const int node = q[head++];
-        const int eb = P.neb[nb + node], ec = P.nterm[nb + node] ? 0 : P.nec[nb + node];
-        for (int base = 0; base < ec; base += 64) {
-            const int i = base + l;
-            const int c = i < ec ? P.ed[e0 + eb + i].k.child : -1;
+        const int nbt = min(64, tail - head);
+        int eb = 0, ec = 0;
+        if (l < nbt) {
+            const int node = q[head + l];
+            eb = P.neb[nb + node];
+            ec = P.nterm[nb + node] ? 0 : P.nec[nb + node];
+        }
+        head += nbt;
+        int incl = ec;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (l >= o) incl += y;
+        }
+        const int tot = __shfl(incl, 63, 64), excl = incl - ec;
+        for (int c0 = 0; c0 < tot; c0 += 64) {
+            const int e = c0 + l;
+            int lo = 0;                                  // last lane with excl <= e
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1)
+                if (__shfl(excl, lo + step, 64) <= e) lo += step;
+            const int ebo = __shfl(eb, lo, 64), exo = __shfl(excl, lo, 64);
+            const int c = e < tot ? P.ed[e0 + ebo + (e - exo)].k.child : -1;
             const bool fresh = c >= 0 && atomicCAS(&mark[c], 0, 1) == 0;
-            const uint64_t b = __ballot(fresh);
-            if (fresh) q[tail + __popcll(b & lanemask_lt())] = c;
-            tail += __popcll(b);
+            const uint64_t bm = __ballot(fresh);
+            if (fresh) q[tail + __popcll(bm & lanemask_lt())] = c;
+            tail += __popcll(bm);
             __threadfence_block();
             __builtin_amdgcn_wave_barrier();
         }
     }
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 struct defeats SROA)
+template <int CR = 4>   // edges per lane per round trip of the edge move (boards: 2 CR units)
 __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int *scr, int sstride,
-                            int bunits, bool linked = false) {
+                            int bunits, bool linked = false, int32_t *lmark = nullptr) {
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const int nc = H->node_count;
     int32_t *remap = P.remap + nb;
-    if (linked) mark_linked(P, t, root);
+    // linked (prune): marks of the nodes reachable from the root — in lmark[0, ncap) with
+    // the BFS queue behind it (LDS, k_gc), or in remap itself with remap_eb as the queue
+    int32_t *mark = lmark ? lmark : remap;
+    if (linked) mark_linked(P, t, root, mark, lmark ? lmark + P.ncap : P.remap_eb + nb);
     int kept = 0;
     for (int base = 0; base < nc; base += 64) {
         const int i = base + l;
-        const bool keep = i < nc && (i == root || (linked ? remap[i] == 1 : P.nround[nb + i] > root_round));
+        const bool keep = i < nc && (i == root || (linked ? mark[i] == 1 : P.nround[nb + i] > root_round));
         const uint64_t b = __ballot(keep);
         if (i < nc) remap[i] = keep ? kept + __popcll(b & lanemask_lt()) : -1;
         kept += __popcll(b);
@@ -438,15 +463,17 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
         if (l == 0) scr[kept] = edges;
         __threadfence_block();                          // (scr may be global memory)
         __builtin_amdgcn_wave_barrier();
-        constexpr int R = 4;
-        for (int k0 = 0; k0 < edges; k0 += 64 * R) {
-            EdgeStat st[R];
-            EdgeLink lk[R];
-            int nch[R], ceb[R];
+        for (int k0 = 0; k0 < edges; k0 += 64 * CR) {
+            // an edge as two uint4 (register arrays: a struct array here lands in scratch);
+            // link word y = child, z = cached child CSR base
+            u32x4 es_[CR], ek_[CR];
+            int nch[CR], ceb[CR];
+            u32x4 *const ed4 = reinterpret_cast<u32x4 *>(P.ed + e0);
 #pragma unroll
-            for (int r = 0; r < R; r++) {
+            for (int r = 0; r < CR; r++) {
                 const int k = k0 + 64 * r + l;
                 nch[r] = -1; ceb[r] = 0;
+                es_[r] = u32x4{0, 0, 0, 0}; ek_[r] = u32x4{0, 0xFFFFFFFFu, 0, 0};
                 if (k < edges) {
                     int lo = 0, hi = kept - 1;                 // last j with scr[j] <= k
                     while (lo < hi) {
@@ -454,29 +481,30 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
                         if (scr[mid] <= k) lo = mid; else hi = mid - 1;
                     }
                     const int src = scr[sstride + lo] + (k - scr[lo]);
-                    st[r] = P.ed[e0 + src].s;
-                    lk[r] = P.ed[e0 + src].k;
+                    es_[r] = ed4[2 * src];
+                    ek_[r] = ed4[2 * src + 1];
                 }
             }
 #pragma unroll
-            for (int r = 0; r < R; r++) {
+            for (int r = 0; r < CR; r++) {
                 const int k = k0 + 64 * r + l;
-                if (k < edges && lk[r].child >= 0) {
-                    nch[r] = remap[lk[r].child];
-                    ceb[r] = remap_eb[lk[r].child];
+                const int ch = (int)ek_[r].y;
+                if (k < edges && ch >= 0) {
+                    nch[r] = remap[ch];
+                    ceb[r] = remap_eb[ch];
                 }
             }
             __threadfence_block();
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int r = 0; r < R; r++) {
+            for (int r = 0; r < CR; r++) {
                 const int k = k0 + 64 * r + l;
                 if (k < edges) {
-                    EdgeLink o = lk[r];
-                    o.child = nch[r];
-                    if (nch[r] >= 0) o.ceb = ceb[r];
-                    P.ed[e0 + k].s = st[r];
-                    P.ed[e0 + k].k = o;
+                    u32x4 o = ek_[r];
+                    o.y = (uint32_t)nch[r];
+                    if (nch[r] >= 0) o.z = (uint32_t)ceb[r];
+                    ed4[2 * k] = es_[r];
+                    ed4[2 * k + 1] = o;
                 }
             }
             __threadfence_block();
@@ -491,11 +519,11 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
             if (remap[i] >= 0) scr[remap[i]] = i;
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
-        uint4 *bb = reinterpret_cast<uint4 *>(P.nbrd) + nb * bunits;
+        u32x4 *bb = reinterpret_cast<u32x4 *>(P.nbrd) + nb * bunits;
         const int units = kept * bunits;
-        constexpr int R = 8;
+        constexpr int R = 2 * CR;
         for (int k0 = 0; k0 < units; k0 += 64 * R) {
-            uint4 d[R];
+            u32x4 d[R];
             int src[R];
 #pragma unroll
             for (int r = 0; r < R; r++) {
@@ -504,8 +532,8 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
                 if (k < units) {
                     const int nn = k / bunits;
                     src[r] = k + bunits * (scr[nn] - nn);
-                    if (src[r] != k) d[r] = bb[src[r]];
                 }
+                d[r] = bb[k < units ? src[r] : 0];   // (unconditional: keeps d in registers)
             }
             __threadfence_block();
             __builtin_amdgcn_wave_barrier();
@@ -536,6 +564,23 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
     return nroot;
 }
 
+// does the next search fit tree t's pools (budget nodes, 409 root edges, edge_reserve per
+// simulation)
+__device__ __forceinline__ bool tree_fits(const Pools &P, const SearchCfg &C, const TreeHdr *H) {
+    return H->node_count + H->budget + 1 <= P.ncap &&
+           (long long)H->edge_count + SPL_ACTIONS + (long long)H->budget * C.edge_reserve <= (long long)P.ecap;
+}
+__device__ __forceinline__ void empty_tree(const Pools &P, int t) {
+    int32_t *hs = P.hslot + (size_t)t * P.hcap;
+    for (int i = lane_id(); i < P.hcap; i += 64) hs[i] = -1;
+    if (lane_id() == 0) { P.hdr[t].node_count = 0; P.hdr[t].edge_count = 0; }
+}
+// queue tree t for k_gc (lane 0)
+__device__ __forceinline__ void gc_push(const Pools &P, int t) {
+    const int k = atomicAdd(&P.counters[2], 1);
+    P.gcq[k] = t;
+}
+
 // ------------------------------------------------------------ search start
 // Re-root tree t at the canonical board staged in LDS `s` (MCTS.getActionProb entry,
 // :45-56): look the root up in the persistent table (keep) and collect garbage, or start
@@ -546,7 +591,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
 // (resets++). Without such an event the kept tree is exactly the reference's reachable table.
 template <int N>
 __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const int8_t *s, bool keep,
-                             bool force_full, int *scr = nullptr) {
+                             bool force_full, int *scr = nullptr, bool defer = false) {
     using Lx = Lay<N>;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
@@ -554,8 +599,8 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
     const int mv = H->move_no;
     const bool full = force_full || philox_u01(C.seed, C.board_base + t, ST_FULL | (uint32_t)mv, 0) < C.prob_full;
     const int budget = full ? C.num_sims : C.num_sims / C.ratio_full;
-    int root = -1;
-    bool empty = true;
+    int root = -1, rr = 0;
+    bool empty = true, deferred = false;
     if (keep && H->node_count > 0) {
         uint64_t k0, k1;
         wave_fingerprint<N>(s, k0, k1);
@@ -571,31 +616,33 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         // reachable table either way. Without k_commit (search-only arenas) every search
         // starts on a compacted tree.
         if (!C.selfplay || !fits()) {
-            const int rr = (uint8_t)bt(row(s, 0), 6);
-            // edge-move scratch: LDS for small trees, the tree's global scratch otherwise
-            int *cs = P.ncap <= SCR_NODES && scr ? scr : P.cscr + (size_t)t * 2 * (P.ncap + 1);
-            const int cstride = P.ncap <= SCR_NODES && scr ? SCR_NODES + 1 : P.ncap + 1;
-            root = compact_tree(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS);
-            if (!fits() && root >= 0) {
-                root = compact_tree(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS, true);
-                if (l == 0) H->prunes += 1;
+            rr = (uint8_t)bt(row(s, 0), 6);
+            if (defer && C.selfplay) {
+                deferred = true;                         // k_gc collects (same result)
+            } else {
+                // edge-move scratch: LDS for small trees, the tree's global scratch otherwise
+                int *cs = P.ncap <= SCR_NODES && scr ? scr : P.cscr + (size_t)t * 2 * (P.ncap + 1);
+                const int cstride = P.ncap <= SCR_NODES && scr ? SCR_NODES + 1 : P.ncap + 1;
+                root = compact_tree(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS);
+                if (!fits() && root >= 0) {
+                    root = compact_tree(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS, true);
+                    if (l == 0) H->prunes += 1;
+                }
             }
         }
-        empty = !fits();
+        empty = !deferred && !fits();
         if (empty && l == 0) H->resets += 1;
     }
     if (empty) {
         root = -1;
-        int32_t *hs = P.hslot + (size_t)t * P.hcap;
-        for (int i = l; i < P.hcap; i += 64) hs[i] = -1;
-        if (l == 0) { H->node_count = 0; H->edge_count = 0; }
+        empty_tree(P, t);
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const int reb = root >= 0 ? P.neb[(size_t)t * P.ncap + root] : 0;
-    const int rec = root >= 0 ? P.nec[(size_t)t * P.ncap + root] : 0;
+    const int reb = root >= 0 && !deferred ? P.neb[(size_t)t * P.ncap + root] : 0;
+    const int rec = root >= 0 && !deferred ? P.nec[(size_t)t * P.ncap + root] : 0;
     if (l == 0) {
-        H->root = root;
+        H->root = root;                                  // (deferred: the pre-GC index)
         H->root_eb = reb;
         H->root_ec = rec;
         H->sims_done = 0;
@@ -605,11 +652,89 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         H->noise_pending = full && C.dirichlet;
         H->leaf_kind = LEAF_NONE;
         H->overflow = 0;
-        H->gc_state = 0;
+        H->gc_state = deferred ? 3 : 0;
+        H->pad1 = rr;                                    // root round, for a deferred GC
         H->move_no = mv + 1;
+        if (deferred) gc_push(P, t);
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
+}
+
+// Garbage collection queued by k_backup (a leaf did not fit mid-search: gc_state 1) and
+// by k_commit's search starts (gc_state 3), one wave per queued tree. Off k_commit, whose
+// other 31,000-odd waves per launch exit at once: it keeps k_commit's registers low, and
+// GC's own registers go to more loads in flight. Exactly begin_search's policy: compact
+// (rounds > the root's), prune to the linked nodes, empty.
+template <int N, bool LDSW>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_gc(Pools P, SearchCfg C) {
+    constexpr bool lds_ok = LDSW;
+    // lds_ok: the edge-move scratch (2 (ncap + 1) ints) and the prune's marks + queue
+    // (2 ncap ints) in dynamic LDS — the binary searches of the edge move and the BFS then
+    // run on LDS instead of dependent HBM round trips
+    extern __shared__ int gsm[];
+    const int l = lane_id();
+    const int tail = P.counters[2];                      // no pushes while k_gc runs
+    const int ftail = P.counters[5];
+    if (tail == 0 && ftail == 0) return;                 // (the usual case)
+    // queued trees come in bursts (games start together, so trees fill up together):
+    // workgroup i takes queue entries i, i + G, ...
+    for (int k = blockIdx.x; k < tail; k += gridDim.x) {     // garbage collection
+        const int t = uniform(P.gcq[k]);
+        TreeHdr *H = P.hdr + t;
+        const size_t nb = (size_t)t * P.ncap;
+        int *cs = lds_ok ? gsm : P.cscr + (size_t)t * 2 * (P.ncap + 1);
+        const int cstride = P.ncap + 1;
+        int32_t *lm = lds_ok ? gsm + 2 * (P.ncap + 1) : nullptr;
+        const int st = H->gc_state;
+        int root = H->root;
+        if (st == 1) {                                   // the descent then repeats
+            root = compact_tree<8>(P, t, root, P.nround[nb + root], cs, cstride, NodeBoard<N>::UNITS);
+        } else if (st == 3) {
+            const int rr = H->pad1;
+            root = compact_tree<8>(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS);
+            if (!tree_fits(P, C, H) && root >= 0) {
+                root = compact_tree<8>(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS, true, lm);
+                if (l == 0) H->prunes += 1;
+            }
+            if (!tree_fits(P, C, H)) {
+                root = -1;
+                empty_tree(P, t);
+                if (l == 0) H->resets += 1;
+            }
+        }
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        const int reb = root >= 0 ? P.neb[nb + root] : 0;
+        const int rec = root >= 0 ? P.nec[nb + root] : 0;
+        if (l == 0) {
+            H->root = root;
+            H->root_eb = reb;
+            H->root_ec = rec;
+            H->gc_state = st == 1 ? 2 : 0;               // (2: once per search)
+        }
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+    }
+    // finished games' example rows (k_commit): the staging rows stay untouched until the
+    // tree's next commit, a later iteration
+    for (int k = blockIdx.x; k < ftail; k += gridDim.x) {
+        const int2 e = P.flq[k];
+        wave_copy_bytes(P.out_state + (size_t)e.y * Lay<N>::S, P.ex_state + (size_t)e.x * Lay<N>::S, Lay<N>::S);
+        const float *src = P.ex_pi + (size_t)e.x * SPL_ACTIONS;
+        float *dst = P.out_pi + (size_t)e.y * SPL_ACTIONS;
+        float v[7];
+#pragma unroll
+        for (int i = 0; i < 7; i++) v[i] = 64 * i + l < SPL_ACTIONS ? src[64 * i + l] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 7; i++)
+            if (64 * i + l < SPL_ACTIONS) dst[64 * i + l] = v[i];
+    }
+    if (l == 0 && atomicAdd(&P.counters[4], 1) == (int)gridDim.x - 1) {
+        P.counters[2] = 0;                               // the last workgroup out resets the queues
+        P.counters[5] = 0;
+        P.counters[4] = 0;
+    }
 }
 
 // active (optional): trees with active[t] == 0 are left as they are, with no search budget
@@ -684,24 +809,15 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][2][Lx::LS];
     __shared__ double ub[WAVES][DEAL_DRAWS];
-    __shared__ int cscr[WAVES][2 * (SCR_NODES + 1)];     // compaction scratch
+    __shared__ double pterm[WAVES][SPL_ACTIONS];         // random_pick's per-edge terms
+    __shared__ int16_t pact[WAVES][SPL_ACTIONS];
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
-    if (H->gc_state == 1) {                              // requested by k_backup (lazy GC)
-        const int root = H->root;
-        const size_t nbr = (size_t)t * P.ncap;
-        int *cs = P.ncap <= SCR_NODES ? cscr[w] : P.cscr + (size_t)t * 2 * (P.ncap + 1);
-        const int nroot = compact_tree(P, t, root, P.nround[nbr + root], cs,
-                                       P.ncap <= SCR_NODES ? SCR_NODES + 1 : P.ncap + 1, NodeBoard<N>::UNITS);
-        if (l == 0) {
-            H->root = nroot; H->root_eb = P.neb[nbr + nroot]; H->root_ec = P.nec[nbr + nroot];
-            H->gc_state = 2;                             // once per search
-        }
-        return;
-    }
-    if (H->sims_done < H->budget || H->overflow || H->root < 0) return;
+    // (a tree whose leaf did not fit waits for k_gc: its simulation was withdrawn, so its
+    // search is not done)
+    if (H->gc_state == 1 || H->sims_done < H->budget || H->overflow || H->root < 0) return;
     const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const uint32_t gb = C.board_base + (uint32_t)t;
     const int root = H->root, eb = P.neb[nb + root], ec = P.nec[nb + root];
@@ -750,21 +866,27 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         nex++;
     }
     // action = random_pick(pi, T) (Coach.py:30-33, 82-83): numpy legacy choice with p
+    // (the per-edge terms lane-parallel into LDS, the order-dependent sums on lane 0)
     int action = 408;
+    const double T = C.temp_threshold > 0 ? (step < C.temp_threshold ? 2.0 : 0.2) : 1.0;
+    for (int i = l; i < ec; i += 64) {
+        pterm[w][i] = temp_pow((double)POLICY_COUNT(i) / (double)tot, T);
+        pact[w][i] = ede[i].k.a;
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
     if (l == 0) {
-        const double T = C.temp_threshold > 0 ? (step < C.temp_threshold ? 2.0 : 0.2) : 1.0;
+        const double *pt = pterm[w];
         double sum = 0.0;
-        for (int i = 0; i < ec; i++)
-            sum += temp_pow((double)POLICY_COUNT(i) / (double)tot, T);
+        for (int i = 0; i < ec; i++) sum += pt[i];
         double last = 0.0;
-        for (int i = 0; i < ec; i++)
-            last += temp_pow((double)POLICY_COUNT(i) / (double)tot, T) / sum;
+        for (int i = 0; i < ec; i++) last += pt[i] / sum;
         const double u = philox_u01(C.seed, gb, ST_PICK | (uint32_t)cm, 0);
         double cdf = 0.0;
-        action = ede[ec - 1].k.a;
+        action = pact[w][ec - 1];
         for (int i = 0; i < ec; i++) {
-            cdf += temp_pow((double)POLICY_COUNT(i) / (double)tot, T) / sum;
-            if (cdf / last > u) { action = ede[i].k.a; break; }
+            cdf += pt[i] / sum;
+            if (cdf / last > u) { action = pact[w][i]; break; }
         }
     }
     action = __shfl(action, 0, 64);
@@ -786,28 +908,38 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         int f[N];
 #pragma unroll
         for (int i = 0; i < N; i++) f[i] = get_score<N>(b, i);
-        for (int j = 0; j < nex; j++) {
+        // the game's examples take queue slots [slot0, slot0 + nex) at once (those past
+        // out_cap are dropped and counted); lane per example for the small columns, the
+        // board and policy rows are copied by k_post (queued as (staging index, slot) pairs)
+        int slot0 = 0;
+        if (l == 0) slot0 = atomicAdd(&P.counters[0], nex);
+        slot0 = __shfl(slot0, 0, 64);
+        const int kept = max(0, min(nex, P.out_cap - slot0));
+        int fq0 = 0;
+        if (l == 0) {
+            if (kept < nex) atomicAdd(&P.counters[1], nex - kept);
+            if (kept) fq0 = atomicAdd(&P.counters[5], kept);
+        }
+        fq0 = __shfl(fq0, 0, 64);
+        const int gno = H->game_no - 1;
+        for (int j = l; j < kept; j += 64) {
             const size_t x = (size_t)t * P.excap + j;
-            int slot = 0;
-            if (l == 0) slot = atomicAdd(&P.counters[0], 1);
-            slot = __shfl(slot, 0, 64);
-            if (slot >= P.out_cap) {
-                if (l == 0) atomicAdd(&P.counters[1], 1);
-                continue;
-            }
+            const size_t slot = (size_t)slot0 + j;
             const int px = P.ex_player[x];
-            wave_copy_bytes(P.out_state + (size_t)slot * Lx::S, P.ex_state + x * Lx::S, Lx::S);
-            for (int a = l; a < SPL_ACTIONS; a += 64)
-                P.out_pi[(size_t)slot * SPL_ACTIONS + a] = P.ex_pi[x * SPL_ACTIONS + a];
-            if (l < 7) P.out_valid[(size_t)slot * 7 + l] = P.ex_valid[x * 7 + l];
-            if (l < 4) {
-                const int src = (l + px) % N;
-                P.out_winner[(size_t)slot * 4 + l] = l < N ? r[src < N ? src : 0] : 0.f;
-                P.out_scdiff[(size_t)slot * 4 + l] = l < N ? f[src < N ? src : 0] - f[px < N ? px : 0] : 0;
-                P.out_q[(size_t)slot * 4 + l] = P.ex_q[x * 4 + l];
-                const int meta[4] = {(int)gb, H->game_no - 1, j, px};
-                P.out_meta[(size_t)slot * 4 + l] = meta[l];
+#pragma unroll
+            for (int k = 0; k < 7; k++) P.out_valid[slot * 7 + k] = P.ex_valid[x * 7 + k];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int src = (i + px) % N;
+                P.out_winner[slot * 4 + i] = i < N ? r[src < N ? src : 0] : 0.f;
+                P.out_scdiff[slot * 4 + i] = i < N ? f[src < N ? src : 0] - f[px < N ? px : 0] : 0;
+                P.out_q[slot * 4 + i] = P.ex_q[x * 4 + i];
             }
+            P.out_meta[slot * 4 + 0] = (int)gb;
+            P.out_meta[slot * 4 + 1] = gno;
+            P.out_meta[slot * 4 + 2] = j;
+            P.out_meta[slot * 4 + 3] = px;
+            P.flq[fq0 + j] = make_int2((int)x, (int)slot);
         }
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
@@ -822,7 +954,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     __builtin_amdgcn_wave_barrier();
     wave_store_board<N>(P.board + (size_t)t * Lx::S, b);
     wave_roll_players<N>(s, b, nxt);                            // getCanonicalForm (:73)
-    begin_search<N>(P, C, t, s, !ended, false, cscr[w]);
+    begin_search<N>(P, C, t, s, !ended, false, nullptr, true);
 }
 
 // flat copy of `bytes` bytes (16-byte vectors when both ends allow it), grid-stride
@@ -861,7 +993,7 @@ __global__ void k_drain_reset(Pools P, int max, int32_t *n_out) {
     const int c = P.counters[0];
     const int k = min(c, min(max, P.out_cap));
     if (n_out) *n_out = k;
-    P.counters[1] += c - k;
+    P.counters[1] += min(c, P.out_cap) - k;              // (k_commit counted those past out_cap)
     P.counters[0] = 0;
 }
 
@@ -1172,7 +1304,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             // room with dead nodes still in the pool: this simulation is withdrawn (no
             // backup, not counted), k_commit collects the garbage (exact: nodes with rounds
             // <= the root's) and the next select repeats the same descent
-            if (l == 0) { H->gc_state = 1; H->leaf_kind = LEAF_NONE; }
+            if (l == 0) {
+                H->gc_state = 1;
+                H->leaf_kind = LEAF_NONE;
+                if (C.selfplay) gc_push(P, t);
+            }
             return;
         }
         if (id >= P.ncap || eb + ec > P.ecap) {          // no room: back up v, do not store
@@ -1469,7 +1605,7 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     acc(4 * nn); acc(4 * nn); acc(8 * ((size_t)B * (L.ncap + 1))); acc((size_t)B * L.S);
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
     acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
-    acc(16 * no); acc(64); acc((size_t)L.nbb * nn);
+    acc(16 * no); acc(64); acc((size_t)L.nbb * nn); acc(4 * (size_t)B); acc(8 * no);
     L.bytes = bytes;
     return L;
 }
@@ -1532,6 +1668,8 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.out_valid = carve<uint64_t>(p, 7 * no); P.out_scdiff = carve<int32_t>(p, 4 * no);
     P.out_meta = carve<int32_t>(p, 4 * no); P.counters = carve<int32_t>(p, 16);
     P.nbrd = L.nbb ? carve<int8_t>(p, (size_t)L.nbb * nn) : nullptr;
+    P.gcq = carve<int32_t>(p, (size_t)B);
+    P.flq = carve<int2>(p, no);
     if (hipMemset(P.hslot, 0xFF, 4 * (size_t)B * P.hcap) != hipSuccess) {
         (void)hipFree(arena); delete m; return SPL_EDEVICE;
     }
@@ -1617,6 +1755,16 @@ int spl_mcts_commit(spl_mcts *m, void *hs) {
     if (!m || !m->cfg.selfplay) return SPL_EINVAL;
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_commit<N>, wave_grid(m->B), dim3(THREADS), 0,
                                           (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit));
+    // garbage collection queued by this iteration's backups and search starts (usually
+    // none, in bursts up to thousands of trees: 1024 single-wave workgroups share the queue)
+    const unsigned gcw = (unsigned)(m->B < 1024 ? m->B : 1024);
+    const size_t gcl = 4 * (4 * (size_t)m->P.ncap + 2);
+    const int lds_ok = gcl <= 160 * 1024;
+    if (lds_ok) {
+        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_gc<N, true>), dim3(gcw), dim3(64), gcl, (hipStream_t)hs, m->P, m->cfg));
+    } else {
+        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_gc<N, false>), dim3(gcw), dim3(64), 0, (hipStream_t)hs, m->P, m->cfg));
+    }
     return check_launch();
 }
 

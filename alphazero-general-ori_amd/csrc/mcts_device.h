@@ -91,7 +91,10 @@ struct Pools {
     float *out_pi, *out_winner, *out_q;  // out_cap x 409 / 4 / 4
     uint64_t *out_valid;                 // out_cap x 7
     int32_t *out_scdiff, *out_meta;      // out_cap x 4, out_cap x 4 (board id, game, index, player)
-    int32_t *counters;                   // [0] queued examples [1] dropped
+    int32_t *counters;                   // [0] queued examples [1] dropped [2] GC queue
+                                         // [5] example-row queue [4] k_gc workgroups done
+    int32_t *gcq;                        // B: trees whose garbage collection k_gc runs
+    int2 *flq;                           // out_cap: (staging row, queue slot) rows k_gc copies
 };
 
 // per-node board slot (Pools::nbrd): the LDS row format padded to 16 bytes

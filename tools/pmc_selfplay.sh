@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 mkdir -p "$OUT"
 CMD=(python3 bench.py --workload selfplay --steps "$STEPS" --warmup "$WARM" --no-cpu-baseline)
 # counters only for the self-play kernels, dispatches WARM .. WARM+STEPS of each
-FILT=(--kernel-include-regex "k_(select|leaf_mask|nn_forward|backup|commit)" --kernel-iteration-range "[$WARM-$((WARM + STEPS))]")
+FILT=(--kernel-include-regex "k_(select|leaf_mask|nn_forward|backup|commit|gc)" --kernel-iteration-range "[$WARM-$((WARM + STEPS))]")
 PASSES=${PASSES:-fetch write sq sq2 mem ea}
 pass() {
     local name=$1; shift

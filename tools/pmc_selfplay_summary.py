@@ -11,7 +11,7 @@ import os
 import re
 import sys
 
-KERNELS = ("k_select", "k_leaf_mask", "k_nn_forward", "k_backup", "k_commit")
+KERNELS = ("k_select", "k_leaf_mask", "k_nn_forward", "k_backup", "k_commit", "k_gc")
 
 
 def per_kernel(d, last=None):
