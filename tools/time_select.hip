@@ -8,12 +8,27 @@
 #include <cstdio>
 #include <vector>
 #include <cstdlib>
+// value-free leaves (v = 0, like a random-init network's near-zero values): deep trees
+__global__ void zero_values(float *v, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = 0.f;
+}
 int main(int argc, char **argv) {
-    // argv: [sims=100] [warm iterations=3000] [timed iterations=1000] [node_cap=2048]
+    // argv: [sims=100] [warm iterations=3000] [timed iterations=1000] [node_cap=2048] [zero values=0]
     // self-play steady state (spl_mcts_commit), genbu args, hash-prior network
     const int B = 32768;
     const int SIMS = argc > 1 ? atoi(argv[1]) : 100;
     const int WARM = argc > 2 ? atoi(argv[2]) : 3000, ITERS = argc > 3 ? atoi(argv[3]) : 1000;
+    const int ZV = argc > 5 ? atoi(argv[5]) : 0;   // 1: hash priors, v = 0; 2: SplendorNNet, small random weights
+    float *nw = nullptr;
+    if (ZV == 2) {
+        const int nf = spl_nn_packed_floats(2);
+        std::vector<float> hw(nf);
+        uint32_t x = 12345;
+        for (auto &f : hw) { x = x * 1664525u + 1013904223u; f = ((x >> 8) * (1.0f / 16777216.0f) - 0.5f) * 0.1f; }
+        (void)hipMalloc(&nw, (size_t)nf * 4);
+        (void)hipMemcpy(nw, hw.data(), (size_t)nf * 4, hipMemcpyHostToDevice);
+    }
     spl_ctx *c; spl_ctx_create(2, 10, &c);
     spl_mcts_config cfg{};
     cfg.num_sims = SIMS; cfg.ratio_full = 5; cfg.prob_full = 0.25; cfg.cpuct = 2.5; cfg.fpu = 0.3;
@@ -34,7 +49,9 @@ int main(int argc, char **argv) {
             (void)hipEventRecord(e0);
         }
         spl_mcts_select(m, leaf, mk, lv, nullptr);
-        spl_hash_eval(c, B, leaf, mk, pi, v, nullptr);
+        if (ZV == 2) spl_nn_forward(2, B, leaf, mk, nw, pi, v, nullptr);   // small random weights
+        else spl_hash_eval(c, B, leaf, mk, pi, v, nullptr);
+        if (ZV == 1) zero_values<<<(2 * B + 255) / 256, 256>>>(v, 2 * B);
         spl_mcts_backup(m, mk, pi, v, nullptr);
         spl_mcts_commit(m, nullptr);
         if (it % 500 == 499) spl_mcts_drain_examples(m, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, cnt, nullptr);
@@ -51,5 +68,7 @@ int main(int argc, char **argv) {
     printf("%d sims, %d trees, steady state after %d iterations: %.1f us per select+hash_eval+backup+commit iteration; "
            "%.0f probed waves, %.2f levels/sim\n", SIMS, B, WARM, ms * 1e3 / ITERS, calls, h[20] / calls);
     for (int k = 0; k < 9; k++) printf("  %-28s %8.0f cycles per select\n", names[k], h[k] / calls);
+    printf("  levels repeating the previous simulation's path: %.2f per simulation (of %.2f)\n", h[22] / calls,
+           h[23] / calls);
     return 0;
 }
