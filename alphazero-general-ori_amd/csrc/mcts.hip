@@ -1029,6 +1029,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
     SPL_PROBE(0)
     int node = H->root, depth = 0, kind = LEAF_NN;
     uint64_t k0 = 0, k1 = 0;
+#if MCTS_TIMING
+    bool prefix_run = true;
+#endif
     float val[4] = {0, 0, 0, 0};
     if (node < 0) {
         wave_fingerprint<N>(s, k0, k1);                  // the root itself is the leaf
@@ -1071,6 +1074,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                                 ? pick_edge64(e64, cpuct, fpu, cf, ec, ns, qs)
                                 : pick_edge_desc(P, C, t, eb, ec, ns, qs, forced && depth == 0, sims, e64);
             const int ge = eb + pk.e;
+#if MCTS_TIMING
+            if (threadIdx.x == 0) {
+                spl_probe_acc[23] += 1;                  // levels
+                if (prefix_run) {                        // levels that repeat the previous path
+                    if (path[2 * depth] == node && path[2 * depth + 1] == ge) spl_probe_acc[22] += 1;
+                    else prefix_run = false;
+                }
+            }
+#endif
             if (l == 0) { path[2 * depth] = node; path[2 * depth + 1] = ge; }
             depth++;
             int child = uniform(pk.child);
@@ -1614,6 +1626,18 @@ static bool valid_cfg(const spl_ctx *ctx, int B, const spl_mcts_config *cfg) {
     return ctx && ctx->n >= 2 && ctx->n <= 4 && B > 0 && cfg && cfg->num_sims > 0 && cfg->ratio_full > 0 &&
            cfg->node_cap > 0 && cfg->edge_cap > 0;
 }
+
+#if MCTS_TIMING
+// diagnostic builds only: the k_select probe accumulators (tools/select_reuse.py)
+int spl_diag_select_timing(unsigned long long *out24, int reset) {
+    if (hipMemcpyFromSymbol(out24, HIP_SYMBOL(g_select_timing), 24 * 8) != hipSuccess) return SPL_EDEVICE;
+    if (reset) {
+        unsigned long long z[24] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_select_timing), z, sizeof(z)) != hipSuccess) return SPL_EDEVICE;
+    }
+    return 0;
+}
+#endif
 
 long long spl_mcts_plan_bytes(const spl_ctx *ctx, int B, const spl_mcts_config *cfg) {
     if (!valid_cfg(ctx, B, cfg)) return SPL_EINVAL;

@@ -5,6 +5,9 @@ libsplendor_diag.so); reports per simulation the levels descended and how many o
 repeat the previous simulation's path (node and edge) from the root — the share a
 speculative prefetch of the previous path could serve.
 
+  (cd alphazero-general-ori_amd && hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC \
+      -ffp-contract=off -DMCTS_TIMING=1 -shared -o ../tools/libsplendor_diag.so \
+      csrc/splendor_env.hip csrc/mcts.hip csrc/nnet.hip)
   SPLENDOR_AMD_LIB=tools/libsplendor_diag.so python tools/select_reuse.py [warm] [iters]
 """
 import ctypes
