@@ -18,7 +18,7 @@ static int run_players(int n) {
     float *end = calloc((size_t)B * T * n, sizeof(float));
     int32_t *games = calloc(B, sizeof(int32_t));
     uint64_t *fold = calloc(B, sizeof(uint64_t));
-    if (or_rollout_run(n, B, T, 0x5EED + n, 0, st, pl, act, end, games, fold) <= 0) return 1;
+    if (or_rollout_run(n, B, T, 0x5EED + n, 0, st, pl, act, end, games, fold, NULL) <= 0) return 1;
     if (or_random_rollouts(n, 64, 200, 7 + n, 2) <= 0) return 1;
 
     /* symmetries and MCTS (with root noise) from the rollout's final boards */

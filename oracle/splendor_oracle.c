@@ -958,7 +958,7 @@ int or_selfplay_run(int n, int B, int iters, uint64_t seed, uint32_t board_base,
  * for B boards x steps. Outputs are optional (NULL = skip). Returns board-steps done. */
 long long or_rollout_run(int n, int B, int steps, uint64_t seed, uint32_t board_base,
                          int8_t *state_out, int8_t *player_out, int16_t *actions,
-                         float *ended, int32_t *games, uint64_t *mask_fold) {
+                         float *ended, int32_t *games, uint64_t *mask_fold, uint64_t *masks) {
     build_tables();
     int S = 7 * or_rows(n);
     int8_t *st = (int8_t *)malloc((size_t)B * S), canon[7 * 88];
@@ -985,6 +985,7 @@ long long or_rollout_run(int n, int B, int steps, uint64_t seed, uint32_t board_
             uint64_t w[7] = {0};
             for (int a = 0; a < 409; a++) { cnt += mask[a]; if (mask[a]) w[a >> 6] |= 1ull << (a & 63); }
             if (mask_fold) for (int j = 0; j < 7; j++) mask_fold[b] ^= (w[j] * (2 * (uint64_t)j + 1)) ^ ((uint64_t)t << 40);
+            if (masks) memcpy(masks + ((size_t)t * B + b) * 7, w, sizeof w);
             int k = (int)(or_uniform(seed, gb, (uint32_t)t, 0) * (double)cnt), a;
             for (a = 0; a < 409; a++) if (mask[a] && k-- == 0) break;
             if (a == 409) a = 408;
@@ -1018,12 +1019,12 @@ long long or_rollout_run(int n, int B, int steps, uint64_t seed, uint32_t board_
 typedef struct { int n, B, steps; uint64_t seed; uint32_t base; long long done; } rr_job;
 static void *rr_thread(void *p) {
     rr_job *j = (rr_job *)p;
-    j->done = or_rollout_run(j->n, j->B, j->steps, j->seed, j->base, NULL, NULL, NULL, NULL, NULL, NULL);
+    j->done = or_rollout_run(j->n, j->B, j->steps, j->seed, j->base, NULL, NULL, NULL, NULL, NULL, NULL, NULL);
     return NULL;
 }
 long long or_random_rollouts(int n, int B, int steps, uint64_t seed, int threads) {
     if (threads <= 1 || B < 2)
-        return or_rollout_run(n, B, steps, seed, 0, NULL, NULL, NULL, NULL, NULL, NULL);
+        return or_rollout_run(n, B, steps, seed, 0, NULL, NULL, NULL, NULL, NULL, NULL, NULL);
     if (threads > B) threads = B;
     build_tables();                              /* shared tables, built before the threads */
     pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);

@@ -93,10 +93,11 @@ int or_selfplay_run(int n, int B, int iters, uint64_t seed, uint32_t board_base,
  * mask -> uniform valid action -> chance step -> end check -> reset on end.
  * Returns total board-steps executed. threads<=0 => 1. */
 long long or_random_rollouts(int n, int B, int steps, uint64_t seed, int threads);
-/* same loop with traces (spl_rollout_step semantics, include/splendor_amd.h); NULL skips */
+/* same loop with traces (spl_rollout_step semantics, include/splendor_amd.h); NULL skips.
+ * masks: steps x B x 7 legality words of every move (mask_fold: their per-board fold) */
 long long or_rollout_run(int n, int B, int steps, uint64_t seed, uint32_t board_base,
                          int8_t *state_out, int8_t *player_out, int16_t *actions,
-                         float *ended, int32_t *games, uint64_t *mask_fold);
+                         float *ended, int32_t *games, uint64_t *mask_fold, uint64_t *masks);
 
 #ifdef __cplusplus
 }

@@ -51,7 +51,8 @@ def lib():
         L.or_random_rollouts.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int]
         L.or_random_rollouts.restype = C.c_longlong
         L.or_rollout_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint32, p8, p8,
-                                     C.POINTER(C.c_int16), pf, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
+                                     C.POINTER(C.c_int16), pf, C.POINTER(C.c_int32), C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_uint64)]
         L.or_rollout_run.restype = C.c_longlong
         L.or_selfplay_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint32, C.c_int, C.c_int,
                                       C.c_double, C.c_double, C.c_double, C.c_int, C.c_int, C.c_double,
@@ -204,8 +205,9 @@ def random_rollouts(n, B, steps, seed, threads=1):
     return lib().or_random_rollouts(n, B, steps, seed, threads)
 
 
-def rollout_run(n, B, steps, seed, board_base=0):
-    """Oracle of spl_rollout_step: returns dict of final state/player and traces."""
+def rollout_run(n, B, steps, seed, board_base=0, masks=False):
+    """Oracle of spl_rollout_step: returns dict of final state/player and traces (with
+    masks=True also every move's legality words, [steps, B, 7] uint64)."""
     S = 7 * rows(n)
     st = np.zeros((B, rows(n), 7), np.int8)
     pl = np.zeros(B, np.int8)
@@ -213,10 +215,14 @@ def rollout_run(n, B, steps, seed, board_base=0):
     end = np.zeros((steps, B, n), np.float32)
     games = np.zeros(B, np.int32)
     fold = np.zeros(B, np.uint64)
+    mk = np.zeros((steps, B, 7), np.uint64) if masks else None
     lib().or_rollout_run(n, B, steps, seed, board_base, _p(st, C.c_int8), _p(pl, C.c_int8),
                          _p(act, C.c_int16), _p(end, C.c_float), _p(games, C.c_int32),
-                         _p(fold, C.c_uint64))
-    return {"state": st, "player": pl, "action": act, "ended": end, "games": games, "mask_fold": fold}
+                         _p(fold, C.c_uint64), _p(mk, C.c_uint64) if masks else None)
+    out = {"state": st, "player": pl, "action": act, "ended": end, "games": games, "mask_fold": fold}
+    if masks:
+        out["masks"] = mk
+    return out
 
 
 def selfplay_run(n, B, iters, seed, num_sims, ratio_full, prob_full, cpuct, fpu, forced, temp_threshold,
