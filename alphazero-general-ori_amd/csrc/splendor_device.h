@@ -169,15 +169,19 @@ struct Chance {
 // 28 HBM bytes = 7 dwords; one lane converts such a quad in registers (funnel shifts), so
 // a board moves as 7-dword global accesses and 64-bit LDS accesses. Boards whose row count
 // is not a multiple of 4 (3 players) go byte by byte.
-__device__ __forceinline__ void quad_to_rows(const uint32_t *g, uint64_t *o) {
-    uint32_t d[7];
-#pragma unroll
-    for (int k = 0; k < 7; k++) d[k] = g[k];
+// (the 7 dwords already in registers -> the 4 LDS rows)
+__device__ __forceinline__ void quad_rows_put(const uint32_t (&d)[7], uint64_t *o) {
     const uint64_t M = 0x00FFFFFFFFFFFFFFull;
     o[0] = ((uint64_t)d[0] | (uint64_t)d[1] << 32) & M;
     o[1] = ((uint64_t)d[1] >> 24 | (uint64_t)d[2] << 8 | (uint64_t)d[3] << 40) & M;
     o[2] = ((uint64_t)d[3] >> 16 | (uint64_t)d[4] << 16 | (uint64_t)d[5] << 48) & M;
     o[3] = ((uint64_t)d[5] >> 8 | (uint64_t)d[6] << 24) & M;
+}
+__device__ __forceinline__ void quad_to_rows(const uint32_t *g, uint64_t *o) {
+    uint32_t d[7];
+#pragma unroll
+    for (int k = 0; k < 7; k++) d[k] = g[k];
+    quad_rows_put(d, o);
 }
 __device__ __forceinline__ void rows_to_quad(const uint64_t *r, uint32_t *g) {
     const uint64_t r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];

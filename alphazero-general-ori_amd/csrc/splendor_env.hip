@@ -206,6 +206,24 @@ struct RolloutLds {
     static constexpr int STRIDE = (Lay<N>::ROWS % 2 ? Lay<N>::ROWS : Lay<N>::ROWS + 1) * 8;
 };
 
+// COUNT elements of a table held in registers across the workgroup's THREADS threads:
+// fetch() issues every load (clamped indices, no branch, so they all go out back to back),
+// put() stores them into LDS after the other fetches
+template <class T, int COUNT>
+struct StageRegs {
+    static constexpr int IT = (COUNT + THREADS - 1) / THREADS;
+    T v[IT];
+    __device__ __forceinline__ void fetch(const T *src, int tid) {
+#pragma unroll
+        for (int k = 0; k < IT; k++) v[k] = src[min(tid + k * THREADS, COUNT - 1)];
+    }
+    __device__ __forceinline__ void put(T *dst, int tid) const {
+#pragma unroll
+        for (int k = 0; k < IT; k++)
+            if (tid + k * THREADS < COUNT) dst[tid + k * THREADS] = v[k];
+    }
+};
+
 template <int N>
 __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__restrict__ state,
                                                      int8_t *__restrict__ player, int lim,
@@ -242,17 +260,59 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     if (tid == 0) spl_probe_last = clock64();
     const uint64_t wall0 = wall_clock64();
 #endif
-    for (int i = tid; i < nb * Cv::UNITS; i += THREADS) {
-        const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
-        Cv::load(lds + b * ST, gst + (size_t)b * Lx::S, u);
+    // prologue: every global load (boards, players, game counters, the LDS tables) is issued
+    // before the first LDS store. Strided copy loops waited one L2 / HBM round trip per
+    // iteration: 13 of them, 15.5 K cycles of a 20-move launch's ~210 K (tools/time_rollout).
+    {
+        StageRegs<double, 41 * 9> q_quot;
+        StageRegs<uint64_t, 240> q_cards;
+        StageRegs<uint64_t, 409> q_take, q_give;
+        StageRegs<int8_t, 409> q_rsv;
+        StageRegs<uint64_t, 7 * 116> q_fac;
+        q_quot.fetch(&K_QUOT[0][0], tid);
+        q_cards.fetch(&K_CARD_ROWS[0][0], tid);
+        q_take.fetch(K_ACT_TAKE, tid);
+        q_give.fetch(K_ACT_GIVE, tid);
+        q_rsv.fetch(K_ACT_RSV, tid);
+        q_fac.fetch(&K_MASK_FACTORS[0][0], tid);
+        const double recip = K_RECIP[min(tid, 8)];
+        const int bi = min(tid, nb - 1);
+        const int8_t p0 = player[b0 + bi];
+        const int32_t g0 = games_done ? games_done[b0 + bi] : 0;
+        if constexpr (Cv::QUAD) {
+            constexpr int BI = (RB * Cv::UNITS + THREADS - 1) / THREADS;
+            uint32_t d[BI][7];
+#pragma unroll
+            for (int k = 0; k < BI; k++) {              // clamped index: every load is valid
+                const int i = min(tid + k * THREADS, nb * Cv::UNITS - 1), b = i / Cv::UNITS, u = i - b * Cv::UNITS;
+                const uint32_t *g = reinterpret_cast<const uint32_t *>(gst + (size_t)b * Lx::S) + 7 * u;
+#pragma unroll
+                for (int j = 0; j < 7; j++) d[k][j] = g[j];
+            }
+#pragma unroll
+            for (int k = 0; k < BI; k++) {
+                const int i = tid + k * THREADS, b = i / Cv::UNITS, u = i - b * Cv::UNITS;
+                if (i < nb * Cv::UNITS) quad_rows_put(d[k], reinterpret_cast<uint64_t *>(lds + b * ST) + 4 * u);
+            }
+        } else {
+            for (int i = tid; i < nb * Cv::UNITS; i += THREADS) {
+                const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
+                Cv::load(lds + b * ST, gst + (size_t)b * Lx::S, u);
+            }
+        }
+        if (tid < nb) {
+            pl[tid] = p0;
+            gdone[tid] = g0;
+        }
+        if (tid < 4) kcount[tid] = 0;
+        q_quot.put(&tabs.quot[0][0], tid);
+        q_cards.put(&tabs.cards[0][0], tid);
+        q_take.put(tabs.act_take, tid);
+        q_give.put(tabs.act_give, tid);
+        q_rsv.put(tabs.act_rsv, tid);
+        q_fac.put(mfac, tid);
+        if (tid < 9) tabs.recip[tid] = recip;
     }
-    if (tid < nb) {
-        pl[tid] = player[b0 + tid];
-        gdone[tid] = games_done ? games_done[b0 + tid] : 0;
-    }
-    if (tid < 4) kcount[tid] = 0;
-    stage_tabs(tabs, tid, THREADS);
-    for (int i = tid; i < 7 * 116; i += THREADS) mfac[i] = (&K_MASK_FACTORS[0][0])[i];
     // the next deals of every board (one for launches of 4-47 moves, two beyond),
     // computed up front by four lanes per deal (3 tiers + nobles, lane_deal_part) so that
     // ending a game costs a row expansion, not the draws; a game ending beyond them draws
