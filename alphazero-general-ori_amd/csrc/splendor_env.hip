@@ -264,6 +264,14 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
     // before the first LDS store. Strided copy loops waited one L2 / HBM round trip per
     // iteration: 13 of them, 15.5 K cycles of a 20-move launch's ~210 K (tools/time_rollout).
     {
+        // (the deal tasks' game counters first: vmcnt retires loads in order, so the deals
+        // below wait for these alone)
+        int32_t gt[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int b = ((tid + j * THREADS) >> 2) % RB;
+            gt[j] = games_done ? games_done[b0 + min(b, nb - 1)] : 0;
+        }
         StageRegs<double, 41 * 9> q_quot;
         StageRegs<uint64_t, 240> q_cards;
         StageRegs<uint64_t, 409> q_take, q_give;
@@ -279,9 +287,9 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         const int bi = min(tid, nb - 1);
         const int8_t p0 = player[b0 + bi];
         const int32_t g0 = games_done ? games_done[b0 + bi] : 0;
+        constexpr int BI = Cv::QUAD ? (RB * Cv::UNITS + THREADS - 1) / THREADS : 1;
+        uint32_t d[BI][7];
         if constexpr (Cv::QUAD) {
-            constexpr int BI = (RB * Cv::UNITS + THREADS - 1) / THREADS;
-            uint32_t d[BI][7];
 #pragma unroll
             for (int k = 0; k < BI; k++) {              // clamped index: every load is valid
                 const int i = min(tid + k * THREADS, nb * Cv::UNITS - 1), b = i / Cv::UNITS, u = i - b * Cv::UNITS;
@@ -289,6 +297,20 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
 #pragma unroll
                 for (int j = 0; j < 7; j++) d[k][j] = g[j];
             }
+        }
+        // the next deals of every board (one for launches of 4-47 moves, two beyond),
+        // computed up front by four lanes per deal (3 tiers + nobles, lane_deal_part) so that
+        // ending a game costs a row expansion, not the draws; a game ending beyond them draws
+        // its deal on the spot (same keys). They read the constant tables and their own game
+        // counters, so they run while the loads above are in flight.
+        const int pre = K >= 48 ? 2 : (K >= 4 ? 1 : 0);
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int task = tid + j * THREADS, part = task & 3, rec = task >> 2, k = rec / RB, b = rec - k * RB;
+            if (task < pre * RB * 4 && b < nb)
+                lane_deal_part<N>(seed, bbase + (uint32_t)(b0 + b), (uint32_t)(gt[j] + 1 + k), part, Tabs{}, drec[k][b]);
+        }
+        if constexpr (Cv::QUAD) {
 #pragma unroll
             for (int k = 0; k < BI; k++) {
                 const int i = tid + k * THREADS, b = i / Cv::UNITS, u = i - b * Cv::UNITS;
@@ -303,6 +325,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         if (tid < nb) {
             pl[tid] = p0;
             gdone[tid] = g0;
+            gd0[tid] = g0;
         }
         if (tid < 4) kcount[tid] = 0;
         q_quot.put(&tabs.quot[0][0], tid);
@@ -313,18 +336,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         q_fac.put(mfac, tid);
         if (tid < 9) tabs.recip[tid] = recip;
     }
-    // the next deals of every board (one for launches of 4-47 moves, two beyond),
-    // computed up front by four lanes per deal (3 tiers + nobles, lane_deal_part) so that
-    // ending a game costs a row expansion, not the draws; a game ending beyond them draws
-    // its deal on the spot (same keys)
     const int pre = K >= 48 ? 2 : (K >= 4 ? 1 : 0);
-    lds_sync();                                            // tables and gdone staged
-    if (tid < nb) gd0[tid] = gdone[tid];
-    for (int task = tid; task < pre * RB * 4; task += THREADS) {
-        const int part = task & 3, rec = task >> 2, k = rec / RB, b = rec - k * RB;
-        if (b < nb) lane_deal_part<N>(seed, bbase + (uint32_t)(b0 + b), (uint32_t)(gdone[b] + 1 + k), part,
-                                      tabs.view(), drec[k][b]);
-    }
     // every barrier of the move loop orders LDS only: the per-move outputs are write-only
     // HBM streams, and waiting for their stores (__syncthreads) cost ~2K cycles a barrier
     lds_sync();
