@@ -270,7 +270,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const int b = ((tid + j * THREADS) >> 2) % RB;
-            gt[j] = games_done ? games_done[b0 + min(b, nb - 1)] : 0;
+            gt[j] = games_done[b0 + min(b, nb - 1)];      // (never null: spl_rollout_run checks)
         }
         StageRegs<double, 41 * 9> q_quot;
         StageRegs<uint64_t, 240> q_cards;
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(THREADS) void k_rollout(int B, int K, int8_t *__res
         const double recip = K_RECIP[min(tid, 8)];
         const int bi = min(tid, nb - 1);
         const int8_t p0 = player[b0 + bi];
-        const int32_t g0 = games_done ? games_done[b0 + bi] : 0;
+        const int32_t g0 = games_done[b0 + bi];
         constexpr int BI = Cv::QUAD ? (RB * Cv::UNITS + THREADS - 1) / THREADS : 1;
         uint32_t d[BI][7];
         if constexpr (Cv::QUAD) {
