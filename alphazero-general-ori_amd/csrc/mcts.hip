@@ -1542,6 +1542,27 @@ __global__ __launch_bounds__(256) void k_nn_input(int B, int R, const int8_t *__
     }
 }
 
+// tree sizes (spl_mcts_tree_sizes): slots in use and the live part of each tree — the root
+// and the nodes whose round exceeds the root's (what garbage collection keeps), with their
+// CSR edges. Diagnostic (capacity planning), one wave per tree.
+__global__ __launch_bounds__(64) void k_tree_sizes(Pools P, int B, int32_t *out) {
+    const int t = blockIdx.x;
+    if (t >= B) return;
+    const int l = lane_id();
+    const TreeHdr *H = P.hdr + t;
+    const size_t nb = (size_t)t * P.ncap;
+    const int nc = H->node_count, root = H->root;
+    const int rr = root >= 0 ? P.nround[nb + root] : 1 << 30;
+    int ln = 0, le = 0;
+    for (int i = l; i < nc; i += 64)
+        if (i == root || P.nround[nb + i] > rr) { ln++; le += P.nterm[nb + i] ? 0 : P.nec[nb + i]; }
+    for (int o = 32; o > 0; o >>= 1) { ln += __shfl_xor(ln, o, 64); le += __shfl_xor(le, o, 64); }
+    if (l == 0) {
+        out[4 * t] = nc; out[4 * t + 1] = H->edge_count;
+        out[4 * t + 2] = root >= 0 ? ln : 0; out[4 * t + 3] = root >= 0 ? le : 0;
+    }
+}
+
 // deterministic hash network (oracle or_fake_predict; used for search-parity tests and
 // tree-only throughput runs)
 template <int N>
@@ -1816,6 +1837,12 @@ int spl_mcts_headers(spl_mcts *m, int32_t *out, void *hs) {
     if (!m || !out) return SPL_EINVAL;
     return hipMemcpyAsync(out, m->P.hdr, sizeof(TreeHdr) * m->B, hipMemcpyDeviceToDevice,
                           (hipStream_t)hs) == hipSuccess ? 0 : SPL_EDEVICE;
+}
+
+int spl_mcts_tree_sizes(spl_mcts *m, int32_t *out, void *hs) {
+    if (!m || !out) return SPL_EINVAL;
+    hipLaunchKernelGGL(k_tree_sizes, dim3((unsigned)m->B), dim3(64), 0, (hipStream_t)hs, m->P, m->B, out);
+    return check_launch();
 }
 
 int spl_nn_input(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask, float *x,

@@ -72,14 +72,28 @@ def _agreed_batch_count(batch_count, device):
 
 
 def _batch_generator(device):
-    """Batch sampling stream: seeded from the global torch RNG (itself unseeded unless the
-    caller seeds it, like the reference's np.random.choice) and decorrelated per rank, so
-    ranks draw different batches and repeated calls differ."""
-    _, rank, _ = _dist_world()
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) ^ (0x9E3779B97F4A7C15 * (rank + 1) & (2 ** 63 - 1))
+    """Batch sampling stream, seeded from the global torch RNG (itself unseeded unless the
+    caller seeds it, like the reference's np.random.choice). Under torch.distributed rank
+    0's seed is broadcast, so every rank draws the same permutations (see `train`)."""
+    dist, _, world = _dist_world()
+    seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
+    if world > 1:
+        seed = seed.to(device)
+        dist.broadcast(seed, src=0)
     g = torch.Generator(device=device)
-    g.manual_seed(seed)
+    g.manual_seed(int(seed.item()))
     return g
+
+
+def _same_everywhere(E, device):
+    """True when every rank holds the same number of examples (Coach.learn all-gathers, so
+    ranks hold the same set)."""
+    dist, _, world = _dist_world()
+    if world == 1:
+        return True
+    t = torch.tensor([E, -E], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t[0]) == -int(t[1]) == E
 
 
 def _allreduce_grads(params):
@@ -126,12 +140,24 @@ class NNetWrapper:
         return (loss_pi(pis, out_pi), loss_v(vs, out_v), loss_scdiff_cdf(t_sd, out_sd),
                 loss_scdiff_pdf(t_sd, out_sd))
 
-    def train(self, examples, generator=None):
+    def train(self, examples, generator=None, sample_ids=None):
         """One GenericNNetWrapper.train call over `examples` (ExampleSet, or the reference's
         list of tuples): epochs x (len // batch_size) Adam steps on batches sampled without
-        replacement, total loss l_pi + vl_weight * l_v + l_cdf + l_pdf. Returns the mean of
-        each loss over the last epoch. Across ranks: gradients averaged in one all-reduce per
-        step, the step count agreed (minimum over ranks), batches drawn per rank."""
+        replacement, total loss l_pi + vl_weight * l_v + l_cdf + l_pdf, OneCycleLR stepped
+        per batch. Returns the mean of each loss over the last epoch.
+
+        sample_ids: the batches themselves (one index array of batch_size per step, epochs x
+        batch_count of them) — the reference's np.random.choice draws (:70) injected, as the
+        parity tests do; then nothing is drawn from any RNG here, so dropout masks come from
+        the global torch generator in the reference's order.
+
+        Across ranks (torch.distributed): with the same example set on every rank (what
+        Coach.learn's all-gather leaves) all ranks draw the same permutation per step and
+        rank r trains on its slice ids[r::world] of the batch, gradients averaged in one
+        all-reduce: the step count and the samples per step are the reference's (a global
+        batch of batch_size; BatchNorm statistics are per rank). Ranks holding different
+        sets sample their own batches of batch_size (the step count is the minimum over
+        ranks, so no rank waits in an all-reduce the others never enter)."""
         if not isinstance(examples, ExampleSet):
             examples = ExampleSet.from_tuples(list(examples))
         if self.args["surprise_weight"]:
@@ -140,21 +166,35 @@ class NNetWrapper:
             raise ValueError("surprise_weight: per-example surprise is a vector (reference raises)")
         ex = examples.to(self.device)
         E, bs, epochs = len(ex), int(self.args["batch_size"]), int(self.args["epochs"])
+        dist, rank, world = _dist_world()
+        shared = _same_everywhere(E, self.device)
         batch_count = _agreed_batch_count(E // bs, self.device)
         if batch_count == 0:
             return None
+        if sample_ids is not None:
+            sample_ids = [torch.as_tensor(np.asarray(i, dtype=np.int64), device=self.device) for i in sample_ids]
+            if len(sample_ids) != epochs * batch_count or any(len(i) != bs for i in sample_ids):
+                raise ValueError(f"sample_ids: need {epochs * batch_count} batches of {bs}")
         params = list(self.nnet.parameters())
         if self.optimizer is None:
             self.optimizer = optim.Adam(params, lr=self.args["learn_rate"])
         scheduler = optim.lr_scheduler.OneCycleLR(self.optimizer, max_lr=self.args["learn_rate"],
                                                   steps_per_epoch=batch_count, epochs=epochs)
-        gen = generator or _batch_generator(self.device)
-        means = None
+        gen = None if sample_ids is not None else (generator or _batch_generator(self.device))
+        if gen is not None and not shared:      # different sets: decorrelate the ranks
+            gen.manual_seed(gen.initial_seed() ^ (0x9E3779B97F4A7C15 * (rank + 1) & (2 ** 63 - 1)))
+        means, step = None, 0
         for _ in range(epochs):
             self.nnet.train()
             acc = torch.zeros(3, dtype=torch.float64, device=self.device)
             for _ in range(batch_count):
-                ids = torch.randperm(E, generator=gen, device=self.device)[:bs]
+                if sample_ids is not None:
+                    ids = sample_ids[step]
+                else:
+                    ids = torch.randperm(E, generator=gen, device=self.device)[:bs]
+                if shared and world > 1:
+                    ids = ids[rank::world]
+                step += 1
                 boards = ex.board.index_select(0, ids).float()
                 valids = unpack_mask(ex.valids.index_select(0, ids))
                 pis = ex.pi.index_select(0, ids)
@@ -168,9 +208,13 @@ class NNetWrapper:
                 self.optimizer.step()
                 scheduler.step()
                 acc += torch.stack([l_pi.detach(), l_v.detach(), (l_c + l_p).detach()]).double()
+                if self._loss_log is not None:
+                    self._loss_log.append([float(x.detach()) for x in (l_pi, l_v, l_c, l_p)])
             means = (acc / batch_count).tolist()
         self.nnet.eval()
         return {"pi": means[0], "v": means[1], "scdiff": means[2]}
+
+    _loss_log = None     # list: per-step (l_pi, l_v, l_cdf, l_pdf) appended by train (tests)
 
     # ------------------------------------------------------------ checkpoints
     def save_checkpoint(self, folder="checkpoint", filename="checkpoint.pt", additional_keys=None):

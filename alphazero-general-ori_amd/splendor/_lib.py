@@ -62,6 +62,7 @@ _SIGS = {
     "spl_mcts_root_stats": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_root_priors": ([C.c_void_p, _vp, _vp], C.c_int),
     "spl_mcts_headers": ([C.c_void_p, _vp, _vp], C.c_int),
+    "spl_mcts_tree_sizes": ([C.c_void_p, _vp, _vp], C.c_int),
     "spl_mcts_reset_games": ([C.c_void_p, _vp], C.c_int),
     "spl_mcts_commit": ([C.c_void_p, _vp], C.c_int),
     "spl_mcts_drain_examples": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int, _vp, _vp], C.c_int),

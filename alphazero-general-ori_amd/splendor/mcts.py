@@ -191,6 +191,13 @@ class BatchedMCTS:
         _lib.check(self.L.spl_mcts_headers(self.h, _ptr(self._hdr), self.e._s()), "spl_mcts_headers")
         return self._hdr.cpu().numpy().view(HDR_DTYPE).reshape(self.B)
 
+    def tree_sizes(self):
+        """int32 [B, 4] per tree: node slots used, edge slots used, live nodes (root + rounds
+        beyond the root's: what GC keeps), live edges."""
+        out = torch.empty((self.B, 4), dtype=torch.int32, device=self.e.device)
+        _lib.check(self.L.spl_mcts_tree_sizes(self.h, _ptr(out), self.e._s()), "spl_mcts_tree_sizes")
+        return out.cpu().numpy()
+
     def root_stats(self, adjusted=False):
         B, dev = self.B, self.e.device
         counts = torch.empty((B, ACTIONS), dtype=torch.int64, device=dev)

@@ -224,6 +224,11 @@ int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *val
 /* copies the B per-tree headers (144 bytes each, layout in splendor/mcts.py) to `out` */
 int spl_mcts_headers(spl_mcts *m, int32_t *out, void *hip_stream);
 
+/* out B x 4 i32 per tree: node slots used, edge slots used, live nodes (the root and every
+ * node whose round exceeds the root's: what garbage collection keeps, MCTS.py:79-85) and
+ * their edges. Capacity planning diagnostic (tools/tree_sizes.py). */
+int spl_mcts_tree_sizes(spl_mcts *m, int32_t *out, void *hip_stream);
+
 /* predict input conversion (GenericNNetWrapper.py:160-161): int8 boards [B][R][7] -> f32
  * written transposed as x[B][7][R] (SplendorNNet.py:129 layout), packed mask -> bool bytes
  * (valid may be NULL) */

@@ -40,7 +40,8 @@ Chance injection (the reference is unseeded):
       device / oracle (tests/golden/detrand.py), so whole episodes (Coach.executeEpisode)
       and arena games (Arena.playGames) replay with the build's random streams.
 
-Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz)
+Usage:  python tests/golden/make_golden.py [nnet3,train]   (writes tests/golden/*.npz; with
+        a list, only those round-3 groups)
 """
 import os
 import sys
@@ -560,6 +561,93 @@ def nnet_fixture(n_players, boards):
 
 
 
+def load_trainer():
+    """GenericNNetWrapper + splendor/NNet.py (the reference's training consumer) with an
+    onnxruntime stub (only predict's onnx mode and export use it; train never does)."""
+    import importlib.machinery
+    ort = types.ModuleType("onnxruntime")
+    ort.__spec__ = importlib.machinery.ModuleSpec("onnxruntime", None)
+    ort.SessionOptions = ort.InferenceSession = object
+    sys.modules["onnxruntime"] = ort
+    _exec_module("utils", f"{REF}/utils.py")
+    _exec_module("NeuralNet", f"{REF}/NeuralNet.py")
+    _exec_module("GenericNNetWrapper", f"{REF}/GenericNNetWrapper.py")
+    if "splendor.SplendorNNet" not in sys.modules:
+        _exec_module("splendor.SplendorNNet", f"{REF}/SplendorNNet.py")
+    return _exec_module("splendor.NNet", f"{REF}/NNet.py")
+
+
+def train_fixture(nnet_mod, n_players, canon, masks, E, bs, epochs, lr, dropout, seed):
+    """GenericNNetWrapper.train (:43-139) on CPU over E synthetic examples built from real
+    positions (board = a recorded canonical state, valids its mask, pi random over the
+    valids, winner +-1, scdiff in [-20, 20], surprise random), with the reference's
+    SplendorNNet under deterministic_weights and every np.random.choice batch (:70)
+    injected from a seeded RandomState and recorded. Records each step's four losses
+    (:94-98) and the final state_dict (parameters and BatchNorm running statistics).
+    dropout > 0: torch.manual_seed(seed) right before train, so a restatement that draws
+    its dropout masks in the reference's order on the CPU generator sees the same masks."""
+    import torch
+    rs = np.random.RandomState(seed)
+    idx = rs.randint(0, len(canon), E)
+    boards = canon[idx].astype(np.int8)
+    valids = masks[idx].astype(bool)
+    pis = np.where(valids, rs.random_sample(valids.shape), 0.0).astype(np.float32)
+    pis /= pis.sum(1, keepdims=True)
+    w = np.where(rs.random_sample(E) < 0.5, 1.0, -1.0)
+    winner = (np.stack([w] + [-w / (n_players - 1)] * (n_players - 1), 1)).astype(np.float32)
+    scdiff = rs.randint(-20, 21, (E, n_players)).astype(np.int8)
+    surprise = rs.random_sample((E, n_players)).astype(np.float32)
+    examples = [(boards[i], pis[i], winner[i], scdiff[i], valids[i], surprise[i]) for i in range(E)]
+
+    class _G:
+        num_players = n_players
+        def getBoardSize(self):
+            return (32 + 10 * n_players + n_players * n_players, 7)
+        def getActionSize(self):
+            return 409
+        def getMaxScoreDiff(self):
+            return 15
+    args = {"nn_version": 1, "dropout": dropout, "learn_rate": lr, "batch_size": bs, "epochs": epochs,
+            "vl_weight": 10.0, "surprise_weight": False, "no_compression": True}
+    w_ = nnet_mod.NNetWrapper(_G(), args)
+    sd0 = deterministic_weights(w_.nnet.state_dict())
+    w_.nnet.load_state_dict(sd0)
+    ids_log, loss_log = [], []
+    orig_choice = np.random.choice
+
+    def choice(a, size=None, replace=True, p=None):
+        assert isinstance(a, int) and size == bs and replace is False and p is None
+        ids = rs.permutation(a)[:size]
+        ids_log.append(ids.copy())
+        return ids
+    wrapped = {}
+    for name in ("loss_pi", "loss_v", "loss_scdiff_cdf", "loss_scdiff_pdf"):
+        f = getattr(w_, name)
+        wrapped[name] = f
+
+        def rec(t, o, _f=f, _n=name):
+            r = _f(t, o)
+            if _n == "loss_pi":
+                loss_log.append([])
+            loss_log[-1].append(float(r.item()))
+            return r
+        setattr(w_, name, rec)
+    np.random.choice = choice
+    try:
+        torch.manual_seed(seed)
+        w_.train(examples)
+    finally:
+        np.random.choice = orig_choice
+    sd = w_.nnet.state_dict()
+    out = {"boards": boards, "valids": valids, "pi": pis, "winner": winner, "scdiff": scdiff,
+           "surprise": surprise, "sample_ids": np.array(ids_log, dtype=np.int64),
+           "losses": np.array(loss_log, dtype=np.float64),
+           "args": np.array([E, bs, epochs, lr, dropout, 10.0, seed], dtype=np.float64),
+           "keys": np.array(sorted(sd))}
+    for k in sorted(sd):
+        out["p:" + k] = sd[k].detach().cpu().numpy()
+    return out
+
 # ------------------------------------------------------------- noise / episode / arena
 ST_FULL, ST_DIR, ST_PICK, ST_MOVE, ST_DEAL, ST_BEST = (1 << 24), (2 << 24), (3 << 24), (4 << 24), (5 << 24), (6 << 24)
 GEM_TOTAL = {2: 4, 3: 5, 4: 7}
@@ -819,9 +907,25 @@ def arena_fixtures(game_mod, mcts_mod, arena_mod, n, G, sims, cpuct, fpu, seed):
             "seed": np.array(seed, dtype=np.uint64)}
 
 
-def main():
+def main(only=None):
     logic, numba_logic, game_mod, mcts_mod = load_reference()
     _patch_np_random()
+    if only:                                 # regenerate just the named groups (round 3)
+        if "nnet3" in only:
+            env = np.load(os.path.join(OUT, "env_3p.npz"))
+            nf = nnet_fixture(3, env["canon"][::37][:12])
+            np.savez_compressed(os.path.join(OUT, "nnet_3p.npz"), **nf)
+            print(f"nnet 3p: params {int(nf['n_params'])}")
+        if "train" in only:
+            nnet_mod = load_trainer()
+            for n, dropout, seed in ((2, 0.0, 71), (2, 0.3, 72), (4, 0.0, 74)):
+                env = np.load(os.path.join(OUT, f"env_{n}p.npz"))
+                tf = train_fixture(nnet_mod, n, env["canon"], env["mask_canon"], E=100, bs=32, epochs=2,
+                                   lr=0.001, dropout=dropout, seed=seed)
+                tag = f"{n}p" + ("_dropout" if dropout else "")
+                np.savez_compressed(os.path.join(OUT, f"train_{tag}.npz"), **tf)
+                print(f"train {tag}: {len(tf['sample_ids'])} steps, first losses {tf['losses'][0].round(4).tolist()}")
+        return
     # tables: checked by the oracle tests against its own restatement
     np.savez_compressed(
         os.path.join(OUT, "tables.npz"),
@@ -885,4 +989,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1].split(",") if len(sys.argv) > 1 else None)

@@ -29,7 +29,7 @@ def deterministic_weights(state_dict):
     return out
 
 
-@pytest.mark.parametrize("n", (2, 4))
+@pytest.mark.parametrize("n", (2, 3, 4))
 def test_matches_reference_network(n):
     from splendor.nnet import FoldedNet, SplendorNNet
     with np.load(os.path.join(GOLD, f"nnet_{n}p.npz")) as z:
@@ -63,7 +63,7 @@ def _pack_mask(valid):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", (2, 4))
+@pytest.mark.parametrize("n", (2, 3, 4))
 def test_fused_kernel_matches_reference_network(n):
     """spl_nn_forward (fused HIP kernel, fp32 MFMA) vs the reference network's recorded
     outputs (same closed-form weights). Tolerance: 1e-6 absolute + 1e-4 relative on the

@@ -57,10 +57,20 @@ def main():
         h = sp.headers()
         sp.drain()
         nc, ec = h["node_count"].astype(np.int64), h["edge_count"].astype(np.int64)
+        ts = sp.tree_sizes().astype(np.int64)
+        ln, le = ts[:, 2], ts[:, 3]
+        live = {"live_nodes": [int(ln.max()), int(np.percentile(ln, 99.9)), int(np.percentile(ln, 99)),
+                               int(np.median(ln)), round(float(ln.mean()), 1)],
+                "live_edges": [int(le.max()), int(np.percentile(le, 99.9)), int(np.percentile(le, 99)),
+                               int(np.median(le)), round(float(le.mean()), 1)]}
         r = {"iter": done, "s": round(time.perf_counter() - t0, 1), "games_done": int(h["games_done"].sum()),
              "overflow": int((h["overflow"] != 0).sum()),
              "nodes": [int(nc.max()), int(np.percentile(nc, 99.9)), int(np.percentile(nc, 99)), int(np.median(nc))],
              "edges": [int(ec.max()), int(np.percentile(ec, 99.9)), int(np.percentile(ec, 99)), int(np.median(ec))],
+             "nodes_mean": round(float(nc.mean()), 1), "edges_mean": round(float(ec.mean()), 1),
+             "nodes_deciles": [int(x) for x in np.percentile(nc, range(10, 100, 10))],
+             "edges_deciles": [int(x) for x in np.percentile(ec, range(10, 100, 10))],
+             "events": sp.capacity_events(h), **live,
              "edges_per_node_max": round(float((ec / np.maximum(nc, 1)).max()), 1),
              "edges_per_node_mean": round(float(ec.sum() / max(nc.sum(), 1)), 1)}
         rows.append(r)
