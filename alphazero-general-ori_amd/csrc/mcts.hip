@@ -63,27 +63,33 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 // child come from its lane by shuffle.
 struct Pick {
     int e, a, child;
-    int2 cr;                                    // child's cached {eb, ec} (valid when child >= 0)
+    int cec;                                    // child's cached CSR count (valid when child >= 0)
+    int64_t ceb;                                // and base (global edge index)
 };
-__device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &C, int t, int eb, int ec,
+__device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)(uint64_t)x, l);
+    const int hi = __builtin_amdgcn_readlane((int)((uint64_t)x >> 32), l);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &C, int64_t eb, int ec,
                                                int ns, double qs, bool forced, int step, const Edge &first) {
     const int l = lane_id();
-    const size_t e0 = (size_t)t * P.ecap + eb;
+    const Edge *E = P.ed + eb;
     float p[2];
-    int n[2], a[2], c[2];
-    int2 r[2];
+    int n[2], a[2], c[2], rc[2];
+    int64_t rb[2];
     double q[2];
 #pragma unroll
     for (int j = 0; j < 2; j++) {               // first: edge l, already requested by the caller
         const int i = 64 * j + l;
         EdgeStat st{0.f, 0, Q_UNSET};
-        EdgeLink lk{0, 0, -1, 0, 0};
+        EdgeLink lk{0, 0, -1, 0};
         if (i < ec) {
-            const Edge &ei = j == 0 ? first : P.ed[e0 + i];
+            const Edge &ei = j == 0 ? first : E[i];
             st = ei.s; lk = ei.k;
         }
         p[j] = st.p; n[j] = st.n; q[j] = st.q;
-        a[j] = lk.a; c[j] = lk.child; r[j] = get_cr(lk);
+        a[j] = lk.a; c[j] = lk.child; rb[j] = lk.ceb; rc[j] = lk.cec;
     }
 #if MCTS_TIMING
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // split load wait / compute
@@ -101,7 +107,7 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         for (int base = 128; bi < 0 && base < ec; base += 64) {
             const int i = base + l;
             bool f = false;
-            if (i < ec) f = (long long)P.ed[e0 + i].s.n < (long long)sqrt(0.5 * (double)P.ed[e0 + i].s.p * (double)step);
+            if (i < ec) f = (long long)E[i].s.n < (long long)sqrt(0.5 * (double)E[i].s.p * (double)step);
             const uint64_t b = __ballot(f);
             if (b) bi = base + __ffsll((unsigned long long)b) - 1;
         }
@@ -161,8 +167,8 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         for (int base = 128; bi < 0 && base < ec; base += 64) {
             const int i = base + l;
             if (i < ec) {
-                const double qq = P.ed[e0 + i].s.q, pp = (double)P.ed[e0 + i].s.p;
-                const double u = qq != Q_UNSET ? qq + C.cpuct * pp * sq / (double)(1 + P.ed[e0 + i].s.n)
+                const double qq = E[i].s.q, pp = (double)E[i].s.p;
+                const double u = qq != Q_UNSET ? qq + C.cpuct * pp * sq / (double)(1 + E[i].s.n)
                                                : fpu_init + C.cpuct * pp * sq_eps;
                 if (u > bu) { bu = u; bj = i; }
             }
@@ -173,17 +179,18 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         }
     }
     const int jb = bi >> 6;
-    int av = a[0], cv = c[0], rx = r[0].x, ry = r[0].y;
+    int av = a[0], cv = c[0], rcv = rc[0];
+    int64_t rbv = rb[0];
 #pragma unroll
     for (int j = 1; j < 2; j++)
-        if (jb == j) { av = a[j]; cv = c[j]; rx = r[j].x; ry = r[j].y; }
+        if (jb == j) { av = a[j]; cv = c[j]; rbv = rb[j]; rcv = rc[j]; }
     bi = uniform(bi);                           // chosen lane -> SGPRs (readlane, no LDS trip)
     av = __builtin_amdgcn_readlane(av, bi & 63);
     cv = __builtin_amdgcn_readlane(cv, bi & 63);
-    rx = __builtin_amdgcn_readlane(rx, bi & 63);
-    ry = __builtin_amdgcn_readlane(ry, bi & 63);
-    if (bi >= 128) { av = P.ed[e0 + bi].k.a; cv = P.ed[e0 + bi].k.child; const int2 rr = get_cr(P.ed[e0 + bi].k); rx = rr.x; ry = rr.y; }
-    return {bi, av, cv, make_int2(rx, ry)};
+    rcv = __builtin_amdgcn_readlane(rcv, bi & 63);
+    rbv = readlane64(rbv, bi & 63);
+    if (bi >= 128) { av = E[bi].k.a; cv = E[bi].k.child; rbv = E[bi].k.ceb; rcv = E[bi].k.cec; }
+    return {bi, av, cv, rcv, rbv};
 }
 
 // the descent's common case: a node with at most 64 edges and no forced playouts at this
@@ -220,7 +227,7 @@ __device__ __forceinline__ Pick pick_edge64(const Edge &e, double cpuct, double 
     }
     bi = uniform(bi);
     return {bi, __builtin_amdgcn_readlane((int)e.k.a, bi), __builtin_amdgcn_readlane(e.k.child, bi),
-            make_int2(__builtin_amdgcn_readlane(e.k.ceb, bi), __builtin_amdgcn_readlane((int)e.k.cec, bi))};
+            __builtin_amdgcn_readlane((int)e.k.cec, bi), readlane64(e.k.ceb, bi)};
 }
 
 // ------------------------------------------------------------ prior sums
@@ -258,10 +265,10 @@ __device__ __forceinline__ float wave_np_sum409(const float *a) {
 // normalised like numpy's dirichlet (sequential sum, times its reciprocal).
 // pr: LDS scratch of 416 floats for this wave; raw: pr already holds the network's priors
 // (a new root, :141-144), else the stored priors of an expanded root are used (:150-154).
-__device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int eb, int ec, uint32_t stream,
+__device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int64_t eb, int ec, uint32_t stream,
                                  float *pr, bool raw) {
     const int l = lane_id();
-    Edge *ede = P.ed + (size_t)t * P.ecap + eb;
+    Edge *ede = P.ed + eb;
     const uint32_t gb = C.board_base + (uint32_t)t;
     if (!raw) {
         for (int a = l; a < 416; a += 64) pr[a] = 0.f;
@@ -312,41 +319,113 @@ __device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int 
     __builtin_amdgcn_wave_barrier();
 }
 
+// ------------------------------------------------------------ page allocation
+// Pop a page from a free stack (one lane). Only k_select / k_backup pop, and no launch both
+// pops and pushes, so an array stack with one atomic top is exact: a pop that finds the
+// stack empty undoes its decrement.
+__device__ __forceinline__ int pop_page(int32_t *stack, int32_t *top) {
+    const int k = atomicSub(top, 1);
+    if (k <= 0) { atomicAdd(top, 1); return -1; }
+    return stack[k - 1];
+}
+
+// global id of tree t's node slot `id` (its next slot, node_count), taking a node page from
+// the pool when the slot opens one; -1 when the tree is at its maximum or the pool is empty.
+// Idempotent until node_count advances (a slot reserved by k_select is the one k_backup
+// fills). One lane.
+__device__ int node_slot(const Pools &P, TreeHdr *H, int t, int id) {
+    if (id >= P.nmax) return -1;
+    const int pi = id >> NPG_SHIFT;
+    int32_t *tab = P.ntab + (size_t)t * P.nptab;
+    if (pi >= H->npg) {
+        const int pg = pop_page(P.nfree, P.alloc + 0);
+        if (pg < 0) { atomicAdd(P.alloc + 2, 1); return -1; }
+        tab[pi] = pg;
+        P.npidx[pg] = pi;
+        H->npg = pi + 1;
+    }
+    return tab[pi] * NPG + (id & (NPG - 1));
+}
+
+// a CSR run of ec edges for a new node (global base), from the tree's current edge page or a
+// fresh one (runs never straddle pages); -1 when the tree's edge pages are at their maximum
+// or the pool is empty. One lane.
+__device__ int64_t edge_run(const Pools &P, TreeHdr *H, int t, int ec) {
+    if (H->eleft < ec) {
+        if (H->epg >= P.eptab) return -1;
+        const int pg = pop_page(P.efree, P.alloc + 1);
+        if (pg < 0) { atomicAdd(P.alloc + 3, 1); return -1; }
+        P.etab[(size_t)t * P.eptab + H->epg] = pg;
+        P.epidx[pg] = H->epg;
+        H->epg += 1;
+        H->enext = (int64_t)pg * EPG;
+        H->eleft = EPG;
+    }
+    const int64_t eb = H->enext;
+    H->enext = eb + ec;
+    H->eleft -= ec;
+    H->edge_count += ec;
+    return eb;
+}
+
+// push n page ids (src[0..n)) back to a free stack, wave-collective
+__device__ __forceinline__ void push_pages(int32_t *stack, int32_t *top, int cap, const int32_t *src, int n) {
+    if (n <= 0) return;
+    int base = 0;
+    if (lane_id() == 0) base = atomicAdd(top, n);
+    base = __shfl(base, 0, 64);
+    for (int i = lane_id(); i < n; i += 64)
+        if (base + i < cap) stack[base + i] = src[i];    // (never false: a page is pushed once)
+}
+
 // ------------------------------------------------------------ garbage collection
 // Keep the root and every node whose round counter exceeds the root's: rounds strictly
 // increase along every move (SplendorLogicNumba.py:287), so no other node is reachable from
 // this root or any later one — an exact subset of the reference's table (which only
-// evicts rounds < R-5, MCTS.py:80-85). Compacts nodes + CSR edges in place, remaps child
-// links, rebuilds the hash table. Wave-collective; returns the root's new index.
+// evicts rounds < R-5, MCTS.py:80-85). Compacts the tree's nodes and CSR edges in place (in
+// its own page order), remaps child links and their cached ranges, rebuilds the
+// transposition table and returns the pages it no longer needs to the pools.
 // linked = true (capacity pressure, see begin_search): keep only the root and the nodes
-// reachable from it through child links (mark_linked), dropping nodes that only a
-// transposition lookup could reach.
-// scr: scratch of 2 x sstride ints (sstride >= ncap + 1; LDS when ncap <= SCR_NODES): the
-// edges then move in batches of 256 new positions (each lane finds its edge's owner by a
-// binary search over the kept nodes' new bases) instead of one kept node at a time.
-constexpr int SCR_NODES = 512;
+// reachable from it through child links, dropping nodes that only a transposition lookup
+// could reach. Wave-collective; runs in k_gc (one wave per tree) with a scratch area of
+// gc_ints(nmax) ints.
+struct GcScr {
+    int32_t *remap;     // old local -> new local (-1: dropped); prune: reachability marks first
+    int32_t *nvs;       // old local -> new local edge position of its CSR run
+    int32_t *cs;        // new local -> new edge position (non-decreasing, + sentinel)
+    int32_t *cnt;       // new local -> edge count
+    int32_t *inv;       // new local -> old local
+    int32_t *queue;     // prune: breadth-first queue (old locals)
+    int64_t *ost;       // new local -> old global edge base
+};
+__host__ __device__ inline size_t gc_ints(int nmax) { return 8 * (size_t)(nmax + 2) + 64; }
+__device__ __forceinline__ GcScr gc_scr(int32_t *base, int nmax) {
+    const size_t m = (size_t)nmax + 2;
+    GcScr S;
+    S.ost = reinterpret_cast<int64_t *>(base);                 // 2m ints, 8-byte aligned
+    S.remap = base + 2 * m; S.nvs = S.remap + m; S.cs = S.nvs + m; S.cnt = S.cs + m;
+    S.inv = S.cnt + m; S.queue = S.inv + m;
+    return S;
+}
 
-// remap[i] = 1 for the root and every node reachable from it through child links, 0 else
-// (breadth-first, the wave walks one node's edges at a time; remap_eb is the queue).
-__device__ void mark_linked(const Pools &P, int t, int root, int32_t *mark, int32_t *q) {
+// mark[i] = 1 for the root (local rootl) and every node reachable from it through child
+// links, 0 else (breadth-first in batches of up to 64 queued nodes, their edges 64 at a time)
+__device__ void mark_linked(const Pools &P, int t, int rootl, int32_t *mark, int32_t *q) {
     const int l = lane_id();
-    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const int nc = P.hdr[t].node_count;
-    for (int i = l; i < nc; i += 64) mark[i] = i == root ? 1 : 0;
-    if (l == 0) q[0] = root;
+    for (int i = l; i < nc; i += 64) mark[i] = i == rootl ? 1 : 0;
+    if (l == 0) q[0] = rootl;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    // breadth-first in batches of up to 64 queued nodes (lane per node), their edges 64 at a
-    // time (lane per edge, owner found by a binary search over the batch's edge offsets):
-    // a round trip per batch and per 64 edges, not per node
     int head = 0, tail = 1;
     while (head < tail) {
         const int nbt = min(64, tail - head);
-        int eb = 0, ec = 0;
+        int64_t eb = 0;
+        int ec = 0;
         if (l < nbt) {
-            const int node = q[head + l];
-            eb = P.neb[nb + node];
-            ec = P.nterm[nb + node] ? 0 : P.nec[nb + node];
+            const int g = node_g(P, t, q[head + l]);
+            eb = P.neb[g];
+            ec = P.nterm[g] ? 0 : P.nec[g];
         }
         head += nbt;
         int incl = ec;
@@ -362,11 +441,13 @@ __device__ void mark_linked(const Pools &P, int t, int root, int32_t *mark, int3
 #pragma unroll
             for (int step = 32; step > 0; step >>= 1)
                 if (__shfl(excl, lo + step, 64) <= e) lo += step;
-            const int ebo = __shfl(eb, lo, 64), exo = __shfl(excl, lo, 64);
-            const int c = e < tot ? P.ed[e0 + ebo + (e - exo)].k.child : -1;
-            const bool fresh = c >= 0 && atomicCAS(&mark[c], 0, 1) == 0;
+            const int64_t ebo = __shfl(eb, lo, 64);
+            const int exo = __shfl(excl, lo, 64);
+            const int c = e < tot ? P.ed[ebo + (e - exo)].k.child : -1;
+            const int cl = c >= 0 ? node_l(P, c) : -1;
+            const bool fresh = cl >= 0 && atomicCAS(&mark[cl], 0, 1) == 0;
             const uint64_t bm = __ballot(fresh);
-            if (fresh) q[tail + __popcll(bm & lanemask_lt())] = c;
+            if (fresh) q[tail + __popcll(bm & lanemask_lt())] = cl;
             tail += __popcll(bm);
             __threadfence_block();
             __builtin_amdgcn_wave_barrier();
@@ -376,122 +457,152 @@ __device__ void mark_linked(const Pools &P, int t, int root, int32_t *mark, int3
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 struct defeats SROA)
 template <int CR = 4>   // edges per lane per round trip of the edge move (boards: 2 CR units)
-__device__ int compact_tree(const Pools &P, int t, int root, int root_round, int *scr, int sstride,
-                            int bunits, bool linked = false, int32_t *lmark = nullptr) {
+__device__ int compact_tree(const Pools &P, int t, int root, int root_round, const GcScr &S, int bunits,
+                            bool linked = false) {
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
-    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const int nc = H->node_count;
-    int32_t *remap = P.remap + nb;
-    // linked (prune): marks of the nodes reachable from the root — in lmark[0, ncap) with
-    // the BFS queue behind it (LDS, k_gc), or in remap itself with remap_eb as the queue
-    int32_t *mark = lmark ? lmark : remap;
-    if (linked) mark_linked(P, t, root, mark, lmark ? lmark + P.ncap : P.remap_eb + nb);
+    const int rootl = root >= 0 ? node_l(P, root) : -1;
+    int32_t *remap = S.remap;
+    if (linked) mark_linked(P, t, rootl, remap, S.queue);
     int kept = 0;
     for (int base = 0; base < nc; base += 64) {
         const int i = base + l;
-        const bool keep = i < nc && (i == root || (linked ? mark[i] == 1 : P.nround[nb + i] > root_round));
+        bool keep = false;
+        if (i < nc) keep = i == rootl || (linked ? remap[i] == 1 : P.nround[node_g(P, t, i)] > root_round);
         const uint64_t b = __ballot(keep);
         if (i < nc) remap[i] = keep ? kept + __popcll(b & lanemask_lt()) : -1;
         kept += __popcll(b);
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    // new CSR base of every kept node (old index -> base), so moved edges can re-point
-    // their cached child record before the child itself has moved
-    int32_t *remap_eb = P.remap_eb + nb;
-    {
-        int run = 0;
-        for (int base = 0; base < nc; base += 64) {
-            const int i = base + l;
-            const int x = i < nc && remap[i] >= 0 ? P.nec[nb + i] : 0;
+    // new edge position of every kept node's CSR run: packed in local order, a run that would
+    // straddle an edge page starts the next page (the lanes before the first straddler of a
+    // batch are placed, the rest retried from that page's start). Positions never exceed the
+    // old ones, so the in-place moves below read every record before it is overwritten.
+    int run = 0;
+    for (int base = 0; base < nc; base += 64) {
+        const int i = base + l;
+        int ec = 0;
+        if (i < nc && remap[i] >= 0) {
+            const int g = node_g(P, t, i);
+            ec = P.nterm[g] ? 0 : P.nec[g];
+        }
+        bool pending = ec > 0;
+        int start = 0;
+        const int run0 = run;
+        for (;;) {
+            const int x = pending ? ec : 0;
             int incl = x;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
-                int y = __shfl_up(incl, o, 64);
+                const int y = __shfl_up(incl, o, 64);
                 if (l >= o) incl += y;
             }
-            if (i < nc) remap_eb[i] = run + incl - x;
-            run += __shfl(incl, 63, 64);
+            const int st = run + incl - x;
+            const bool strad = pending && (st & (EPG - 1)) + ec > EPG;
+            const uint64_t sb = __ballot(strad);
+            if (!sb) {
+                if (pending) start = st;
+                run += __shfl(incl, 63, 64);
+                break;
+            }
+            const int f = __ffsll((unsigned long long)sb) - 1;
+            if (pending && l < f) { start = st; pending = false; }
+            run = (__shfl(st, f, 64) & ~(EPG - 1)) + EPG;
         }
+        // edge-less nodes take the end of the runs before them (keeps positions sorted)
+        int end = ec > 0 ? start + ec : run0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(end, o, 64);
+            if (l >= o) end = max(end, y);
+        }
+        if (i < nc && remap[i] >= 0) S.nvs[i] = ec > 0 ? start : end;
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
+    // node records, in local order (new slot <= old slot)
     int edges = 0;
     for (int base = 0; base < nc; base += 64) {
         const int i = base + l;
-        const bool valid = i < nc;
-        const int ni = valid ? remap[i] : -1;
+        const int ni = i < nc ? remap[i] : -1;
         uint64_t k0 = 0, k1 = 0;
-        int oeb = 0, ec = 0, ns = 0, rd = 0;
+        int64_t oeb = 0;
+        int ec = 0, ns = 0, rd = 0, vs = 0;
         double qs = 0;
         int8_t term = 0;
         float es[4] = {0, 0, 0, 0};
         if (ni >= 0) {
-            k0 = P.nkey0[nb + i]; k1 = P.nkey1[nb + i];
-            oeb = P.neb[nb + i]; ec = P.nec[nb + i]; ns = P.nst[nb + i].ns; rd = P.nround[nb + i];
-            qs = P.nst[nb + i].qs; term = P.nterm[nb + i];
+            const int g = node_g(P, t, i);
+            k0 = P.nkey0[g]; k1 = P.nkey1[g];
+            oeb = P.neb[g]; ec = P.nec[g]; ns = P.nst[g].ns; rd = P.nround[g];
+            qs = P.nst[g].qs; term = P.nterm[g];
 #pragma unroll
-            for (int j = 0; j < 4; j++) es[j] = P.nes[(nb + i) * 4 + j];
+            for (int j = 0; j < 4; j++) es[j] = P.nes[(size_t)g * 4 + j];
+            vs = S.nvs[i];
         }
-        // exclusive scan of kept edge counts -> new edge base
-        int x = ni >= 0 ? ec : 0, incl = x;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            int y = __shfl_up(incl, o, 64);
-            if (l >= o) incl += y;
-        }
-        const int neb = edges + incl - x;
-        const int total = __shfl(incl, 63, 64);
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         if (ni >= 0) {
-            P.nkey0[nb + ni] = k0; P.nkey1[nb + ni] = k1;
-            P.neb[nb + ni] = neb; P.nec[nb + ni] = ec; P.nst[nb + ni].ns = ns; P.nround[nb + ni] = rd;
-            P.nst[nb + ni].qs = qs; P.nterm[nb + ni] = term;
+            const int ng = node_g(P, t, ni);
+            const int run_ec = term ? 0 : ec;
+            P.nkey0[ng] = k0; P.nkey1[ng] = k1;
+            P.neb[ng] = run_ec > 0 ? edge_g(P, t, vs) : 0; P.nec[ng] = ec; P.nst[ng].ns = ns; P.nround[ng] = rd;
+            P.nst[ng].qs = qs; P.nterm[ng] = term;
 #pragma unroll
-            for (int j = 0; j < 4; j++) P.nes[(nb + ni) * 4 + j] = es[j];
-            scr[ni] = neb; scr[sstride + ni] = oeb;
+            for (int j = 0; j < 4; j++) P.nes[(size_t)ng * 4 + j] = es[j];
+            S.cs[ni] = vs; S.cnt[ni] = run_ec; S.inv[ni] = i; S.ost[ni] = oeb;
         }
-        edges += total;                                  // edges move in batches below
+        int x = ni >= 0 && !term ? ec : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        edges += x;
     }
+    if (l == 0) S.cs[kept] = run;
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
     {
-        // new position k of batch [k0, k0 + 256) comes from old position oeb(j) + k - neb(j),
-        // j = the kept node whose new range holds k. Every old position is >= its new one
-        // and batches run in increasing k with all reads before the writes, so no write
-        // reaches an edge that is still to be read.
-        if (l == 0) scr[kept] = edges;
-        __threadfence_block();                          // (scr may be global memory)
-        __builtin_amdgcn_wave_barrier();
-        for (int k0 = 0; k0 < edges; k0 += 64 * CR) {
-            // an edge as two uint4 (register arrays: a struct array here lands in scratch);
-            // link word y = child, z = cached child CSR base
+        // edge records by new position k (batches of 64 CR in increasing k, all reads before
+        // the writes): owner j = the last kept node with cs[j] <= k; positions in the gaps
+        // before a page start have no owner
+        u32x4 *const ed4 = reinterpret_cast<u32x4 *>(P.ed);
+        for (int k0 = 0; k0 < run; k0 += 64 * CR) {
             u32x4 es_[CR], ek_[CR];
-            int nch[CR], ceb[CR];
-            u32x4 *const ed4 = reinterpret_cast<u32x4 *>(P.ed + e0);
+            int cl[CR];
+            bool own[CR];
 #pragma unroll
             for (int r = 0; r < CR; r++) {
                 const int k = k0 + 64 * r + l;
-                nch[r] = -1; ceb[r] = 0;
+                own[r] = false; cl[r] = -1;
                 es_[r] = u32x4{0, 0, 0, 0}; ek_[r] = u32x4{0, 0xFFFFFFFFu, 0, 0};
-                if (k < edges) {
-                    int lo = 0, hi = kept - 1;                 // last j with scr[j] <= k
+                if (k < run) {
+                    int lo = 0, hi = kept - 1;                 // last j with cs[j] <= k
                     while (lo < hi) {
                         const int mid = (lo + hi + 1) >> 1;
-                        if (scr[mid] <= k) lo = mid; else hi = mid - 1;
+                        if (S.cs[mid] <= k) lo = mid; else hi = mid - 1;
                     }
-                    const int src = scr[sstride + lo] + (k - scr[lo]);
-                    es_[r] = ed4[2 * src];
-                    ek_[r] = ed4[2 * src + 1];
+                    if (k - S.cs[lo] < S.cnt[lo]) {
+                        own[r] = true;
+                        const int64_t src = S.ost[lo] + (k - S.cs[lo]);
+                        es_[r] = ed4[2 * src];
+                        ek_[r] = ed4[2 * src + 1];
+                    }
                 }
             }
 #pragma unroll
             for (int r = 0; r < CR; r++) {
-                const int k = k0 + 64 * r + l;
                 const int ch = (int)ek_[r].y;
-                if (k < edges && ch >= 0) {
-                    nch[r] = remap[ch];
-                    ceb[r] = remap_eb[ch];
+                if (own[r] && ch >= 0) cl[r] = node_l(P, ch);
+            }
+            int nch[CR];
+            int64_t ceb[CR];
+#pragma unroll
+            for (int r = 0; r < CR; r++) {
+                nch[r] = -1; ceb[r] = 0;
+                if (cl[r] >= 0) {
+                    const int nl = remap[cl[r]];
+                    if (nl >= 0) { nch[r] = node_g(P, t, nl); ceb[r] = S.cnt[nl] > 0 ? edge_g(P, t, S.cs[nl]) : 0; }
                 }
             }
             __threadfence_block();
@@ -499,12 +610,13 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
 #pragma unroll
             for (int r = 0; r < CR; r++) {
                 const int k = k0 + 64 * r + l;
-                if (k < edges) {
+                if (own[r]) {
                     u32x4 o = ek_[r];
                     o.y = (uint32_t)nch[r];
-                    if (nch[r] >= 0) o.z = (uint32_t)ceb[r];
-                    ed4[2 * k] = es_[r];
-                    ed4[2 * k + 1] = o;
+                    if (nch[r] >= 0) { o.z = (uint32_t)(uint64_t)ceb[r]; o.w = (uint32_t)((uint64_t)ceb[r] >> 32); }
+                    const int64_t dst = edge_g(P, t, k);
+                    ed4[2 * dst] = es_[r];
+                    ed4[2 * dst + 1] = o;
                 }
             }
             __threadfence_block();
@@ -512,36 +624,33 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
         }
     }
     if (P.nbrd) {
-        // node boards (bunits 16-byte units each) move the same way: unit k of the kept
-        // boards comes from unit k + bunits * (old - new), old = scr[new] >= new,
-        // batches run in increasing k with all reads before the writes
-        for (int i = l; i < nc; i += 64)
-            if (remap[i] >= 0) scr[remap[i]] = i;
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        u32x4 *bb = reinterpret_cast<u32x4 *>(P.nbrd) + nb * bunits;
+        // node boards (bunits 16-byte units each) of new slot nn come from old slot inv[nn]
+        // (>= nn), batches in increasing unit with all reads before the writes
+        u32x4 *bb = reinterpret_cast<u32x4 *>(P.nbrd);
         const int units = kept * bunits;
         constexpr int R = 2 * CR;
         for (int k0 = 0; k0 < units; k0 += 64 * R) {
             u32x4 d[R];
-            int src[R];
+            size_t dst[R];
+            bool mv[R];
 #pragma unroll
             for (int r = 0; r < R; r++) {
                 const int k = k0 + 64 * r + l;
-                src[r] = k;
+                mv[r] = false; dst[r] = 0; d[r] = u32x4{0, 0, 0, 0};
                 if (k < units) {
-                    const int nn = k / bunits;
-                    src[r] = k + bunits * (scr[nn] - nn);
+                    const int nn = k / bunits, u = k - nn * bunits, on = S.inv[nn];
+                    if (on != nn) {
+                        mv[r] = true;
+                        dst[r] = (size_t)node_g(P, t, nn) * bunits + u;
+                        d[r] = bb[(size_t)node_g(P, t, on) * bunits + u];
+                    }
                 }
-                d[r] = bb[k < units ? src[r] : 0];   // (unconditional: keeps d in registers)
             }
             __threadfence_block();
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int k = k0 + 64 * r + l;
-                if (k < units && src[r] != k) bb[k] = d[r];
-            }
+            for (int r = 0; r < R; r++)
+                if (mv[r]) bb[dst[r]] = d[r];
             __threadfence_block();
             __builtin_amdgcn_wave_barrier();
         }
@@ -552,46 +661,81 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, int
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     for (int i = l; i < kept; i += 64) {
-        const uint64_t k0 = P.nkey0[nb + i];
+        const int g = node_g(P, t, i);
+        const uint64_t k0 = P.nkey0[g];
         uint32_t h = (uint32_t)(k0 ^ (k0 >> 32)) & (uint32_t)(P.hcap - 1);
-        while (atomicCAS(&hs[h], -1, i) != -1) h = (h + 1) & (uint32_t)(P.hcap - 1);
+        while (atomicCAS(&hs[h], -1, g) != -1) h = (h + 1) & (uint32_t)(P.hcap - 1);
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const int nroot = root >= 0 ? remap[root] : -1;
-    if (l == 0) { H->node_count = kept; H->edge_count = edges; }
+    // pages past the compacted tree go back to the pools
+    const int npg = (kept + NPG - 1) >> NPG_SHIFT, epg = (run + EPG - 1) >> EPG_SHIFT;
+    const int onpg = H->npg, oepg = H->epg;
+    push_pages(P.nfree, P.alloc + 0, P.npages, P.ntab + (size_t)t * P.nptab + npg, onpg - npg);
+    push_pages(P.efree, P.alloc + 1, P.epages, P.etab + (size_t)t * P.eptab + epg, oepg - epg);
+    const int nroot = rootl >= 0 && remap[rootl] >= 0 ? node_g(P, t, remap[rootl]) : -1;
+    const int eleft = epg * EPG - run;
+    const int64_t enext = eleft > 0 ? edge_g(P, t, run) : 0;
+    __builtin_amdgcn_wave_barrier();
+    if (l == 0) {
+        H->node_count = kept; H->edge_count = edges;
+        H->npg = npg; H->epg = epg; H->eleft = eleft; H->enext = enext;
+        H->live_gc = kept; H->gcs += 1;
+    }
     __builtin_amdgcn_wave_barrier();
     return nroot;
 }
 
-// does the next search fit tree t's pools (budget nodes, 409 root edges, edge_reserve per
-// simulation)
+// does the next search fit tree t's maxima (budget nodes; 409 root edges plus edge_reserve
+// per simulation, in edge positions counting the tail of the current page)
 __device__ __forceinline__ bool tree_fits(const Pools &P, const SearchCfg &C, const TreeHdr *H) {
-    return H->node_count + H->budget + 1 <= P.ncap &&
-           (long long)H->edge_count + SPL_ACTIONS + (long long)H->budget * C.edge_reserve <= (long long)P.ecap;
+    const long long used = (long long)H->epg * EPG - H->eleft;
+    return H->node_count + H->budget + 1 <= P.nmax &&
+           used + SPL_ACTIONS + (long long)H->budget * C.edge_reserve <= (long long)P.eptab * EPG;
 }
-__device__ __forceinline__ void empty_tree(const Pools &P, int t) {
+// every page of tree t back to the pools, empty table. Wave-collective.
+__device__ void empty_tree(const Pools &P, int t) {
+    TreeHdr *H = P.hdr + t;
+    const int npg = H->npg, epg = H->epg;
+    push_pages(P.nfree, P.alloc + 0, P.npages, P.ntab + (size_t)t * P.nptab, npg);
+    push_pages(P.efree, P.alloc + 1, P.epages, P.etab + (size_t)t * P.eptab, epg);
     int32_t *hs = P.hslot + (size_t)t * P.hcap;
-    for (int i = lane_id(); i < P.hcap; i += 64) hs[i] = -1;
-    if (lane_id() == 0) { P.hdr[t].node_count = 0; P.hdr[t].edge_count = 0; }
+    if (H->node_count > 0 || npg > 0)
+        for (int i = lane_id(); i < P.hcap; i += 64) hs[i] = -1;
+    __builtin_amdgcn_wave_barrier();
+    if (lane_id() == 0) {
+        H->node_count = 0; H->edge_count = 0; H->npg = 0; H->epg = 0; H->eleft = 0; H->enext = 0;
+        H->live_gc = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
 }
-// queue tree t for k_gc (lane 0)
-__device__ __forceinline__ void gc_push(const Pools &P, int t) {
+// queue tree t for k_gc (one lane); at most one entry per tree (gc_queued), so the queue
+// of B entries cannot overflow
+__device__ __forceinline__ void gc_push(const Pools &P, TreeHdr *H, int t) {
+    if (H->gc_queued) return;
+    H->gc_queued = 1;
     const int k = atomicAdd(&P.counters[2], 1);
     P.gcq[k] = t;
 }
 
 // ------------------------------------------------------------ search start
 // Re-root tree t at the canonical board staged in LDS `s` (MCTS.getActionProb entry,
-// :45-56): look the root up in the persistent table (keep) and collect garbage, or start
-// empty; draw the full/fast search decision (ST_FULL) and arm root noise. Wave-collective.
-// Capacity: a search adds at most `budget` nodes; when the kept tree plus that (and 409
-// edges for the root plus edge_reserve per simulation) does not fit the tree's pool, the tree is pruned to
-// the nodes linked from the root (prunes++), and emptied if that is still too large
-// (resets++). Without such an event the kept tree is exactly the reference's reachable table.
+// :45-56): look the root up in the persistent table (keep) or start empty; draw the
+// full/fast search decision (ST_FULL) and arm root noise. Wave-collective.
+// Garbage (nodes with rounds <= the root's: unreachable, and no lookup can match them) is
+// collected by k_gc, queued here:
+//   must (gc_state 3): the search would not fit the tree's maxima (node slots, edge page
+//     table), or the arena has no self-play commit (search-only arenas never withdraw a
+//     simulation, so every search starts compacted); after compaction k_gc prunes the tree
+//     to the nodes linked from the root (prunes++) and empties it if that is still too
+//     large (resets++);
+//   should (gc_state 5): a tree holding more than twice its live size (amortised: each
+//     collection copies at most as many nodes as were added since the last), or any tree
+//     with garbage while the shared pools run low; k_gc may defer these (GC_SHOULD_CAP).
+// Without an event the kept table is exactly the reference's reachable table.
 template <int N>
 __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const int8_t *s, bool keep,
-                             bool force_full, int *scr = nullptr, bool defer = false) {
+                             bool force_full) {
     using Lx = Lay<N>;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
@@ -599,50 +743,29 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
     const int mv = H->move_no;
     const bool full = force_full || philox_u01(C.seed, C.board_base + t, ST_FULL | (uint32_t)mv, 0) < C.prob_full;
     const int budget = full ? C.num_sims : C.num_sims / C.ratio_full;
-    int root = -1, rr = 0;
-    bool empty = true, deferred = false;
+    int root = -1, gcs = 0;
+    const int rr = (uint8_t)bt(row(s, 0), 6);
     if (keep && H->node_count > 0) {
         uint64_t k0, k1;
         wave_fingerprint<N>(s, k0, k1);
         root = hash_lookup(P, t, k0, k1);
-        const auto fits = [&]() {
-            return H->node_count + budget + 1 <= P.ncap &&
-                   (long long)H->edge_count + SPL_ACTIONS + (long long)budget * C.edge_reserve <= (long long)P.ecap;
-        };
-        // lazy garbage collection (self-play): nodes with rounds <= the root's are
-        // unreachable (and no lookup can match them), so they are only compacted away when
-        // the search would not fit otherwise, or when a leaf does not fit mid-search
-        // (k_backup withdraws the simulation, k_commit collects) — the search sees the same
-        // reachable table either way. Without k_commit (search-only arenas) every search
-        // starts on a compacted tree.
-        if (!C.selfplay || !fits()) {
-            rr = (uint8_t)bt(row(s, 0), 6);
-            if (defer && C.selfplay) {
-                deferred = true;                         // k_gc collects (same result)
-            } else {
-                // edge-move scratch: LDS for small trees, the tree's global scratch otherwise
-                int *cs = P.ncap <= SCR_NODES && scr ? scr : P.cscr + (size_t)t * 2 * (P.ncap + 1);
-                const int cstride = P.ncap <= SCR_NODES && scr ? SCR_NODES + 1 : P.ncap + 1;
-                root = compact_tree(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS);
-                if (!fits() && root >= 0) {
-                    root = compact_tree(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS, true);
-                    if (l == 0) H->prunes += 1;
-                }
-            }
-        }
-        empty = !deferred && !fits();
-        if (empty && l == 0) H->resets += 1;
-    }
-    if (empty) {
-        root = -1;
+        const int nc = H->node_count;
+        const long long used = (long long)H->epg * EPG - H->eleft;
+        const bool must = nc + budget + 1 > P.nmax ||
+                          used + SPL_ACTIONS + (long long)budget * C.edge_reserve > (long long)P.eptab * EPG;
+        const bool pressure = P.alloc[0] < P.low_n || P.alloc[1] < P.low_e;
+        const bool should = nc > 2 * H->live_gc + budget + NPG || (pressure && nc > H->live_gc + budget);
+        gcs = must || !C.selfplay ? 3 : (should ? 5 : 0);   // search-only arenas: every search
+                                                           // starts compacted (no withdrawals there)
+    } else {
         empty_tree(P, t);
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const int reb = root >= 0 && !deferred ? P.neb[(size_t)t * P.ncap + root] : 0;
-    const int rec = root >= 0 && !deferred ? P.nec[(size_t)t * P.ncap + root] : 0;
+    const int64_t reb = root >= 0 ? P.neb[root] : 0;
+    const int rec = root >= 0 ? P.nec[root] : 0;
     if (l == 0) {
-        H->root = root;                                  // (deferred: the pre-GC index)
+        H->root = root;                                  // (a queued GC moves it)
         H->root_eb = reb;
         H->root_ec = rec;
         H->sims_done = 0;
@@ -652,49 +775,48 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         H->noise_pending = full && C.dirichlet;
         H->leaf_kind = LEAF_NONE;
         H->overflow = 0;
-        H->gc_state = deferred ? 3 : 0;
-        H->pad1 = rr;                                    // root round, for a deferred GC
+        H->gc_state = gcs;
+        H->root_round = rr;
         H->move_no = mv + 1;
-        if (deferred) gc_push(P, t);
+        if (gcs) gc_push(P, H, t);
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
 }
 
-// Garbage collection queued by k_backup (a leaf did not fit mid-search: gc_state 1) and
-// by k_commit's search starts (gc_state 3), one wave per queued tree. Off k_commit, whose
-// other 31,000-odd waves per launch exit at once: it keeps k_commit's registers low, and
-// GC's own registers go to more loads in flight. Exactly begin_search's policy: compact
-// (rounds > the root's), prune to the linked nodes, empty.
-template <int N, bool LDSW>
+// Garbage collection queued by k_backup (a leaf did not fit mid-search: gc_state 1) and by
+// search starts (3 must, 5 should), one wave per queued tree, GC_WG single-wave workgroups
+// sharing the queue (a workgroup's scratch: gc_ints(nmax) ints of P.gscr). Exactly
+// begin_search's policy: compact (rounds > the root's), prune to the linked nodes, empty.
+// Queued trees come in bursts (games start together, so trees fill up together): entries
+// past GC_SHOULD_CAP that only "should" be collected are skipped this time (their search
+// fits; the next search start queues them again), so no launch carries a whole burst.
+constexpr int GC_WG = 1024;
+#ifndef GC_SHOULD_CAP
+#define GC_SHOULD_CAP 1024
+#endif
+template <int N>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_gc(Pools P, SearchCfg C) {
-    constexpr bool lds_ok = LDSW;
-    // lds_ok: the edge-move scratch (2 (ncap + 1) ints) and the prune's marks + queue
-    // (2 ncap ints) in dynamic LDS — the binary searches of the edge move and the BFS then
-    // run on LDS instead of dependent HBM round trips
-    extern __shared__ int gsm[];
     const int l = lane_id();
     const int tail = P.counters[2];                      // no pushes while k_gc runs
     const int ftail = P.counters[5];
     if (tail == 0 && ftail == 0) return;                 // (the usual case)
-    // queued trees come in bursts (games start together, so trees fill up together):
-    // workgroup i takes queue entries i, i + G, ...
+    const GcScr S = gc_scr(P.gscr + (size_t)blockIdx.x * P.gc_stride, P.nmax);
     for (int k = blockIdx.x; k < tail; k += gridDim.x) {     // garbage collection
         const int t = uniform(P.gcq[k]);
         TreeHdr *H = P.hdr + t;
-        const size_t nb = (size_t)t * P.ncap;
-        int *cs = lds_ok ? gsm : P.cscr + (size_t)t * 2 * (P.ncap + 1);
-        const int cstride = P.ncap + 1;
-        int32_t *lm = lds_ok ? gsm + 2 * (P.ncap + 1) : nullptr;
         const int st = H->gc_state;
         int root = H->root;
-        if (st == 1) {                                   // the descent then repeats
-            root = compact_tree<8>(P, t, root, P.nround[nb + root], cs, cstride, NodeBoard<N>::UNITS);
-        } else if (st == 3) {
-            const int rr = H->pad1;
-            root = compact_tree<8>(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS);
+        int nst = st == 1 ? 2 : 0;
+        if (st == 5 && k >= GC_SHOULD_CAP) {
+            // deferred (its search fits as it is)
+        } else if (st == 1) {                            // the descent then repeats
+            root = compact_tree<8>(P, t, root, P.nround[root], S, NodeBoard<N>::UNITS);
+        } else if (st == 3 || st == 5) {
+            const int rr = H->root_round;
+            root = compact_tree<8>(P, t, root, rr, S, NodeBoard<N>::UNITS);
             if (!tree_fits(P, C, H) && root >= 0) {
-                root = compact_tree<8>(P, t, root, rr, cs, cstride, NodeBoard<N>::UNITS, true, lm);
+                root = compact_tree<8>(P, t, root, rr, S, NodeBoard<N>::UNITS, true);
                 if (l == 0) H->prunes += 1;
             }
             if (!tree_fits(P, C, H)) {
@@ -705,13 +827,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         }
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
-        const int reb = root >= 0 ? P.neb[nb + root] : 0;
-        const int rec = root >= 0 ? P.nec[nb + root] : 0;
+        const int64_t reb = root >= 0 ? P.neb[root] : 0;
+        const int rec = root >= 0 ? P.nec[root] : 0;
         if (l == 0) {
             H->root = root;
             H->root_eb = reb;
             H->root_ec = rec;
-            H->gc_state = st == 1 ? 2 : 0;               // (2: once per search)
+            H->gc_state = nst;                           // (2: once per search)
+            H->gc_queued = 0;
         }
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
@@ -746,7 +869,6 @@ __global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int
                                                        int force_full) {
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
-    __shared__ int cscr[WAVES][2 * (SCR_NODES + 1)];     // compaction scratch
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     if (active && !active[t]) {
@@ -758,7 +880,7 @@ __global__ __launch_bounds__(THREADS) void k_set_roots(Pools P, SearchCfg C, int
     }
     int8_t *s = lds[w];
     wave_load_board<N>(s, roots + (size_t)t * Lx::S);
-    begin_search<N>(P, C, t, s, keep != 0, force_full != 0, cscr[w]);
+    begin_search<N>(P, C, t, s, keep != 0, force_full != 0);
 }
 
 // ------------------------------------------------------------ self-play
@@ -818,12 +940,11 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     // (a tree whose leaf did not fit waits for k_gc: its simulation was withdrawn, so its
     // search is not done)
     if (H->gc_state == 1 || H->sims_done < H->budget || H->overflow || H->root < 0) return;
-    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const uint32_t gb = C.board_base + (uint32_t)t;
-    const int root = H->root, eb = P.neb[nb + root], ec = P.nec[nb + root];
+    const int root = H->root, ec = P.nec[root];
     const bool forced = H->forced;
     const int sims = H->budget, cm = H->move_no;
-    const Edge *ede = P.ed + e0 + eb;
+    const Edge *ede = P.ed + P.neb[root];
     int best = 0;
     for (int i = l; i < ec; i += 64) best = max(best, ede[i].s.n);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
@@ -858,7 +979,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         wave_valid_moves<N>(s, 0, lim, m);
         store_mask(P.ex_valid + x * 7, m);
         if (l == 0) {
-            const double q0 = P.nst[nb + root].qs;
+            const double q0 = P.nst[root].qs;
             P.ex_player[x] = player;
             for (int i = 0; i < 4; i++)
                 P.ex_q[x * 4 + i] = i == 0 ? (float)q0 : (i < N ? (float)(-q0 / (double)(N - 1)) : 0.f);
@@ -901,7 +1022,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     bool ended = false;
 #pragma unroll
     for (int i = 0; i < N; i++) ended |= r[i] != 0.f;
-    if (l == 0) { H->n_examples = nex; H->pad0 += 1; }      // pad0 = moves played
+    if (l == 0) { H->n_examples = nex; H->moves += 1; }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     if (ended) {                                            // Coach.py:89-98
@@ -954,7 +1075,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     __builtin_amdgcn_wave_barrier();
     wave_store_board<N>(P.board + (size_t)t * Lx::S, b);
     wave_roll_players<N>(s, b, nxt);                            // getCanonicalForm (:73)
-    begin_search<N>(P, C, t, s, !ended, false, nullptr, true);
+    begin_search<N>(P, C, t, s, !ended, false);
 }
 
 // flat copy of `bytes` bytes (16-byte vectors when both ends allow it), grid-stride
@@ -1024,8 +1145,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         spl_probe_last = clock64();
     }
 #endif
-    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
-    int32_t *path = P.path + (size_t)t * P.pcap * 2;
+    int32_t *path_n = P.path_n + (size_t)t * P.pcap;
+    int64_t *path_e = P.path_e + (size_t)t * P.pcap;
     SPL_PROBE(0)
     int node = H->root, depth = 0, kind = LEAF_NN;
     uint64_t k0 = 0, k1 = 0;
@@ -1039,7 +1160,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         // CSR range of the current node: the root's from the header, every child's from the
         // {eb, ec} cached on the edge that led to it, so a level costs ONE round trip (the
         // node's visit stats travel with its edges); ec < 0 marks a terminal child
-        int eb = H->root_eb, ec = H->root_ec;
+        int64_t eb = H->root_eb;
+        int ec = H->root_ec;
         if (sims == 0 && H->noise_pending) {
             apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no, lpr[w], false);
             if (l == 0) H->noise_pending = 0;           // (a withdrawn simulation must not re-noise)
@@ -1048,11 +1170,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         // node_boards: a linked child's board is stored, so the descent follows links without
         // the in-tree transition and stages a board only where it needs one (the edge to
         // expand); `bnode` is the node whose board is in LDS (the root's, from root_state)
-        const uint64_t *nbrd = P.nbrd ? reinterpret_cast<const uint64_t *>(P.nbrd + nb * NodeBoard<N>::BYTES) : nullptr;
+        const uint64_t *nbrd = reinterpret_cast<const uint64_t *>(P.nbrd);
         int bnode = node;
-        // per-tree bases and search constants of the hot loop, set up once
-        const Edge *ed_t = P.ed + e0;
-        const NodeStat *nst_t = P.nst + nb;
+        // pool bases and search constants of the hot loop, set up once
+        const Edge *ed_t = P.ed;
+        const NodeStat *nst_t = P.nst;
         const double cpuct = C.cpuct, fpu = C.fpu;
         const float cf = (float)C.cpuct;
         for (;;) {
@@ -1060,7 +1182,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             if (depth > 0 && ec < 0) {
                 kind = LEAF_TERMINAL;
 #pragma unroll
-                for (int i = 0; i < 4; i++) val[i] = P.nes[(nb + node) * 4 + i];
+                for (int i = 0; i < 4; i++) val[i] = P.nes[(size_t)node * 4 + i];
                 break;
             }
             if (depth >= P.pcap) { kind = LEAF_NONE; if (l == 0) H->overflow = 2; break; }
@@ -1072,26 +1194,27 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             const double qs = nsq.qs;
             const Pick pk = ec <= 64 && !(forced && depth == 0)
                                 ? pick_edge64(e64, cpuct, fpu, cf, ec, ns, qs)
-                                : pick_edge_desc(P, C, t, eb, ec, ns, qs, forced && depth == 0, sims, e64);
-            const int ge = eb + pk.e;
+                                : pick_edge_desc(P, C, eb, ec, ns, qs, forced && depth == 0, sims, e64);
+            const int64_t ge = eb + pk.e;
 #if MCTS_TIMING
             if (threadIdx.x == 0) {
                 spl_probe_acc[23] += 1;                  // levels
                 if (prefix_run) {                        // levels that repeat the previous path
-                    if (path[2 * depth] == node && path[2 * depth + 1] == ge) spl_probe_acc[22] += 1;
+                    if (path_n[depth] == node && path_e[depth] == ge) spl_probe_acc[22] += 1;
                     else prefix_run = false;
                 }
             }
 #endif
-            if (l == 0) { path[2 * depth] = node; path[2 * depth + 1] = ge; }
+            if (l == 0) { path_n[depth] = node; path_e[depth] = ge; }
             depth++;
             int child = uniform(pk.child);
-            int2 cr = make_int2(uniform(pk.cr.x), uniform(pk.cr.y));
+            int64_t ceb = pk.ceb;
+            int cec = uniform(pk.cec);
             SPL_PROBE(2)
             if (child >= 0 && nbrd) {                        // linked: no transition needed
                 node = child;
-                eb = cr.x;
-                ec = cr.y;
+                eb = ceb;
+                ec = cec;
                 continue;
             }
             if (bnode != node) {                             // stage this node's stored board
@@ -1116,8 +1239,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                 k0 = uniform64(k0); k1 = uniform64(k1);
                 child = uniform(hash_lookup(P, t, k0, k1));
                 if (child >= 0) {                            // transposition: link + cache
-                    cr = make_int2(P.neb[nb + child], P.nterm[nb + child] ? -1 : P.nec[nb + child]);
-                    if (l == 0) { P.ed[e0 + ge].k.child = child; set_cr(P.ed[e0 + ge].k, cr.x, cr.y); }
+                    ceb = P.neb[child];
+                    cec = P.nterm[child] ? -1 : P.nec[child];
+                    if (l == 0) { P.ed[ge].k.child = child; set_cr(P.ed[ge].k, ceb, cec); }
                 }
             }
             SPL_PROBE(4)
@@ -1127,8 +1251,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             if (child >= 0) {
                 node = child;
                 bnode = child;
-                eb = cr.x;
-                ec = cr.y;
+                eb = ceb;
+                ec = cec;
                 continue;
             }
             float es[N];
@@ -1137,25 +1261,26 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
 #pragma unroll
             for (int i = 0; i < N; i++) any |= es[i] != 0.f;
             if (any) {
-                const int id = H->node_count;
                 kind = LEAF_TERMINAL;
 #pragma unroll
                 for (int i = 0; i < N; i++) val[i] = es[i];
-                if (id >= P.ncap) {                          // no room: back up, do not store
-                    if (l == 0) H->unexpanded += 1;
-                    break;
-                }
                 __builtin_amdgcn_wave_barrier();
                 if (l == 0) {
-                    P.nkey0[nb + id] = k0; P.nkey1[nb + id] = k1; P.neb[nb + id] = 0;
-                    P.nec[nb + id] = 0; P.nst[nb + id].ns = 0; P.nst[nb + id].qs = 0;
-                    P.nround[nb + id] = (uint8_t)bt(row(s, 0), 6); P.nterm[nb + id] = 1;
+                    const int id = H->node_count;
+                    const int g = node_slot(P, H, t, id);
+                    if (g < 0) {                             // no room: back up, do not store
+                        H->unexpanded += 1;
+                    } else {
+                        P.nkey0[g] = k0; P.nkey1[g] = k1; P.neb[g] = 0;
+                        P.nec[g] = 0; P.nst[g].ns = 0; P.nst[g].qs = 0;
+                        P.nround[g] = (uint8_t)bt(row(s, 0), 6); P.nterm[g] = 1;
 #pragma unroll
-                    for (int i = 0; i < 4; i++) P.nes[(nb + id) * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
-                    hash_insert(P, t, k0, id);
-                    P.ed[e0 + ge].k.child = id;
-                    set_cr(P.ed[e0 + ge].k, 0, -1);
-                    H->node_count = id + 1;
+                        for (int i = 0; i < 4; i++) P.nes[(size_t)g * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
+                        hash_insert(P, t, k0, g);
+                        P.ed[ge].k.child = g;
+                        set_cr(P.ed[ge].k, 0, -1);
+                        H->node_count = id + 1;
+                    }
                 }
                 break;
             }
@@ -1166,10 +1291,14 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
     SPL_PROBE(5)
     if (kind == LEAF_NN) {                                   // its mask: k_leaf_mask
         wave_store_board<N>(leaf_state + (size_t)t * Lx::S, s);
-        const int id = H->node_count;                        // the slot k_backup will insert it at
-        if (P.nbrd && id < P.ncap) {
-            uint64_t *dst = reinterpret_cast<uint64_t *>(P.nbrd + (nb + id) * NodeBoard<N>::BYTES);
-            for (int r = l; r < Lx::ROWS; r += 64) dst[r] = row(s, r);
+        if (P.nbrd) {                                        // the slot k_backup will insert it at
+            int g = -1;
+            if (l == 0) g = node_slot(P, H, t, H->node_count);
+            g = __shfl(g, 0, 64);
+            if (g >= 0) {
+                uint64_t *dst = reinterpret_cast<uint64_t *>(P.nbrd + (size_t)g * NodeBoard<N>::BYTES);
+                for (int r = l; r < Lx::ROWS; r += 64) dst[r] = row(s, r);
+            }
         }
     }
     SPL_PROBE(6)
@@ -1287,22 +1416,23 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
     TreeHdr *H = P.hdr + t;
     const int kind = H->leaf_kind;
     if (kind == LEAF_NONE) return;
-    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const int depth = H->depth;
-    const int32_t *path = P.path + (size_t)t * P.pcap * 2;
+    const int32_t *path_n = P.path_n + (size_t)t * P.pcap;
+    const int64_t *path_e = P.path_e + (size_t)t * P.pcap;
     // this simulation's path (lane per level) and the statistics its backup updates are
     // requested before the expansion, so their round trips overlap it (the expansion never
     // touches them: the new node is not on its own path)
-    int pnode = 0, pge = 0, pcnt = 0, pns = 0;
+    int pnode = 0, pcnt = 0, pns = 0;
+    int64_t pge = 0;
     double pq = 0.0, pqs = 0.0;
     if (l < depth) {
-        pnode = path[2 * l];
-        pge = path[2 * l + 1];
-        const EdgeStat st = P.ed[e0 + pge].s;
+        pnode = path_n[l];
+        pge = path_e[l];
+        const EdgeStat st = P.ed[pge].s;
         pcnt = st.n;
         pq = st.q;
-        pns = P.nst[nb + pnode].ns;
-        pqs = P.nst[nb + pnode].qs;
+        pns = P.nst[pnode].ns;
+        pqs = P.nst[pnode].qs;
     }
     float val[4] = {0, 0, 0, 0};
     if (kind == LEAF_NN) {
@@ -1310,28 +1440,38 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         int ec = 0;
 #pragma unroll
         for (int k = 0; k < 7; k++) ec += __popcll(m[k]);
-        int id = H->node_count, eb = H->edge_count;
-        if (eb + ec > P.ecap && depth > 0 && H->gc_state == 0) {
-            // garbage is collected lazily (begin_search), so a search may run out of edge
-            // room with dead nodes still in the pool: this simulation is withdrawn (no
-            // backup, not counted), k_commit collects the garbage (exact: nodes with rounds
-            // <= the root's) and the next select repeats the same descent
+        // the new node's slot and CSR run (pages from the shared pools)
+        int g = -1;
+        int64_t eb = -1;
+        if (l == 0) {
+            g = node_slot(P, H, t, H->node_count);
+            if (g >= 0) eb = edge_run(P, H, t, ec);
+        }
+        g = __shfl(g, 0, 64);
+        eb = readlane64(eb, 0);
+        if (eb < 0 && C.selfplay && depth > 0 && H->gc_state == 0) {
+            // garbage is collected lazily (begin_search), so a self-play search may run out
+            // of room with dead nodes still held: this simulation is withdrawn (no backup,
+            // not counted), k_gc (launched behind every backup of a self-play arena) collects
+            // the garbage (exact: nodes with rounds <= the root's) and the next select repeats
+            // the same descent. Search-only arenas never withdraw.
             if (l == 0) {
                 H->gc_state = 1;
                 H->leaf_kind = LEAF_NONE;
-                if (C.selfplay) gc_push(P, t);
+                H->withdrawals += 1;
+                gc_push(P, H, t);
             }
             return;
         }
-        if (id >= P.ncap || eb + ec > P.ecap) {          // no room: back up v, do not store
+        if (eb < 0) {                                    // no room: back up v, do not store
 #pragma unroll
             for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
             if (l == 0) H->unexpanded += 1;
             goto backup;
         }
         float *pr = lpi[w];
-        const float *g = pi + (size_t)t * SPL_ACTIONS;
-        for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = g[a];      // coalesced stage
+        const float *gp = pi + (size_t)t * SPL_ACTIONS;
+        for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = gp[a];     // coalesced stage
         __builtin_amdgcn_wave_barrier();
         const float sum = wave_np_sum409(pr);                        // normalise (MCTS.py:144)
         int run = 0;
@@ -1339,13 +1479,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         for (int k = 0; k < 7; k++) {
             const uint64_t wd = m[k];
             if ((wd >> l) & 1) {
-                const int r = eb + run + __popcll(wd & lanemask_lt());
+                const int64_t r = eb + run + __popcll(wd & lanemask_lt());
                 const int a = 64 * k + l;
-                P.ed[e0 + r].k.a = (int16_t)a;
-                P.ed[e0 + r].s.p = pr[a] / sum;
-                P.ed[e0 + r].s.n = 0;
-                P.ed[e0 + r].s.q = Q_UNSET;
-                P.ed[e0 + r].k.child = -1;
+                P.ed[r].k.a = (int16_t)a;
+                P.ed[r].s.p = pr[a] / sum;
+                P.ed[r].s.n = 0;
+                P.ed[r].s.q = Q_UNSET;
+                P.ed[r].k.child = -1;
             }
             run += __popcll(wd);
         }
@@ -1354,17 +1494,17 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         if (l == 0) {
-            P.nkey0[nb + id] = H->leaf_k0; P.nkey1[nb + id] = H->leaf_k1;
-            P.neb[nb + id] = eb; P.nec[nb + id] = ec; P.nst[nb + id].ns = 0;
-            P.nst[nb + id].qs = (double)val[0]; P.nround[nb + id] = H->leaf_round; P.nterm[nb + id] = 0;
-            hash_insert(P, t, H->leaf_k0, id);
-            if (depth == 0) { H->root = id; H->root_eb = eb; H->root_ec = ec; }
+            P.nkey0[g] = H->leaf_k0; P.nkey1[g] = H->leaf_k1;
+            P.neb[g] = eb; P.nec[g] = ec; P.nst[g].ns = 0;
+            P.nst[g].qs = (double)val[0]; P.nround[g] = H->leaf_round; P.nterm[g] = 0;
+            hash_insert(P, t, H->leaf_k0, g);
+            if (depth == 0) { H->root = g; H->root_eb = eb; H->root_ec = ec; }
             else {
-                P.ed[e0 + path[2 * (depth - 1) + 1]].k.child = id;
-                set_cr(P.ed[e0 + path[2 * (depth - 1) + 1]].k, eb, ec);
+                const int64_t pe = path_e[depth - 1];
+                P.ed[pe].k.child = g;
+                set_cr(P.ed[pe].k, eb, ec);
             }
-            H->node_count = id + 1;
-            H->edge_count = eb + ec;
+            H->node_count += 1;
         }
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
@@ -1381,17 +1521,18 @@ backup:
     for (int d = l; d < depth; d += 64) {
         const int rot = (depth - d) % N;
         const double v0 = (double)val[(N - rot) % N];
-        int node = pnode, ge = pge, cnt = pcnt, ns = pns;
+        int node = pnode, cnt = pcnt, ns = pns;
+        int64_t ge = pge;
         double q = pq, qs = pqs;
         if (d >= 64) {                                   // levels beyond the prefetched 64
-            node = path[2 * d]; ge = path[2 * d + 1];
-            cnt = P.ed[e0 + ge].s.n; q = P.ed[e0 + ge].s.q;
-            ns = P.nst[nb + node].ns; qs = P.nst[nb + node].qs;
+            node = path_n[d]; ge = path_e[d];
+            cnt = P.ed[ge].s.n; q = P.ed[ge].s.q;
+            ns = P.nst[node].ns; qs = P.nst[node].qs;
         }
-        P.ed[e0 + ge].s.q = ((double)cnt * q + v0) / (double)(cnt + 1);
-        P.nst[nb + node].qs = ((double)(ns + 1) * qs + v0) / (double)(ns + 2);
-        P.ed[e0 + ge].s.n = cnt + 1;
-        P.nst[nb + node].ns = ns + 1;
+        P.ed[ge].s.q = ((double)cnt * q + v0) / (double)(cnt + 1);
+        P.nst[node].qs = ((double)(ns + 1) * qs + v0) / (double)(ns + 2);
+        P.ed[ge].s.n = cnt + 1;
+        P.nst[node].ns = ns + 1;
     }
     if (l == 0) {
         H->sims_done += 1;
@@ -1421,16 +1562,16 @@ __global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int
         if (l == 0) action[t] = (int16_t)(int)(u * (double)SPL_ACTIONS);
         return;
     }
-    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
-    const int eb = P.neb[nb + root], ec = P.nec[nb + root];
+    const Edge *E = P.ed + P.neb[root];
+    const int ec = P.nec[root];
     const int sims = H->budget;
     const bool forced = H->forced;
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, P.ed[e0 + eb + i].s.n);
+    for (int i = l; i < ec; i += 64) best = max(best, E[i].s.n);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
     long long top = 0;
     for (int i = l; i < ec; i += 64)
-        top = max(top, pruned_count(P.ed[e0 + eb + i].s.n, best, forced, P.ed[e0 + eb + i].s.p, sims));
+        top = max(top, pruned_count(E[i].s.n, best, forced, E[i].s.p, sims));
     for (int o = 32; o > 0; o >>= 1) top = max(top, (long long)__shfl_xor(top, o, 64));
     if (top == 0) {
         if (l == 0) action[t] = (int16_t)(int)(u * (double)SPL_ACTIONS);
@@ -1439,20 +1580,20 @@ __global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int
     int nbest = 0;
     for (int base = 0; base < ec; base += 64) {
         const int i = base + l;
-        const bool hit = i < ec && pruned_count(P.ed[e0 + eb + i].s.n, best, forced, P.ed[e0 + eb + i].s.p, sims) == top;
+        const bool hit = i < ec && pruned_count(E[i].s.n, best, forced, E[i].s.p, sims) == top;
         nbest += __popcll(__ballot(hit));
     }
     int k = (int)(u * (double)nbest);                    // k-th best in action order
     for (int base = 0; base < ec; base += 64) {
         const int i = base + l;
-        const bool hit = i < ec && pruned_count(P.ed[e0 + eb + i].s.n, best, forced, P.ed[e0 + eb + i].s.p, sims) == top;
+        const bool hit = i < ec && pruned_count(E[i].s.n, best, forced, E[i].s.p, sims) == top;
         const uint64_t b = __ballot(hit);
         const int c = __popcll(b);
         if (k < c) {
             uint64_t x = b;
             for (int j = 0; j < k; j++) x &= x - 1;
             const int pos = __ffsll((unsigned long long)x) - 1;
-            if (l == 0) action[t] = P.ed[e0 + eb + base + pos].k.a;
+            if (l == 0) action[t] = E[base + pos].k.a;
             return;
         }
         k -= c;
@@ -1469,7 +1610,6 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
     if (t >= B) return;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
-    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
     const int root = H->root;
     for (int a = l; a < SPL_ACTIONS; a += 64) {
         if (counts) counts[(size_t)t * SPL_ACTIONS + a] = 0;
@@ -1480,29 +1620,30 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
     if (root < 0) return;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const int eb = P.neb[nb + root], ec = P.nec[nb + root];
+    const Edge *E = P.ed + P.neb[root];
+    const int ec = P.nec[root];
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, P.ed[e0 + eb + i].s.n);
+    for (int i = l; i < ec; i += 64) best = max(best, E[i].s.n);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
     const int sims = H->budget;
     const bool forced = H->forced;
     long long tot = 0;
     for (int i = l; i < ec; i += 64) {
-        const int a = P.ed[e0 + eb + i].k.a;
-        const long long c = pruned_count(P.ed[e0 + eb + i].s.n, best, forced, P.ed[e0 + eb + i].s.p, sims);
-        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = P.ed[e0 + eb + i].s.n;
+        const int a = E[i].k.a;
+        const long long c = pruned_count(E[i].s.n, best, forced, E[i].s.p, sims);
+        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = E[i].s.n;
         if (adjusted) adjusted[(size_t)t * SPL_ACTIONS + a] = c;
-        if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = P.ed[e0 + eb + i].s.q;
+        if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = E[i].s.q;
         tot += c;
     }
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
     for (int i = l; i < ec; i += 64) {
-        const int a = P.ed[e0 + eb + i].k.a;
-        const long long c = pruned_count(P.ed[e0 + eb + i].s.n, best, forced, P.ed[e0 + eb + i].s.p, sims);
+        const int a = E[i].k.a;
+        const long long c = pruned_count(E[i].s.n, best, forced, E[i].s.p, sims);
         if (probs) probs[(size_t)t * SPL_ACTIONS + a] = (double)c / (double)tot;
     }
     if (q && l == 0) {
-        const double q0 = P.nst[nb + root].qs;
+        const double q0 = P.nst[root].qs;
         q[(size_t)t * n] = q0;
         for (int i = 1; i < n; i++) q[(size_t)t * n + i] = -q0 / (double)(n - 1);
     }
@@ -1519,9 +1660,9 @@ __global__ __launch_bounds__(THREADS) void k_root_priors(Pools P, int B, float *
     if (root < 0) return;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const size_t nb = (size_t)t * P.ncap, e0 = (size_t)t * P.ecap;
-    const int eb = P.neb[nb + root], ec = P.nec[nb + root];
-    for (int i = l; i < ec; i += 64) o[P.ed[e0 + eb + i].k.a] = P.ed[e0 + eb + i].s.p;
+    const Edge *E = P.ed + P.neb[root];
+    const int ec = P.nec[root];
+    for (int i = l; i < ec; i += 64) o[E[i].k.a] = E[i].s.p;
 }
 
 // leaf int8 [B,R,7] + packed mask -> float32 board and bool mask (predict, :160-161).
@@ -1550,12 +1691,13 @@ __global__ __launch_bounds__(64) void k_tree_sizes(Pools P, int B, int32_t *out)
     if (t >= B) return;
     const int l = lane_id();
     const TreeHdr *H = P.hdr + t;
-    const size_t nb = (size_t)t * P.ncap;
     const int nc = H->node_count, root = H->root;
-    const int rr = root >= 0 ? P.nround[nb + root] : 1 << 30;
+    const int rr = root >= 0 ? P.nround[root] : 1 << 30;
     int ln = 0, le = 0;
-    for (int i = l; i < nc; i += 64)
-        if (i == root || P.nround[nb + i] > rr) { ln++; le += P.nterm[nb + i] ? 0 : P.nec[nb + i]; }
+    for (int i = l; i < nc; i += 64) {
+        const int g = node_g(P, t, i);
+        if (g == root || P.nround[g] > rr) { ln++; le += P.nterm[g] ? 0 : P.nec[g]; }
+    }
     for (int o = 32; o > 0; o >>= 1) { ln += __shfl_xor(ln, o, 64); le += __shfl_xor(le, o, 64); }
     if (l == 0) {
         out[4 * t] = nc; out[4 * t + 1] = H->edge_count;
@@ -1590,6 +1732,14 @@ __global__ __launch_bounds__(256) void k_hash_eval(int B, const int8_t *__restri
             (float)((double)(mix64(h ^ (0xA5A5ull + threadIdx.x)) >> 40) * 0x1p-23 - 1.0);
 }
 
+// free stacks = every page, allocation counters
+__global__ void k_init_pools(Pools P) {
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = tid; i < (size_t)P.npages; i += nth) P.nfree[i] = (int32_t)i;
+    for (size_t i = tid; i < (size_t)P.epages; i += nth) P.efree[i] = (int32_t)i;
+    if (tid == 0) { P.alloc[0] = P.npages; P.alloc[1] = P.epages; P.alloc[2] = 0; P.alloc[3] = 0; }
+}
+
 inline int check_launch() { return hipGetLastError() == hipSuccess ? 0 : SPL_EDEVICE; }
 inline dim3 wave_grid(int B) { return dim3((unsigned)((B + WAVES - 1) / WAVES)); }
 
@@ -1614,28 +1764,39 @@ extern "C" {
 
 // Pool layout of spl_mcts_create (also what spl_mcts_plan_bytes reports).
 struct Plan {
-    int ncap, ecap, hcap, pcap, S, excap, out_cap, nbb;   // nbb: bytes per node board (0: none)
+    int nmax, emax, hcap, pcap, nptab, eptab, S, excap, out_cap, nbb;   // nbb: bytes per node board
+    long long npages, epages;
     size_t bytes;
 };
 static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     Plan L;
-    L.ncap = cfg->node_cap; L.ecap = cfg->edge_cap;
-    int h = 1;
-    while (h < 2 * L.ncap) h <<= 1;
+    L.nptab = (cfg->node_cap + NPG - 1) / NPG;
+    L.eptab = (cfg->edge_cap + EPG - 1) / EPG;
+    L.nmax = L.nptab * NPG; L.emax = L.eptab * EPG;
+    // transposition table: power of two with load <= 0.7 at the tree's maximum
+    int h = 64;
+    while ((long long)h * 7 < (long long)L.nmax * 10) h <<= 1;
     L.hcap = h;
     L.pcap = cfg->num_sims + 64 > 256 ? cfg->num_sims + 64 : 256;
     L.S = 7 * (32 + 10 * n + n * n);
     L.excap = cfg->selfplay ? 62 * n + 2 : 0;
     L.out_cap = cfg->selfplay ? (cfg->out_cap > 0 ? cfg->out_cap : 4 * B) : 0;
     L.nbb = cfg->node_boards ? (8 * (32 + 10 * n + n * n) + 15) & ~15 : 0;
-    const size_t nn = (size_t)B * L.ncap, ne = (size_t)B * L.ecap;
+    const long long pn = cfg->pool_nodes > 0 ? cfg->pool_nodes : (long long)B * L.nmax;
+    const long long pe = cfg->pool_edges > 0 ? cfg->pool_edges : (long long)B * L.emax;
+    L.npages = (pn + NPG - 1) / NPG;
+    L.epages = (pe + EPG - 1) / EPG;
+    const size_t nn = (size_t)L.npages * NPG, ne = (size_t)L.epages * EPG;
     const size_t nx = (size_t)B * L.excap, no = (size_t)L.out_cap;
+    const int gcw = B < GC_WG ? B : GC_WG;
     size_t bytes = 0;
     auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
-    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn); acc(sizeof(NodeStat) * nn);
-    acc(4 * nn); acc(nn); acc(16 * nn); acc(sizeof(Edge) * ne);
-    acc(4 * (size_t)B * L.hcap); acc(8 * (size_t)B * L.pcap);
-    acc(4 * nn); acc(4 * nn); acc(8 * ((size_t)B * (L.ncap + 1))); acc((size_t)B * L.S);
+    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn);
+    acc(sizeof(NodeStat) * nn); acc(nn); acc(16 * nn); acc(sizeof(Edge) * ne);
+    acc(4 * (size_t)B * L.nptab); acc(4 * (size_t)B * L.eptab); acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages);
+    acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages); acc(64);
+    acc(4 * (size_t)B * L.hcap); acc(4 * (size_t)B * L.pcap); acc(8 * (size_t)B * L.pcap);
+    acc(4 * (size_t)gcw * gc_ints(L.nmax)); acc((size_t)B * L.S);
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
     acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
     acc(16 * no); acc(64); acc((size_t)L.nbb * nn); acc(4 * (size_t)B); acc(8 * no);
@@ -1644,8 +1805,16 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
 }
 
 static bool valid_cfg(const spl_ctx *ctx, int B, const spl_mcts_config *cfg) {
-    return ctx && ctx->n >= 2 && ctx->n <= 4 && B > 0 && cfg && cfg->num_sims > 0 && cfg->ratio_full > 0 &&
-           cfg->node_cap > 0 && cfg->edge_cap > 0;
+    if (!(ctx && ctx->n >= 2 && ctx->n <= 4 && B > 0 && cfg && cfg->num_sims > 0 && cfg->ratio_full > 0 &&
+          cfg->node_cap > 0 && cfg->edge_cap > 0 && cfg->pool_nodes >= 0 && cfg->pool_edges >= 0))
+        return false;
+    // global node ids are int32; page ids too
+    const long long nmax = (long long)((cfg->node_cap + NPG - 1) / NPG) * NPG;
+    const long long emax = (long long)((cfg->edge_cap + EPG - 1) / EPG) * EPG;
+    const long long pn = cfg->pool_nodes > 0 ? cfg->pool_nodes : (long long)B * nmax;
+    const long long pe = cfg->pool_edges > 0 ? cfg->pool_edges : (long long)B * emax;
+    return cfg->node_cap <= (1 << 24) && cfg->edge_cap <= (1 << 28) && pn + NPG < (1LL << 31) &&
+           pe / EPG + 1 < (1LL << 31);
 }
 
 #if MCTS_TIMING
@@ -1678,30 +1847,37 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     C.forced_playouts = cfg->forced_playouts; C.dirichlet = cfg->dirichlet_alpha > 0;
     C.temp_threshold = cfg->temp_threshold; C.seed = cfg->seed; C.board_base = cfg->board_base;
     C.selfplay = cfg->selfplay;
+    C.edge_reserve = 32;
     Pools &P = m->P;
     const Plan L = plan_pools(ctx->n, B, cfg);
-    P.ncap = L.ncap; P.ecap = L.ecap; P.hcap = L.hcap; P.pcap = L.pcap;
-    C.edge_reserve = P.ecap / P.ncap < 32 ? P.ecap / P.ncap : 32;
-    const size_t nn = (size_t)B * P.ncap, ne = (size_t)B * P.ecap;
+    P.nmax = L.nmax; P.emax = L.emax; P.hcap = L.hcap; P.pcap = L.pcap;
+    P.nptab = L.nptab; P.eptab = L.eptab;
+    P.npages = (int)L.npages; P.epages = (int)L.epages;
+    P.low_n = P.npages / 16; P.low_e = P.epages / 16;
+    const size_t nn = (size_t)L.npages * NPG, ne = (size_t)L.epages * EPG;
     const int excap = L.excap;
     const size_t nx = (size_t)B * excap, no = (size_t)L.out_cap;
-    const size_t bytes = L.bytes;
+    const int gcw = B < GC_WG ? B : GC_WG;
     void *arena = nullptr;
-    if (hipMalloc(&arena, bytes) != hipSuccess) { delete m; return SPL_EDEVICE; }
-    if (hipMemset(arena, 0, bytes) != hipSuccess) { (void)hipFree(arena); delete m; return SPL_EDEVICE; }
+    if (hipMalloc(&arena, L.bytes) != hipSuccess) { delete m; return SPL_EDEVICE; }
     m->arena = arena;
-    m->bytes = bytes;
+    m->bytes = L.bytes;
     char *p = (char *)arena;
     P.hdr = carve<TreeHdr>(p, B);
     P.nkey0 = carve<uint64_t>(p, nn); P.nkey1 = carve<uint64_t>(p, nn);
-    P.neb = carve<int32_t>(p, nn); P.nec = carve<int32_t>(p, nn); P.nst = carve<NodeStat>(p, nn);
-    P.nround = carve<int32_t>(p, nn); P.nterm = carve<int8_t>(p, nn);
+    P.neb = carve<int64_t>(p, nn); P.nec = carve<int32_t>(p, nn); P.nround = carve<int32_t>(p, nn);
+    P.nst = carve<NodeStat>(p, nn); P.nterm = carve<int8_t>(p, nn);
     P.nes = carve<float>(p, 4 * nn);
     P.ed = carve<Edge>(p, ne);
+    P.ntab = carve<int32_t>(p, (size_t)B * P.nptab); P.etab = carve<int32_t>(p, (size_t)B * P.eptab);
+    P.npidx = carve<int32_t>(p, (size_t)P.npages); P.epidx = carve<int32_t>(p, (size_t)P.epages);
+    P.nfree = carve<int32_t>(p, (size_t)P.npages); P.efree = carve<int32_t>(p, (size_t)P.epages);
+    P.alloc = carve<int32_t>(p, 16);
     P.hslot = carve<int32_t>(p, (size_t)B * P.hcap);
-    P.path = carve<int32_t>(p, 2 * (size_t)B * P.pcap);
-    P.remap = carve<int32_t>(p, nn); P.remap_eb = carve<int32_t>(p, nn);
-    P.cscr = carve<int32_t>(p, 2 * ((size_t)B * (P.ncap + 1)));
+    P.path_n = carve<int32_t>(p, (size_t)B * P.pcap);
+    P.path_e = carve<int64_t>(p, (size_t)B * P.pcap);
+    P.gc_stride = gc_ints(P.nmax);
+    P.gscr = carve<int32_t>(p, (size_t)gcw * P.gc_stride);
     P.root_state = carve<int8_t>(p, (size_t)B * m->S);
     P.excap = excap; P.out_cap = (int)no;
     P.board = carve<int8_t>(p, (size_t)B * m->S);
@@ -1715,9 +1891,16 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.nbrd = L.nbb ? carve<int8_t>(p, (size_t)L.nbb * nn) : nullptr;
     P.gcq = carve<int32_t>(p, (size_t)B);
     P.flq = carve<int2>(p, no);
-    if (hipMemset(P.hslot, 0xFF, 4 * (size_t)B * P.hcap) != hipSuccess) {
-        (void)hipFree(arena); delete m; return SPL_EDEVICE;
+    // zero the small state (headers, counters); the pools need no initialisation (a slot
+    // is written before it is read); free stacks hold every page, tables are empty
+    bool ok = hipMemset(P.hdr, 0, sizeof(TreeHdr) * B) == hipSuccess &&
+              hipMemset(P.counters, 0, 64) == hipSuccess &&
+              hipMemset(P.hslot, 0xFF, 4 * (size_t)B * P.hcap) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_init_pools, dim3(1024), dim3(256), 0, (hipStream_t)0, P);
+        ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess;
     }
+    if (!ok) { (void)hipFree(arena); delete m; return SPL_EDEVICE; }
     *out = m;
     return 0;
 }
@@ -1738,12 +1921,20 @@ int spl_mcts_set_roots(spl_mcts *m, const int8_t *roots, int keep_tree, int forc
     return spl_mcts_set_roots_active(m, roots, nullptr, keep_tree, force_full, hs);
 }
 
+// garbage collection queued by search starts / backups (usually none; in bursts up to
+// thousands of trees, GC_WG single-wave workgroups share the queue)
+static void launch_gc(spl_mcts *m, hipStream_t hs) {
+    const unsigned gcw = (unsigned)(m->B < GC_WG ? m->B : GC_WG);
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_gc<N>, dim3(gcw), dim3(64), 0, hs, m->P, m->cfg));
+}
+
 int spl_mcts_set_roots_active(spl_mcts *m, const int8_t *roots, const uint8_t *active, int keep_tree,
                               int force_full, void *hs) {
     if (!m || !roots) return SPL_EINVAL;
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_set_roots<N>, wave_grid(m->B), dim3(THREADS), 0,
                                           (hipStream_t)hs, m->P, m->cfg, m->B, roots, active, keep_tree,
                                           force_full));
+    launch_gc(m, (hipStream_t)hs);
     return check_launch();
 }
 
@@ -1772,6 +1963,7 @@ int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, con
     if (!m || !leaf_mask || !pi || !v) return SPL_EINVAL;
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_backup<N>, wave_grid(m->B), dim3(THREADS), 0,
                                           (hipStream_t)hs, m->P, m->cfg, m->B, leaf_mask, pi, v));
+    if (m->cfg.selfplay) launch_gc(m, (hipStream_t)hs);   // trees whose simulation was withdrawn
     return check_launch();
 }
 
@@ -1800,16 +1992,7 @@ int spl_mcts_commit(spl_mcts *m, void *hs) {
     if (!m || !m->cfg.selfplay) return SPL_EINVAL;
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_commit<N>, wave_grid(m->B), dim3(THREADS), 0,
                                           (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit));
-    // garbage collection queued by this iteration's backups and search starts (usually
-    // none, in bursts up to thousands of trees: 1024 single-wave workgroups share the queue)
-    const unsigned gcw = (unsigned)(m->B < 1024 ? m->B : 1024);
-    const size_t gcl = 4 * (4 * (size_t)m->P.ncap + 2);
-    const int lds_ok = gcl <= 160 * 1024;
-    if (lds_ok) {
-        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_gc<N, true>), dim3(gcw), dim3(64), gcl, (hipStream_t)hs, m->P, m->cfg));
-    } else {
-        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_gc<N, false>), dim3(gcw), dim3(64), 0, (hipStream_t)hs, m->P, m->cfg));
-    }
+    launch_gc(m, (hipStream_t)hs);                        // collections queued by the new searches
     return check_launch();
 }
 
@@ -1825,6 +2008,18 @@ int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *val
     }
     hipLaunchKernelGGL(k_drain_reset, dim3(1), dim3(1), 0, (hipStream_t)hs, m->P, max, n_out);
     return check_launch();
+}
+
+int spl_mcts_pool_state(spl_mcts *m, int32_t *out, void *hs) {
+    if (!m || !out) return SPL_EINVAL;
+    return hipMemcpyAsync(out, m->P.alloc, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)hs) ==
+                   hipSuccess ? 0 : SPL_EDEVICE;
+}
+
+int spl_mcts_pool_pages(const spl_mcts *m, long long *out4) {
+    if (!m || !out4) return SPL_EINVAL;
+    out4[0] = m->P.npages; out4[1] = m->P.epages; out4[2] = NPG; out4[3] = EPG;
+    return 0;
 }
 
 int spl_mcts_counters(spl_mcts *m, int32_t *out, void *hs) {

@@ -18,20 +18,30 @@ namespace spl {
 constexpr double Q_UNSET = -42.0;   // MCTS.py:9 NAN sentinel
 
 struct TreeHdr {
-    int32_t node_count, edge_count, root, sims_done;
-    int32_t budget, full, noise_pending, depth;
+    int32_t node_count, edge_count, root, sims_done;   // node_count: the tree's node slots in use
+    int32_t budget, full, noise_pending, depth;         // (local order), edge_count: edges in use
     int32_t leaf_kind, player, episode_step, move_no;
     int32_t game_no, overflow, n_examples, leaf_round;
     uint64_t leaf_k0, leaf_k1;
     float leaf_v[4];
-    int32_t games_done, forced, pad0, root_eb;
+    int32_t games_done, forced, moves, root_ec;
     // capacity events: searches that started on a tree pruned to the nodes
     // linked from the root / on an emptied tree, and simulations whose leaf did not fit
-    // (evaluated and backed up without being stored); root_eb / root_ec: the root's CSR
-    // range (so the descent's first level needs no node load)
-    int32_t prunes, resets, unexpanded, root_ec;
-    int32_t gc_state, pad1, pad2, pad3;  // 1: a leaf did not fit, k_commit collects garbage; 2: done
+    // (evaluated and backed up without being stored)
+    int32_t prunes, resets, unexpanded, gc_state;
+    int64_t root_eb;                     // the root's CSR range (global edge index, count root_ec):
+                                         // the descent's first level needs no node load
+    int64_t enext;                       // next free edge of the tree's current edge page
+    int32_t npg, epg, eleft, live_gc;    // node / edge pages held, edges left in the current
+                                         // edge page, nodes kept by the last collection
+    int32_t root_round, gc_queued, withdrawals, gcs;   // root round (deferred GC), queued for
+                                         // k_gc, simulations withdrawn for GC, collections run
 };
+static_assert(sizeof(TreeHdr) == 176, "TreeHdr layout (splendor/mcts.py HDR_DTYPE)");
+// gc_state: 0 none; 1 a leaf did not fit mid-search (withdrawn, k_gc collects, the descent
+// repeats); 2 collected once this search; 3 collection before this search (must: the
+// search does not fit the tree's maxima); 5 collection before this search (should: garbage
+// or pool pressure; k_gc may skip it, see GC_SHOULD_CAP)
 enum { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2 };
 
 // Edge records, two 16-byte halves: the UCB inputs and the link (both read by the scan in
@@ -44,17 +54,15 @@ struct __align__(16) EdgeStat {
 struct __align__(16) EdgeLink {
     int16_t a;     // action
     int16_t cec;   // cached child CSR count (-1: terminal child); valid when child >= 0
-    int32_t child; // child node (-1: not linked yet)
-    int32_t ceb;   // cached child CSR base
-    int32_t pad;
+    int32_t child; // child node, global id (-1: not linked yet)
+    int64_t ceb;   // cached child CSR base (global edge index)
 };
 // one edge = both halves in one 32-byte record (one pool pointer: fewer live SGPRs)
 struct __align__(16) Edge {
     EdgeStat s;
     EdgeLink k;
 };
-__device__ __forceinline__ int2 get_cr(const EdgeLink &e) { return make_int2(e.ceb, e.cec); }
-__device__ __forceinline__ void set_cr(EdgeLink &e, int eb, int ec) { e.ceb = eb; e.cec = (int16_t)ec; }
+__device__ __forceinline__ void set_cr(EdgeLink &e, int64_t eb, int ec) { e.ceb = eb; e.cec = (int16_t)ec; }
 
 // a node's visit statistics (Ns, Qs), read together by the descent
 struct __align__(16) NodeStat {
@@ -63,21 +71,43 @@ struct __align__(16) NodeStat {
     int32_t pad;
 };
 
-// per-tree SoA pools; tree t owns [t*ncap, (t+1)*ncap) nodes, [t*ecap, ...) edges
+// Per-GPU shared arena. Nodes and edges live in pools shared by all trees and
+// are handed out in pages: node page = NPG consecutive global node ids, edge page = EPG
+// consecutive global edge indices. A tree holds a list of node pages and a list of edge
+// pages (its page tables, in allocation order) and addresses everything by GLOBAL id: child
+// links, cached child CSR ranges, the path, the root and the transposition table hold global
+// ids, so the descent never translates. A tree's "local" node index (0 .. node_count) is its
+// allocation order (slot i = page ntab[i / NPG], offset i % NPG); its edges are contiguous per
+// node and never straddle an edge page. Pages are popped from the free stacks by k_select /
+// k_backup only and pushed back by k_gc / k_commit / k_set_roots / k_reset_games only, so
+// pops and pushes never share a launch (an array stack with one atomic top is then exact).
+constexpr int NPG_SHIFT = 6, NPG = 1 << NPG_SHIFT;     // nodes per node page
+constexpr int EPG_SHIFT = 10, EPG = 1 << EPG_SHIFT;    // edges per edge page (> 409)
+
 struct Pools {
-    int ncap, ecap, hcap, pcap;          // nodes, edges, hash slots (pow2), path depth
+    int nmax, emax, hcap, pcap;          // per tree: node slots, edges (page tables), hash slots, path
+    int nptab, eptab;                    // page-table entries per tree (nmax / NPG, emax / EPG)
+    int npages, epages;                  // pages in the pools
+    int low_n, low_e;                    // free-page low-water marks (pool pressure: collect garbage)
     TreeHdr *hdr;
-    uint64_t *nkey0, *nkey1;
-    int32_t *neb, *nec, *nround;
+    uint64_t *nkey0, *nkey1;             // node pool, indexed by global node id
+    int64_t *neb;
+    int32_t *nec, *nround;
     NodeStat *nst;                       // visit count and value of every node (one 16-byte load)
     int8_t *nterm;
-    float *nes;                          // ncap x 4 terminal values
-    Edge *ed;                            // edges: UCB inputs + action, child, child's CSR range
-    int32_t *hslot;
-    int32_t *path;                       // pcap x 2 (node, edge)
-    int32_t *remap, *remap_eb;           // ncap scratch for compaction (new index, new CSR base)
-    int32_t *cscr;                       // 2 x (ncap + 1) per tree: edge-move scratch of large trees
-    int8_t *nbrd;                        // ncap x LS canonical board per node (LDS row format), or
+    float *nes;                          // 4 terminal values per node
+    Edge *ed;                            // edge pool: UCB inputs + action, child, child's CSR range
+    int32_t *ntab, *etab;                // B x nptab / B x eptab page tables
+    int32_t *npidx, *epidx;              // per page: its index in the owning tree's page table
+    int32_t *nfree, *efree;              // free page stacks
+    int32_t *alloc;                      // [0] / [1] free node / edge pages (stack tops),
+                                         // [2] / [3] failed node / edge page requests
+    int32_t *hslot;                      // B x hcap transposition table (global node ids)
+    int32_t *path_n;                     // B x pcap descent path: node (global id)
+    int64_t *path_e;                     // B x pcap and the edge taken (global index)
+    int32_t *gscr;                       // k_gc scratch, GC_WG x gc_stride ints
+    size_t gc_stride;
+    int8_t *nbrd;                        // per node slot its canonical board (LDS row format), or
                                          // nullptr (node_boards = 0: the descent re-applies moves)
     int8_t *root_state;                  // B x S (canonical root)
     // self-play (Coach.executeEpisode) state
@@ -96,6 +126,17 @@ struct Pools {
     int32_t *gcq;                        // B: trees whose garbage collection k_gc runs
     int2 *flq;                           // out_cap: (staging row, queue slot) rows k_gc copies
 };
+
+// tree t's local node slot i / local (virtual) edge position v -> global
+__device__ __forceinline__ int node_g(const Pools &P, int t, int i) {
+    return P.ntab[(size_t)t * P.nptab + (i >> NPG_SHIFT)] * NPG + (i & (NPG - 1));
+}
+__device__ __forceinline__ int node_l(const Pools &P, int g) {
+    return P.npidx[g >> NPG_SHIFT] * NPG + (g & (NPG - 1));
+}
+__device__ __forceinline__ int64_t edge_g(const Pools &P, int t, int v) {
+    return (int64_t)P.etab[(size_t)t * P.eptab + (v >> EPG_SHIFT)] * EPG + (v & (EPG - 1));
+}
 
 // per-node board slot (Pools::nbrd): the LDS row format padded to 16 bytes
 template <int N>
@@ -199,7 +240,7 @@ __device__ __forceinline__ void wave_fingerprint(const int8_t *s, uint64_t &k0, 
 
 __device__ __forceinline__ int hash_lookup(const Pools &P, int t, uint64_t k0, uint64_t k1) {
     const int32_t *hs = P.hslot + (size_t)t * P.hcap;
-    const uint64_t *K0 = P.nkey0 + (size_t)t * P.ncap, *K1 = P.nkey1 + (size_t)t * P.ncap;
+    const uint64_t *K0 = P.nkey0, *K1 = P.nkey1;
     uint32_t h = (uint32_t)(k0 ^ (k0 >> 32)) & (uint32_t)(P.hcap - 1);
     for (int probe = 0; probe < P.hcap; probe++) {
         const int c = hs[h];

@@ -10,7 +10,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("SPLENDOR_AMD_LIB") or os.path.join(PKG_ROOT, "libsplendor_amd.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 EINVAL, EDEVICE = -1, -2
 
 
@@ -54,6 +54,8 @@ _SIGS = {
     "spl_mcts_device_bytes": ([C.c_void_p], C.c_longlong),
     "spl_mcts_plan_bytes": ([_vp, C.c_int, _vp], C.c_longlong),
     "spl_mcts_counters": ([C.c_void_p, _vp, _vp], C.c_int),
+    "spl_mcts_pool_state": ([C.c_void_p, _vp, _vp], C.c_int),
+    "spl_mcts_pool_pages": ([C.c_void_p, _vp], C.c_int),
     "spl_mcts_set_roots": ([C.c_void_p, _vp, C.c_int, C.c_int, _vp], C.c_int),
     "spl_mcts_set_roots_active": ([C.c_void_p, _vp, _vp, C.c_int, C.c_int, _vp], C.c_int),
     "spl_mcts_pick_best": ([C.c_void_p, _vp, C.c_uint32, C.c_uint32, _vp, _vp], C.c_int),
@@ -78,7 +80,8 @@ class MctsConfig(C.Structure):
                 ("dirichlet_alpha", C.c_double), ("dirichlet_temp", C.c_double),
                 ("temp_threshold", C.c_int), ("node_cap", C.c_int), ("edge_cap", C.c_int),
                 ("seed", C.c_uint64), ("board_base", C.c_uint32), ("selfplay", C.c_int),
-                ("out_cap", C.c_int), ("node_boards", C.c_int)]
+                ("out_cap", C.c_int), ("node_boards", C.c_int), ("pool_nodes", C.c_longlong),
+                ("pool_edges", C.c_longlong)]
 
 
 def exported_symbols():

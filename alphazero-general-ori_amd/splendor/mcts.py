@@ -21,17 +21,19 @@ import torch
 from . import _lib
 from .env import ACTIONS, MASK_WORDS, _ptr
 
-# TreeHdr (csrc/mcts_device.h), 144 bytes
+# TreeHdr (csrc/mcts_device.h), 176 bytes
 HDR_DTYPE = np.dtype([
     ("node_count", "<i4"), ("edge_count", "<i4"), ("root", "<i4"), ("sims_done", "<i4"),
     ("budget", "<i4"), ("full", "<i4"), ("noise_pending", "<i4"), ("depth", "<i4"),
     ("leaf_kind", "<i4"), ("player", "<i4"), ("episode_step", "<i4"), ("move_no", "<i4"),
     ("game_no", "<i4"), ("overflow", "<i4"), ("n_examples", "<i4"), ("leaf_round", "<i4"),
     ("leaf_k0", "<u8"), ("leaf_k1", "<u8"), ("leaf_v", "<f4", (4,)),
-    ("games_done", "<i4"), ("forced", "<i4"), ("pad0", "<i4"), ("root_eb", "<i4"),
-    ("prunes", "<i4"), ("resets", "<i4"), ("unexpanded", "<i4"), ("root_ec", "<i4"),
-    ("gc_state", "<i4"), ("pad1", "<i4"), ("pad2", "<i4"), ("pad3", "<i4")])
-assert HDR_DTYPE.itemsize == 144
+    ("games_done", "<i4"), ("forced", "<i4"), ("moves", "<i4"), ("root_ec", "<i4"),
+    ("prunes", "<i4"), ("resets", "<i4"), ("unexpanded", "<i4"), ("gc_state", "<i4"),
+    ("root_eb", "<i8"), ("enext", "<i8"),
+    ("npg", "<i4"), ("epg", "<i4"), ("eleft", "<i4"), ("live_gc", "<i4"),
+    ("root_round", "<i4"), ("gc_queued", "<i4"), ("withdrawals", "<i4"), ("gcs", "<i4")])
+assert HDR_DTYPE.itemsize == 176
 
 DEFAULT_ARGS = dict(numMCTSSims=100, cpuct=1.0, fpu=0.0, prob_fullMCTS=1.0, ratio_fullMCTS=5,
                     forced_playouts=False, dirichletAlpha=0.0, temperature=[1.25, 0.8],
@@ -64,7 +66,8 @@ class HashEvaluator:
 
 class BatchedMCTS:
     def __init__(self, engine, B, args=None, evaluator=None, dirichlet_noise=False, seed=0x5EED,
-                 board_base=0, node_cap=None, edge_cap=None, selfplay=False, node_boards=None):
+                 board_base=0, node_cap=None, edge_cap=None, selfplay=False, node_boards=None,
+                 pool_nodes=None, pool_edges=None, mem_budget=None):
         self.e = engine
         self.L = engine.L
         self.B = B
@@ -85,7 +88,8 @@ class BatchedMCTS:
         cfg.selfplay = int(bool(selfplay))
         cfg.out_cap = int(getattr(self, "_selfplay_out_cap", 0))
         cfg.node_boards = 1 if node_boards is None else int(bool(node_boards))
-        cfg.node_cap, cfg.edge_cap = self._caps(engine, B, sims, cfg, node_cap, edge_cap, node_boards is None)
+        self._plan(engine, B, sims, cfg, node_cap, edge_cap, pool_nodes, pool_edges, node_boards is None,
+                   mem_budget)
         self.cfg = cfg
         h = C.c_void_p()
         _lib.check(self.L.spl_mcts_create(engine.ctx, B, C.byref(cfg), C.byref(h)), "spl_mcts_create")
@@ -97,45 +101,68 @@ class BatchedMCTS:
         self.evaluator = evaluator or HashEvaluator(engine)
         self._hdr = torch.empty((B, HDR_DTYPE.itemsize // 4), dtype=torch.int32, device=dev)
 
-    MEM_FRACTION = 0.8     # of the device's free memory a default-sized arena may take
+    MEM_FRACTION = 0.8      # of the device's free memory a default-sized arena may take
+    EDGES_PER_NODE = 20     # pool edge:node ratio (live trees: 15-21 edges per node, profiles/r03_tree_sizes_*)
+    NODE_MAX = 45056        # per-tree node maximum (transposition table 64 K slots at most)
 
-    def _caps(self, engine, B, sims, cfg, node_cap, edge_cap, auto_boards=False):
-        """Per-tree pool sizes. A search adds at most `sims` nodes, but the
-        kept table (every node whose round exceeds the root's, MCTS.py semantics) keeps
-        growing through a game: at genbu's arguments and 100 simulations, steady-state
-        trees reach ~1,850 nodes / 50 K edges (tools/tree_sizes.py, 15-19 edges per node on
-        average). Default: 16 x sims + 256 node slots, 32 edges per slot (garbage is only
-        collected when a search would not fit, so the slots also hold dead nodes); when B
-        such trees do not fit MEM_FRACTION of the free HBM, 24 edges per slot and as many
-        slots as fit (searches then start on pruned trees under pressure, counted in the
-        tree headers). Node boards (cfg.node_boards, a speed option) are kept unless the
-        caller chose (auto_boards False); under memory pressure they are dropped first, so
-        capacity (the reference's exact table) wins over descent speed."""
-        if node_cap and edge_cap:
-            return int(node_cap), int(edge_cap)
-        nc = int(node_cap or 16 * sims + 256)
+    @staticmethod
+    def default_node_cap(sims):
+        """Per-tree node maximum: live self-play trees reach ~18 x sims nodes at 100
+        simulations and ~22 x sims at 1,600 (profiles/r03_tree_sizes_*: max 1,845 / 35,407);
+        lazy collection lets a tree hold up to twice its live size, so 64 x sims + 4,096,
+        at most NODE_MAX."""
+        return min(64 * sims + 4096, BatchedMCTS.NODE_MAX)
+
+    def _plan(self, engine, B, sims, cfg, node_cap, edge_cap, pool_nodes, pool_edges, auto_boards, mem_budget):
+        """Tree maxima and the shared pools. node_cap / edge_cap: the largest
+        single tree (transposition table, page tables); pool_nodes / pool_edges: node slots
+        and edges shared by all B trees. Explicit caps without pools keep the static
+        layout (pool = B x cap). Default: pools fill MEM_FRACTION of the free HBM (or
+        mem_budget bytes) at EDGES_PER_NODE edges per node slot; node boards (a speed
+        option) are kept when the pools then still hold 8 x sims + 512 node slots per tree,
+        else dropped first: capacity (the reference's exact table) wins over descent speed."""
+        nc = int(node_cap or self.default_node_cap(sims))
         ec = int(edge_cap or 32 * nc)
+        cfg.node_cap, cfg.edge_cap = nc, ec
+        cfg.pool_nodes, cfg.pool_edges = int(pool_nodes or 0), int(pool_edges or 0)
+        if (node_cap or edge_cap) and not (pool_nodes or pool_edges):
+            return                                          # static: B x caps
+        if pool_nodes and pool_edges:
+            return
+        if engine.device.type != "cuda":
+            cfg.pool_nodes = cfg.pool_nodes or B * nc
+            cfg.pool_edges = cfg.pool_edges or B * ec
+            return
+        budget = int(mem_budget) if mem_budget else int(self.MEM_FRACTION * torch.cuda.mem_get_info(engine.device)[0])
+        R = self.EDGES_PER_NODE
 
-        def plan(nc_, ec_):
-            cfg.node_cap, cfg.edge_cap = int(nc_), int(ec_)
+        def plan(pn):
+            cfg.pool_nodes, cfg.pool_edges = int(pn), int(pn) * R
             return int(self.L.spl_mcts_plan_bytes(engine.ctx, B, C.byref(cfg)))
-        if engine.device.type != "cuda" or (node_cap or edge_cap):
-            return nc, ec
-        free = torch.cuda.mem_get_info(engine.device)[0]
-        limit = int(self.MEM_FRACTION * free)
-        if plan(nc, ec) <= limit:
-            return nc, ec
-        if auto_boards and cfg.node_boards:
+
+        def fit():
+            lo = plan(B * 64)
+            per = (plan(B * 64 + (1 << 20)) - lo) / float(1 << 20)
+            return max(B * 64, int((budget - lo) / per) + B * 64 - 4096)
+        pn = fit()
+        if auto_boards and cfg.node_boards and pn < B * (8 * sims + 512):
             cfg.node_boards = 0
-            if plan(nc, ec) <= limit:
-                return nc, ec
-        ratio = 24
-        lo = plan(64, 64 * ratio)
-        per = (plan(1064, 1064 * ratio) - lo) / 1000.0
-        nc = max(64, int((limit - lo) / per) + 64)
-        while nc > 64 and plan(nc, nc * ratio) > limit:
-            nc = int(nc * 0.97)
-        return nc, nc * ratio
+            pn = fit()
+        while pn > B * 64 and plan(pn) > budget:
+            pn = int(pn * 0.98)
+        cfg.pool_nodes, cfg.pool_edges = int(pool_nodes or pn), int(pool_edges or pn * R)
+
+    def pool_state(self):
+        """(free node pages, free edge pages, failed node-page requests, failed edge-page
+        requests) of the shared pools, and their sizes in pages."""
+        out = torch.empty(4, dtype=torch.int32, device=self.e.device)
+        _lib.check(self.L.spl_mcts_pool_state(self.h, _ptr(out), self.e._s()), "spl_mcts_pool_state")
+        pages = (C.c_longlong * 4)()
+        _lib.check(self.L.spl_mcts_pool_pages(self.h, pages), "spl_mcts_pool_pages")
+        f = out.tolist()
+        return {"free_node_pages": f[0], "free_edge_pages": f[1], "node_page_misses": f[2],
+                "edge_page_misses": f[3], "node_pages": int(pages[0]), "edge_pages": int(pages[1]),
+                "nodes_per_page": int(pages[2]), "edges_per_page": int(pages[3])}
 
     def __del__(self):
         if getattr(self, "h", None) is not None:
@@ -152,6 +179,15 @@ class BatchedMCTS:
         h = self.headers() if hdr is None else hdr
         return {"prunes": int(h["prunes"].sum()), "resets": int(h["resets"].sum()),
                 "unexpanded": int(h["unexpanded"].sum())}
+
+    def check_capacity(self, allow=False, hdr=None):
+        """Raise EngineError on any capacity event (a search that deviated from the
+        reference's table) unless allow; returns the events."""
+        ev = self.capacity_events(hdr)
+        if not allow and any(ev.values()):
+            raise _lib.EngineError(f"capacity events {ev}: searches deviated from the reference table "
+                                   f"(raise node_cap / pool sizes)")
+        return ev
 
     # ---------------------------------------------------------------- primitives
     def set_roots(self, roots, keep_tree=True, force_full=True):
@@ -229,6 +265,12 @@ class BatchedMCTS:
         hdr = self.headers()
         if hdr["overflow"].any():
             raise _lib.EngineError(f"tree capacity exceeded on {int((hdr['overflow'] != 0).sum())} trees")
+        ev = self.capacity_events(hdr)
+        if any(ev.values()) and not getattr(self, "_warned_capacity", False):
+            import warnings
+            warnings.warn(f"BatchedMCTS capacity events {ev}: some searches ran on pruned trees or "
+                          f"left leaves unstored (raise node_cap / the pools)")
+            self._warned_capacity = True
         counts, _, probs, q = self.root_stats()
         return probs, q, torch.from_numpy(hdr["full"] != 0), counts
 

@@ -26,12 +26,14 @@ class SelfPlay(BatchedMCTS):
     are counted and `drain` raises)."""
 
     def __init__(self, engine, B, args=None, evaluator=None, dirichlet_noise=True, seed=0x5EED,
-                 board_base=0, out_cap=None, node_cap=None, edge_cap=None, node_boards=None):
+                 board_base=0, out_cap=None, node_cap=None, edge_cap=None, node_boards=None,
+                 pool_nodes=None, pool_edges=None, mem_budget=None):
         self._selfplay_out_cap = int(out_cap or B * (62 * engine.n + 2))
         self._dropped_seen = 0
         super().__init__(engine, B, args, evaluator, dirichlet_noise=dirichlet_noise, seed=seed,
                          board_base=board_base, node_cap=node_cap, edge_cap=edge_cap, selfplay=True,
-                         node_boards=node_boards)
+                         node_boards=node_boards, pool_nodes=pool_nodes, pool_edges=pool_edges,
+                         mem_budget=mem_budget)
         self.graph = None
         self.graph_k = None
 
@@ -123,34 +125,65 @@ class SelfPlay(BatchedMCTS):
 
     def stats(self):
         h = self.headers()
-        return {"games_done": int(h["games_done"].sum()), "moves": int(h["pad0"].sum()),
+        return {"games_done": int(h["games_done"].sum()), "moves": int(h["moves"].sum()),
+                "withdrawals": int(h["withdrawals"].sum()), "collections": int(h["gcs"].sum()),
                 "overflow": int((h["overflow"] != 0).sum()),
                 "nodes_max": int(h["node_count"].max()), "edges_max": int(h["edge_count"].max()),
                 "leaf_depth_mean": float(h["depth"].mean()), "leaf_depth_max": int(h["depth"].max()),
                 **self.capacity_events(h), "examples_dropped": self.dropped_examples()}
 
 
+def pack_examples(examples):
+    """Columns -> one fixed-size byte record per example ([E, bytes] uint8), in key order;
+    returns (records, layout) for unpack_examples."""
+    E = next(iter(examples.values())).shape[0]
+    cols, layout = [], []
+    for key, t in examples.items():
+        row = 1
+        for d in t.shape[1:]:
+            row *= int(d)
+        b = t.contiguous().reshape(E, row).view(torch.uint8)
+        cols.append(b)
+        layout.append((key, t.dtype, tuple(t.shape[1:]), b.shape[1]))
+    return torch.cat(cols, 1), layout
+
+
+def unpack_examples(records, layout):
+    out, off = {}, 0
+    E = records.shape[0]
+    for key, dtype, shape, nb in layout:
+        col = torch.empty((E, nb), dtype=torch.uint8, device=records.device)
+        col.copy_(records[:, off:off + nb])
+        out[key] = col.view(dtype).reshape((E,) + shape)
+        off += nb
+    return out
+
+
 def gather_examples(examples, group=None):
-    """Episode-end exchange across ranks (torch.distributed all_gather; RCCL on ROCm):
-    sizes first, then records padded to the largest shard."""
+    """Episode-end exchange across ranks (torch.distributed, RCCL on
+    ROCm): every example packed into one fixed-size byte record (board, pi, valids, winner,
+    scdiff, surprise, meta), then one all_gather of the counts and one all_gather of the
+    records padded to the largest shard; rank order and per-rank example order preserved.
+    Under the gloo backend device tensors travel through host memory."""
     import torch.distributed as dist
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return examples
     world = dist.get_world_size(group)
-    any_t = next(iter(examples.values()))
-    k = torch.tensor([any_t.shape[0]], dtype=torch.int64, device=any_t.device)
+    rec, layout = pack_examples(examples)
+    dev = rec.device
+    if dist.get_backend(group) == "gloo" and dev.type == "cuda":
+        rec = rec.cpu()
+    k = torch.tensor([rec.shape[0]], dtype=torch.int64, device=rec.device)
     sizes = [torch.zeros_like(k) for _ in range(world)]
     dist.all_gather(sizes, k, group=group)
     sizes = [int(s.item()) for s in sizes]
     mx = max(sizes)
-    out = {}
-    for key, t in examples.items():
-        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        pad[:t.shape[0]] = t
-        parts = [torch.zeros_like(pad) for _ in range(world)]
-        dist.all_gather(parts, pad, group=group)
-        out[key] = torch.cat([p[:s] for p, s in zip(parts, sizes)])
-    return out
+    pad = torch.zeros((mx, rec.shape[1]), dtype=torch.uint8, device=rec.device)
+    pad[:rec.shape[0]] = rec
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    allrec = torch.cat([p[:s] for p, s in zip(parts, sizes)]).to(dev)
+    return unpack_examples(allrec, layout)
 
 
 def broadcast_network(net, src=0, group=None):

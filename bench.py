@@ -1,18 +1,28 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X Splendor self-play hot path (BASELINE.json).
 
-Default workload = BASELINE config 2: 2-player Splendor, 32,768 concurrent boards per GPU,
-random-policy self-play by the fused HIP rollout kernel (canonical form -> 409-action
-legality mask -> action -> chance transition -> end check -> auto-reset). One bench "step"
-is one move of every board (a board-step); a launch runs --chunk moves
-with the boards kept on chip and writes every move's mask, action and end result to HBM.
-The line's unit is board-steps/s; the config-3 self-play object reports rollouts = MCTS
-simulations. Data are synthetic: boards start from Philox-seeded deals (seed
-0x5EED, board id) and reset on game end.
+Headline = BASELINE.json's metric, "self-play rollouts/sec (32k boards, 2p Splendor)", a
+rollout being one MCTS simulation (BASELINE.md units): BASELINE config 3, 32,768 concurrent
+self-play games per GPU, numMCTSSims=100 with genbu.pt's search arguments, SplendorNNet leaf
+evaluation by the fused fp32 MFMA kernel (random init: genbu.pt cannot be loaded safely),
+moves, examples and re-rooting on device. One bench "step" = one self-play iteration: one
+simulation (select -> network -> expand/backup) on every game plus the move commit of every
+game whose search is done. The games are first brought to a steady state (--prefill
+iterations: games at every stage, trees at their steady size — the synthetic input), then W
+warm-up steps, then exactly K timed steps; after them an extended window (--window
+iterations, default ~68 K finished games) reports capacity events, finished examples drained
++ gathered, and tree sizes.
+
+Secondary objects in the same line (N = 1 only): config 2 (env-step-only random policy,
+fused rollout kernel, board-steps/s), config 5 (4 players, 16,384 games, 400 simulations)
+and config 4's per-GPU shard (32,768 games, 1,600 simulations), each at steady state with
+its window statistics and CPU baselines (the oracle, a scalar C port of the reference, on
+one host core and on every granted core).
 
 Contract: `python bench.py --gpus N --steps K --warmup W`; for N>1 launched by
-torch.distributed.run, one rank per GPU; boards are sharded by board id (board_base =
-rank * B), no data-path collective; rank 0 prints ONE JSON line.
+torch.distributed.run, one rank per GPU; games are sharded by board id (board_base =
+rank * B), examples all-gathered over RCCL at the end of the window; rank 0 prints ONE JSON
+line.
 """
 import argparse
 import ctypes
@@ -30,6 +40,12 @@ METRIC = "self-play rollouts/sec (32k boards, 2p Splendor) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP32_MFMA_PEAK = 157.3    # TFLOP/s, dense fp32 MFMA (MI355X_MICROARCH.md)
 RAMP_S = 0.05             # untimed launches before the env window (GPU clock ramp)
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    """Progress on stderr (a long run keeps writing, so it is never taken for a hang)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def bytes_per_board_step(n):
@@ -85,6 +101,7 @@ def cpu_baseline(n, seed, target_s=5.0):
         done = L.or_random_rollouts(n, B, steps, seed, threads)
         return done, steps, time.perf_counter() - t
 
+    log("cpu baseline: rollouts")
     d1, s1, t1 = timed(1)
     T = host_threads()
     dT, sT, tT = timed(T)
@@ -95,12 +112,16 @@ def cpu_baseline(n, seed, target_s=5.0):
                             "sample": f"{B} boards x {s1} steps on 1 host core, {t1:.1f} s"}}
 
 
-def cpu_baseline_selfplay(n, seed, args, target_s=4.0):
-    """CPU reference point for config 3 (rollouts = MCTS simulations), one core: the
-    oracle's sequential search + self-play loop (hash-prior network, genbu search args)
-    timed directly, and one SplendorNNet forward at batch 1 on the CPU (PyTorch fp32, as
-    GenericNNetWrapper.predict does per leaf) timed separately; the estimate charges one
-    network call per simulation."""
+def cpu_baseline_selfplay(n, seed, sims, target_s=4.0):
+    """CPU reference point for the self-play configs (rollouts = MCTS simulations): the
+    oracle's sequential search + self-play loop (oracle/splendor_oracle.c or_selfplay_run,
+    hash-prior network, genbu search args) timed directly, plus one SplendorNNet forward at
+    batch 1 on the CPU per simulation (PyTorch fp32, as GenericNNetWrapper.predict does per
+    leaf) timed separately: value = 1 / (1/search + network). On one host core (the
+    reference's self-play is single-threaded) and on every granted core (T Python threads
+    over board shards: ctypes and torch release the GIL, so both parts run in parallel)."""
+    import threading
+    import numpy as np
     L = _oracle_lib()
     p8, pf = ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(ctypes.c_float)
     L.or_selfplay_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32,
@@ -110,48 +131,70 @@ def cpu_baseline_selfplay(n, seed, args, target_s=4.0):
                                   p8, pf, ctypes.POINTER(ctypes.c_uint64), pf, ctypes.POINTER(ctypes.c_int32), pf,
                                   ctypes.POINTER(ctypes.c_int32)]
     L.or_selfplay_run.restype = ctypes.c_int
-    import numpy as np
     R = 32 + 10 * n + n * n
-    g = dict(GENBU_ARGS, numMCTSSims=args.sims)
-    B = 16
+    g = dict(GENBU_ARGS, numMCTSSims=sims)
+    B = 8
 
-    def run(iters):
+    def search(iters, base):
         board = np.zeros((B, R, 7), np.int8)
         hdr = np.zeros((B, 8), np.int32)
         t = time.perf_counter()
-        L.or_selfplay_run(n, B, iters, seed, 0, g["numMCTSSims"], g["ratio_fullMCTS"], g["prob_fullMCTS"],
+        L.or_selfplay_run(n, B, iters, seed, base, g["numMCTSSims"], g["ratio_fullMCTS"], g["prob_fullMCTS"],
                           g["cpuct"], g["fpu"], int(g["forced_playouts"]), g["tempThreshold"],
-                          g["dirichletAlpha"], g["temperature"][0], board.ctypes.data_as(p8), hdr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 0,
+                          g["dirichletAlpha"], g["temperature"][0], board.ctypes.data_as(p8),
+                          hdr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 0,
                           None, None, None, None, None, None, None)
         return time.perf_counter() - t
 
-    probe = run(20)
-    iters = max(20, int(20 * target_s / max(probe, 1e-6)))
-    dt = run(iters)
-    tree_rate = B * iters / dt
     from splendor.nnet import random_net
     nthreads = torch.get_num_threads()
     torch.set_num_threads(1)
-    try:
-        net = random_net(n, seed=0, device="cpu")
-        x = torch.zeros((1, R, 7))
-        va = torch.ones((1, 409), dtype=torch.bool)
+    net = random_net(n, seed=0, device="cpu")
+    x = torch.zeros((1, R, 7))
+    va = torch.ones((1, 409), dtype=torch.bool)
+
+    def network(k):
         with torch.no_grad():
-            for _ in range(20):
-                net(x, va)
-            k = 300
             t = time.perf_counter()
             for _ in range(k):
                 net(x, va)
-            t_nn = (time.perf_counter() - t) / k
+            return (time.perf_counter() - t) / k
+
+    def parallel(T, fn, *args):
+        out = [None] * T
+        th = [threading.Thread(target=lambda i=i: out.__setitem__(i, fn(*args, i))) for i in range(T)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return out
+
+    log(f"cpu baseline: {n} players, {sims} sims")
+    try:
+        search(4, 0)                                     # builds the oracle's tables once
+        network(20)
+        probe = search(10, 0)
+        iters = max(10, int(10 * target_s / 2 / max(probe, 1e-6)))
+        dt1 = search(iters, 0)
+        rate1 = B * iters / dt1
+        nn1 = network(200)
+        T = host_threads()
+        dts = parallel(T, lambda it, i: search(it, B * (i + 1)), iters)
+        rateT = T * B * iters / max(dts)
+        nnT = max(parallel(T, lambda k, i: network(k), 200))
     finally:
         torch.set_num_threads(nthreads)
-    return {"value": 1.0 / (1.0 / tree_rate + t_nn), "unit": "rollouts/s (MCTS simulations)", "cores": 1,
-            "kind": "port",
-            "sample": f"oracle self-play {B} games x {iters} simulations ({dt:.1f} s, hash-prior network: "
-                      f"{tree_rate:.0f} sims/s search alone) + SplendorNNet batch-1 CPU forward "
-                      f"{t_nn * 1e6:.0f} us per leaf (PyTorch fp32, 1 thread); value = 1/(1/search + network)",
-            "search_only": tree_rate, "network_us_per_leaf": t_nn * 1e6}
+    one = 1.0 / (1.0 / rate1 + nn1)
+    allc = T / (T / rateT + nnT)
+    return {"value": allc, "unit": "rollouts/s (MCTS simulations)", "cores": T, "kind": "port",
+            "sample": f"{T} threads x oracle self-play {B} games x {iters} simulations each ({max(dts):.1f} s, "
+                      f"search alone {rateT:.0f} sims/s) + SplendorNNet batch-1 CPU forward {nnT * 1e6:.0f} us "
+                      f"per leaf per thread (PyTorch fp32, 1 intra-op thread each, all threads at once); "
+                      f"value = T / (T/search + network)",
+            "single_core": {"value": one, "cores": 1,
+                            "sample": f"{B} games x {iters} simulations ({dt1:.1f} s, search alone {rate1:.0f} "
+                                      f"sims/s) + {nn1 * 1e6:.0f} us network per leaf"},
+            "search_only": rateT, "network_us_per_leaf": nnT * 1e6}
 
 
 # saved args of the reference's only checkpoint, genbu.pt, = BASELINE config 3
@@ -167,44 +210,63 @@ def nn_flops_per_eval(n):
     return 2 * macs
 
 
-def selfplay_config_name(args):
-    """BASELINE.json config the self-play arguments correspond to (per GPU)."""
-    if args.players == 4:
-        return "config5"
-    return "config4" if args.sims >= 1600 else "config3"
+def bytes_per_rollout(n, depth):
+    """SURVEY.md §8(d) algorithmic HBM bytes of one MCTS simulation: leaf state as the f32
+    network input (4S), bool mask (409), f32 policy out (4 x 409), f32 values (4n), and the
+    path (16 B per level: P, Q, N, child). §8(d) uses the reference's measured depth 4.8
+    (3.7 KB at 2 players); `depth` = the measured mean leaf depth of the trees here."""
+    S = 7 * (32 + 10 * n + n * n)
+    return 4 * S + 409 + 4 * 409 + 4 * n + 16 * depth
 
 
-def run_selfplay(args, rank, world, dev, dist, steps=None, warmup=None):
-    """BASELINE config 3 (config 4 per GPU at N>1, config 5 with --players 4): B concurrent
-    self-play games, one MCTS simulation per game per iteration, leaves evaluated by the
-    fused SplendorNNet kernel (fp32, random init: the reference's genbu.pt cannot be loaded
-    safely), moves committed on device. Warm-up first (the games desynchronise and trees
-    reach their steady size), then a timed window of `steps` iterations (default ~3 full
-    games per board) that ends with draining the finished examples and the
-    RCCL all-gather of them; symmetry expansion is timed separately."""
+CONFIGS = {  # BASELINE.json configs: (players, games per GPU, numMCTSSims)
+    "config3": (2, 32768, 100),
+    "config4": (2, 32768, 1600),
+    "config5": (4, 16384, 400),
+}
+
+
+def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, seed, node_boards=-1,
+                 stats_every=0):
+    """Self-play at one BASELINE config: B games per GPU (shard board_base = rank * B), one
+    MCTS simulation per game per iteration, leaves evaluated by the fused SplendorNNet kernel
+    (fp32, random init), moves committed on device. `prefill` untimed iterations bring the
+    games to a steady state, `warmup` more, then exactly `steps` timed iterations (barrier +
+    synchronize on both sides, max over ranks); then `window` iterations whose statistics
+    (capacity events, games, moves) are reported, ending with the finished examples drained
+    and all-gathered over RCCL; symmetry expansion is timed after it."""
     from splendor.coach import expand_symmetries
     from splendor.env import SplendorEngine
     from splendor.nnet import LeafEvaluator, random_net
     from splendor.selfplay import SelfPlay, broadcast_network, gather_examples
-    B = args.boards
-    steps = args.steps if steps is None else steps
-    warmup = args.warmup if warmup is None else warmup
-    eng = SplendorEngine(args.players, device=dev)
-    sargs = dict(GENBU_ARGS, numMCTSSims=args.sims)
-    net = random_net(args.players, seed=rank, device=dev)
+    n, B, sims = CONFIGS[cfg]
+    eng = SplendorEngine(n, device=dev)
+    sargs = dict(GENBU_ARGS, numMCTSSims=sims)
+    net = random_net(n, seed=rank, device=dev)
     if dist:
         broadcast_network(net)                 # every rank searches with rank 0's network
     ev = LeafEvaluator(eng, net, B, use_graph=False)
-    sp = SelfPlay(eng, B, sargs, evaluator=ev, dirichlet_noise=True, seed=args.seed, board_base=rank * B,
-                  node_boards=None if args.node_boards < 0 else bool(args.node_boards))
+    sp = SelfPlay(eng, B, sargs, evaluator=ev, dirichlet_noise=True, seed=seed, board_base=rank * B,
+                  node_boards=None if node_boards < 0 else bool(node_boards))
     sp.reset()
-    sp.run(max(warmup, 9), use_graph=True)     # (captures both graphs)
+    t_fill = time.perf_counter()
+    done = 0
+    log(f"{cfg}: {B} games, {sims} sims, pools {sp.cfg.pool_nodes} nodes / {sp.cfg.pool_edges} edges, "
+        f"node boards {sp.cfg.node_boards}, {sp.device_bytes / 2**30:.1f} GiB; prefill {prefill}")
+    while done < prefill:                      # (in chunks: a sync now and then keeps the
+        k = min(2000, prefill - done)          #  host's view of progress; drained as it goes)
+        sp.run(max(k, 9), use_graph=True)
+        done += max(k, 9)
+        sp.drain(allow_drops=False)
+        torch.cuda.synchronize(dev)
+        log(f"{cfg}: prefill {done}/{prefill}")
+    prefill_s = time.perf_counter() - t_fill
+    sp.run(max(warmup, 1), use_graph=True)
     sp.drain()
-    torch.cuda.synchronize(dev)
-    st0 = sp.stats()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     ev1.record()
+    torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -212,27 +274,45 @@ def run_selfplay(args, rank, world, dev, dist, steps=None, warmup=None):
     ev0.record()
     sp.run(steps, use_graph=True)
     ev1.record()
-    torch.cuda.synchronize(dev)              # (the graph replays run asynchronously)
-    tg = time.perf_counter()
-    ex = sp.drain()
-    ex_local = int(ex["board"].shape[0])
-    if dist:
-        ex = gather_examples(ex)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    gather_s = time.perf_counter() - tg
-    st = sp.stats()
     if dist:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # symmetry expansion of the window's examples (Board.get_symmetries), outside the window
-    nsym = min(ex_local, 200000)
-    ts = time.perf_counter()
+    iter_ms_events = ev0.elapsed_time(ev1) / steps
+    # extended window: capacity events, games, examples drained + gathered
+    st0 = sp.stats()
+    pool0 = sp.pool_state()
+    ex_local = 0
+    tw = time.perf_counter()
+    done = 0
+    log(f"{cfg}: timed {steps} iterations, {elapsed:.2f} s; window {window}")
+    while done < window:
+        k = min(2000, window - done)
+        sp.run(k, use_graph=True)
+        done += k
+        if done < window:
+            ex_local += int(sp.drain()["board"].shape[0])
+            log(f"{cfg}: window {done}/{window}")
+    torch.cuda.synchronize(dev)
+    tg = time.perf_counter()
+    ex = sp.drain()
+    ex_local += int(ex["board"].shape[0])
+    if dist:
+        ex = gather_examples(ex)
+    torch.cuda.synchronize(dev)
+    gather_s = time.perf_counter() - tg
+    window_s = time.perf_counter() - tw
+    st = sp.stats()
+    pool = sp.pool_state()
+    ts = sp.tree_sizes()
+    nsym = min(int(ex["board"].shape[0]), 200000)
+    t_s = time.perf_counter()
     sym = expand_symmetries(eng, {k: v[:nsym] for k, v in ex.items()}) if nsym else None
     torch.cuda.synchronize(dev)
-    sym_s = time.perf_counter() - ts
+    sym_s = time.perf_counter() - t_s
     # the network kernel on its own: k_nn_forward over B leaves, HIP events on its stream
     nk = 20
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -243,37 +323,66 @@ def run_selfplay(args, rank, world, dev, dist, steps=None, warmup=None):
     e1.record()
     torch.cuda.synchronize(dev)
     nn_us = e0.elapsed_time(e1) / nk * 1e3
-    delta = {k: st[k] - st0[k] for k in ("games_done", "moves", "prunes", "resets", "unexpanded")}
-    return {"elapsed": elapsed, "iter_ms": ev0.elapsed_time(ev1) / steps, "stats": st, "window": delta,
-            "examples": ex_local, "examples_gathered": int(ex["board"].shape[0]), "gather_s": gather_s,
-            "symmetry": {"examples": nsym, "variants": int(sym["board"].shape[0]) if sym else 0, "s": sym_s},
-            "device_bytes": sp.device_bytes, "node_cap": int(sp.cfg.node_cap), "edge_cap": int(sp.cfg.edge_cap), "node_boards": int(sp.cfg.node_boards),
-            "nn_kernel_us": nn_us}
+    keys = ("games_done", "moves", "prunes", "resets", "unexpanded", "withdrawals", "collections")
+    delta = {k: st[k] - st0[k] for k in keys}
+    delta["iterations"] = window
+    delta["seconds"] = window_s
+    delta["rollouts_per_s"] = world * B * window / window_s
+    delta["node_page_misses"] = pool["node_page_misses"] - pool0["node_page_misses"]
+    delta["edge_page_misses"] = pool["edge_page_misses"] - pool0["edge_page_misses"]
+    delta["events_per_1000_moves"] = {k: 1000.0 * delta[k] / max(1, delta["moves"])
+                                      for k in ("prunes", "resets", "unexpanded")}
+    delta["examples_drained"] = ex_local
+    delta["examples_gathered"] = int(ex["board"].shape[0])
+    delta["drain_allgather_s"] = gather_s
+    live_n, live_e = ts[:, 2].astype("int64"), ts[:, 3].astype("int64")
+    tree = {"nodes_max": st["nodes_max"], "edges_max": st["edges_max"],
+            "live_nodes_mean": float(live_n.mean()), "live_nodes_max": int(live_n.max()),
+            "live_edges_mean": float(live_e.mean()), "live_edges_max": int(live_e.max()),
+            "leaf_depth_mean": st["leaf_depth_mean"], "leaf_depth_max": st["leaf_depth_max"],
+            "overflow": st["overflow"], "examples_dropped": st["examples_dropped"],
+            "node_cap_per_tree": int(sp.cfg.node_cap), "pool_nodes": int(sp.cfg.pool_nodes),
+            "pool_edges": int(sp.cfg.pool_edges), "node_boards": int(sp.cfg.node_boards),
+            "device_bytes": sp.device_bytes,
+            "pool_free_at_end": {"node_pages": pool["free_node_pages"], "of": pool["node_pages"],
+                                 "edge_pages": pool["free_edge_pages"], "of_edge": pool["edge_pages"]}}
+    res = {"elapsed": elapsed, "iter_ms_events": iter_ms_events, "window": delta, "tree": tree,
+           "prefill": prefill, "prefill_s": prefill_s,
+           "symmetry": {"examples": nsym, "variants": int(sym["board"].shape[0]) if sym else 0, "s": sym_s},
+           "nn_kernel_us": nn_us}
+    del sp, ev, net
+    return res
 
 
-def selfplay_record(args, r, world, steps, warmup):
-    """Secondary object of the bench line for the self-play workload."""
-    B = args.boards
-    fl = nn_flops_per_eval(args.players) * B
-    return {"workload": f"{selfplay_config_name(args)}: batched self-play, numMCTSSims={args.sims}, genbu args, "
-                        "SplendorNNet fp32 leaf eval (random init), device move commit",
+def selfplay_record(cfg, r, world, steps, warmup):
+    """The JSON object of one self-play config."""
+    n, B, sims = CONFIGS[cfg]
+    fl = nn_flops_per_eval(n) * B
+    return {"workload": f"{cfg}: {n}-player batched self-play, {B} games per GPU, numMCTSSims={sims}, genbu "
+                        "search args, SplendorNNet fp32 leaf eval (random init), device move commit",
             "value": world * B * steps / r["elapsed"], "unit": "rollouts/s (MCTS simulations)",
-            "ms_per_iteration": r["elapsed"] / steps * 1e3, "steps": steps, "warmup": warmup,
-            "window": {**r["window"], "examples_drained": r["examples"], "examples_gathered": r["examples_gathered"],
-                       "drain_allgather_s": r["gather_s"]},
-            "tree": {k: r["stats"][k] for k in ("nodes_max", "edges_max", "leaf_depth_mean", "leaf_depth_max",
-                                                 "overflow", "examples_dropped")}
-                    | {"node_cap": r["node_cap"], "edge_cap": r["edge_cap"], "device_bytes": r["device_bytes"], "node_boards": r["node_boards"]},
-            "symmetry_expansion": r["symmetry"],
-            "network_kernel": {"kernel": f"k_nn_forward<{args.players}>", "avg_us": r["nn_kernel_us"],
+            "ms_per_iteration": r["elapsed"] / steps * 1e3, "ms_per_iteration_events": r["iter_ms_events"],
+            "steps": steps, "warmup": warmup, "prefill_iterations": r["prefill"], "prefill_s": r["prefill_s"],
+            "window": r["window"], "tree": r["tree"], "symmetry_expansion": r["symmetry"],
+            "network_kernel": {"kernel": f"k_nn_forward<{n}>", "avg_us": r["nn_kernel_us"],
                                "tflops": fl / (r["nn_kernel_us"] * 1e-6) / 1e12,
                                "frac_fp32_mfma_peak": fl / (r["nn_kernel_us"] * 1e-6) / 1e12 / FP32_MFMA_PEAK,
                                "note": "k_nn_forward alone over B leaves (HIP events, 20 launches)"}}
 
 
+def load_json_profile(pattern):
+    """The newest committed summary matching profiles/<pattern> (sorted names: rNN order)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    if not paths:
+        return None
+    with open(paths[-1]) as f:
+        return dict(json.load(f), file=os.path.relpath(paths[-1], ROOT))
+
+
 def load_traffic(path, B, moves):
-    """The newest committed rocprofv3 --pmc summary of this workload (profiles/
-    rNN_rollout_pmc.json, tools/pmc_rollout.sh; HBM bytes corrected as DESIGN.md §6
+    """The newest committed rocprofv3 --pmc summary of the rollout workload (profiles/
+    rNN_rollout_pmc*.json, tools/pmc_rollout.sh; HBM bytes corrected as DESIGN.md §5
     describes), if it was taken at this board count and launch size."""
     import glob
     paths = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_rollout_pmc*.json")))
@@ -288,73 +397,52 @@ def load_traffic(path, B, moves):
     return best
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--boards", type=int, default=32768, help="boards per GPU")
-    ap.add_argument("--players", type=int, default=2)
-    ap.add_argument("--seed", type=int, default=0x5EED)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=None)
-    ap.add_argument("--workload", choices=("env", "selfplay"), default="env")
-    ap.add_argument("--sims", type=int, default=100, help="selfplay: numMCTSSims")
-    ap.add_argument("--no-selfplay", action="store_true",
-                    help="env workload: skip the secondary config-3 self-play measurement")
-    ap.add_argument("--selfplay-steps", type=int, default=10000,
-                    help="env workload: timed self-play iterations (~3 full games per board)")
-    ap.add_argument("--selfplay-warmup", type=int, default=3000,
-                    help="env workload: untimed self-play iterations first (games finish, trees grow)")
-    ap.add_argument("--chunk", type=int, default=100, help="env: moves per rollout launch")
-    ap.add_argument("--node-boards", type=int, default=-1, help="selfplay: 1/0 force node boards on/off "
-                    "(default: on unless the pools do not fit)")
-    args = ap.parse_args()
+def selfplay_roofline(rec, n, depth):
+    """Roofline block of the headline: the dominant kernel is k_nn_forward (MFMA-bound, fp32):
+    achieved = 1.19 MFLOP per leaf x B leaves / its HIP-event launch time. traffic = its HBM
+    bytes per launch from the newest committed PMC summary (profiles/rNN_selfplay_pmc.json,
+    tools/pmc_selfplay.sh); the tree kernels' measured bytes per simulation are set beside
+    SURVEY §8(d)'s algorithmic figure."""
+    nk = rec["network_kernel"]
+    prof = load_json_profile("r*_selfplay_pmc.json")
+    kern = (prof or {}).get("kernels", {})
+    B = CONFIGS["config3"][1]
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    def per_sim(k):
+        v = kern.get(k, {}).get("hbm_bytes_per_launch")
+        return v / B if v else None
+    tree = {k: {"hbm_bytes_per_sim": per_sim(k), "avg_us_rocprof": kern.get(k, {}).get("avg_us")}
+            for k in ("k_select", "k_backup", "k_leaf_mask", "k_commit", "k_gc")}
+    tot = sum(v["hbm_bytes_per_sim"] or 0.0 for v in tree.values())
+    return {"bound": "mfma", "achieved": nk["tflops"], "peak": FP32_MFMA_PEAK, "unit": "TFLOP/s",
+            "frac": nk["frac_fp32_mfma_peak"],
+            "traffic": kern.get("k_nn_forward", {}).get("hbm_bytes_per_launch"),
+            "kernel": nk["kernel"], "kernel_avg_us": nk["avg_us"],
+            "kernel_avg_us_rocprof": kern.get("k_nn_forward", {}).get("avg_us"),
+            "flop_per_launch": nn_flops_per_eval(n) * B,
+            "tree_kernels": {"per_kernel": tree, "hbm_bytes_per_sim_total": tot or None,
+                             "algorithmic_bytes_per_sim_survey": bytes_per_rollout(n, 4.8),
+                             "algorithmic_bytes_per_sim_at_measured_depth": bytes_per_rollout(n, depth),
+                             "note": "PMC FETCH_SIZE x1024 x2 (gfx950) + WRITE_SIZE x1024 per launch / B"},
+            "pmc_file": (prof or {}).get("file")}
 
-    if args.workload == "selfplay":
-        r = run_selfplay(args, rank, world, dev, dist)
-        if rank == 0:
-            B, K = args.boards, args.steps
-            rec = selfplay_record(args, r, world, K, args.warmup)
-            nk = rec["network_kernel"]
-            print(json.dumps({
-                "metric": METRIC, "value": rec["value"], "unit": "rollouts/s (MCTS simulations)",
-                "n_gpus": world, "steps": K, "warmup": args.warmup,
-                "ms_per_step": rec["ms_per_iteration"], "higher_is_better": True, "scaling": "weak",
-                "vs_baseline": None, "dtype": "fp32 (network) / int8 (boards) / f64 (tree stats)",
-                "data": "synthetic (Philox-seeded deals), random-init SplendorNNet",
-                "config": {"workload": rec["workload"], "players": args.players, "games_per_gpu": B,
-                           "global_games": world * B,
-                           "parallelism": f"dp{world} (game shards; RCCL all-gather of examples)"},
-                "roofline": {"bound": "mfma", "achieved": nk["tflops"], "peak": FP32_MFMA_PEAK, "unit": "TFLOP/s",
-                             "frac": nk["frac_fp32_mfma_peak"], "traffic": None, "kernel": nk["kernel"],
-                             "kernel_avg_us": nk["avg_us"]},
-                "selfplay": rec, "cpu_baseline": None}))
-        if dist:
-            dist.destroy_process_group()
-        return
 
+def run_env(args, rank, world, dev, dist, K, warmup, cpu=True):
+    """BASELINE config 2: 32,768 boards, uniform-random legal actions, fused rollout kernel
+    (canonical form -> mask -> action -> chance step -> end check -> auto-reset), K moves in
+    launches of --chunk moves, HIP events on the launch stream around the timed launches."""
     from splendor.env import RolloutBatch, SplendorEngine
-    eng = SplendorEngine(args.players, device=dev)
+    eng = SplendorEngine(args.players if args.workload == "env" else 2, device=dev)
+    n = eng.n
     B = args.boards
     rb = RolloutBatch(eng, B, seed=args.seed, board_base=rank * B)
-    K, chunk = args.steps, max(1, min(args.chunk, args.steps))
+    chunk = max(1, min(args.chunk, K))
     launches = [chunk] * (K // chunk) + ([K % chunk] if K % chunk else [])
     outs = {}
+
     def run(k):
         outs[k] = rb.run(k, out=outs.get(k))
-    w = args.warmup
+    w = warmup
     while w > 0:
         run(min(chunk, w))
         w -= chunk
@@ -371,10 +459,6 @@ def main():
         if ramp % 16 == 0:
             torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
-
-    # HIP events on the stream the kernel is launched on (torch's current stream): one
-    # pair around the back-to-back launches -> average launch duration (recorded once before:
-    # torch creates the HIP event at its first record, which must not land in the window)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     ev1.record()
@@ -397,62 +481,129 @@ def main():
         elapsed = float(t.item())
     kernel_ms = ev0.elapsed_time(ev1) / len(launches)
     games = int(rb.games.sum().item())
+    del rb, outs, launchers
+    torch.cuda.empty_cache()
+    step_b = bytes_per_board_step(n)
+    achieved = step_b * B * chunk / (kernel_ms * 1e-3) / 1e9
+    moved = bytes_per_board_launch(n, chunk)
+    moved_gbs = moved * B / (kernel_ms * 1e-3) / 1e9
+    prof = load_traffic(args.traffic_json, B, chunk)
+    traffic = prof.get("hbm_bytes_per_launch") if prof else None
+    issue = ({k: prof.get(k) for k in ("valu_insts_per_board_move", "valu_issue_frac", "effective_clock_ghz",
+                                        "kernel_avg_us_rocprof", "file")}
+             if prof else None)
+    rec = {"workload": "config2: env-step-only random-policy self-play, fused canonical+mask+action+chance "
+                       "step+end check+auto-reset",
+           "value": world * B * K / elapsed, "unit": "board-steps/s", "steps": K, "warmup": warmup,
+           "ms_per_step": elapsed / K * 1e3, "players": n, "boards_per_gpu": B, "moves_per_launch": chunk,
+           "roofline": {"bound": "valu-latency", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                        "kernel": f"k_rollout<{n}>", "kernel_avg_us": kernel_ms * 1e3,
+                        "algorithmic_bytes_per_board_step": step_b,
+                        "algorithmic_bytes_per_launch": step_b * B * chunk,
+                        "moved_bytes_per_launch": moved * B, "moved_gbs": moved_gbs,
+                        "moved_frac": moved_gbs / HBM_PEAK_GBS,
+                        "limiter": "VALU issue + per-move dependency chains (PMC: ~22-25 % of VALU issue peak, "
+                                   "~10 % of HBM); boards stay on chip for the launch, so 'achieved' is the "
+                                   "SURVEY 8(d) algorithmic rate of a one-kernel-per-step design",
+                        "pmc": issue},
+           "games_completed": games, "untimed_ramp_launches": ramp}
+    if cpu:
+        rec["cpu_baseline"] = cpu_baseline(n, args.seed)
+    return rec
 
-    cpu = None                                 # (after the GPU window: the CPU sample runs for seconds)
-    if rank == 0 and world == 1 and args.gpus == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.players, args.seed)
 
-    secondary = None
-    if not args.no_selfplay:
-        del rb, outs
-        torch.cuda.empty_cache()
-        r = run_selfplay(args, rank, world, dev, dist, steps=args.selfplay_steps, warmup=args.selfplay_warmup)
-        secondary = selfplay_record(args, r, world, args.selfplay_steps, args.selfplay_warmup)
-        if rank == 0 and not args.no_cpu_baseline and world == 1:
-            secondary["cpu_baseline"] = cpu_baseline_selfplay(args.players, args.seed, args)
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000, help="timed self-play iterations (headline)")
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--prefill", type=int, default=3000, help="untimed iterations to the steady state first")
+    ap.add_argument("--window", type=int, default=10000, help="statistics window after the timed steps")
+    ap.add_argument("--boards", type=int, default=32768, help="env workload: boards per GPU")
+    ap.add_argument("--players", type=int, default=2, help="env workload: players")
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=None)
+    ap.add_argument("--workload", choices=("all", "selfplay", "env", "config3", "config4", "config5"), default="all",
+                    help="all: config-3 headline + config 2/5/4 objects (N=1); selfplay = config3 alone")
+    ap.add_argument("--no-secondary", action="store_true", help="all: the headline only")
+    ap.add_argument("--chunk", type=int, default=100, help="env: moves per rollout launch")
+    ap.add_argument("--env-steps", type=int, default=1000, help="config-2 object: timed moves")
+    ap.add_argument("--c5-prefill", type=int, default=40000)
+    ap.add_argument("--c5-window", type=int, default=6000)
+    ap.add_argument("--c4-prefill", type=int, default=45000)
+    ap.add_argument("--c4-window", type=int, default=4000)
+    ap.add_argument("--node-boards", type=int, default=-1, help="selfplay: 1/0 force node boards on/off "
+                    "(default: on unless the pools do not fit)")
+    args = ap.parse_args()
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    t_start = time.perf_counter()
+
+    if args.workload == "env":
+        rec = run_env(args, rank, world, dev, dist, args.steps, args.warmup,
+                      cpu=rank == 0 and world == 1 and not args.no_cpu_baseline)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": rec["value"], "unit": rec["unit"], "n_gpus": world,
+                              "steps": args.steps, "warmup": args.warmup, "ms_per_step": rec["ms_per_step"],
+                              "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+                              "data": "synthetic (Philox-seeded deals, uniform-random legal actions)",
+                              "config": {"workload": rec["workload"], "players": rec["players"],
+                                         "boards_per_gpu": rec["boards_per_gpu"],
+                                         "parallelism": f"dp{world} (board shards, no data-path collective)"},
+                              "roofline": rec["roofline"], "cpu_baseline": rec.get("cpu_baseline")}))
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    head = "config3" if args.workload in ("all", "selfplay") else args.workload
+    n, B, sims = CONFIGS[head]
+    r = run_selfplay(head, rank, world, dev, dist, args.steps, args.warmup, args.prefill, args.window, args.seed,
+                     args.node_boards)
+    rec = selfplay_record(head, r, world, args.steps, args.warmup)
+    torch.cuda.empty_cache()
+    extra = {}
+    secondary = args.workload == "all" and world == 1 and not args.no_secondary
+    cpu_ok = rank == 0 and world == 1 and not args.no_cpu_baseline
+    if cpu_ok:
+        rec["cpu_baseline"] = cpu_baseline_selfplay(n, args.seed, sims)
+    if secondary:
+        extra["config2_env"] = run_env(args, rank, world, dev, dist, args.env_steps, 100, cpu=cpu_ok)
+        for cfg, pf, win in (("config5", args.c5_prefill, args.c5_window), ("config4", args.c4_prefill, args.c4_window)):
+            rr = run_selfplay(cfg, rank, world, dev, dist, 1000, 100, pf, win, args.seed, args.node_boards)
+            o = selfplay_record(cfg, rr, world, 1000, 100)
+            if cpu_ok:
+                o["cpu_baseline"] = cpu_baseline_selfplay(CONFIGS[cfg][0], args.seed, CONFIGS[cfg][2],
+                                                          target_s=2.0 if cfg == "config4" else 4.0)
+            extra[{"config5": "config5_selfplay", "config4": "config4_shard"}[cfg]] = o
+            torch.cuda.empty_cache()
     if rank == 0:
-        step_b = bytes_per_board_step(args.players)
-        achieved = step_b * B * chunk / (kernel_ms * 1e-3) / 1e9
-        moved = bytes_per_board_launch(args.players, chunk)
-        moved_gbs = moved * B / (kernel_ms * 1e-3) / 1e9
-        prof = load_traffic(args.traffic_json, B, chunk)
-        traffic = prof.get("hbm_bytes_per_launch") if prof else None
-        issue = ({k: prof.get(k) for k in ("valu_insts_per_board_move", "valu_issue_frac", "effective_clock_ghz",
-                                            "kernel_avg_us_rocprof", "file")}
-                 if prof else None)
+        cpu = rec.get("cpu_baseline")
         out = {
-            "metric": METRIC,
-            "value": world * B * K / elapsed,
-            "unit": "board-steps/s",
-            "n_gpus": world,
-            "steps": K,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / K * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int8",
-            "data": "synthetic (Philox-seeded deals, uniform-random legal actions)",
-            "config": {"workload": "config2: env-step-only random-policy self-play, fused "
-                                   "canonical+mask+action+chance step+end check+auto-reset",
-                       "players": args.players, "boards_per_gpu": B, "global_boards": world * B,
-                       "moves_per_launch": chunk,
-                       "parallelism": f"dp{world} (board shards, no data-path collective)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": f"k_rollout<{args.players}>", "kernel_avg_us": kernel_ms * 1e3,
-                         "moves_per_launch": chunk, "algorithmic_bytes_per_board_step": step_b,
-                         "algorithmic_bytes_per_launch": step_b * B * chunk,
-                         "moved_bytes_per_launch": moved * B, "moved_gbs": moved_gbs,
-                         "moved_frac": moved_gbs / HBM_PEAK_GBS,
-                         "limiter": "VALU issue + dependency latency, not HBM (boards stay on chip for the "
-                                    "launch; traffic = the measured bytes of the launch size, PMC)",
-                         "pmc": issue},
+            "metric": METRIC, "value": rec["value"], "unit": "rollouts/s (MCTS simulations)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": rec["ms_per_iteration"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32 (network) / int8 (boards) / f64 (tree statistics)",
+            "data": "synthetic (Philox-seeded deals), random-init SplendorNNet (genbu.pt is refused by the "
+                    "weights-only loader)",
+            "config": {"workload": rec["workload"], "players": n, "games_per_gpu": B, "global_games": world * B,
+                       "numMCTSSims": sims, "prefill_iterations": args.prefill,
+                       "parallelism": f"dp{world} (game shards; RCCL all-gather of examples)"},
+            "roofline": selfplay_roofline(rec, n, rec["tree"]["leaf_depth_mean"]),
             "cpu_baseline": cpu,
-            "games_completed": games,
-            "untimed_ramp_launches": ramp,
-            "config3_selfplay": secondary,
+            "selfplay": rec,
+            **extra,
+            "bench_seconds": time.perf_counter() - t_start,
         }
         print(json.dumps(out))
     if dist:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 2
+#define SPL_ABI_VERSION 3
 #define SPL_ACTIONS 409
 #define SPL_MASK_WORDS 7
 #define SPL_EINVAL (-1)
@@ -148,8 +148,9 @@ typedef struct {
     double dirichlet_alpha;  /* > 0 enables root noise at step 0 of full searches */
     double dirichlet_temp;   /* temperature[0]: softmax before noise (MCTS.py:142) */
     int temp_threshold;      /* tempThreshold (Coach.py:82-83), self-play only */
-    int node_cap;            /* nodes per tree */
-    int edge_cap;            /* CSR edges per tree */
+    int node_cap;            /* maximum node slots of one tree (its transposition table and
+                                node page table are sized for it) */
+    int edge_cap;            /* maximum CSR edges of one tree (its edge page table) */
     uint64_t seed;           /* Philox key for search/self-play randomness */
     uint32_t board_base;     /* global id of tree 0 (multi-GPU sharding) */
     int selfplay;            /* 1: trees play games (spl_mcts_reset_games / spl_mcts_commit) */
@@ -158,12 +159,17 @@ typedef struct {
                                 slot), so a descent through linked edges skips the in-tree
                                 transition (getNextState, MCTS.py:155-157) — the descent then
                                 runs one transition per simulation instead of one per level */
+    long long pool_nodes;    /* node slots shared by all B trees (0: B x node_cap) */
+    long long pool_edges;    /* edges shared by all B trees (0: B x edge_cap). Trees draw node
+                                pages (64 slots) and edge pages (1024 edges) from these pools
+                                on demand and return them when garbage is collected, so memory
+                                follows the sum of the live trees, not B x the largest one */
 } spl_mcts_config;
 
 int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_mcts **out);
 int spl_mcts_destroy(spl_mcts *m);
-/* HBM bytes of the whole search arena: trees (node_cap nodes, edge_cap edges, hash table,
- * path per tree) + self-play buffers. plan_bytes: the same figure before creating it (pool
+/* HBM bytes of the whole search arena: the shared node / edge pools, per tree its page
+ * tables, transposition table (power of two >= node_cap / 0.7) and path, + self-play buffers. plan_bytes: the same figure before creating it (pool
  * sizing by the caller); device_bytes: of a created arena. */
 long long spl_mcts_plan_bytes(const spl_ctx *ctx, int B, const spl_mcts_config *cfg);
 long long spl_mcts_device_bytes(const spl_mcts *m);
@@ -218,6 +224,12 @@ int spl_mcts_commit(spl_mcts *m, void *hip_stream);
  * so far because the queue (out_cap) was full when their game ended or a drain asked for
  * fewer than were queued. Self-play arenas only. */
 int spl_mcts_counters(spl_mcts *m, int32_t *out, void *hip_stream);
+/* out (device, 4 x i32): free node pages, free edge pages, node / edge page requests that
+ * found the pool empty so far (each such leaf was withdrawn for collection or counted as
+ * unexpanded in its tree's header). pool_pages (host): pages in the node / edge pools and
+ * their sizes (node slots / edges per page). */
+int spl_mcts_pool_state(spl_mcts *m, int32_t *out, void *hip_stream);
+int spl_mcts_pool_pages(const spl_mcts *m, long long *out4);
 int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *valid,
                             float *winner, int32_t *scdiff, float *q, int32_t *meta, int max,
                             int32_t *n_out, void *hip_stream);

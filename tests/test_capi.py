@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(LIB)
     missing = [n for n in declared() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.spl_abi_version() == 2
+    assert lib.spl_abi_version() == 3
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libsplendor_amd.so not built")
@@ -70,17 +70,20 @@ def test_mcts_config_struct_layout(tmp_path):
     from splendor import _lib
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "splendor_amd.h"\n'
-                   'int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(spl_mcts_config),'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(spl_mcts_config),'
                    'offsetof(spl_mcts_config, seed), offsetof(spl_mcts_config, node_cap),'
                    'offsetof(spl_mcts_config, dirichlet_temp), offsetof(spl_mcts_config, out_cap),'
-                   'offsetof(spl_mcts_config, node_boards));return 0;}\n')
+                   'offsetof(spl_mcts_config, node_boards), offsetof(spl_mcts_config, pool_nodes),'
+                   'offsetof(spl_mcts_config, pool_edges));return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
-    size, off_seed, off_cap, off_temp, off_out, off_nb = map(int, subprocess.check_output([str(exe)]).split())
+    size, off_seed, off_cap, off_temp, off_out, off_nb, off_pn, off_pe = map(
+        int, subprocess.check_output([str(exe)]).split())
     M = _lib.MctsConfig
     assert ctypes.sizeof(M) == size
     assert M.seed.offset == off_seed and M.node_cap.offset == off_cap and M.dirichlet_temp.offset == off_temp
     assert M.out_cap.offset == off_out and M.node_boards.offset == off_nb
+    assert M.pool_nodes.offset == off_pn and M.pool_edges.offset == off_pe
 
 
 def test_search_and_arena_entry_points_reject_bad_arguments():

@@ -59,7 +59,7 @@ def test_selfplay_matches_oracle(n, forced, graph, noise, boards):
     np.testing.assert_array_equal(hdr["game_no"], rh[:, 3])
     np.testing.assert_array_equal(hdr["games_done"], rh[:, 4])
     np.testing.assert_array_equal(hdr["sims_done"], rh[:, 6])
-    np.testing.assert_array_equal(hdr["pad0"], rh[:, 5])
+    np.testing.assert_array_equal(hdr["moves"], rh[:, 5])
     ex = {k: v.cpu().numpy() for k, v in sp.drain().items()}
     assert len(ex["pi"]) == len(ref["pi"]) > 0
     # the device queue order is nondeterministic: order both sides by (board id, game, index)
