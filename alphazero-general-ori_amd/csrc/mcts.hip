@@ -392,19 +392,20 @@ __device__ __forceinline__ void push_pages(int32_t *stack, int32_t *top, int cap
 struct GcScr {
     int32_t *remap;     // old local -> new local (-1: dropped); prune: reachability marks first
     int32_t *nvs;       // old local -> new local edge position of its CSR run
-    int32_t *cs;        // new local -> new edge position (non-decreasing, + sentinel)
+    int32_t *cs;        // new local -> new edge position
     int32_t *cnt;       // new local -> edge count
     int32_t *inv;       // new local -> old local
     int32_t *queue;     // prune: breadth-first queue (old locals)
+    int32_t *own;       // new edge position -> new local of its node (-1: page-end gap)
     int64_t *ost;       // new local -> old global edge base
 };
-__host__ __device__ inline size_t gc_ints(int nmax) { return 8 * (size_t)(nmax + 2) + 64; }
+__host__ __device__ inline size_t gc_ints(int nmax, int emax) { return 8 * (size_t)(nmax + 2) + (size_t)emax + 64; }
 __device__ __forceinline__ GcScr gc_scr(int32_t *base, int nmax) {
     const size_t m = (size_t)nmax + 2;
     GcScr S;
     S.ost = reinterpret_cast<int64_t *>(base);                 // 2m ints, 8-byte aligned
     S.remap = base + 2 * m; S.nvs = S.remap + m; S.cs = S.nvs + m; S.cnt = S.cs + m;
-    S.inv = S.cnt + m; S.queue = S.inv + m;
+    S.inv = S.cnt + m; S.queue = S.inv + m; S.own = S.queue + m;
     return S;
 }
 
@@ -456,76 +457,110 @@ __device__ void mark_linked(const Pools &P, int t, int rootl, int32_t *mark, int
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 struct defeats SROA)
-template <int CR = 4>   // edges per lane per round trip of the edge move (boards: 2 CR units)
-__device__ int compact_tree(const Pools &P, int t, int root, int root_round, const GcScr &S, int bunits,
-                            bool linked = false) {
-    const int l = lane_id();
+
+// k_gc collects one tree per workgroup of GCT threads (block-wide scans through LDS), so a
+// large tree's collection (config 4: ~40 K nodes, ~1 M edges) is spread over 8 waves
+constexpr int GCT = 512, GCW8 = GCT / 64;
+struct GcLds {
+    int32_t wsum[GCW8];
+    int32_t bc[4];
+};
+__device__ __forceinline__ int block_scan(int x, int &total, GcLds &L) {   // exclusive
+    const int l = lane_id(), w = threadIdx.x >> 6;
+    int incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (l >= o) incl += y;
+    }
+    if (l == 63) L.wsum[w] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < GCW8; i++) {
+        const int v = L.wsum[i];
+        off += i < w ? v : 0;
+        tot += v;
+    }
+    __syncthreads();
+    total = tot;
+    return off + incl - x;
+}
+__device__ __forceinline__ int block_min(int x, GcLds &L) {
+    const int l = lane_id(), w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
+    if (l == 0) L.wsum[w] = x;
+    __syncthreads();
+    int m = L.wsum[0];
+#pragma unroll
+    for (int i = 1; i < GCW8; i++) m = min(m, L.wsum[i]);
+    __syncthreads();
+    return m;
+}
+
+template <int CR = 4>   // edges per thread per round trip of the edge move (boards: 2 CR units)
+__device__ int compact_tree(const Pools &P, int t, int root, int root_round, const GcScr &S, GcLds &L,
+                            int bunits, bool linked = false) {
+    const int tid = threadIdx.x;
     TreeHdr *H = P.hdr + t;
     const int nc = H->node_count;
     const int rootl = root >= 0 ? node_l(P, root) : -1;
     int32_t *remap = S.remap;
-    if (linked) mark_linked(P, t, rootl, remap, S.queue);
+    if (linked) {
+        if (tid < 64) mark_linked(P, t, rootl, remap, S.queue);
+        __syncthreads();
+    }
     int kept = 0;
-    for (int base = 0; base < nc; base += 64) {
-        const int i = base + l;
+    for (int base = 0; base < nc; base += GCT) {
+        const int i = base + tid;
         bool keep = false;
         if (i < nc) keep = i == rootl || (linked ? remap[i] == 1 : P.nround[node_g(P, t, i)] > root_round);
-        const uint64_t b = __ballot(keep);
-        if (i < nc) remap[i] = keep ? kept + __popcll(b & lanemask_lt()) : -1;
-        kept += __popcll(b);
+        int tot;
+        const int ex = block_scan(keep ? 1 : 0, tot, L);
+        if (i < nc) remap[i] = keep ? kept + ex : -1;
+        kept += tot;
     }
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads();
     // new edge position of every kept node's CSR run: packed in local order, a run that would
-    // straddle an edge page starts the next page (the lanes before the first straddler of a
-    // batch are placed, the rest retried from that page's start). Positions never exceed the
+    // straddle an edge page starts the next page (the nodes before the first straddler of a
+    // chunk are placed, the rest retried from that page's start). Positions never exceed the
     // old ones, so the in-place moves below read every record before it is overwritten.
     int run = 0;
-    for (int base = 0; base < nc; base += 64) {
-        const int i = base + l;
+    for (int base = 0; base < nc; base += GCT) {
+        const int i = base + tid;
         int ec = 0;
         if (i < nc && remap[i] >= 0) {
             const int g = node_g(P, t, i);
             ec = P.nterm[g] ? 0 : P.nec[g];
         }
         bool pending = ec > 0;
-        int start = 0;
-        const int run0 = run;
+        int start = run;
         for (;;) {
             const int x = pending ? ec : 0;
-            int incl = x;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int y = __shfl_up(incl, o, 64);
-                if (l >= o) incl += y;
-            }
-            const int st = run + incl - x;
+            int tot;
+            const int ex = block_scan(x, tot, L);
+            const int st = run + ex;
             const bool strad = pending && (st & (EPG - 1)) + ec > EPG;
-            const uint64_t sb = __ballot(strad);
-            if (!sb) {
+            const int f = block_min(strad ? tid : GCT, L);
+            if (f == GCT) {
                 if (pending) start = st;
-                run += __shfl(incl, 63, 64);
+                run += tot;
                 break;
             }
-            const int f = __ffsll((unsigned long long)sb) - 1;
-            if (pending && l < f) { start = st; pending = false; }
-            run = (__shfl(st, f, 64) & ~(EPG - 1)) + EPG;
+            if (pending && tid < f) { start = st; pending = false; }
+            if (tid == f) L.bc[0] = (st & ~(EPG - 1)) + EPG;
+            __syncthreads();
+            run = L.bc[0];
+            __syncthreads();
         }
-        // edge-less nodes take the end of the runs before them (keeps positions sorted)
-        int end = ec > 0 ? start + ec : run0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(end, o, 64);
-            if (l >= o) end = max(end, y);
-        }
-        if (i < nc && remap[i] >= 0) S.nvs[i] = ec > 0 ? start : end;
+        if (i < nc && remap[i] >= 0) S.nvs[i] = start;
     }
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
-    // node records, in local order (new slot <= old slot)
-    int edges = 0;
-    for (int base = 0; base < nc; base += 64) {
-        const int i = base + l;
+    __syncthreads();
+    // node records, chunk by chunk in local order (new slot <= old slot): reads, then writes
+    int my_edges = 0;
+    for (int base = 0; base < nc; base += GCT) {
+        const int i = base + tid;
         const int ni = i < nc ? remap[i] : -1;
         uint64_t k0 = 0, k1 = 0;
         int64_t oeb = 0;
@@ -542,8 +577,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
             for (int j = 0; j < 4; j++) es[j] = P.nes[(size_t)g * 4 + j];
             vs = S.nvs[i];
         }
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
         if (ni >= 0) {
             const int ng = node_g(P, t, ni);
             const int run_ec = term ? 0 : ec;
@@ -553,63 +587,53 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
 #pragma unroll
             for (int j = 0; j < 4; j++) P.nes[(size_t)ng * 4 + j] = es[j];
             S.cs[ni] = vs; S.cnt[ni] = run_ec; S.inv[ni] = i; S.ost[ni] = oeb;
+            my_edges += run_ec;
         }
-        int x = ni >= 0 && !term ? ec : 0;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        edges += x;
     }
-    if (l == 0) S.cs[kept] = run;
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
+    int edges;
+    (void)block_scan(my_edges, edges, L);
+    // the owner of every new edge position (gaps before a page start: -1)
+    for (int k = tid; k < run; k += GCT) S.own[k] = -1;
+    __syncthreads();
+    for (int ni = tid; ni < kept; ni += GCT) {
+        const int c0 = S.cs[ni], c = S.cnt[ni];
+        for (int e = 0; e < c; e++) S.own[c0 + e] = ni;
+    }
+    __syncthreads();
     {
-        // edge records by new position k (batches of 64 CR in increasing k, all reads before
-        // the writes): owner j = the last kept node with cs[j] <= k; positions in the gaps
-        // before a page start have no owner
+        // edge records by new position k, batches of GCT x CR in increasing k (all reads
+        // before the writes); child links and their cached ranges remapped
         u32x4 *const ed4 = reinterpret_cast<u32x4 *>(P.ed);
-        for (int k0 = 0; k0 < run; k0 += 64 * CR) {
+        for (int k0 = 0; k0 < run; k0 += GCT * CR) {
             u32x4 es_[CR], ek_[CR];
-            int cl[CR];
+            int nch[CR];
+            int64_t ceb[CR];
             bool own[CR];
 #pragma unroll
             for (int r = 0; r < CR; r++) {
-                const int k = k0 + 64 * r + l;
-                own[r] = false; cl[r] = -1;
+                const int k = k0 + GCT * r + tid;
+                const int j = k < run ? S.own[k] : -1;
+                own[r] = j >= 0;
                 es_[r] = u32x4{0, 0, 0, 0}; ek_[r] = u32x4{0, 0xFFFFFFFFu, 0, 0};
-                if (k < run) {
-                    int lo = 0, hi = kept - 1;                 // last j with cs[j] <= k
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (S.cs[mid] <= k) lo = mid; else hi = mid - 1;
-                    }
-                    if (k - S.cs[lo] < S.cnt[lo]) {
-                        own[r] = true;
-                        const int64_t src = S.ost[lo] + (k - S.cs[lo]);
-                        es_[r] = ed4[2 * src];
-                        ek_[r] = ed4[2 * src + 1];
-                    }
+                if (j >= 0) {
+                    const int64_t src = S.ost[j] + (k - S.cs[j]);
+                    es_[r] = ed4[2 * src];
+                    ek_[r] = ed4[2 * src + 1];
                 }
             }
-#pragma unroll
-            for (int r = 0; r < CR; r++) {
-                const int ch = (int)ek_[r].y;
-                if (own[r] && ch >= 0) cl[r] = node_l(P, ch);
-            }
-            int nch[CR];
-            int64_t ceb[CR];
 #pragma unroll
             for (int r = 0; r < CR; r++) {
                 nch[r] = -1; ceb[r] = 0;
-                if (cl[r] >= 0) {
-                    const int nl = remap[cl[r]];
+                const int ch = (int)ek_[r].y;
+                if (own[r] && ch >= 0) {
+                    const int nl = remap[node_l(P, ch)];
                     if (nl >= 0) { nch[r] = node_g(P, t, nl); ceb[r] = S.cnt[nl] > 0 ? edge_g(P, t, S.cs[nl]) : 0; }
                 }
             }
-            __threadfence_block();
-            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
 #pragma unroll
             for (int r = 0; r < CR; r++) {
-                const int k = k0 + 64 * r + l;
+                const int k = k0 + GCT * r + tid;
                 if (own[r]) {
                     u32x4 o = ek_[r];
                     o.y = (uint32_t)nch[r];
@@ -619,8 +643,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                     ed4[2 * dst + 1] = o;
                 }
             }
-            __threadfence_block();
-            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
         }
     }
     if (P.nbrd) {
@@ -629,13 +652,13 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         u32x4 *bb = reinterpret_cast<u32x4 *>(P.nbrd);
         const int units = kept * bunits;
         constexpr int R = 2 * CR;
-        for (int k0 = 0; k0 < units; k0 += 64 * R) {
+        for (int k0 = 0; k0 < units; k0 += GCT * R) {
             u32x4 d[R];
             size_t dst[R];
             bool mv[R];
 #pragma unroll
             for (int r = 0; r < R; r++) {
-                const int k = k0 + 64 * r + l;
+                const int k = k0 + GCT * r + tid;
                 mv[r] = false; dst[r] = 0; d[r] = u32x4{0, 0, 0, 0};
                 if (k < units) {
                     const int nn = k / bunits, u = k - nn * bunits, on = S.inv[nn];
@@ -646,43 +669,40 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                     }
                 }
             }
-            __threadfence_block();
-            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
 #pragma unroll
             for (int r = 0; r < R; r++)
                 if (mv[r]) bb[dst[r]] = d[r];
-            __threadfence_block();
-            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
         }
     }
     // rebuild the transposition table
     int32_t *hs = P.hslot + (size_t)t * P.hcap;
-    for (int i = l; i < P.hcap; i += 64) hs[i] = -1;
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
-    for (int i = l; i < kept; i += 64) {
+    for (int i = tid; i < P.hcap; i += GCT) hs[i] = -1;
+    __syncthreads();
+    for (int i = tid; i < kept; i += GCT) {
         const int g = node_g(P, t, i);
         const uint64_t k0 = P.nkey0[g];
         uint32_t h = (uint32_t)(k0 ^ (k0 >> 32)) & (uint32_t)(P.hcap - 1);
         while (atomicCAS(&hs[h], -1, g) != -1) h = (h + 1) & (uint32_t)(P.hcap - 1);
     }
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
     // pages past the compacted tree go back to the pools
     const int npg = (kept + NPG - 1) >> NPG_SHIFT, epg = (run + EPG - 1) >> EPG_SHIFT;
     const int onpg = H->npg, oepg = H->epg;
-    push_pages(P.nfree, P.alloc + 0, P.npages, P.ntab + (size_t)t * P.nptab + npg, onpg - npg);
-    push_pages(P.efree, P.alloc + 1, P.epages, P.etab + (size_t)t * P.eptab + epg, oepg - epg);
     const int nroot = rootl >= 0 && remap[rootl] >= 0 ? node_g(P, t, remap[rootl]) : -1;
     const int eleft = epg * EPG - run;
     const int64_t enext = eleft > 0 ? edge_g(P, t, run) : 0;
-    __builtin_amdgcn_wave_barrier();
-    if (l == 0) {
+    __syncthreads();
+    if (tid < 64) {
+        push_pages(P.nfree, P.alloc + 0, P.npages, P.ntab + (size_t)t * P.nptab + npg, onpg - npg);
+        push_pages(P.efree, P.alloc + 1, P.epages, P.etab + (size_t)t * P.eptab + epg, oepg - epg);
+    }
+    if (tid == 0) {
         H->node_count = kept; H->edge_count = edges;
         H->npg = npg; H->epg = epg; H->eleft = eleft; H->enext = enext;
         H->live_gc = kept; H->gcs += 1;
     }
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads();
     return nroot;
 }
 
@@ -729,9 +749,9 @@ __device__ __forceinline__ void gc_push(const Pools &P, TreeHdr *H, int t) {
 //     simulation, so every search starts compacted); after compaction k_gc prunes the tree
 //     to the nodes linked from the root (prunes++) and empties it if that is still too
 //     large (resets++);
-//   should (gc_state 5): a tree holding more than twice its live size (amortised: each
-//     collection copies at most as many nodes as were added since the last), or any tree
-//     with garbage while the shared pools run low; k_gc may defer these (GC_SHOULD_CAP).
+//   should (gc_state 5): a tree whose garbage exceeds alpha x its live size, alpha from 4
+//     (pools at most half full) down to 1/8 as they fill; k_gc may defer these
+//     (GC_SHOULD_CAP per launch).
 // Without an event the kept table is exactly the reference's reachable table.
 template <int N>
 __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const int8_t *s, bool keep,
@@ -753,8 +773,12 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         const long long used = (long long)H->epg * EPG - H->eleft;
         const bool must = nc + budget + 1 > P.nmax ||
                           used + SPL_ACTIONS + (long long)budget * C.edge_reserve > (long long)P.eptab * EPG;
-        const bool pressure = P.alloc[0] < P.low_n || P.alloc[1] < P.low_e;
-        const bool should = nc > 2 * H->live_gc + budget + NPG || (pressure && nc > H->live_gc + budget);
+        // garbage allowance alpha x the live size (at the last collection): a collection
+        // copies the live tree to free its garbage, so a large alpha is cheap per freed node;
+        // it shrinks as the shared pools fill (free share f: alpha = 4 down to 1/8)
+        const float f = fminf((float)P.alloc[0] / (float)P.npages, (float)P.alloc[1] / (float)P.epages);
+        const float alpha = f >= 0.5f ? 4.f : fmaxf(0.125f, 8.f * f);
+        const bool should = nc > (int)((1.f + alpha) * (float)H->live_gc) + budget + NPG;
         gcs = must || !C.selfplay ? 3 : (should ? 5 : 0);   // search-only arenas: every search
                                                            // starts compacted (no withdrawals there)
     } else {
@@ -785,75 +809,73 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
 }
 
 // Garbage collection queued by k_backup (a leaf did not fit mid-search: gc_state 1) and by
-// search starts (3 must, 5 should), one wave per queued tree, GC_WG single-wave workgroups
-// sharing the queue (a workgroup's scratch: gc_ints(nmax) ints of P.gscr). Exactly
+// search starts (3 must, 5 should), one workgroup of GCT threads per queued tree, GC_WG
+// workgroups sharing the queue (a workgroup's scratch: gc_stride ints of P.gscr). Exactly
 // begin_search's policy: compact (rounds > the root's), prune to the linked nodes, empty.
 // Queued trees come in bursts (games start together, so trees fill up together): entries
 // past GC_SHOULD_CAP that only "should" be collected are skipped this time (their search
 // fits; the next search start queues them again), so no launch carries a whole burst.
-constexpr int GC_WG = 1024;
+constexpr int GC_WG = 256;      // one per CU
 #ifndef GC_SHOULD_CAP
-#define GC_SHOULD_CAP 1024
+#define GC_SHOULD_CAP 256
 #endif
 template <int N>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_gc(Pools P, SearchCfg C) {
-    const int l = lane_id();
+__global__ __launch_bounds__(GCT) void k_gc(Pools P, SearchCfg C) {
+    __shared__ GcLds L;
+    const int tid = threadIdx.x;
     const int tail = P.counters[2];                      // no pushes while k_gc runs
     const int ftail = P.counters[5];
     if (tail == 0 && ftail == 0) return;                 // (the usual case)
     const GcScr S = gc_scr(P.gscr + (size_t)blockIdx.x * P.gc_stride, P.nmax);
     for (int k = blockIdx.x; k < tail; k += gridDim.x) {     // garbage collection
-        const int t = uniform(P.gcq[k]);
+        const int t = P.gcq[k];
         TreeHdr *H = P.hdr + t;
         const int st = H->gc_state;
         int root = H->root;
-        int nst = st == 1 ? 2 : 0;
+        const int nst = st == 1 ? 2 : 0;
         if (st == 5 && k >= GC_SHOULD_CAP) {
             // deferred (its search fits as it is)
         } else if (st == 1) {                            // the descent then repeats
-            root = compact_tree<8>(P, t, root, P.nround[root], S, NodeBoard<N>::UNITS);
+            root = compact_tree<4>(P, t, root, P.nround[root], S, L, NodeBoard<N>::UNITS);
         } else if (st == 3 || st == 5) {
             const int rr = H->root_round;
-            root = compact_tree<8>(P, t, root, rr, S, NodeBoard<N>::UNITS);
+            root = compact_tree<4>(P, t, root, rr, S, L, NodeBoard<N>::UNITS);
             if (!tree_fits(P, C, H) && root >= 0) {
-                root = compact_tree<8>(P, t, root, rr, S, NodeBoard<N>::UNITS, true);
-                if (l == 0) H->prunes += 1;
+                root = compact_tree<4>(P, t, root, rr, S, L, NodeBoard<N>::UNITS, true);
+                if (tid == 0) H->prunes += 1;
             }
+            __syncthreads();
             if (!tree_fits(P, C, H)) {
                 root = -1;
-                empty_tree(P, t);
-                if (l == 0) H->resets += 1;
+                if (tid < 64) empty_tree(P, t);
+                if (tid == 0) H->resets += 1;
             }
         }
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
         const int64_t reb = root >= 0 ? P.neb[root] : 0;
         const int rec = root >= 0 ? P.nec[root] : 0;
-        if (l == 0) {
+        if (tid == 0) {
             H->root = root;
             H->root_eb = reb;
             H->root_ec = rec;
             H->gc_state = nst;                           // (2: once per search)
             H->gc_queued = 0;
         }
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
     }
     // finished games' example rows (k_commit): the staging rows stay untouched until the
     // tree's next commit, a later iteration
     for (int k = blockIdx.x; k < ftail; k += gridDim.x) {
         const int2 e = P.flq[k];
-        wave_copy_bytes(P.out_state + (size_t)e.y * Lay<N>::S, P.ex_state + (size_t)e.x * Lay<N>::S, Lay<N>::S);
+        const int8_t *bs = P.ex_state + (size_t)e.x * Lay<N>::S;
+        int8_t *bd = P.out_state + (size_t)e.y * Lay<N>::S;
+        for (int i = tid; i < Lay<N>::S; i += GCT) bd[i] = bs[i];
         const float *src = P.ex_pi + (size_t)e.x * SPL_ACTIONS;
         float *dst = P.out_pi + (size_t)e.y * SPL_ACTIONS;
-        float v[7];
-#pragma unroll
-        for (int i = 0; i < 7; i++) v[i] = 64 * i + l < SPL_ACTIONS ? src[64 * i + l] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 7; i++)
-            if (64 * i + l < SPL_ACTIONS) dst[64 * i + l] = v[i];
+        for (int i = tid; i < SPL_ACTIONS; i += GCT) dst[i] = src[i];
     }
-    if (l == 0 && atomicAdd(&P.counters[4], 1) == (int)gridDim.x - 1) {
+    __syncthreads();
+    if (tid == 0 && atomicAdd(&P.counters[4], 1) == (int)gridDim.x - 1) {
         P.counters[2] = 0;                               // the last workgroup out resets the queues
         P.counters[5] = 0;
         P.counters[4] = 0;
@@ -1796,7 +1818,7 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     acc(4 * (size_t)B * L.nptab); acc(4 * (size_t)B * L.eptab); acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages);
     acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages); acc(64);
     acc(4 * (size_t)B * L.hcap); acc(4 * (size_t)B * L.pcap); acc(8 * (size_t)B * L.pcap);
-    acc(4 * (size_t)gcw * gc_ints(L.nmax)); acc((size_t)B * L.S);
+    acc(4 * (size_t)gcw * gc_ints(L.nmax, L.emax)); acc((size_t)B * L.S);
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
     acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
     acc(16 * no); acc(64); acc((size_t)L.nbb * nn); acc(4 * (size_t)B); acc(8 * no);
@@ -1853,7 +1875,6 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.nmax = L.nmax; P.emax = L.emax; P.hcap = L.hcap; P.pcap = L.pcap;
     P.nptab = L.nptab; P.eptab = L.eptab;
     P.npages = (int)L.npages; P.epages = (int)L.epages;
-    P.low_n = P.npages / 16; P.low_e = P.epages / 16;
     const size_t nn = (size_t)L.npages * NPG, ne = (size_t)L.epages * EPG;
     const int excap = L.excap;
     const size_t nx = (size_t)B * excap, no = (size_t)L.out_cap;
@@ -1876,7 +1897,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.hslot = carve<int32_t>(p, (size_t)B * P.hcap);
     P.path_n = carve<int32_t>(p, (size_t)B * P.pcap);
     P.path_e = carve<int64_t>(p, (size_t)B * P.pcap);
-    P.gc_stride = gc_ints(P.nmax);
+    P.gc_stride = gc_ints(P.nmax, P.eptab * EPG);
     P.gscr = carve<int32_t>(p, (size_t)gcw * P.gc_stride);
     P.root_state = carve<int8_t>(p, (size_t)B * m->S);
     P.excap = excap; P.out_cap = (int)no;
@@ -1925,7 +1946,7 @@ int spl_mcts_set_roots(spl_mcts *m, const int8_t *roots, int keep_tree, int forc
 // thousands of trees, GC_WG single-wave workgroups share the queue)
 static void launch_gc(spl_mcts *m, hipStream_t hs) {
     const unsigned gcw = (unsigned)(m->B < GC_WG ? m->B : GC_WG);
-    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_gc<N>, dim3(gcw), dim3(64), 0, hs, m->P, m->cfg));
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_gc<N>, dim3(gcw), dim3(GCT), 0, hs, m->P, m->cfg));
 }
 
 int spl_mcts_set_roots_active(spl_mcts *m, const int8_t *roots, const uint8_t *active, int keep_tree,

@@ -88,7 +88,6 @@ struct Pools {
     int nmax, emax, hcap, pcap;          // per tree: node slots, edges (page tables), hash slots, path
     int nptab, eptab;                    // page-table entries per tree (nmax / NPG, emax / EPG)
     int npages, epages;                  // pages in the pools
-    int low_n, low_e;                    // free-page low-water marks (pool pressure: collect garbage)
     TreeHdr *hdr;
     uint64_t *nkey0, *nkey1;             // node pool, indexed by global node id
     int64_t *neb;

@@ -102,7 +102,8 @@ class BatchedMCTS:
         self._hdr = torch.empty((B, HDR_DTYPE.itemsize // 4), dtype=torch.int32, device=dev)
 
     MEM_FRACTION = 0.8      # of the device's free memory a default-sized arena may take
-    EDGES_PER_NODE = 20     # pool edge:node ratio (live trees: 15-21 edges per node, profiles/r03_tree_sizes_*)
+    EDGES_PER_NODE = 15     # pool edge:node ratio (live trees: 15-19 edges per node, profiles/r03_tree_sizes_*;
+                            # node slots are ~65 B, so erring towards nodes is cheap)
     NODE_MAX = 45056        # per-tree node maximum (transposition table 64 K slots at most)
 
     @staticmethod
