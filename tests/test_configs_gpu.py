@@ -189,3 +189,53 @@ def test_search_arena_spends_whole_budget_under_pressure():
     assert m.capacity_events(h)["unexpanded"] > 0
     counts = m.root_stats()[0]
     assert bool((counts.sum(1) == sims - 1).all())
+
+
+@pytest.mark.parametrize("n,B,sims,prefill,window", [(2, 32768, 100, 3000, 3000), (4, 16384, 400, 30000, 8000)])
+def test_steady_state_search_is_reference_exact(n, B, sims, prefill, window):
+    """Configs 3 and 5 at full size with SplendorNNet leaves on the default shared pools, run
+    to their steady state (config 3: games finish from ~2,400 iterations on; config 5: the
+    first games end near 16,000 and the trees that all started together peak around 20,000)
+    and then through a window: no search in the window ran on a pruned or emptied tree and
+    every leaf was stored (prunes == resets == unexpanded == 0), so each tree is the
+    reference's table. Events during the synchronised start-up transient are printed."""
+    from splendor.nnet import LeafEvaluator, random_net
+    from splendor.env import SplendorEngine
+    e = SplendorEngine(n)
+    ev = LeafEvaluator(e, random_net(n, seed=0), B, use_graph=False)
+    _, sp = selfplay(n, B, sims, evaluator=ev)
+
+    def run(k):
+        done = 0
+        while done < k:
+            sp.run(min(4000, k - done), use_graph=True)
+            done += min(4000, k - done)
+            sp.drain()
+    run(prefill)
+    ev0 = sp.check_capacity(allow=True)
+    g0 = sp.stats()["games_done"]
+    run(window)
+    torch.cuda.synchronize()
+    st = sp.stats()
+    ev1 = sp.check_capacity(allow=True)
+    pool = sp.pool_state()
+    del sp, ev                                  # (freed before asserting: a failed test's
+    free_all()                                  #  traceback must not pin ~230 GB of pools)
+    delta = {k: ev1[k] - ev0[k] for k in ev1}
+    print(f"steady state n={n} B={B} sims={sims}: start-up events {ev0}, window events {delta}, "
+          f"window games {st['games_done'] - g0}, {st}, pool {pool}")
+    assert st["games_done"] - g0 > 0 and st["overflow"] == 0
+    assert delta == {"prunes": 0, "resets": 0, "unexpanded": 0}
+
+
+def test_check_capacity_raises_on_events():
+    """Capacity events are an error unless the caller allows them."""
+    from splendor import _lib
+    n, B, sims = 2, 64, 64
+    _, sp = selfplay(n, B, sims, node_cap=96, edge_cap=96 * 24)
+    sp.run(1200, use_graph=True)
+    sp.drain()
+    with pytest.raises(_lib.EngineError):
+        sp.check_capacity()
+    ev = sp.check_capacity(allow=True)
+    assert ev["prunes"] > 0

@@ -9,7 +9,7 @@ ROUND=${2:-r02}
 CHUNK=${3:-100}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
-CMD=(python3 bench.py --steps $((2 * CHUNK)) --warmup "$CHUNK" --chunk "$CHUNK" --no-cpu-baseline --no-selfplay)
+CMD=(python3 bench.py --workload env --steps $((2 * CHUNK)) --warmup "$CHUNK" --chunk "$CHUNK" --no-cpu-baseline)
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- "${CMD[@]}" > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- "${CMD[@]}" > "$OUT/write.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE \

@@ -7,14 +7,15 @@
 # usage: tools/pmc_selfplay.sh OUTDIR ROUND [WARMUP] [STEPS]   (PASSES="sq sq2 ..." for a subset)
 set -euo pipefail
 OUT=${1:-gpurun_out/pmc_sp}
-ROUND=${2:-r02}
-WARM=${3:-2000}
+ROUND=${2:-r03}
+WARM=${3:-3000}
 STEPS=${4:-200}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
-CMD=(python3 bench.py --workload selfplay --steps "$STEPS" --warmup "$WARM" --no-cpu-baseline)
-# counters only for the self-play kernels, dispatches WARM .. WARM+STEPS of each
-FILT=(--kernel-include-regex "k_(select|leaf_mask|nn_forward|backup|commit|gc)" --kernel-iteration-range "[$WARM-$((WARM + STEPS))]")
+CMD=(python3 bench.py --workload selfplay --prefill "$WARM" --warmup 20 --steps "$STEPS" --window 0 --no-cpu-baseline)
+# counters only for the self-play kernels, dispatches WARM+40 .. WARM+40+STEPS of each (the
+# timed steps; k_gc runs twice per iteration, so its range covers the second half of them)
+FILT=(--kernel-include-regex "k_(select|leaf_mask|nn_forward|backup|commit|gc)" --kernel-iteration-range "[$((WARM + 40))-$((WARM + 40 + STEPS))]")
 PASSES=${PASSES:-fetch write sq sq2 mem ea}
 pass() {
     local name=$1; shift
