@@ -1145,13 +1145,18 @@ template <int N>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_WAVES))) void k_select(Pools P, SearchCfg C, int B, int lim,
                                                     int8_t *__restrict__ leaf_state,
                                                     uint64_t *__restrict__ leaf_mask,
-                                                    uint8_t *__restrict__ leaf_valid) {
+                                                    uint8_t *__restrict__ leaf_valid,
+                                                    int32_t *__restrict__ leaf_count) {
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
     __shared__ __align__(16) float lpr[WAVES][416];         // root-noise scratch
-    const int w = uniform(threadIdx.x >> 6), t = blockIdx.x * WAVES + w;
-    if (t >= B) return;
+    // trees start in P.order (deep descents first: the launch ends with its deepest descent)
+    const int w = uniform(threadIdx.x >> 6), slot = blockIdx.x * WAVES + w;
+    if (slot >= B) return;
+    const int t = uniform(P.order[slot]);
     const int l = lane_id();
+    if (slot == 0 && l < 2) P.counters[6 + l] = 0;           // k_leaf_mask's filing counters
+    if (slot == 0 && l == 2 && leaf_count) *leaf_count = 0;
     TreeHdr *H = P.hdr + t;
     int8_t *s = lds[w];
     // the root board is requested together with the header (no dependency between them)
@@ -1199,6 +1204,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         const NodeStat *nst_t = P.nst;
         const double cpuct = C.cpuct, fpu = C.fpu;
         const float cf = (float)C.cpuct;
+        int pend = -1, pend_n = 0;                           // path entry not yet stored
+        int64_t pend_e = 0;
         for (;;) {
             SPL_PROBE(1)
             if (depth > 0 && ec < 0) {
@@ -1212,6 +1219,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             // node's visit stats are requested together: one round trip per level
             const NodeStat nsq = nst_t[node];
             const Edge e64 = ed_t[eb + (l < ec ? l : 0)];
+            // the previous level's path entry is stored behind this level's loads: vmcnt counts
+            // stores too, in issue order, so a store issued first would delay the loads' wait
+            if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_e[pend] = pend_e; }
+            pend = -1;
             const int ns = nsq.ns;
             const double qs = nsq.qs;
             const Pick pk = ec <= 64 && !(forced && depth == 0)
@@ -1227,7 +1238,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                 }
             }
 #endif
-            if (l == 0) { path_n[depth] = node; path_e[depth] = ge; }
+            pend = depth; pend_n = node; pend_e = ge;
             depth++;
             int child = uniform(pk.child);
             int64_t ceb = pk.ceb;
@@ -1308,6 +1319,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             }
             break;                                           // new NN leaf
         }
+        if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_e[pend] = pend_e; }
     }
     __builtin_amdgcn_wave_barrier();
     SPL_PROBE(5)
@@ -1348,10 +1360,21 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
 // (splendor_device.h lane_predicates_part / lane_mask_word_fast, exact path for boards
 // outside the fast domain), then the pass bit iff nothing else is legal (:263). Replaces
 // the wave-per-board mask of the descent kernel (its lanes are idle for it anyway).
+// A select's launch time is set by its deepest descents (one dependent round trip per level,
+// up to ~115 levels at steady state), so the next select dispatches the trees whose leaf was
+// at least DEEP_FIRST deep first: k_leaf_mask files every tree into P.order (one atomic per
+// 64 trees and bucket; counters [6] [7] are cleared by k_select).
+#ifndef DEEP_FIRST
+#define DEEP_FIRST 48
+#endif
+// leaf_index / leaf_count (optional): the NN leaves listed compactly (any order) for the
+// indexed network kernel, one atomic per 64 leaves (the count is cleared by k_select)
 template <int N>
-__global__ __launch_bounds__(256) void k_leaf_mask(int B, int lim, const int8_t *__restrict__ leaf_state,
+__global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, const int8_t *__restrict__ leaf_state,
                                                    const uint8_t *__restrict__ leaf_valid,
-                                                   uint64_t *__restrict__ leaf_mask) {
+                                                   uint64_t *__restrict__ leaf_mask,
+                                                   int32_t *__restrict__ leaf_index,
+                                                   int32_t *__restrict__ leaf_count) {
     using Lx = Lay<N>;
     using Cv = Conv<N>;
     constexpr int RB = 64, ST = (Lx::ROWS % 2 ? Lx::ROWS : Lx::ROWS + 1) * 8;
@@ -1363,6 +1386,26 @@ __global__ __launch_bounds__(256) void k_leaf_mask(int B, int lim, const int8_t 
     __shared__ uint64_t msk[RB][7];
     const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
+    if (w == 3) {                                        // launch order of the next select
+        const bool in = l < nb;
+        const bool deep = in && P.hdr[b0 + l].depth >= DEEP_FIRST;
+        const uint64_t bd = __ballot(deep), bs = __ballot(in && !deep);
+        int kd = 0, ks = 0;
+        if (l == 0) {
+            if (bd) kd = atomicAdd(&P.counters[6], __popcll(bd));
+            if (bs) ks = atomicAdd(&P.counters[7], __popcll(bs));
+        }
+        kd = __shfl(kd, 0, 64); ks = __shfl(ks, 0, 64);
+        if (deep) P.order[kd + __popcll(bd & lanemask_lt())] = b0 + l;
+        else if (in) P.order[B - 1 - (ks + __popcll(bs & lanemask_lt()))] = b0 + l;
+    } else if (w == 2 && leaf_index) {                   // the NN leaves, compacted
+        const bool v = l < nb && leaf_valid[b0 + l];
+        const uint64_t bv = __ballot(v);
+        int k = 0;
+        if (l == 0 && bv) k = atomicAdd(leaf_count, __popcll(bv));
+        k = __shfl(k, 0, 64);
+        if (v) leaf_index[k + __popcll(bv & lanemask_lt())] = b0 + l;
+    }
     for (int i = tid; i < nb * Cv::UNITS; i += 256) {
         const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
         Cv::load(lds + b * ST, leaf_state + (size_t)(b0 + b) * Lx::S, u);
@@ -1755,8 +1798,9 @@ __global__ __launch_bounds__(256) void k_hash_eval(int B, const int8_t *__restri
 }
 
 // free stacks = every page, allocation counters
-__global__ void k_init_pools(Pools P) {
+__global__ void k_init_pools(Pools P, int B) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = tid; i < (size_t)B; i += nth) P.order[i] = (int32_t)i;
     for (size_t i = tid; i < (size_t)P.npages; i += nth) P.nfree[i] = (int32_t)i;
     for (size_t i = tid; i < (size_t)P.epages; i += nth) P.efree[i] = (int32_t)i;
     if (tid == 0) { P.alloc[0] = P.npages; P.alloc[1] = P.epages; P.alloc[2] = 0; P.alloc[3] = 0; }
@@ -1821,7 +1865,7 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     acc(4 * (size_t)gcw * gc_ints(L.nmax, L.emax)); acc((size_t)B * L.S);
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
     acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
-    acc(16 * no); acc(64); acc((size_t)L.nbb * nn); acc(4 * (size_t)B); acc(8 * no);
+    acc(16 * no); acc(64); acc((size_t)L.nbb * nn); acc(4 * (size_t)B); acc(8 * no); acc(4 * (size_t)B);
     L.bytes = bytes;
     return L;
 }
@@ -1912,13 +1956,14 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.nbrd = L.nbb ? carve<int8_t>(p, (size_t)L.nbb * nn) : nullptr;
     P.gcq = carve<int32_t>(p, (size_t)B);
     P.flq = carve<int2>(p, no);
+    P.order = carve<int32_t>(p, (size_t)B);
     // zero the small state (headers, counters); the pools need no initialisation (a slot
     // is written before it is read); free stacks hold every page, tables are empty
     bool ok = hipMemset(P.hdr, 0, sizeof(TreeHdr) * B) == hipSuccess &&
               hipMemset(P.counters, 0, 64) == hipSuccess &&
               hipMemset(P.hslot, 0xFF, 4 * (size_t)B * P.hcap) == hipSuccess;
     if (ok) {
-        hipLaunchKernelGGL(k_init_pools, dim3(1024), dim3(256), 0, (hipStream_t)0, P);
+        hipLaunchKernelGGL(k_init_pools, dim3(1024), dim3(256), 0, (hipStream_t)0, P, B);
         ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess;
     }
     if (!ok) { (void)hipFree(arena); delete m; return SPL_EDEVICE; }
@@ -1967,16 +2012,27 @@ int spl_mcts_pick_best(spl_mcts *m, const uint8_t *active, uint32_t board_base, 
     return check_launch();
 }
 
+static int launch_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
+                         int32_t *leaf_index, int32_t *leaf_count, void *hs) {
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select<N>, wave_grid(m->B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
+                                          leaf_state, leaf_mask, leaf_valid, leaf_count));
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_leaf_mask<N>, dim3((unsigned)((m->B + 63) / 64)), dim3(256), 0,
+                                          (hipStream_t)hs, m->P, m->B, m->token_limit, leaf_state, leaf_valid,
+                                          leaf_mask, leaf_index, leaf_count));
+    return check_launch();
+}
+
 int spl_mcts_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
                     void *hs) {
     if (!m || !leaf_state || !leaf_mask || !leaf_valid) return SPL_EINVAL;
-    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select<N>, wave_grid(m->B), dim3(THREADS), 0,
-                                          (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
-                                          leaf_state, leaf_mask, leaf_valid));
-    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_leaf_mask<N>, dim3((unsigned)((m->B + 63) / 64)), dim3(256), 0,
-                                          (hipStream_t)hs, m->B, m->token_limit, leaf_state, leaf_valid,
-                                          leaf_mask));
-    return check_launch();
+    return launch_select(m, leaf_state, leaf_mask, leaf_valid, nullptr, nullptr, hs);
+}
+
+int spl_mcts_select_compact(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
+                            int32_t *leaf_index, int32_t *leaf_count, void *hs) {
+    if (!m || !leaf_state || !leaf_mask || !leaf_valid || !leaf_index || !leaf_count) return SPL_EINVAL;
+    return launch_select(m, leaf_state, leaf_mask, leaf_valid, leaf_index, leaf_count, hs);
 }
 
 int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v,

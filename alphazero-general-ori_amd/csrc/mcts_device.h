@@ -122,8 +122,10 @@ struct Pools {
     int32_t *out_scdiff, *out_meta;      // out_cap x 4, out_cap x 4 (board id, game, index, player)
     int32_t *counters;                   // [0] queued examples [1] dropped [2] GC queue
                                          // [5] example-row queue [4] k_gc workgroups done
+                                         // [6] [7] deep / other trees filed by k_leaf_mask
     int32_t *gcq;                        // B: trees whose garbage collection k_gc runs
     int2 *flq;                           // out_cap: (staging row, queue slot) rows k_gc copies
+    int32_t *order;                      // B: the trees in k_select's launch order (deep first)
 };
 
 // tree t's local node slot i / local (virtual) edge position v -> global

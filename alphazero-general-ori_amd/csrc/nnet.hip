@@ -283,10 +283,15 @@ __device__ __forceinline__ float wave_sum_f32(float v) {
 template <int NP>
 // one workgroup per CU (LDS) = 2 waves per SIMD: the register budget is 256, and without
 // saying so the scheduler sinks the prefetched weight loads next to their MFMAs
+// idx (optional): the kernel evaluates rows idx[0 .. *count) — board / mask / output row
+// idx[k] — instead of 0 .. B (the search's NN leaves, compacted by k_leaf_mask); tiles past
+// *count exit at once.
 __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_nn_forward(int B, const int8_t *__restrict__ state,
                                                     const uint64_t *__restrict__ mask,
                                                     const float *__restrict__ W, float *__restrict__ pi_out,
-                                                    float *__restrict__ v_out) {
+                                                    float *__restrict__ v_out,
+                                                    const int32_t *__restrict__ idx,
+                                                    const int32_t *__restrict__ count) {
     using Nt = Net<NP>;
     constexpr int R = Nt::R, X0S = Nt::X0S;
     __shared__ __align__(16) float bufA[7 * ML * XS];      // per-column activations / logits
@@ -300,7 +305,12 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (tid < 16) nn_probe_acc[tid] = 0;
     if (tid == 0) nn_probe_last = clock64();
 #endif
-    const int b0 = blockIdx.x * ML, nb = min(ML, B - b0);
+    const int b0 = blockIdx.x * ML;
+    const int cnt = count ? __builtin_amdgcn_readfirstlane(*count) : B;
+    if (b0 >= cnt) return;
+    const int nb = min(ML, cnt - b0);
+    // row of leaf i of this tile (its board, mask and outputs)
+    const auto rowof = [&](int i) -> size_t { return idx ? (size_t)idx[b0 + i] : (size_t)(b0 + i); };
     const float *aff = W + Nt::AFF;                        // s1, t1, sp1, tp1
     const int t0 = 4 * wg, ntok = wg ? 3 : 4;              // this wave's token tiles (per-column layers)
     constexpr int S1 = kpad(R) / 2;
@@ -311,17 +321,17 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     int8_t *x0 = reinterpret_cast<int8_t *>(bufA);
     for (int j = tid; j < 7 * ML * X0S / 4; j += NNT) reinterpret_cast<int32_t *>(x0)[j] = 0;
     lds_barrier();
-    if (tid < nb * 7) mskl[tid] = mask[(size_t)b0 * 7 + tid];
+    if (tid < nb * 7) mskl[tid] = mask[rowof(tid / 7) * 7 + tid % 7];
     if constexpr ((7 * R) % 4 == 0) {
-        // the workgroup's boards are one contiguous block: dword loads, all in flight at
-        // once, then each byte scattered to its (column, leaf, row) slot
-        const int32_t *src = reinterpret_cast<const int32_t *>(state + (size_t)b0 * R * 7);
-        constexpr int PER = (ML * R * 7 / 4 + NNT - 1) / NNT;
+        // the workgroup's boards: dword loads (a board is a whole number of dwords), all in
+        // flight at once, then each byte scattered to its (column, leaf, row) slot
+        constexpr int BW = R * 7 / 4;                      // dwords per board
+        constexpr int PER = (ML * BW + NNT - 1) / NNT;
         int32_t d[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int j = tid + k * NNT;
-            d[k] = j < nb * R * 7 / 4 ? src[j] : 0;
+            const int j = tid + k * NNT, i = j / BW;
+            d[k] = j < nb * BW ? reinterpret_cast<const int32_t *>(state + rowof(i) * R * 7)[j - i * BW] : 0;
         }
 #pragma unroll
         for (int k = 0; k < PER; k++) {
@@ -337,7 +347,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     } else {
         for (int j = tid; j < nb * R; j += NNT) {          // one board row (7 bytes) per thread
             const int i = j / R, r = j - i * R;
-            const int8_t *src = state + ((size_t)(b0 + i) * R + r) * 7;
+            const int8_t *src = state + (rowof(i) * R + r) * 7;
 #pragma unroll
             for (int c = 0; c < 7; c++) x0[(c * ML + i) * X0S + r] = src[c];
         }
@@ -562,7 +572,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const int i = 16 * rt + acc16_row(r);
-                        if (i < nb) v_out[(size_t)(b0 + i) * NP + n] = tanhf(a16[0][rt][r] + bv);
+                        if (i < nb) v_out[rowof(i) * NP + n] = tanhf(a16[0][rt][r] + bv);
                     }
             }
         }
@@ -608,7 +618,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
                 for (int k = 0; k < 7; k++) {
                     const int a = 64 * k + lane;
-                    if (a < ACT) pi_out[(size_t)(b0 + i) * ACT + a] = x[q][k] * inv;
+                    if (a < ACT) pi_out[rowof(i) * ACT + a] = x[q][k] * inv;
                 }
             }
         }
@@ -635,21 +645,34 @@ int spl_nn_packed_floats(int n_players) {
     }
 }
 
-int spl_nn_forward(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
-                   const float *packed_weights, float *pi, float *v, void *hs) {
+static int launch_nn(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
+                     const float *packed_weights, float *pi, float *v, const int32_t *idx, const int32_t *count,
+                     void *hs) {
     if (n_players < 2 || n_players > 4 || B < 0 || (B && (!leaf_state || !leaf_mask || !packed_weights || !pi || !v)))
         return SPL_EINVAL;
     if (!B) return 0;
     const dim3 grid((unsigned)((B + ML - 1) / ML));
     switch (n_players) {
         case 2: hipLaunchKernelGGL(k_nn_forward<2>, grid, dim3(NNT), 0, (hipStream_t)hs, B, leaf_state, leaf_mask,
-                                   packed_weights, pi, v); break;
+                                   packed_weights, pi, v, idx, count); break;
         case 3: hipLaunchKernelGGL(k_nn_forward<3>, grid, dim3(NNT), 0, (hipStream_t)hs, B, leaf_state, leaf_mask,
-                                   packed_weights, pi, v); break;
+                                   packed_weights, pi, v, idx, count); break;
         default: hipLaunchKernelGGL(k_nn_forward<4>, grid, dim3(NNT), 0, (hipStream_t)hs, B, leaf_state, leaf_mask,
-                                    packed_weights, pi, v); break;
+                                    packed_weights, pi, v, idx, count); break;
     }
     return check_launch();
+}
+
+int spl_nn_forward(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
+                   const float *packed_weights, float *pi, float *v, void *hs) {
+    return launch_nn(n_players, B, leaf_state, leaf_mask, packed_weights, pi, v, nullptr, nullptr, hs);
+}
+
+int spl_nn_forward_indexed(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
+                           const int32_t *leaf_index, const int32_t *leaf_count, const float *packed_weights,
+                           float *pi, float *v, void *hs) {
+    if (!leaf_index || !leaf_count) return SPL_EINVAL;
+    return launch_nn(n_players, B, leaf_state, leaf_mask, packed_weights, pi, v, leaf_index, leaf_count, hs);
 }
 
 }  // extern "C"

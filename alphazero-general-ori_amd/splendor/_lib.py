@@ -47,6 +47,7 @@ _SIGS = {
                           C.c_uint32, _vp], C.c_int),
     "spl_nn_packed_floats": ([C.c_int], C.c_int),
     "spl_nn_forward": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_nn_forward_indexed": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_rollout_run": ([C.c_void_p, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64,
                          C.c_uint32, C.c_uint32, _vp], C.c_int),
     "spl_mcts_create": ([C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)], C.c_int),
@@ -60,6 +61,7 @@ _SIGS = {
     "spl_mcts_set_roots_active": ([C.c_void_p, _vp, _vp, C.c_int, C.c_int, _vp], C.c_int),
     "spl_mcts_pick_best": ([C.c_void_p, _vp, C.c_uint32, C.c_uint32, _vp, _vp], C.c_int),
     "spl_mcts_select": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_mcts_select_compact": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_backup": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_root_stats": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_root_priors": ([C.c_void_p, _vp, _vp], C.c_int),

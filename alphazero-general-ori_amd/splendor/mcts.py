@@ -98,6 +98,8 @@ class BatchedMCTS:
         self.leaf_state = engine.new_state(B)
         self.leaf_mask = torch.zeros((B, MASK_WORDS), dtype=torch.int64, device=dev)
         self.leaf_valid = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.leaf_index = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.leaf_count = torch.zeros(1, dtype=torch.int32, device=dev)
         self.evaluator = evaluator or HashEvaluator(engine)
         self._hdr = torch.empty((B, HDR_DTYPE.itemsize // 4), dtype=torch.int32, device=dev)
 
@@ -216,11 +218,20 @@ class BatchedMCTS:
             self.simulate()
 
     def simulate(self):
-        """One simulation on every tree with budget left: select -> evaluate -> backup."""
+        """One simulation on every tree with budget left: select -> evaluate -> backup. An
+        evaluator that can take a compacted leaf list (`indexed`, the fused network) runs on
+        the trees whose leaf needs the network only."""
         s = self.e._s()
-        _lib.check(self.L.spl_mcts_select(self.h, _ptr(self.leaf_state), _ptr(self.leaf_mask),
-                                          _ptr(self.leaf_valid), s), "spl_mcts_select")
-        pi, v = self.evaluator(self.leaf_state, self.leaf_mask, self.leaf_valid)
+        if getattr(self.evaluator, "indexed", False):
+            _lib.check(self.L.spl_mcts_select_compact(self.h, _ptr(self.leaf_state), _ptr(self.leaf_mask),
+                                                      _ptr(self.leaf_valid), _ptr(self.leaf_index),
+                                                      _ptr(self.leaf_count), s), "spl_mcts_select_compact")
+            pi, v = self.evaluator(self.leaf_state, self.leaf_mask, self.leaf_valid, index=self.leaf_index,
+                                   count=self.leaf_count)
+        else:
+            _lib.check(self.L.spl_mcts_select(self.h, _ptr(self.leaf_state), _ptr(self.leaf_mask),
+                                              _ptr(self.leaf_valid), s), "spl_mcts_select")
+            pi, v = self.evaluator(self.leaf_state, self.leaf_mask, self.leaf_valid)
         _lib.check(self.L.spl_mcts_backup(self.h, _ptr(self.leaf_mask), _ptr(pi), _ptr(v), s),
                    "spl_mcts_backup")
 

@@ -238,13 +238,20 @@ class FusedNet:
         self.device = torch.device(device)
         self.w = pack_weights(FoldedNet(net).to(self.device).eval(), n_players)
 
-    def __call__(self, leaf_state, leaf_mask, pi=None, v=None):
+    def __call__(self, leaf_state, leaf_mask, pi=None, v=None, index=None, count=None):
+        """index / count (device int32 [B] / [1], spl_mcts_select_compact): evaluate only rows
+        index[:count] (other rows of pi / v are left as they are)."""
         B = leaf_state.shape[0]
         pi = pi if pi is not None else torch.empty((B, ACTIONS), dtype=torch.float32, device=self.device)
         v = v if v is not None else torch.empty((B, self.n), dtype=torch.float32, device=self.device)
         s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        _lib.check(_lib.lib().spl_nn_forward(self.n, B, _ptr(leaf_state), _ptr(leaf_mask), _ptr(self.w), _ptr(pi),
-                                             _ptr(v), s), "spl_nn_forward")
+        if index is None:
+            _lib.check(_lib.lib().spl_nn_forward(self.n, B, _ptr(leaf_state), _ptr(leaf_mask), _ptr(self.w),
+                                                 _ptr(pi), _ptr(v), s), "spl_nn_forward")
+        else:
+            _lib.check(_lib.lib().spl_nn_forward_indexed(self.n, B, _ptr(leaf_state), _ptr(leaf_mask), _ptr(index),
+                                                         _ptr(count), _ptr(self.w), _ptr(pi), _ptr(v), s),
+                       "spl_nn_forward_indexed")
         return pi, v
 
 
@@ -291,10 +298,15 @@ class LeafEvaluator:
         self._convert(leaf_state, leaf_mask)
         return self.net(self.x, self.valid, transposed=True)
 
+    @property
+    def indexed(self):
+        """The fused kernel can evaluate a compacted leaf list (spl_nn_forward_indexed)."""
+        return self.fused is not None
+
     @torch.no_grad()
-    def __call__(self, leaf_state, leaf_mask, leaf_valid=None):
+    def __call__(self, leaf_state, leaf_mask, leaf_valid=None, index=None, count=None):
         if self.fused is not None:
-            return self.fused(leaf_state, leaf_mask, self.pi_buf, self.v_buf)
+            return self.fused(leaf_state, leaf_mask, self.pi_buf, self.v_buf, index=index, count=count)
         if not self.use_graph:
             return self._run(leaf_state, leaf_mask)
         key = (leaf_state.data_ptr(), leaf_mask.data_ptr())

@@ -192,6 +192,13 @@ int spl_mcts_pick_best(spl_mcts *m, const uint8_t *active, uint32_t board_base, 
 /* leaf_state: B x S int8, leaf_mask: B x 7 u64, leaf_valid: B u8 (1 = needs the network) */
 int spl_mcts_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
                     void *hip_stream);
+/* select + the trees whose leaf needs the network listed compactly: leaf_index (B i32,
+ * device) holds their tree ids in [0, *leaf_count) in no particular order, leaf_count (device
+ * i32) their number; pair with spl_nn_forward_indexed so the network runs on those leaves
+ * only (terminal leaves and idle trees need no evaluation: ~half of all trees per iteration
+ * at BASELINE config 3's steady state). */
+int spl_mcts_select_compact(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
+                            int32_t *leaf_index, int32_t *leaf_count, void *hip_stream);
 /* pi: B x 409 f32 (policy over all actions, as predict returns), v: B x n f32 */
 int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v,
                     void *hip_stream);
@@ -274,6 +281,12 @@ int spl_hash_eval(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t
 int spl_nn_packed_floats(int n_players);
 int spl_nn_forward(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
                    const float *packed_weights, float *pi, float *v, void *hip_stream);
+/* the same network on the rows leaf_index[0 .. *leaf_count) only (device i32 list and count,
+ * as spl_mcts_select_compact writes them): boards, masks and outputs of row r = leaf_index[k]
+ * (B bounds the list); other rows of pi / v are left untouched. */
+int spl_nn_forward_indexed(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
+                           const int32_t *leaf_index, const int32_t *leaf_count, const float *packed_weights,
+                           float *pi, float *v, void *hip_stream);
 
 #ifdef __cplusplus
 }

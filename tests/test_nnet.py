@@ -142,3 +142,33 @@ def test_fused_kernel_many_tiles(n):
         p1, v1 = fused(bt[s:s + 32].contiguous(), mt[s:s + 32].contiguous())
         k = min(32, B - s)
         assert torch.equal(p1[:k], pi[s:s + k]) and torch.equal(v1[:k], v[s:s + k])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", (2, 3, 4))
+def test_fused_kernel_indexed_rows(n):
+    """spl_nn_forward_indexed on a scattered subset of rows (the search's compacted NN leaves)
+    writes exactly those rows, bit-identical to the full-batch kernel, and leaves every other
+    row untouched."""
+    from splendor.nnet import FusedNet, random_net
+    with np.load(os.path.join(GOLD, f"env_{n}p.npz")) as z:
+        st, mk = z["state"], z["mask_player"]
+    rng = np.random.default_rng(10 + n)
+    B = 777
+    idx = rng.integers(0, len(st), B)
+    boards = torch.from_numpy(st[idx].copy()).cuda()
+    mask = torch.from_numpy(_pack_mask(mk[idx].astype(bool))).cuda()
+    fused = FusedNet(random_net(n, seed=5), n, "cuda")
+    pi_full, v_full = fused(boards, mask)
+    rows = np.sort(rng.choice(B, 301, replace=False)).astype(np.int32)[::-1].copy()    # any order
+    index = torch.zeros(B, dtype=torch.int32, device="cuda")
+    index[:len(rows)] = torch.from_numpy(rows).cuda()
+    count = torch.tensor([len(rows)], dtype=torch.int32, device="cuda")
+    pi = torch.full((B, 409), -7.0, device="cuda")
+    v = torch.full((B, n), -7.0, device="cuda")
+    fused(boards, mask, pi, v, index=index, count=count)
+    sel = torch.from_numpy(rows.astype(np.int64)).cuda()
+    assert torch.equal(pi[sel], pi_full[sel]) and torch.equal(v[sel], v_full[sel])
+    other = torch.ones(B, dtype=torch.bool, device="cuda")
+    other[sel] = False
+    assert bool((pi[other] == -7.0).all()) and bool((v[other] == -7.0).all())

@@ -254,3 +254,38 @@ def test_coach_learn_iteration(tmp_path):
     assert {"temp.pt", "checkpoint.examples.npz"} <= files
     assert ("best.pt" in files) == ok
     assert len(c.trainExamplesHistory.iters) == 1 and len(c.trainExamplesHistory) > 0
+
+
+@pytest.mark.gpu
+def test_compacted_leaf_evaluation_matches_full_batch():
+    """Self-play with the network evaluated on the compacted NN-leaf list
+    (spl_mcts_select_compact + spl_nn_forward_indexed) plays exactly the games of the
+    full-batch evaluation: headers, root counts and drained examples bit-identical."""
+    from splendor.env import SplendorEngine
+    from splendor.nnet import LeafEvaluator, random_net
+    from splendor.selfplay import SelfPlay
+    args = dict(numMCTSSims=24, cpuct=2.5, fpu=0.3, prob_fullMCTS=0.5, ratio_fullMCTS=4, forced_playouts=False,
+                dirichletAlpha=0.3, temperature=[1.25, 0.8], tempThreshold=10)
+    e = SplendorEngine(2)
+    net = random_net(2, seed=1)
+    out = []
+    for indexed in (True, False):
+        ev = LeafEvaluator(e, net, 256, use_graph=False)
+        if not indexed:
+            ev.__class__ = type("FullBatch", (LeafEvaluator,), {"indexed": property(lambda self: False)})
+        sp = SelfPlay(e, 256, args, evaluator=ev, seed=0x5EED)
+        sp.reset()
+        sp.run(1500, use_graph=True)
+        torch.cuda.synchronize()
+        h = sp.headers()
+        ex = sp.drain()
+        out.append((h, sp.root_stats()[0].cpu().numpy(), {k: v.cpu().numpy() for k, v in ex.items()}))
+        del sp
+    (h0, c0, e0), (h1, c1, e1) = out
+    for k in ("player", "episode_step", "move_no", "game_no", "games_done", "moves", "sims_done", "depth"):
+        np.testing.assert_array_equal(h0[k], h1[k], err_msg=k)
+    np.testing.assert_array_equal(c0, c1)
+    assert len(e0["meta"]) > 0
+    o0, o1 = np.lexsort(e0["meta"].T[::-1]), np.lexsort(e1["meta"].T[::-1])
+    for k in e0:
+        np.testing.assert_array_equal(e0[k][o0], e1[k][o1], err_msg=k)
