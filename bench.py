@@ -112,16 +112,13 @@ def cpu_baseline(n, seed, target_s=5.0):
                             "sample": f"{B} boards x {s1} steps on 1 host core, {t1:.1f} s"}}
 
 
-def cpu_baseline_selfplay(n, seed, sims, target_s=4.0):
-    """CPU reference point for the self-play configs (rollouts = MCTS simulations): the
-    oracle's sequential search + self-play loop (oracle/splendor_oracle.c or_selfplay_run,
-    hash-prior network, genbu search args) timed directly, plus one SplendorNNet forward at
-    batch 1 on the CPU per simulation (PyTorch fp32, as GenericNNetWrapper.predict does per
-    leaf) timed separately: value = 1 / (1/search + network). On one host core (the
-    reference's self-play is single-threaded) and on every granted core (T Python threads
-    over board shards: ctypes and torch release the GIL, so both parts run in parallel)."""
-    import threading
+def _selfplay_cpu_worker(args):
+    """One host core: the oracle's self-play search on its own 8 games (board ids shifted by
+    its index) for `iters` iterations, then `k` batch-1 SplendorNNet CPU forwards (PyTorch
+    fp32, one intra-op thread) — both timed."""
+    n, seed, sims, iters, k, i = args
     import numpy as np
+    torch.set_num_threads(1)
     L = _oracle_lib()
     p8, pf = ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(ctypes.c_float)
     L.or_selfplay_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32,
@@ -134,67 +131,64 @@ def cpu_baseline_selfplay(n, seed, sims, target_s=4.0):
     R = 32 + 10 * n + n * n
     g = dict(GENBU_ARGS, numMCTSSims=sims)
     B = 8
+    board = np.zeros((B, R, 7), np.int8)
+    hdr = np.zeros((B, 8), np.int32)
 
-    def search(iters, base):
-        board = np.zeros((B, R, 7), np.int8)
-        hdr = np.zeros((B, 8), np.int32)
+    def search(it):
         t = time.perf_counter()
-        L.or_selfplay_run(n, B, iters, seed, base, g["numMCTSSims"], g["ratio_fullMCTS"], g["prob_fullMCTS"],
+        L.or_selfplay_run(n, B, it, seed, B * i, g["numMCTSSims"], g["ratio_fullMCTS"], g["prob_fullMCTS"],
                           g["cpuct"], g["fpu"], int(g["forced_playouts"]), g["tempThreshold"],
                           g["dirichletAlpha"], g["temperature"][0], board.ctypes.data_as(p8),
                           hdr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 0,
                           None, None, None, None, None, None, None)
         return time.perf_counter() - t
-
     from splendor.nnet import random_net
-    nthreads = torch.get_num_threads()
-    torch.set_num_threads(1)
     net = random_net(n, seed=0, device="cpu")
     x = torch.zeros((1, R, 7))
     va = torch.ones((1, 409), dtype=torch.bool)
+    with torch.no_grad():
+        for _ in range(20):
+            net(x, va)
+        if iters is None:                                # probe: size the sample
+            return search(10)
+        dt = search(iters)
+        t = time.perf_counter()
+        for _ in range(k):
+            net(x, va)
+        nn = (time.perf_counter() - t) / k
+    return B * iters / dt, nn, dt
 
-    def network(k):
-        with torch.no_grad():
-            t = time.perf_counter()
-            for _ in range(k):
-                net(x, va)
-            return (time.perf_counter() - t) / k
 
-    def parallel(T, fn, *args):
-        out = [None] * T
-        th = [threading.Thread(target=lambda i=i: out.__setitem__(i, fn(*args, i))) for i in range(T)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        return out
-
+def cpu_baseline_selfplay(n, seed, sims, target_s=4.0):
+    """CPU reference point for the self-play configs (rollouts = MCTS simulations): the
+    oracle's sequential search + self-play loop (oracle/splendor_oracle.c or_selfplay_run,
+    hash-prior network, genbu search args) timed directly, plus one SplendorNNet forward at
+    batch 1 on the CPU per simulation (PyTorch fp32, as GenericNNetWrapper.predict does per
+    leaf) timed separately: per core, value = 1 / (1/search + network). On one host core (the
+    reference's self-play is single-threaded) and on every granted core: T worker processes
+    (one core each, their own games) run at once and their rates add up."""
+    import multiprocessing as mp
     log(f"cpu baseline: {n} players, {sims} sims")
-    try:
-        search(4, 0)                                     # builds the oracle's tables once
-        network(20)
-        probe = search(10, 0)
+    ctx = mp.get_context("spawn")
+    T = host_threads()
+    with ctx.Pool(1) as pool:
+        probe = pool.map(_selfplay_cpu_worker, [(n, seed, sims, None, 0, 0)])[0]
         iters = max(10, int(10 * target_s / 2 / max(probe, 1e-6)))
-        dt1 = search(iters, 0)
-        rate1 = B * iters / dt1
-        nn1 = network(200)
-        T = host_threads()
-        dts = parallel(T, lambda it, i: search(it, B * (i + 1)), iters)
-        rateT = T * B * iters / max(dts)
-        nnT = max(parallel(T, lambda k, i: network(k), 200))
-    finally:
-        torch.set_num_threads(nthreads)
-    one = 1.0 / (1.0 / rate1 + nn1)
-    allc = T / (T / rateT + nnT)
+        r1, nn1, dt1 = pool.map(_selfplay_cpu_worker, [(n, seed, sims, iters, 200, 0)])[0]
+    with ctx.Pool(T) as pool:
+        res = pool.map(_selfplay_cpu_worker, [(n, seed, sims, iters, 200, i) for i in range(T)])
+    one = 1.0 / (1.0 / r1 + nn1)
+    allc = sum(1.0 / (1.0 / r + nnv) for r, nnv, _ in res)
+    dts = max(d for _, _, d in res)
+    nnT = sum(v for _, v, _ in res) / T
     return {"value": allc, "unit": "rollouts/s (MCTS simulations)", "cores": T, "kind": "port",
-            "sample": f"{T} threads x oracle self-play {B} games x {iters} simulations each ({max(dts):.1f} s, "
-                      f"search alone {rateT:.0f} sims/s) + SplendorNNet batch-1 CPU forward {nnT * 1e6:.0f} us "
-                      f"per leaf per thread (PyTorch fp32, 1 intra-op thread each, all threads at once); "
-                      f"value = T / (T/search + network)",
+            "sample": f"{T} processes (one core each) x oracle self-play 8 games x {iters} simulations ({dts:.1f} s) "
+                      f"+ SplendorNNet batch-1 CPU forward, {nnT * 1e6:.0f} us per leaf (PyTorch fp32, 1 thread), "
+                      f"all at once; value = sum over processes of 1 / (1/search + network)",
             "single_core": {"value": one, "cores": 1,
-                            "sample": f"{B} games x {iters} simulations ({dt1:.1f} s, search alone {rate1:.0f} "
-                                      f"sims/s) + {nn1 * 1e6:.0f} us network per leaf"},
-            "search_only": rateT, "network_us_per_leaf": nnT * 1e6}
+                            "sample": f"8 games x {iters} simulations ({dt1:.1f} s, search alone {r1:.0f} sims/s) + "
+                                      f"{nn1 * 1e6:.0f} us network per leaf"},
+            "network_us_per_leaf": nnT * 1e6}
 
 
 # saved args of the reference's only checkpoint, genbu.pt (SURVEY.md §0.7), = BASELINE config 3
