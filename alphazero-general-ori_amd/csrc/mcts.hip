@@ -24,8 +24,16 @@ __device__ unsigned long long g_select_timing[24];
 #endif
 #include "mcts_device.h"
 
+#ifndef SELECT_SPEC
+#define SELECT_SPEC 1      // k_select requests the previous simulation's next level during a pick
+#endif
 #ifndef SELECT_WAVES
-#define SELECT_WAVES 7     // k_select waves per SIMD (SGPR budget: 6 at 106 SGPRs, 7 at <= 96)
+#if SELECT_SPEC
+#define SELECT_WAVES 6     // k_select waves per SIMD (80 VGPRs with the speculative next level;
+                           // A/B on the box: 6 > 5 > no speculation at 7, tools/ab_select.sh)
+#else
+#define SELECT_WAVES 7     // (72 VGPRs)
+#endif
 #endif
 
 using namespace spl;
@@ -1174,6 +1182,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
 #endif
     int32_t *path_n = P.path_n + (size_t)t * P.pcap;
     int64_t *path_e = P.path_e + (size_t)t * P.pcap;
+    // the previous simulation's path (lane per level, first 64 levels), read before this
+    // descent overwrites it: most levels repeat it, so at each level the child the previous
+    // simulation took is requested speculatively while the pick runs
+    const int pdep = SELECT_SPEC ? min(H->depth, 64) : 0;
+    int pv_n = -2;
+    int64_t pv_e = -1;
+    if (l < pdep) { pv_n = path_n[l]; pv_e = path_e[l]; }
     SPL_PROBE(0)
     int node = H->root, depth = 0, kind = LEAF_NN;
     uint64_t k0 = 0, k1 = 0;
@@ -1206,6 +1221,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         const float cf = (float)C.cpuct;
         int pend = -1, pend_n = 0;                           // path entry not yet stored
         int64_t pend_e = 0;
+        bool spec = false;                                   // snsq / se64 hold this level
+        NodeStat snsq{0.0, 0, 0};
+        Edge se64{EdgeStat{0.f, 0, Q_UNSET}, EdgeLink{0, 0, -1, 0}};
         for (;;) {
             SPL_PROBE(1)
             if (depth > 0 && ec < 0) {
@@ -1217,17 +1235,42 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             if (depth >= P.pcap) { kind = LEAF_NONE; if (l == 0) H->overflow = 2; break; }
             // the level's edges (first 64; lanes past the range read the first edge) and the
             // node's visit stats are requested together: one round trip per level
-            const NodeStat nsq = nst_t[node];
-            const Edge e64 = ed_t[eb + (l < ec ? l : 0)];
+            NodeStat nsq;
+            Edge e64;
+            if (spec) {                                  // requested during the previous pick
+                nsq = snsq;
+                e64 = se64;
+            } else {
+                nsq = nst_t[node];
+                e64 = ed_t[eb + (l < ec ? l : 0)];
+            }
+            spec = false;
             // the previous level's path entry is stored behind this level's loads: vmcnt counts
             // stores too, in issue order, so a store issued first would delay the loads' wait
             if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_e[pend] = pend_e; }
             pend = -1;
+            // speculation: the child the previous simulation took here, if linked
+            int pj = -1;
+            if (SELECT_SPEC && depth < pdep && __builtin_amdgcn_readlane(pv_n, depth) == node) {
+                const int64_t jj = readlane64(pv_e, depth) - eb;
+                if (jj >= 0 && jj < ec && jj < 64) {
+                    const int j = (int)jj;
+                    const int pc = __builtin_amdgcn_readlane(e64.k.child, j);
+                    const int pcec = __builtin_amdgcn_readlane((int)e64.k.cec, j);
+                    if (pc >= 0 && pcec >= 0) {
+                        const int64_t pceb = readlane64(e64.k.ceb, j);
+                        snsq = nst_t[pc];
+                        se64 = ed_t[pceb + (l < pcec ? l : 0)];
+                        pj = j;
+                    }
+                }
+            }
             const int ns = nsq.ns;
             const double qs = nsq.qs;
             const Pick pk = ec <= 64 && !(forced && depth == 0)
                                 ? pick_edge64(e64, cpuct, fpu, cf, ec, ns, qs)
                                 : pick_edge_desc(P, C, eb, ec, ns, qs, forced && depth == 0, sims, e64);
+            spec = pk.e == pj;
             const int64_t ge = eb + pk.e;
 #if MCTS_TIMING
             if (threadIdx.x == 0) {
