@@ -1191,6 +1191,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
     if (l < pdep) { pv_n = path_n[l]; pv_e = path_e[l]; }
     SPL_PROBE(0)
     int node = H->root, depth = 0, kind = LEAF_NN;
+    int miss = -1;                                       // the NN leaf's empty table slot
     uint64_t k0 = 0, k1 = 0;
 #if MCTS_TIMING
     bool prefix_run = true;
@@ -1313,7 +1314,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             if (child < 0) {
                 wave_fingerprint<N>(s, k0, k1);
                 k0 = uniform64(k0); k1 = uniform64(k1);
-                child = uniform(hash_lookup(P, t, k0, k1));
+                child = uniform(hash_lookup(P, t, k0, k1, &miss));
+                miss = uniform(miss);
                 if (child >= 0) {                            // transposition: link + cache
                     ceb = P.neb[child];
                     cec = P.nterm[child] ? -1 : P.nec[child];
@@ -1372,6 +1374,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             int g = -1;
             if (l == 0) g = node_slot(P, H, t, H->node_count);
             g = __shfl(g, 0, 64);
+            if (l == 0) H->leaf_slot = g;
             if (g >= 0) {
                 uint64_t *dst = reinterpret_cast<uint64_t *>(P.nbrd + (size_t)g * NodeBoard<N>::BYTES);
                 for (int r = l; r < Lx::ROWS; r += 64) dst[r] = row(s, r);
@@ -1382,6 +1385,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
     if (l == 0) {
         H->depth = depth;
         H->leaf_kind = kind;
+        H->leaf_hslot = kind == LEAF_NN ? miss : -1;
+        if (!P.nbrd || kind != LEAF_NN) H->leaf_slot = -1;
         H->leaf_k0 = k0; H->leaf_k1 = k1;
         H->leaf_round = (uint8_t)bt(row(s, 0), 6);
 #pragma unroll
@@ -1552,7 +1557,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         int g = -1;
         int64_t eb = -1;
         if (l == 0) {
-            g = node_slot(P, H, t, H->node_count);
+            const int rs = H->leaf_slot;                 // reserved by k_select (node boards)
+            g = rs >= 0 ? rs : node_slot(P, H, t, H->node_count);
             if (g >= 0) eb = edge_run(P, H, t, ec);
         }
         g = __shfl(g, 0, 64);
@@ -1605,7 +1611,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             P.nkey0[g] = H->leaf_k0; P.nkey1[g] = H->leaf_k1;
             P.neb[g] = eb; P.nec[g] = ec; P.nst[g].ns = 0;
             P.nst[g].qs = (double)val[0]; P.nround[g] = H->leaf_round; P.nterm[g] = 0;
-            hash_insert(P, t, H->leaf_k0, g);
+            const int hslot = H->leaf_hslot;             // the select's lookup ended there
+            if (hslot >= 0) P.hslot[(size_t)t * P.hcap + hslot] = g;
+            else hash_insert(P, t, H->leaf_k0, g);
             if (depth == 0) { H->root = g; H->root_eb = eb; H->root_ec = ec; }
             else {
                 const int64_t pe = path_e[depth - 1];

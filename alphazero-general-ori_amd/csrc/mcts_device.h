@@ -36,8 +36,10 @@ struct TreeHdr {
                                          // edge page, nodes kept by the last collection
     int32_t root_round, gc_queued, withdrawals, gcs;   // root round (deferred GC), queued for
                                          // k_gc, simulations withdrawn for GC, collections run
+    int32_t leaf_hslot, leaf_slot, pad1, pad2;   // the NN leaf's empty table slot (found by the
+                                         // select's lookup) and reserved node slot, or -1
 };
-static_assert(sizeof(TreeHdr) == 176, "TreeHdr layout (splendor/mcts.py HDR_DTYPE)");
+static_assert(sizeof(TreeHdr) == 192, "TreeHdr layout (splendor/mcts.py HDR_DTYPE)");
 // gc_state: 0 none; 1 a leaf did not fit mid-search (withdrawn, k_gc collects, the descent
 // repeats); 2 collected once this search; 3 collection before this search (must: the
 // search does not fit the tree's maxima); 5 collection before this search (should: garbage
@@ -239,13 +241,19 @@ __device__ __forceinline__ void wave_fingerprint(const int8_t *s, uint64_t &k0, 
     k1 = wave_xor64(b) | 1ull;  // never equal to an empty key
 }
 
-__device__ __forceinline__ int hash_lookup(const Pools &P, int t, uint64_t k0, uint64_t k1) {
+// miss_slot (optional): on a miss, the empty slot that ended the probe — where an insert
+// of this key goes while the table is unchanged
+__device__ __forceinline__ int hash_lookup(const Pools &P, int t, uint64_t k0, uint64_t k1, int *miss_slot = nullptr) {
     const int32_t *hs = P.hslot + (size_t)t * P.hcap;
     const uint64_t *K0 = P.nkey0, *K1 = P.nkey1;
     uint32_t h = (uint32_t)(k0 ^ (k0 >> 32)) & (uint32_t)(P.hcap - 1);
+    if (miss_slot) *miss_slot = -1;
     for (int probe = 0; probe < P.hcap; probe++) {
         const int c = hs[h];
-        if (c < 0) return -1;
+        if (c < 0) {
+            if (miss_slot) *miss_slot = (int)h;
+            return -1;
+        }
         if (K0[c] == k0 && K1[c] == k1) return c;
         h = (h + 1) & (uint32_t)(P.hcap - 1);
     }
