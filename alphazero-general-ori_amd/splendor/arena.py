@@ -67,9 +67,15 @@ class BatchedArena:
                      forced_playouts=bool(_arg(args, "forced_playouts", False)), dirichletAlpha=0.0,
                      temperature=list(_arg(args, "temperature", [1.25, 0.8])),
                      tempThreshold=int(_arg(args, "tempThreshold", 10)))
+        # the two players' arenas share what is free now (each would otherwise plan 80 % of it)
+        budget = None
+        if self.e.device.type == "cuda":
+            budget = int(0.4 * torch.cuda.mem_get_info(self.e.device)[0])
         self.mcts = [BatchedMCTS(self.e, self.B, margs, evaluators[k], dirichlet_noise=False,
-                                 seed=self.mcts_seed(k), board_base=self.game_base) for k in range(2)]
+                                 seed=self.mcts_seed(k), board_base=self.game_base, mem_budget=budget)
+                     for k in range(2)]
         self.last = None
+        self.capacity = {"prunes": 0, "resets": 0, "unexpanded": 0}
 
     def mcts_seed(self, k):
         return self.seed ^ (k + 1)
@@ -145,6 +151,13 @@ class BatchedArena:
         recs = []
         for g0 in range(0, num, self.B):
             recs.append(self._play_batch(g0, min(self.B, num - g0)))
+        # capacity events of both players' searches (a deviation from the reference's table)
+        ev = [m.capacity_events() for m in self.mcts]
+        self.capacity = {k: sum(e[k] for e in ev) for k in ev[0]}
+        if any(self.capacity.values()):
+            import warnings
+            warnings.warn(f"BatchedArena capacity events {self.capacity}: some searches ran on pruned trees or "
+                          f"left leaves unstored")
         last = {k: np.concatenate([r[k] for r in recs]) for k in recs[0]}
         r0 = last["result"][:, 0]
         ovt = last["one_vs_two"]

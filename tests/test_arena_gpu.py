@@ -69,6 +69,7 @@ def test_arena_matches_oracle(n, G, sims):
     assert one == int(np.sum(np.where(ovt, r0 == 1.0, r0 == -1.0)))
     assert two == int(np.sum(np.where(ovt, r0 == -1.0, r0 == 1.0)))
     assert one + two + draws == G
+    assert ar.capacity == {"prunes": 0, "resets": 0, "unexpanded": 0}
 
 
 class NegatedHash:
