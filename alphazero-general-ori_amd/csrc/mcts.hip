@@ -24,16 +24,8 @@ __device__ unsigned long long g_select_timing[24];
 #endif
 #include "mcts_device.h"
 
-#ifndef SELECT_SPEC
-#define SELECT_SPEC 1      // k_select requests the previous simulation's next level during a pick
-#endif
 #ifndef SELECT_WAVES
-#if SELECT_SPEC
-#define SELECT_WAVES 6     // k_select waves per SIMD (80 VGPRs with the speculative next level;
-                           // A/B on the box: 6 > 5 > no speculation at 7, tools/ab_select.sh)
-#else
-#define SELECT_WAVES 7     // (72 VGPRs)
-#endif
+#define SELECT_WAVES 6     // k_select waves per SIMD (80 VGPRs; 7 spills)
 #endif
 
 using namespace spl;
@@ -79,6 +71,16 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
     const int hi = __builtin_amdgcn_readlane((int)((uint64_t)x >> 32), l);
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    return __longlong_as_double(readlane64(__double_as_longlong(x), l));
+}
+
+// path_x: a path level's edge offset in its node's CSR run, the run's count and the action
+__device__ __forceinline__ int px_pack(int off, int ec, int a) { return off | (ec << 9) | (a << 18); }
+__device__ __forceinline__ int px_off(int x) { return x & 0x1ff; }
+__device__ __forceinline__ int px_count(int x) { return (x >> 9) & 0x1ff; }
+__device__ __forceinline__ int px_action(int x) { return (x >> 18) & 0x1ff; }
+
 __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &C, int64_t eb, int ec,
                                                int ns, double qs, bool forced, int step, const Edge &first) {
     const int l = lane_id();
@@ -201,24 +203,23 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
     return {bi, av, cv, rcv, rbv};
 }
 
-// the descent's common case: a node with at most 64 edges and no forced playouts at this
-// level — one edge per lane, straight-line (lanes past the node's range read its first edge
-// and take no part), the float32 screen of pick_edge_desc with the exact float64 arg-max as
-// the fallback. Same result as pick_edge_desc.
-__device__ __forceinline__ Pick pick_edge64(const Edge &e, double cpuct, double fpu, float cf, int ec, int ns,
+// pick_highest_UCB's arg-max over a node with at most 64 edges and no forced playouts at this
+// level, one edge per lane (lanes >= ec hold anything and take no part), straight-line: the
+// float32 screen of pick_edge_desc with the exact float64 arg-max as the fallback. Uniform.
+__device__ __forceinline__ int ucb_argmax64(const EdgeStat &e, double cpuct, double fpu, float cf, int ec, int ns,
                                             double qs) {
     const int l = lane_id();
     const bool in = l < ec;
     const double fpu_init = fpu > 0 ? qs - fpu : fpu;
-    const bool vis = e.s.q != Q_UNSET;
+    const bool vis = e.q != Q_UNSET;
     int bi;
     {
         // branch-free estimate; v_sqrt_f32 / v_rcp_f32 (1 ulp) are inside the error bound
         const float nf = (float)ns;
         const float sq = vis ? __builtin_amdgcn_sqrtf(nf) : __builtin_amdgcn_sqrtf(nf + 1e-8f);
-        const float rc = vis ? __builtin_amdgcn_rcpf(1.f + (float)e.s.n) : 1.f;
-        const float qf = vis ? (float)e.s.q : (float)fpu_init;
-        const float uf = qf + cf * e.s.p * sq * rc;
+        const float rc = vis ? __builtin_amdgcn_rcpf(1.f + (float)e.n) : 1.f;
+        const float qf = vis ? (float)e.q : (float)fpu_init;
+        const float uf = qf + cf * e.p * sq * rc;
         const float er = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
         const float L = wave_max_f32(in ? uf - er : -INFINITY);
         const uint64_t c = __ballot(in && uf + er >= L);
@@ -228,14 +229,45 @@ __device__ __forceinline__ Pick pick_edge64(const Edge &e, double cpuct, double 
         const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
         double u = -INFINITY;
         if (in)
-            u = vis ? e.s.q + cpuct * (double)e.s.p * sq / (double)(1 + e.s.n)
-                    : fpu_init + cpuct * (double)e.s.p * sq_eps;
+            u = vis ? e.q + cpuct * (double)e.p * sq / (double)(1 + e.n)
+                    : fpu_init + cpuct * (double)e.p * sq_eps;
         const double m = wave_max_f64(u);
         bi = __ffsll((unsigned long long)__ballot(u == m)) - 1;
     }
-    bi = uniform(bi);
+    return uniform(bi);
+}
+
+// the descent's root level in the common case (<= 64 edges, no forced playouts): the arg-max
+// and the chosen edge's link by readlane. Same result as pick_edge_desc.
+__device__ __forceinline__ Pick pick_edge64(const Edge &e, double cpuct, double fpu, float cf, int ec, int ns,
+                                            double qs) {
+    const int bi = ucb_argmax64(e.s, cpuct, fpu, cf, ec, ns, qs);
     return {bi, __builtin_amdgcn_readlane((int)e.k.a, bi), __builtin_amdgcn_readlane(e.k.child, bi),
             __builtin_amdgcn_readlane((int)e.k.cec, bi), readlane64(e.k.ceb, bi)};
+}
+
+// exact pick_highest_UCB arg-max (float64, strict '>' in edge order = lowest index holding the
+// maximum) over any number of edges, the edge at offset `off` taking the statistics (on, oq)
+// (just written by this wave). Uniform.
+__device__ int ucb_argmax_wide(const Edge *E, int ec, int ns, double qs, double cpuct, double fpu, int off, int on,
+                               double oq) {
+    const int l = lane_id();
+    const double fpu_init = fpu > 0 ? qs - fpu : fpu;
+    const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
+    double bu = -INFINITY;
+    int bj = 0x7fffffff;
+    for (int base = 0; base < ec; base += 64) {
+        const int i = base + l;
+        if (i < ec) {
+            EdgeStat e = E[i].s;
+            if (i == off) { e.n = on; e.q = oq; }
+            const double u = e.q != Q_UNSET ? e.q + cpuct * (double)e.p * sq / (double)(1 + e.n)
+                                            : fpu_init + cpuct * (double)e.p * sq_eps;
+            if (u > bu) { bu = u; bj = i; }
+        }
+    }
+    wave_argmax(bu, bj);
+    return uniform(bj);
 }
 
 // ------------------------------------------------------------ prior sums
@@ -572,15 +604,15 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         const int ni = i < nc ? remap[i] : -1;
         uint64_t k0 = 0, k1 = 0;
         int64_t oeb = 0;
-        int ec = 0, ns = 0, rd = 0, vs = 0;
-        double qs = 0;
+        int ec = 0, rd = 0, vs = 0;
+        NodeStat nst{0.0, 0, -1, 0, -1, 0, 0, 0};
         int8_t term = 0;
         float es[4] = {0, 0, 0, 0};
         if (ni >= 0) {
             const int g = node_g(P, t, i);
             k0 = P.nkey0[g]; k1 = P.nkey1[g];
-            oeb = P.neb[g]; ec = P.nec[g]; ns = P.nst[g].ns; rd = P.nround[g];
-            qs = P.nst[g].qs; term = P.nterm[g];
+            oeb = P.neb[g]; ec = P.nec[g]; nst = P.nst[g]; rd = P.nround[g];
+            term = P.nterm[g];
 #pragma unroll
             for (int j = 0; j < 4; j++) es[j] = P.nes[(size_t)g * 4 + j];
             vs = S.nvs[i];
@@ -590,8 +622,9 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
             const int ng = node_g(P, t, ni);
             const int run_ec = term ? 0 : ec;
             P.nkey0[ng] = k0; P.nkey1[ng] = k1;
-            P.neb[ng] = run_ec > 0 ? edge_g(P, t, vs) : 0; P.nec[ng] = ec; P.nst[ng].ns = ns; P.nround[ng] = rd;
-            P.nst[ng].qs = qs; P.nterm[ng] = term;
+            P.neb[ng] = run_ec > 0 ? edge_g(P, t, vs) : 0; P.nec[ng] = ec; P.nround[ng] = rd;
+            P.nst[ng] = nst; P.nterm[ng] = term;
+            S.queue[ni] = nst.bchild;                    // (the arg-max's link, remapped below)
 #pragma unroll
             for (int j = 0; j < 4; j++) P.nes[(size_t)ng * 4 + j] = es[j];
             S.cs[ni] = vs; S.cnt[ni] = run_ec; S.inv[ni] = i; S.ost[ni] = oeb;
@@ -600,6 +633,16 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     }
     int edges;
     (void)block_scan(my_edges, edges, L);
+    // the cached arg-max's link (NodeStat) remapped like the edges' links below
+    for (int ni = tid; ni < kept; ni += GCT) {
+        const int ch = S.queue[ni];
+        if (ch >= 0) {
+            const int nl = remap[node_l(P, ch)];
+            NodeStat *ns = P.nst + node_g(P, t, ni);
+            ns->bchild = nl >= 0 ? node_g(P, t, nl) : -1;
+            if (nl >= 0) ns->bceb = S.cnt[nl] > 0 ? edge_g(P, t, S.cs[nl]) : 0;
+        }
+    }
     // the owner of every new edge position (gaps before a page start: -1)
     for (int k = tid; k < run; k += GCT) S.own[k] = -1;
     __syncthreads();
@@ -868,6 +911,7 @@ __global__ __launch_bounds__(GCT) void k_gc(Pools P, SearchCfg C) {
             H->root_ec = rec;
             H->gc_state = nst;                           // (2: once per search)
             H->gc_queued = 0;
+            H->depth = 0;                                // (node ids moved: no path reuse)
         }
         __syncthreads();
     }
@@ -1182,34 +1226,32 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
 #endif
     int32_t *path_n = P.path_n + (size_t)t * P.pcap;
     int64_t *path_e = P.path_e + (size_t)t * P.pcap;
-    // the previous simulation's path (lane per level, first 64 levels), read before this
-    // descent overwrites it: most levels repeat it, so at each level the child the previous
-    // simulation took is requested speculatively while the pick runs
-    const int pdep = SELECT_SPEC ? min(H->depth, 64) : 0;
-    int pv_n = -2;
-    int64_t pv_e = -1;
-    if (l < pdep) { pv_n = path_n[l]; pv_e = path_e[l]; }
+    int32_t *path_x = P.path_x + (size_t)t * P.pcap;
+    // the previous simulation's path, first 64 levels (lane per level), requested with the header
+    int ppn = -1, ppx = 0;
+    int64_t ppe = 0;
+    if (l < P.pcap) { ppn = path_n[l]; ppx = path_x[l]; ppe = path_e[l]; }
     SPL_PROBE(0)
     int node = H->root, depth = 0, kind = LEAF_NN;
     int miss = -1;                                       // the NN leaf's empty table slot
     uint64_t k0 = 0, k1 = 0;
-#if MCTS_TIMING
-    bool prefix_run = true;
-#endif
     float val[4] = {0, 0, 0, 0};
     if (node < 0) {
         wave_fingerprint<N>(s, k0, k1);                  // the root itself is the leaf
     } else {
         // CSR range of the current node: the root's from the header, every child's from the
-        // {eb, ec} cached on the edge that led to it, so a level costs ONE round trip (the
-        // node's visit stats travel with its edges); ec < 0 marks a terminal child
+        // link cached with its parent's arg-max (NodeStat) or on the edge that led to it
         int64_t eb = H->root_eb;
         int ec = H->root_ec;
-        if (sims == 0 && H->noise_pending) {
+        const bool noised = sims == 0 && H->noise_pending;
+        if (noised) {
             apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no, lpr[w], false);
             if (l == 0) H->noise_pending = 0;           // (a withdrawn simulation must not re-noise)
         }
         const bool forced = H->forced;
+        // the root's cached arg-max holds unless its priors were just noised or forced
+        // playouts make its pick depend on the simulation index (MCTS.py:208-213)
+        const bool root_cache = !forced && !noised;
         // node_boards: a linked child's board is stored, so the descent follows links without
         // the in-tree transition and stages a board only where it needs one (the edge to
         // expand); `bnode` is the node whose board is in LDS (the root's, from root_state)
@@ -1220,11 +1262,59 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         const NodeStat *nst_t = P.nst;
         const double cpuct = C.cpuct, fpu = C.fpu;
         const float cf = (float)C.cpuct;
-        int pend = -1, pend_n = 0;                           // path entry not yet stored
+        int pend = -1, pend_n = 0, pend_x = 0;               // path entry not yet stored
         int64_t pend_e = 0;
-        bool spec = false;                                   // snsq / se64 hold this level
-        NodeStat snsq{0.0, 0, 0};
-        Edge se64{EdgeStat{0.f, 0, Q_UNSET}, EdgeLink{0, 0, -1, 0}};
+        // The previous simulation's path (this search's, same root; k_gc clears H->depth when
+        // it moves nodes) is this descent's as far as its nodes' cached arg-maxes still pick
+        // its edges: k_backup rewrote exactly those nodes' records, so one round trip for the
+        // path and one for its nodes' records (lane per level) replace the first levels'
+        // dependent loads. The descent resumes at level q = the first level whose node now
+        // picks another edge (or the previous leaf's parent), with that node's record in hand.
+        bool have = false;
+        NodeStat hq{0.0, 0, -1, 0, -1, 0, 0, 0};
+        {
+            const int pd = min(H->depth, 64);
+            const bool ok = sims > 0 && pd > 0 && __builtin_amdgcn_readfirstlane(ppn) == node;
+            if (ok) {
+                NodeStat h{0.0, 0, -1, 0, -1, 0, 0, 0};
+                if (l < pd) h = nst_t[ppn];
+                const bool agree = l < pd && h.best == px_off(ppx) && (l > 0 || root_cache);
+                const uint64_t dis = ~__ballot(agree) & (pd < 64 ? (1ull << pd) - 1 : ~0ull);
+                const int p = dis ? __ffsll((unsigned long long)dis) - 1 : pd;
+                const int q = uniform(min(p, pd - 1));
+                const int xq = __builtin_amdgcn_readlane(ppx, q);
+                node = __builtin_amdgcn_readlane(ppn, q);
+                ec = px_count(xq);
+                eb = readlane64(ppe, q) - px_off(xq);
+                depth = q;
+                hq.qs = readlane_f64(h.qs, q);
+                hq.ns = __builtin_amdgcn_readlane(h.ns, q);
+                hq.best = (int16_t)__builtin_amdgcn_readlane((int)h.best, q);
+                hq.ba = (int16_t)__builtin_amdgcn_readlane((int)h.ba, q);
+                hq.bchild = __builtin_amdgcn_readlane(h.bchild, q);
+                hq.bcec = (int16_t)__builtin_amdgcn_readlane((int)h.bcec, q);
+                hq.bceb = readlane64(h.bceb, q);
+                have = true;
+                if (!nbrd) {
+                    // no node boards: the board of the resume node is the root's with the
+                    // path's moves applied (the in-tree transition, MCTS.py:227-235)
+                    for (int d = 0; d < q; d++) {
+                        const int a = px_action(__builtin_amdgcn_readlane(ppx, d));
+                        Chance ch{nullptr, 0, 0, 0, 0};
+                        int nxt;
+                        switch (move_kind_of(a)) {
+                            case MK_GEMS: nxt = make_move<N, MK_GEMS>(s, a, 0, true, ch); break;
+                            case MK_BUY: nxt = make_move<N, MK_BUY>(s, a, 0, true, ch); break;
+                            case MK_RESERVE: nxt = make_move<N, MK_RESERVE>(s, a, 0, true, ch); break;
+                            default: nxt = make_move<N, MK_BUY_RESERVED>(s, a, 0, true, ch); break;
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        if (nxt) wave_roll_players<N>(s, s, nxt);
+                    }
+                    bnode = node;
+                }
+            }
+        }
         for (;;) {
             SPL_PROBE(1)
             if (depth > 0 && ec < 0) {
@@ -1234,55 +1324,34 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                 break;
             }
             if (depth >= P.pcap) { kind = LEAF_NONE; if (l == 0) H->overflow = 2; break; }
-            // the level's edges (first 64; lanes past the range read the first edge) and the
-            // node's visit stats are requested together: one round trip per level
-            NodeStat nsq;
-            Edge e64;
-            if (spec) {                                  // requested during the previous pick
-                nsq = snsq;
-                e64 = se64;
-            } else {
-                nsq = nst_t[node];
-                e64 = ed_t[eb + (l < ec ? l : 0)];
-            }
-            spec = false;
+            // below the root a level is ONE 32-byte load: the node's statistics with its cached
+            // arg-max and that edge's link (NodeStat); the root's edges (first 64; lanes past
+            // the range read the first edge) are requested with its statistics
+            NodeStat nsq = hq;
+            if (!have) nsq = nst_t[node];
+            have = false;
+            const bool use_cache = depth > 0 || root_cache;
+            Edge e64{EdgeStat{0.f, 0, Q_UNSET}, EdgeLink{0, 0, -1, 0}};
+            if (!use_cache) e64 = ed_t[eb + (l < ec ? l : 0)];
             // the previous level's path entry is stored behind this level's loads: vmcnt counts
             // stores too, in issue order, so a store issued first would delay the loads' wait
-            if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_e[pend] = pend_e; }
+            if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_e[pend] = pend_e; path_x[pend] = pend_x; }
             pend = -1;
-            // speculation: the child the previous simulation took here, if linked
-            int pj = -1;
-            if (SELECT_SPEC && depth < pdep && __builtin_amdgcn_readlane(pv_n, depth) == node) {
-                const int64_t jj = readlane64(pv_e, depth) - eb;
-                if (jj >= 0 && jj < ec && jj < 64) {
-                    const int j = (int)jj;
-                    const int pc = __builtin_amdgcn_readlane(e64.k.child, j);
-                    const int pcec = __builtin_amdgcn_readlane((int)e64.k.cec, j);
-                    if (pc >= 0 && pcec >= 0) {
-                        const int64_t pceb = readlane64(e64.k.ceb, j);
-                        snsq = nst_t[pc];
-                        se64 = ed_t[pceb + (l < pcec ? l : 0)];
-                        pj = j;
-                    }
-                }
+            const int cbest = uniform(nsq.best);
+            Pick pk;
+            if (use_cache && cbest >= 0) {
+                pk = Pick{cbest, uniform(nsq.ba), uniform(nsq.bchild), uniform(nsq.bcec),
+                          (int64_t)uniform64((uint64_t)nsq.bceb)};
+            } else {
+                if (use_cache) e64 = ed_t[eb + (l < ec ? l : 0)];   // (no cached arg-max)
+                const int ns = nsq.ns;
+                const double qs = nsq.qs;
+                pk = ec <= 64 && !(forced && depth == 0)
+                         ? pick_edge64(e64, cpuct, fpu, cf, ec, ns, qs)
+                         : pick_edge_desc(P, C, eb, ec, ns, qs, forced && depth == 0, sims, e64);
             }
-            const int ns = nsq.ns;
-            const double qs = nsq.qs;
-            const Pick pk = ec <= 64 && !(forced && depth == 0)
-                                ? pick_edge64(e64, cpuct, fpu, cf, ec, ns, qs)
-                                : pick_edge_desc(P, C, eb, ec, ns, qs, forced && depth == 0, sims, e64);
-            spec = pk.e == pj;
             const int64_t ge = eb + pk.e;
-#if MCTS_TIMING
-            if (threadIdx.x == 0) {
-                spl_probe_acc[23] += 1;                  // levels
-                if (prefix_run) {                        // levels that repeat the previous path
-                    if (path_n[depth] == node && path_e[depth] == ge) spl_probe_acc[22] += 1;
-                    else prefix_run = false;
-                }
-            }
-#endif
-            pend = depth; pend_n = node; pend_e = ge;
+            pend = depth; pend_n = node; pend_e = ge; pend_x = px_pack(pk.e, ec, pk.a);
             depth++;
             int child = uniform(pk.child);
             int64_t ceb = pk.ceb;
@@ -1311,6 +1380,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             __builtin_amdgcn_wave_barrier();
             if (nxt) wave_roll_players<N>(s, s, nxt);
             SPL_PROBE(3)
+            // a link written here is copied into the node's cached arg-max when that is the edge
+            // (k_backup rewrites it anyway; this keeps it exact when the simulation is withdrawn)
+            const bool cached = uniform(nsq.best) == pk.e;
             if (child < 0) {
                 wave_fingerprint<N>(s, k0, k1);
                 k0 = uniform64(k0); k1 = uniform64(k1);
@@ -1319,13 +1391,16 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                 if (child >= 0) {                            // transposition: link + cache
                     ceb = P.neb[child];
                     cec = P.nterm[child] ? -1 : P.nec[child];
-                    if (l == 0) { P.ed[ge].k.child = child; set_cr(P.ed[ge].k, ceb, cec); }
+                    if (l == 0) {
+                        P.ed[ge].k.child = child;
+                        set_cr(P.ed[ge].k, ceb, cec);
+                        if (cached) {
+                            P.nst[node].bchild = child; P.nst[node].bcec = (int16_t)cec; P.nst[node].bceb = ceb;
+                        }
+                    }
                 }
             }
             SPL_PROBE(4)
-#if MCTS_TIMING
-            if (threadIdx.x == 0) spl_probe_acc[20] += 1;
-#endif
             if (child >= 0) {
                 node = child;
                 bnode = child;
@@ -1350,13 +1425,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                         H->unexpanded += 1;
                     } else {
                         P.nkey0[g] = k0; P.nkey1[g] = k1; P.neb[g] = 0;
-                        P.nec[g] = 0; P.nst[g].ns = 0; P.nst[g].qs = 0;
+                        P.nec[g] = 0;
+                        P.nst[g] = NodeStat{0.0, 0, -1, 0, -1, 0, 0, 0};
                         P.nround[g] = (uint8_t)bt(row(s, 0), 6); P.nterm[g] = 1;
 #pragma unroll
                         for (int i = 0; i < 4; i++) P.nes[(size_t)g * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
                         hash_insert(P, t, k0, g);
                         P.ed[ge].k.child = g;
                         set_cr(P.ed[ge].k, 0, -1);
+                        if (cached) { P.nst[node].bchild = g; P.nst[node].bcec = -1; P.nst[node].bceb = 0; }
                         H->node_count = id + 1;
                     }
                 }
@@ -1364,7 +1441,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             }
             break;                                           // new NN leaf
         }
-        if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_e[pend] = pend_e; }
+        if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_e[pend] = pend_e; path_x[pend] = pend_x; }
     }
     __builtin_amdgcn_wave_barrier();
     SPL_PROBE(5)
@@ -1517,8 +1594,19 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
         if (leaf_valid[b0 + i / 7]) leaf_mask[(size_t)b0 * 7 + i] = (&msk[0][0])[i];
 }
 
+// k_backup: expansion of the NN leaf, the path backup (MCTS.py:169-176) and every path node's
+// cached arg-max (NodeStat): after its update the wave scans each level's edges (the edges of
+// BK_G levels requested together), so the next descent through the node reads its pick
+// instead of scanning (one dependent load per level in k_select).
+#ifndef BK_G
+#define BK_G 4
+#endif
+#ifndef BACKUP_WAVES
+#define BACKUP_WAVES 6
+#endif
+
 template <int N>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) void k_backup(Pools P, SearchCfg C, int B,
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_WAVES))) void k_backup(Pools P, SearchCfg C, int B,
                                                     const uint64_t *__restrict__ leaf_mask,
                                                     const float *__restrict__ pi,
                                                     const float *__restrict__ v) {
@@ -1532,15 +1620,17 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
     const int depth = H->depth;
     const int32_t *path_n = P.path_n + (size_t)t * P.pcap;
     const int64_t *path_e = P.path_e + (size_t)t * P.pcap;
+    const int32_t *path_x = P.path_x + (size_t)t * P.pcap;
     // this simulation's path (lane per level) and the statistics its backup updates are
     // requested before the expansion, so their round trips overlap it (the expansion never
     // touches them: the new node is not on its own path)
-    int pnode = 0, pcnt = 0, pns = 0;
+    int pnode = 0, pcnt = 0, pns = 0, px = 0;
     int64_t pge = 0;
     double pq = 0.0, pqs = 0.0;
     if (l < depth) {
         pnode = path_n[l];
         pge = path_e[l];
+        px = path_x[l];
         const EdgeStat st = P.ed[pge].s;
         pcnt = st.n;
         pq = st.q;
@@ -1548,6 +1638,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         pqs = P.nst[pnode].qs;
     }
     float val[4] = {0, 0, 0, 0};
+    int lg = -1, lec = 0;                                // the new leaf, linked to the last path edge
+    int64_t leb = 0;
     if (kind == LEAF_NN) {
         const uint64_t *m = leaf_mask + (size_t)t * 7;
         int ec = 0;
@@ -1577,9 +1669,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             }
             return;
         }
-        if (eb < 0) {                                    // no room: back up v, do not store
 #pragma unroll
-            for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
+        for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
+        if (eb < 0) {                                    // no room: back up v, do not store
             if (l == 0) H->unexpanded += 1;
             goto backup;
         }
@@ -1588,29 +1680,42 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = gp[a];     // coalesced stage
         __builtin_amdgcn_wave_barrier();
         const float sum = wave_np_sum409(pr);                        // normalise (MCTS.py:144)
+        // the new node's arg-max: every edge unvisited (Ns = 0, Qs = v), so u = fpu_init +
+        // cpuct * P * sqrt(0 + EPS) (MCTS.py:214), evaluated exactly, lowest index on ties
+        const double fpu_init = C.fpu > 0 ? (double)val[0] - C.fpu : C.fpu;
+        const double sq_eps = sqrt(1e-8);
+        double bu = -INFINITY;
+        int bj = 0x7fffffff, bact = 0;
         int run = 0;
 #pragma unroll
         for (int k = 0; k < 7; k++) {
             const uint64_t wd = m[k];
             if ((wd >> l) & 1) {
-                const int64_t r = eb + run + __popcll(wd & lanemask_lt());
+                const int r = run + __popcll(wd & lanemask_lt());
                 const int a = 64 * k + l;
-                P.ed[r].k.a = (int16_t)a;
-                P.ed[r].s.p = pr[a] / sum;
-                P.ed[r].s.n = 0;
-                P.ed[r].s.q = Q_UNSET;
-                P.ed[r].k.child = -1;
+                const float p = pr[a] / sum;
+                P.ed[eb + r].k.a = (int16_t)a;
+                P.ed[eb + r].s.p = p;
+                P.ed[eb + r].s.n = 0;
+                P.ed[eb + r].s.q = Q_UNSET;
+                P.ed[eb + r].k.child = -1;
+                const double u = fpu_init + C.cpuct * (double)p * sq_eps;
+                if (u > bu) { bu = u; bj = r; bact = a; }
             }
             run += __popcll(wd);
         }
-#pragma unroll
-        for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
+        const int mine = bj;
+        wave_argmax(bu, bj);
+        bj = uniform(bj);
+        bact = __builtin_amdgcn_readlane(bact, __ffsll((unsigned long long)__ballot(mine == bj)) - 1);
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         if (l == 0) {
             P.nkey0[g] = H->leaf_k0; P.nkey1[g] = H->leaf_k1;
-            P.neb[g] = eb; P.nec[g] = ec; P.nst[g].ns = 0;
-            P.nst[g].qs = (double)val[0]; P.nround[g] = H->leaf_round; P.nterm[g] = 0;
+            P.neb[g] = eb; P.nec[g] = ec;
+            // (a new root: its priors may still be noised below, and a root always scans)
+            P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)(depth == 0 ? -1 : bj), (int16_t)bact, -1, 0, 0, 0};
+            P.nround[g] = H->leaf_round; P.nterm[g] = 0;
             const int hslot = H->leaf_hslot;             // the select's lookup ended there
             if (hslot >= 0) P.hslot[(size_t)t * P.hcap + hslot] = g;
             else hash_insert(P, t, H->leaf_k0, g);
@@ -1622,6 +1727,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
             }
             H->node_count += 1;
         }
+        lg = g; leb = eb; lec = ec;
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         if (depth == 0 && H->sims_done == 0 && H->noise_pending)   // noise on a new root (raw priors)
@@ -1631,24 +1737,83 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(6))) vo
         for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
     }
 backup:
-    // backup (MCTS.py:169-176): level d sees the leaf value rolled (depth - d) times; the
-    // levels touch distinct nodes/edges (rounds strictly increase along a path), so one
-    // lane per level applies exactly the sequential update.
-    for (int d = l; d < depth; d += 64) {
-        const int rot = (depth - d) % N;
-        const double v0 = (double)val[(N - rot) % N];
-        int node = pnode, cnt = pcnt, ns = pns;
-        int64_t ge = pge;
-        double q = pq, qs = pqs;
-        if (d >= 64) {                                   // levels beyond the prefetched 64
-            node = path_n[d]; ge = path_e[d];
-            cnt = P.ed[ge].s.n; q = P.ed[ge].s.q;
-            ns = P.nst[node].ns; qs = P.nst[node].qs;
+    {
+        const float cf = (float)C.cpuct;
+        // levels in groups of 64, lane per level (the first group prefetched above)
+        for (int d0 = 0; d0 < depth; d0 += 64) {
+            const int cnt = min(64, depth - d0);
+            const int d = d0 + l;
+            int node = pnode, ecnt = pcnt, ns = pns, x = px;
+            int64_t ge = pge;
+            double q = pq, qs = pqs;
+            if (d0 > 0 && l < cnt) {
+                node = path_n[d]; ge = path_e[d]; x = path_x[d];
+                const EdgeStat st = P.ed[ge].s;
+                ecnt = st.n; q = st.q;
+                ns = P.nst[node].ns; qs = P.nst[node].qs;
+            }
+            // MCTS.py:169-176: level d sees the leaf value rolled (depth - d) times; the levels
+            // touch distinct nodes/edges (rounds strictly increase along a path), so one lane
+            // per level applies exactly the sequential update
+            double nq = 0.0, nqs = 0.0;
+            int nn = 0, nns = 0;
+            if (l < cnt) {
+                const int rot = (depth - d) % N, vi = (N - rot) % N;
+                float vr = val[0];
+#pragma unroll
+                for (int i = 1; i < N; i++) vr = vi == i ? val[i] : vr;   // (no dynamic index: scratch)
+                const double v0 = (double)vr;
+                nq = ((double)ecnt * q + v0) / (double)(ecnt + 1);
+                nqs = ((double)(ns + 1) * qs + v0) / (double)(ns + 2);
+                nn = ecnt + 1;
+                nns = ns + 1;
+                P.ed[ge].s.q = nq;
+                P.ed[ge].s.n = nn;
+            }
+            const int off = px_off(x), ec = px_count(x);
+            const int64_t eb = ge - off;
+            // each level's arg-max under its new statistics (the updated edge from registers)
+            int bsel = 0;
+            for (int j0 = 0; j0 < cnt; j0 += BK_G) {
+                EdgeStat es[BK_G];
+#pragma unroll
+                for (int j = 0; j < BK_G; j++) {
+                    es[j] = EdgeStat{0.f, 0, Q_UNSET};
+                    const int lv = j0 + j;
+                    if (lv < cnt) {
+                        const int ecj = __builtin_amdgcn_readlane(ec, lv);
+                        es[j] = P.ed[readlane64(eb, lv) + (l < ecj ? l : 0)].s;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < BK_G; j++) {
+                    const int lv = j0 + j;
+                    if (lv < cnt) {
+                        const int ecj = __builtin_amdgcn_readlane(ec, lv);
+                        const int offj = __builtin_amdgcn_readlane(off, lv);
+                        const int nsj = __builtin_amdgcn_readlane(nns, lv);
+                        const int onj = __builtin_amdgcn_readlane(nn, lv);
+                        const double qsj = readlane_f64(nqs, lv), oqj = readlane_f64(nq, lv);
+                        int b;
+                        if (ecj <= 64) {
+                            EdgeStat e = es[j];
+                            if (l == offj) { e.n = onj; e.q = oqj; }
+                            b = ucb_argmax64(e, C.cpuct, C.fpu, cf, ecj, nsj, qsj);
+                        } else {
+                            b = ucb_argmax_wide(P.ed + readlane64(eb, lv), ecj, nsj, qsj, C.cpuct, C.fpu, offj, onj,
+                                                oqj);
+                        }
+                        if (l == lv) bsel = b;
+                    }
+                }
+            }
+            // the node record: statistics, arg-max and that edge's link
+            if (l < cnt) {
+                EdgeLink lk = P.ed[eb + bsel].k;
+                if (d == depth - 1 && lg >= 0 && bsel == off) { lk.child = lg; lk.cec = (int16_t)lec; lk.ceb = leb; }
+                P.nst[node] = NodeStat{nqs, nns, (int16_t)bsel, lk.a, lk.child, lk.cec, 0, lk.ceb};
+            }
         }
-        P.ed[ge].s.q = ((double)cnt * q + v0) / (double)(cnt + 1);
-        P.nst[node].qs = ((double)(ns + 1) * qs + v0) / (double)(ns + 2);
-        P.ed[ge].s.n = cnt + 1;
-        P.nst[node].ns = ns + 1;
     }
     if (l == 0) {
         H->sims_done += 1;
@@ -1912,7 +2077,7 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     acc(sizeof(NodeStat) * nn); acc(nn); acc(16 * nn); acc(sizeof(Edge) * ne);
     acc(4 * (size_t)B * L.nptab); acc(4 * (size_t)B * L.eptab); acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages);
     acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages); acc(64);
-    acc(4 * (size_t)B * L.hcap); acc(4 * (size_t)B * L.pcap); acc(8 * (size_t)B * L.pcap);
+    acc(4 * (size_t)B * L.hcap); acc(4 * (size_t)B * L.pcap); acc(8 * (size_t)B * L.pcap); acc(4 * (size_t)B * L.pcap);
     acc(4 * (size_t)gcw * gc_ints(L.nmax, L.emax)); acc((size_t)B * L.S);
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
     acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
@@ -1992,6 +2157,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.hslot = carve<int32_t>(p, (size_t)B * P.hcap);
     P.path_n = carve<int32_t>(p, (size_t)B * P.pcap);
     P.path_e = carve<int64_t>(p, (size_t)B * P.pcap);
+    P.path_x = carve<int32_t>(p, (size_t)B * P.pcap);
     P.gc_stride = gc_ints(P.nmax, P.eptab * EPG);
     P.gscr = carve<int32_t>(p, (size_t)gcw * P.gc_stride);
     P.root_state = carve<int8_t>(p, (size_t)B * m->S);

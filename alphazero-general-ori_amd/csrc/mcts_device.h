@@ -66,12 +66,25 @@ struct __align__(16) Edge {
 };
 __device__ __forceinline__ void set_cr(EdgeLink &e, int64_t eb, int ec) { e.ceb = eb; e.cec = (int16_t)ec; }
 
-// a node's visit statistics (Ns, Qs), read together by the descent
+// a node's visit statistics (Ns, Qs) and its cached arg-max edge, one 32-byte record.
+// pick_highest_UCB (MCTS.py:199-219) at a non-root node reads only that node's Ns, Qs and its
+// edges' P, N, Q; all of them change only when a simulation backs up through the node (priors
+// change only at a root: Dirichlet noise, :150-154; forced playouts are root-only, :157). So the
+// arg-max k_backup computes right after a node's update is exactly the edge the next descent
+// through the node picks: the descent follows `best` and the link copied from that edge (one
+// 32-byte load per level, no edge scan). The root level always scans. Invariant (k_backup,
+// k_select's links, k_gc's remap): {bchild, bcec, bceb} == the link of edge best.
 struct __align__(16) NodeStat {
-    double qs;     // Qs
-    int32_t ns;    // Ns
-    int32_t pad;
+    double qs;       // Qs
+    int32_t ns;      // Ns
+    int16_t best;    // cached arg-max: edge offset in the CSR run (-1: unknown, scan)
+    int16_t ba;      // its action
+    int32_t bchild;  // its child (global id, -1: not linked)
+    int16_t bcec;    // the child's CSR count (-1: terminal)
+    int16_t pad;
+    int64_t bceb;    // the child's CSR base (global edge index)
 };
+static_assert(sizeof(NodeStat) == 32, "NodeStat layout");
 
 // Per-GPU shared arena. Nodes and edges live in pools shared by all trees and
 // are handed out in pages: node page = NPG consecutive global node ids, edge page = EPG
@@ -106,6 +119,7 @@ struct Pools {
     int32_t *hslot;                      // B x hcap transposition table (global node ids)
     int32_t *path_n;                     // B x pcap descent path: node (global id)
     int64_t *path_e;                     // B x pcap and the edge taken (global index)
+    int32_t *path_x;                     // B x pcap its offset in the node's CSR run | count << 16
     int32_t *gscr;                       // k_gc scratch, GC_WG x gc_stride ints
     size_t gc_stride;
     int8_t *nbrd;                        // per node slot its canonical board (LDS row format), or
