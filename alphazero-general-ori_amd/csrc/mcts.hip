@@ -1595,47 +1595,98 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
 }
 
 // k_backup: expansion of the NN leaf, the path backup (MCTS.py:169-176) and every path node's
-// cached arg-max (NodeStat): after its update the wave scans each level's edges (the edges of
-// BK_G levels requested together), so the next descent through the node reads its pick
-// instead of scanning (one dependent load per level in k_select).
-#ifndef BK_G
-#define BK_G 4
+// cached arg-max (NodeStat), so the next descent through the node reads its pick instead of
+// scanning. Lane per level: each lane scans its node's edges (batches of BK_BATCH requested
+// together) in one pass of pick_edge_desc's float32 screen — the running maximum L of u - e
+// with its edge, and the largest u + e of every other edge; that is below L exactly when one
+// edge can hold the maximum, which is then the strict-'>' arg-max. Otherwise (ties, near
+// ties) the wave evaluates that level exactly in float64 (ucb_argmax_wide).
+#ifndef BK_BATCH
+#define BK_BATCH 8
 #endif
 #ifndef BACKUP_WAVES
-#define BACKUP_WAVES 6
+#define BACKUP_WAVES 5
 #endif
 
-template <int N>
+// per-level view of a group of path levels after their update (lane j = level j)
+struct LevelV {
+    int64_t eb;       // CSR base of the level's node
+    int ec, off;      // its edge count, the offset of the edge taken
+    int nn, nns;      // the taken edge's and the node's new visit counts
+    double nq, nqs;   // their new values
+};
+
+// lane-serial screened arg-max of one node (ec edges at E; the edge at `off` takes (on, oq));
+// returns the edge offset, or -1 when the screen cannot decide (exact evaluation needed).
+// `maxec`: the wave's largest ec (uniform trip count)
+__device__ __forceinline__ int lane_argmax_screen(const Edge *E, int ec, int maxec, int ns, double qs, double cpuct,
+                                                  double fpu, int off, int on, double oq) {
+    const float cf = (float)cpuct;
+    const float ff = (float)(fpu > 0 ? qs - fpu : fpu);
+    const float nf = (float)ns;
+    const float sqv = __builtin_amdgcn_sqrtf(nf), sqe = __builtin_amdgcn_sqrtf(nf + 1e-8f);
+    float L1 = -INFINITY, H1 = -INFINITY, H2 = -INFINITY;
+    int i1 = 0;
+    for (int base = 0; base < maxec; base += BK_BATCH) {
+        EdgeStat es[BK_BATCH];
+#pragma unroll
+        for (int j = 0; j < BK_BATCH; j++) {
+            es[j] = EdgeStat{0.f, 0, Q_UNSET};
+            if (base + j < ec) es[j] = E[base + j].s;
+        }
+#pragma unroll
+        for (int j = 0; j < BK_BATCH; j++) {
+            const int i = base + j;
+            if (i < ec) {
+                EdgeStat st = es[j];
+                if (i == off) { st.n = on; st.q = oq; }   // the edge this wave just updated
+                const bool vis = st.q != Q_UNSET;
+                const float rc = vis ? __builtin_amdgcn_rcpf(1.f + (float)st.n) : 1.f;
+                const float qf = vis ? (float)st.q : ff;
+                const float uf = qf + cf * st.p * (vis ? sqv : sqe) * rc;
+                const float er = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
+                const float lo = uf - er, hi = uf + er;
+                if (lo > L1) { H2 = fmaxf(H2, H1); L1 = lo; H1 = hi; i1 = i; }
+                else H2 = fmaxf(H2, hi);
+            }
+        }
+    }
+    return H2 < L1 ? i1 : -1;
+}
+
+// KINDS: the leaf kinds this launch backs up (bit 0 NN, bit 1 terminal; spl_mcts_backup_kind)
+template <int N, int KINDS>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_WAVES))) void k_backup(Pools P, SearchCfg C, int B,
                                                     const uint64_t *__restrict__ leaf_mask,
                                                     const float *__restrict__ pi,
                                                     const float *__restrict__ v) {
-    __shared__ __align__(16) float lpi[WAVES][416];
+    __shared__ __align__(16) float lpi[WAVES][(KINDS & 1) ? 416 : 4];
     const int w = uniform(threadIdx.x >> 6), t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
-    const int kind = H->leaf_kind;
-    if (kind == LEAF_NONE) return;
-    const int depth = H->depth;
     const int32_t *path_n = P.path_n + (size_t)t * P.pcap;
     const int64_t *path_e = P.path_e + (size_t)t * P.pcap;
     const int32_t *path_x = P.path_x + (size_t)t * P.pcap;
-    // this simulation's path (lane per level) and the statistics its backup updates are
-    // requested before the expansion, so their round trips overlap it (the expansion never
-    // touches them: the new node is not on its own path)
-    int pnode = 0, pcnt = 0, pns = 0, px = 0;
-    int64_t pge = 0;
+    // the header and the path's first 64 levels (lane per level) are requested together
+    int pnode = path_n[l], px = path_x[l];               // (pcap >= 256)
+    int64_t pge = path_e[l];
+    const int kind = H->leaf_kind;
+    if (kind == LEAF_NONE || !((KINDS >> (kind - 1)) & 1)) return;
+    const int depth = H->depth;
+    // the first group's statistics and its first window's edges, requested before the
+    // expansion (which never touches them: the new node is not on its own path)
+    int cnt = min(depth, 64);
+    LevelV V{0, 0, 0, 0, 0, 0.0, 0.0};
+    int pcnt = 0, pns = 0;
     double pq = 0.0, pqs = 0.0;
-    if (l < depth) {
-        pnode = path_n[l];
-        pge = path_e[l];
-        px = path_x[l];
+    if (l < cnt) {
+        V.off = px_off(px);
+        V.ec = px_count(px);
+        V.eb = pge - V.off;
         const EdgeStat st = P.ed[pge].s;
-        pcnt = st.n;
-        pq = st.q;
-        pns = P.nst[pnode].ns;
-        pqs = P.nst[pnode].qs;
+        pcnt = st.n; pq = st.q;
+        pns = P.nst[pnode].ns; pqs = P.nst[pnode].qs;
     }
     float val[4] = {0, 0, 0, 0};
     int lg = -1, lec = 0;                                // the new leaf, linked to the last path edge
@@ -1737,82 +1788,61 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
     }
 backup:
-    {
-        const float cf = (float)C.cpuct;
-        // levels in groups of 64, lane per level (the first group prefetched above)
-        for (int d0 = 0; d0 < depth; d0 += 64) {
-            const int cnt = min(64, depth - d0);
-            const int d = d0 + l;
-            int node = pnode, ecnt = pcnt, ns = pns, x = px;
-            int64_t ge = pge;
-            double q = pq, qs = pqs;
-            if (d0 > 0 && l < cnt) {
-                node = path_n[d]; ge = path_e[d]; x = path_x[d];
-                const EdgeStat st = P.ed[ge].s;
-                ecnt = st.n; q = st.q;
-                ns = P.nst[node].ns; qs = P.nst[node].qs;
-            }
-            // MCTS.py:169-176: level d sees the leaf value rolled (depth - d) times; the levels
-            // touch distinct nodes/edges (rounds strictly increase along a path), so one lane
-            // per level applies exactly the sequential update
-            double nq = 0.0, nqs = 0.0;
-            int nn = 0, nns = 0;
+    // levels in groups of 64, lane per level (the first group's data is in hand)
+    for (int g0 = 0; g0 < depth; g0 += 64) {
+        const int d = g0 + l;
+        if (g0 > 0) {
+            cnt = min(64, depth - g0);
+            V = LevelV{0, 0, 0, 0, 0, 0.0, 0.0};
             if (l < cnt) {
-                const int rot = (depth - d) % N, vi = (N - rot) % N;
-                float vr = val[0];
-#pragma unroll
-                for (int i = 1; i < N; i++) vr = vi == i ? val[i] : vr;   // (no dynamic index: scratch)
-                const double v0 = (double)vr;
-                nq = ((double)ecnt * q + v0) / (double)(ecnt + 1);
-                nqs = ((double)(ns + 1) * qs + v0) / (double)(ns + 2);
-                nn = ecnt + 1;
-                nns = ns + 1;
-                P.ed[ge].s.q = nq;
-                P.ed[ge].s.n = nn;
+                pnode = path_n[d]; pge = path_e[d]; px = path_x[d];
+                V.off = px_off(px);
+                V.ec = px_count(px);
+                V.eb = pge - V.off;
+                const EdgeStat st = P.ed[pge].s;
+                pcnt = st.n; pq = st.q;
+                pns = P.nst[pnode].ns; pqs = P.nst[pnode].qs;
             }
-            const int off = px_off(x), ec = px_count(x);
-            const int64_t eb = ge - off;
-            // each level's arg-max under its new statistics (the updated edge from registers)
-            int bsel = 0;
-            for (int j0 = 0; j0 < cnt; j0 += BK_G) {
-                EdgeStat es[BK_G];
+        }
+        // MCTS.py:169-176: level d sees the leaf value rolled (depth - d) times; the levels
+        // touch distinct nodes/edges (rounds strictly increase along a path), so one lane per
+        // level applies exactly the sequential update
+        if (l < cnt) {
+            const int rot = (depth - d) % N, vi = (N - rot) % N;
+            float vr = val[0];
 #pragma unroll
-                for (int j = 0; j < BK_G; j++) {
-                    es[j] = EdgeStat{0.f, 0, Q_UNSET};
-                    const int lv = j0 + j;
-                    if (lv < cnt) {
-                        const int ecj = __builtin_amdgcn_readlane(ec, lv);
-                        es[j] = P.ed[readlane64(eb, lv) + (l < ecj ? l : 0)].s;
-                    }
-                }
+            for (int i = 1; i < N; i++) vr = vi == i ? val[i] : vr;   // (no dynamic index: scratch)
+            const double v0 = (double)vr;
+            V.nq = ((double)pcnt * pq + v0) / (double)(pcnt + 1);
+            V.nqs = ((double)(pns + 1) * pqs + v0) / (double)(pns + 2);
+            V.nn = pcnt + 1;
+            V.nns = pns + 1;
+            P.ed[pge].s.q = V.nq;
+            P.ed[pge].s.n = V.nn;
+        }
+        // each level's arg-max under its new statistics: screened lane-serial scan, exact
+        // float64 for the levels the screen leaves open
+        int maxec = V.ec;
 #pragma unroll
-                for (int j = 0; j < BK_G; j++) {
-                    const int lv = j0 + j;
-                    if (lv < cnt) {
-                        const int ecj = __builtin_amdgcn_readlane(ec, lv);
-                        const int offj = __builtin_amdgcn_readlane(off, lv);
-                        const int nsj = __builtin_amdgcn_readlane(nns, lv);
-                        const int onj = __builtin_amdgcn_readlane(nn, lv);
-                        const double qsj = readlane_f64(nqs, lv), oqj = readlane_f64(nq, lv);
-                        int b;
-                        if (ecj <= 64) {
-                            EdgeStat e = es[j];
-                            if (l == offj) { e.n = onj; e.q = oqj; }
-                            b = ucb_argmax64(e, C.cpuct, C.fpu, cf, ecj, nsj, qsj);
-                        } else {
-                            b = ucb_argmax_wide(P.ed + readlane64(eb, lv), ecj, nsj, qsj, C.cpuct, C.fpu, offj, onj,
-                                                oqj);
-                        }
-                        if (l == lv) bsel = b;
-                    }
-                }
-            }
-            // the node record: statistics, arg-max and that edge's link
-            if (l < cnt) {
-                EdgeLink lk = P.ed[eb + bsel].k;
-                if (d == depth - 1 && lg >= 0 && bsel == off) { lk.child = lg; lk.cec = (int16_t)lec; lk.ceb = leb; }
-                P.nst[node] = NodeStat{nqs, nns, (int16_t)bsel, lk.a, lk.child, lk.cec, 0, lk.ceb};
-            }
+        for (int o = 32; o > 0; o >>= 1) maxec = max(maxec, __shfl_xor(maxec, o, 64));
+        int bsel = l < cnt ? lane_argmax_screen(P.ed + V.eb, V.ec, uniform(maxec), V.nns, V.nqs, C.cpuct, C.fpu,
+                                                V.off, V.nn, V.nq)
+                           : 0;
+        uint64_t ex = __ballot(l < cnt && bsel < 0);
+        while (ex) {
+            const int j = __ffsll((unsigned long long)ex) - 1;
+            ex &= ex - 1;
+            const int b = ucb_argmax_wide(P.ed + readlane64(V.eb, j), __builtin_amdgcn_readlane(V.ec, j),
+                                          __builtin_amdgcn_readlane(V.nns, j), readlane_f64(V.nqs, j), C.cpuct, C.fpu,
+                                          __builtin_amdgcn_readlane(V.off, j), __builtin_amdgcn_readlane(V.nn, j),
+                                          readlane_f64(V.nq, j));
+            if (l == j) bsel = b;
+        }
+        // the node record: statistics, arg-max and that edge's link
+        if (l < cnt) {
+            EdgeLink lk = P.ed[V.eb + bsel].k;
+            if (d == depth - 1 && lg >= 0 && bsel == V.off) { lk.child = lg; lk.cec = (int16_t)lec; lk.ceb = leb; }
+            P.nst[pnode] = NodeStat{V.nqs, V.nns, (int16_t)bsel, lk.a, lk.child, lk.cec, 0, lk.ceb};
         }
     }
     if (l == 0) {
@@ -2252,13 +2282,28 @@ int spl_mcts_select_compact(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask
     return launch_select(m, leaf_state, leaf_mask, leaf_valid, leaf_index, leaf_count, hs);
 }
 
+int spl_mcts_backup_kind(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v, int kinds,
+                         void *hs) {
+    if (!m || kinds < 1 || kinds > 3 || ((kinds & SPL_LEAF_NN) && (!leaf_mask || !pi || !v))) return SPL_EINVAL;
+    if (kinds == 3) {
+        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup<N, 3>), wave_grid(m->B), dim3(THREADS), 0,
+                                              (hipStream_t)hs, m->P, m->cfg, m->B, leaf_mask, pi, v));
+    } else if (kinds == SPL_LEAF_NN) {
+        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup<N, 1>), wave_grid(m->B), dim3(THREADS), 0,
+                                              (hipStream_t)hs, m->P, m->cfg, m->B, leaf_mask, pi, v));
+    } else {
+        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup<N, 2>), wave_grid(m->B), dim3(THREADS), 0,
+                                              (hipStream_t)hs, m->P, m->cfg, m->B, leaf_mask, pi, v));
+    }
+    // trees whose simulation was withdrawn (NN leaves only)
+    if (m->cfg.selfplay && (kinds & SPL_LEAF_NN)) launch_gc(m, (hipStream_t)hs);
+    return check_launch();
+}
+
 int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v,
                     void *hs) {
     if (!m || !leaf_mask || !pi || !v) return SPL_EINVAL;
-    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_backup<N>, wave_grid(m->B), dim3(THREADS), 0,
-                                          (hipStream_t)hs, m->P, m->cfg, m->B, leaf_mask, pi, v));
-    if (m->cfg.selfplay) launch_gc(m, (hipStream_t)hs);   // trees whose simulation was withdrawn
-    return check_launch();
+    return spl_mcts_backup_kind(m, leaf_mask, pi, v, 3, hs);
 }
 
 int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs, double *q,

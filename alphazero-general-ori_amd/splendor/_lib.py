@@ -10,7 +10,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("SPLENDOR_AMD_LIB") or os.path.join(PKG_ROOT, "libsplendor_amd.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 EINVAL, EDEVICE = -1, -2
 
 
@@ -63,6 +63,7 @@ _SIGS = {
     "spl_mcts_select": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_select_compact": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_backup": ([C.c_void_p, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_mcts_backup_kind": ([C.c_void_p, _vp, _vp, _vp, C.c_int, _vp], C.c_int),
     "spl_mcts_root_stats": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_mcts_root_priors": ([C.c_void_p, _vp, _vp], C.c_int),
     "spl_mcts_headers": ([C.c_void_p, _vp, _vp], C.c_int),

@@ -14,6 +14,7 @@ float32[B,409], v float32[B,n])` is the batched `nnet.predict` (GenericNNetWrapp
 (SplendorNNet under PyTorch-ROCm).
 """
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -218,15 +219,33 @@ class BatchedMCTS:
         for _ in range(int(self.headers()["budget"].max())):
             self.simulate()
 
+    # terminal leaves backed up on a side stream during the network (SPLENDOR_OVERLAP=1: on; measured slower: the backup waves delay the network workgroups)
+    OVERLAP_TERMINAL = os.environ.get("SPLENDOR_OVERLAP", "0") != "0"
+
     def simulate(self):
         """One simulation on every tree with budget left: select -> evaluate -> backup. An
         evaluator that can take a compacted leaf list (`indexed`, the fused network) runs on
-        the trees whose leaf needs the network only."""
+        the trees whose leaf needs the network only; the trees whose leaf is terminal are
+        backed up meanwhile on a side stream (trees are independent; spl_mcts_backup_kind)."""
         s = self.e._s()
         if getattr(self.evaluator, "indexed", False):
             _lib.check(self.L.spl_mcts_select_compact(self.h, _ptr(self.leaf_state), _ptr(self.leaf_mask),
                                                       _ptr(self.leaf_valid), _ptr(self.leaf_index),
                                                       _ptr(self.leaf_count), s), "spl_mcts_select_compact")
+            if self.OVERLAP_TERMINAL and self.e.device.type == "cuda":
+                cur = torch.cuda.current_stream(self.e.device)
+                side = getattr(self, "_side", None)
+                if side is None:
+                    side = self._side = torch.cuda.Stream(device=self.e.device)
+                side.wait_stream(cur)
+                _lib.check(self.L.spl_mcts_backup_kind(self.h, None, None, None, 2, C.c_void_p(side.cuda_stream)),
+                           "spl_mcts_backup_kind")
+                pi, v = self.evaluator(self.leaf_state, self.leaf_mask, self.leaf_valid, index=self.leaf_index,
+                                       count=self.leaf_count)
+                cur.wait_stream(side)
+                _lib.check(self.L.spl_mcts_backup_kind(self.h, _ptr(self.leaf_mask), _ptr(pi), _ptr(v), 1, s),
+                           "spl_mcts_backup_kind")
+                return
             pi, v = self.evaluator(self.leaf_state, self.leaf_mask, self.leaf_valid, index=self.leaf_index,
                                    count=self.leaf_count)
         else:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 3
+#define SPL_ABI_VERSION 4
 #define SPL_ACTIONS 409
 #define SPL_MASK_WORDS 7
 #define SPL_EINVAL (-1)
@@ -202,6 +202,14 @@ int spl_mcts_select_compact(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask
 /* pi: B x 409 f32 (policy over all actions, as predict returns), v: B x n f32 */
 int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v,
                     void *hip_stream);
+/* spl_mcts_backup for the trees whose leaf is of the given kinds only (bit 0: NN leaves, the
+ * expansion + backup of MCTS.py:134-176; bit 1: terminal leaves, :125-131 then :169-176).
+ * Trees are independent, so a caller may back up the terminal leaves on a second stream
+ * while the network evaluates the NN leaves (their backup needs no pi / v: NULL allowed). */
+#define SPL_LEAF_NN 1
+#define SPL_LEAF_TERMINAL 2
+int spl_mcts_backup_kind(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v, int kinds,
+                         void *hip_stream);
 /* counts B x 409 i64 (root visit counts Nsa), qsa B x 409 f64 (-42 = unvisited), probs
  * B x 409 f64 (temp = 1), q B x n f64, adjusted B x 409 i64 (counts after policy-target
  * pruning, MCTS.py:69-74; = counts without forced playouts); any may be NULL */
