@@ -1604,6 +1604,9 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
 #ifndef BK_BATCH
 #define BK_BATCH 8
 #endif
+#ifndef BK_PRELOAD
+#define BK_PRELOAD 0       // first batch of every level requested before the expansion
+#endif
 #ifndef BACKUP_WAVES
 #define BACKUP_WAVES 5
 #endif
@@ -1616,42 +1619,51 @@ struct LevelV {
     double nq, nqs;   // their new values
 };
 
-// lane-serial screened arg-max of one node (ec edges at E; the edge at `off` takes (on, oq));
-// returns the edge offset, or -1 when the screen cannot decide (exact evaluation needed).
-// `maxec`: the wave's largest ec (uniform trip count)
-__device__ __forceinline__ int lane_argmax_screen(const Edge *E, int ec, int maxec, int ns, double qs, double cpuct,
-                                                  double fpu, int off, int on, double oq) {
-    const float cf = (float)cpuct;
-    const float ff = (float)(fpu > 0 ? qs - fpu : fpu);
+// lane-serial screened arg-max of one node, one batch of edges at a time: the running
+// maximum L1 of u - e with its edge i1 and its u + e (H1), and the largest u + e of all other
+// edges (H2). One edge can hold the maximum exactly when H2 < L1.
+struct Screen {
+    float L1, H1, H2, cf, ff, sqv, sqe;
+    int i1;
+};
+__device__ __forceinline__ Screen screen_init(int ns, double qs, double cpuct, double fpu) {
+    Screen S;
+    S.cf = (float)cpuct;
+    S.ff = (float)(fpu > 0 ? qs - fpu : fpu);
     const float nf = (float)ns;
-    const float sqv = __builtin_amdgcn_sqrtf(nf), sqe = __builtin_amdgcn_sqrtf(nf + 1e-8f);
-    float L1 = -INFINITY, H1 = -INFINITY, H2 = -INFINITY;
-    int i1 = 0;
-    for (int base = 0; base < maxec; base += BK_BATCH) {
-        EdgeStat es[BK_BATCH];
+    S.sqv = __builtin_amdgcn_sqrtf(nf);
+    S.sqe = __builtin_amdgcn_sqrtf(nf + 1e-8f);
+    S.L1 = -INFINITY; S.H1 = -INFINITY; S.H2 = -INFINITY;
+    S.i1 = 0;
+    return S;
+}
+// edges base .. base + BK_BATCH - 1 (those < ec) in es[]; the edge at `off` takes (on, oq)
+// (just written by this wave)
+__device__ __forceinline__ void screen_batch(Screen &S, const EdgeStat *es, int base, int ec, int off, int on,
+                                             double oq) {
 #pragma unroll
-        for (int j = 0; j < BK_BATCH; j++) {
-            es[j] = EdgeStat{0.f, 0, Q_UNSET};
-            if (base + j < ec) es[j] = E[base + j].s;
-        }
-#pragma unroll
-        for (int j = 0; j < BK_BATCH; j++) {
-            const int i = base + j;
-            if (i < ec) {
-                EdgeStat st = es[j];
-                if (i == off) { st.n = on; st.q = oq; }   // the edge this wave just updated
-                const bool vis = st.q != Q_UNSET;
-                const float rc = vis ? __builtin_amdgcn_rcpf(1.f + (float)st.n) : 1.f;
-                const float qf = vis ? (float)st.q : ff;
-                const float uf = qf + cf * st.p * (vis ? sqv : sqe) * rc;
-                const float er = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
-                const float lo = uf - er, hi = uf + er;
-                if (lo > L1) { H2 = fmaxf(H2, H1); L1 = lo; H1 = hi; i1 = i; }
-                else H2 = fmaxf(H2, hi);
-            }
+    for (int j = 0; j < BK_BATCH; j++) {
+        const int i = base + j;
+        if (i < ec) {
+            EdgeStat st = es[j];
+            if (i == off) { st.n = on; st.q = oq; }
+            const bool vis = st.q != Q_UNSET;
+            const float rc = vis ? __builtin_amdgcn_rcpf(1.f + (float)st.n) : 1.f;
+            const float qf = vis ? (float)st.q : S.ff;
+            const float uf = qf + S.cf * st.p * (vis ? S.sqv : S.sqe) * rc;
+            const float er = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
+            const float lo = uf - er, hi = uf + er;
+            if (lo > S.L1) { S.H2 = fmaxf(S.H2, S.H1); S.L1 = lo; S.H1 = hi; S.i1 = i; }
+            else S.H2 = fmaxf(S.H2, hi);
         }
     }
-    return H2 < L1 ? i1 : -1;
+}
+__device__ __forceinline__ void batch_load(const Edge *E, int base, int ec, EdgeStat *es) {
+#pragma unroll
+    for (int j = 0; j < BK_BATCH; j++) {
+        es[j] = EdgeStat{0.f, 0, Q_UNSET};
+        if (base + j < ec) es[j] = E[base + j].s;
+    }
 }
 
 // KINDS: the leaf kinds this launch backs up (bit 0 NN, bit 1 terminal; spl_mcts_backup_kind)
@@ -1668,18 +1680,41 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     const int32_t *path_n = P.path_n + (size_t)t * P.pcap;
     const int64_t *path_e = P.path_e + (size_t)t * P.pcap;
     const int32_t *path_x = P.path_x + (size_t)t * P.pcap;
-    // the header and the path's first 64 levels (lane per level) are requested together
+    // every input that depends on nothing else is requested at once: the header fields, the
+    // path's first 64 levels (lane per level), and for an NN leaf its mask, value and policy
     int pnode = path_n[l], px = path_x[l];               // (pcap >= 256)
     int64_t pge = path_e[l];
     const int kind = H->leaf_kind;
     if (kind == LEAF_NONE || !((KINDS >> (kind - 1)) & 1)) return;
     const int depth = H->depth;
-    // the first group's statistics and its first window's edges, requested before the
-    // expansion (which never touches them: the new node is not on its own path)
+    const int h_slot = H->leaf_slot, h_hslot = H->leaf_hslot, h_round = H->leaf_round;
+    const uint64_t h_k0 = H->leaf_k0, h_k1 = H->leaf_k1;
+    const int h_sims = H->sims_done, h_noise = H->noise_pending, h_gc = H->gc_state;
+    const int h_eleft = H->eleft;
+    const int64_t h_enext = H->enext;
+    float val[4] = {0, 0, 0, 0};
+    float piv[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t mw[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (kind == LEAF_NN) {
+        const float *gp = pi + (size_t)t * SPL_ACTIONS;
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            mw[k] = leaf_mask[(size_t)t * 7 + k];
+            if (64 * k + l < SPL_ACTIONS) piv[k] = gp[64 * k + l];
+        }
+#pragma unroll
+        for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
+    }
+    // the first group's statistics and the first batch of every level's edges, requested
+    // before the expansion (which never touches them: the new node is not on its own path)
     int cnt = min(depth, 64);
     LevelV V{0, 0, 0, 0, 0, 0.0, 0.0};
     int pcnt = 0, pns = 0;
     double pq = 0.0, pqs = 0.0;
+    EdgeStat b0[BK_BATCH];
     if (l < cnt) {
         V.off = px_off(px);
         V.ec = px_count(px);
@@ -1688,25 +1723,35 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         pcnt = st.n; pq = st.q;
         pns = P.nst[pnode].ns; pqs = P.nst[pnode].qs;
     }
-    float val[4] = {0, 0, 0, 0};
+#if BK_PRELOAD
+    batch_load(P.ed + V.eb, 0, l < cnt ? V.ec : 0, b0);
+#endif
     int lg = -1, lec = 0;                                // the new leaf, linked to the last path edge
     int64_t leb = 0;
     if (kind == LEAF_NN) {
-        const uint64_t *m = leaf_mask + (size_t)t * 7;
         int ec = 0;
 #pragma unroll
-        for (int k = 0; k < 7; k++) ec += __popcll(m[k]);
-        // the new node's slot and CSR run (pages from the shared pools)
+        for (int k = 0; k < 7; k++) ec += __popcll(mw[k]);
+        // the new node's slot (reserved by k_select with node boards) and CSR run (from the
+        // tree's current edge page or a fresh one from the shared pool)
         int g = -1;
         int64_t eb = -1;
         if (l == 0) {
-            const int rs = H->leaf_slot;                 // reserved by k_select (node boards)
-            g = rs >= 0 ? rs : node_slot(P, H, t, H->node_count);
-            if (g >= 0) eb = edge_run(P, H, t, ec);
+            g = h_slot >= 0 ? h_slot : node_slot(P, H, t, H->node_count);
+            if (g >= 0) {
+                if (h_eleft >= ec) {
+                    eb = h_enext;
+                    H->enext = eb + ec;
+                    H->eleft = h_eleft - ec;
+                    H->edge_count += ec;
+                } else {
+                    eb = edge_run(P, H, t, ec);
+                }
+            }
         }
         g = __shfl(g, 0, 64);
         eb = readlane64(eb, 0);
-        if (eb < 0 && C.selfplay && depth > 0 && H->gc_state == 0) {
+        if (eb < 0 && C.selfplay && depth > 0 && h_gc == 0) {
             // garbage is collected lazily (begin_search), so a self-play search may run out
             // of room with dead nodes still held: this simulation is withdrawn (no backup,
             // not counted), k_gc (launched behind every backup of a self-play arena) collects
@@ -1720,74 +1765,69 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             }
             return;
         }
-#pragma unroll
-        for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
         if (eb < 0) {                                    // no room: back up v, do not store
             if (l == 0) H->unexpanded += 1;
-            goto backup;
-        }
-        float *pr = lpi[w];
-        const float *gp = pi + (size_t)t * SPL_ACTIONS;
-        for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = gp[a];     // coalesced stage
-        __builtin_amdgcn_wave_barrier();
-        const float sum = wave_np_sum409(pr);                        // normalise (MCTS.py:144)
-        // the new node's arg-max: every edge unvisited (Ns = 0, Qs = v), so u = fpu_init +
-        // cpuct * P * sqrt(0 + EPS) (MCTS.py:214), evaluated exactly, lowest index on ties
-        const double fpu_init = C.fpu > 0 ? (double)val[0] - C.fpu : C.fpu;
-        const double sq_eps = sqrt(1e-8);
-        double bu = -INFINITY;
-        int bj = 0x7fffffff, bact = 0;
-        int run = 0;
+        } else {
+            float *pr = lpi[w];
 #pragma unroll
-        for (int k = 0; k < 7; k++) {
-            const uint64_t wd = m[k];
-            if ((wd >> l) & 1) {
-                const int r = run + __popcll(wd & lanemask_lt());
-                const int a = 64 * k + l;
-                const float p = pr[a] / sum;
-                P.ed[eb + r].k.a = (int16_t)a;
-                P.ed[eb + r].s.p = p;
-                P.ed[eb + r].s.n = 0;
-                P.ed[eb + r].s.q = Q_UNSET;
-                P.ed[eb + r].k.child = -1;
-                const double u = fpu_init + C.cpuct * (double)p * sq_eps;
-                if (u > bu) { bu = u; bj = r; bact = a; }
-            }
-            run += __popcll(wd);
-        }
-        const int mine = bj;
-        wave_argmax(bu, bj);
-        bj = uniform(bj);
-        bact = __builtin_amdgcn_readlane(bact, __ffsll((unsigned long long)__ballot(mine == bj)) - 1);
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        if (l == 0) {
-            P.nkey0[g] = H->leaf_k0; P.nkey1[g] = H->leaf_k1;
-            P.neb[g] = eb; P.nec[g] = ec;
-            // (a new root: its priors may still be noised below, and a root always scans)
-            P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)(depth == 0 ? -1 : bj), (int16_t)bact, -1, 0, 0, 0};
-            P.nround[g] = H->leaf_round; P.nterm[g] = 0;
-            const int hslot = H->leaf_hslot;             // the select's lookup ended there
-            if (hslot >= 0) P.hslot[(size_t)t * P.hcap + hslot] = g;
-            else hash_insert(P, t, H->leaf_k0, g);
-            if (depth == 0) { H->root = g; H->root_eb = eb; H->root_ec = ec; }
-            else {
-                const int64_t pe = path_e[depth - 1];
-                P.ed[pe].k.child = g;
-                set_cr(P.ed[pe].k, eb, ec);
-            }
-            H->node_count += 1;
-        }
-        lg = g; leb = eb; lec = ec;
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        if (depth == 0 && H->sims_done == 0 && H->noise_pending)   // noise on a new root (raw priors)
-            apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no, pr, true);
-    } else {
+            for (int k = 0; k < 7; k++)
+                if (64 * k + l < SPL_ACTIONS) pr[64 * k + l] = piv[k];
+            __builtin_amdgcn_wave_barrier();
+            const float sum = wave_np_sum409(pr);                    // normalise (MCTS.py:144)
+            // the new node's arg-max: every edge unvisited (Ns = 0, Qs = v), so u = fpu_init +
+            // cpuct * P * sqrt(0 + EPS) (MCTS.py:214), evaluated exactly, lowest index on ties
+            const double fpu_init = C.fpu > 0 ? (double)val[0] - C.fpu : C.fpu;
+            const double sq_eps = sqrt(1e-8);
+            double bu = -INFINITY;
+            int bj = 0x7fffffff, bact = 0;
+            int run = 0;
 #pragma unroll
-        for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
+            for (int k = 0; k < 7; k++) {
+                const uint64_t wd = mw[k];
+                if ((wd >> l) & 1) {
+                    const int r = run + __popcll(wd & lanemask_lt());
+                    const int a = 64 * k + l;
+                    const float p = piv[k] / sum;
+                    P.ed[eb + r].k.a = (int16_t)a;
+                    P.ed[eb + r].s.p = p;
+                    P.ed[eb + r].s.n = 0;
+                    P.ed[eb + r].s.q = Q_UNSET;
+                    P.ed[eb + r].k.child = -1;
+                    const double u = fpu_init + C.cpuct * (double)p * sq_eps;
+                    if (u > bu) { bu = u; bj = r; bact = a; }
+                }
+                run += __popcll(wd);
+            }
+            const int mine = bj;
+            wave_argmax(bu, bj);
+            bj = uniform(bj);
+            bact = __builtin_amdgcn_readlane(bact, __ffsll((unsigned long long)__ballot(mine == bj)) - 1);
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+            if (l == 0) {
+                P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
+                P.neb[g] = eb; P.nec[g] = ec;
+                // (a new root: its priors may still be noised below, and a root always scans)
+                P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)(depth == 0 ? -1 : bj), (int16_t)bact, -1, 0, 0, 0};
+                P.nround[g] = h_round; P.nterm[g] = 0;
+                if (h_hslot >= 0) P.hslot[(size_t)t * P.hcap + h_hslot] = g;   // the select's lookup ended there
+                else hash_insert(P, t, h_k0, g);
+                if (depth == 0) { H->root = g; H->root_eb = eb; H->root_ec = ec; }
+                else {
+                    const int64_t pe = readlane64(pge, depth - 1 < 64 ? depth - 1 : 0);
+                    const int64_t pe2 = depth - 1 < 64 ? pe : path_e[depth - 1];
+                    P.ed[pe2].k.child = g;
+                    set_cr(P.ed[pe2].k, eb, ec);
+                }
+                H->node_count += 1;
+            }
+            lg = g; leb = eb; lec = ec;
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+            if (depth == 0 && h_sims == 0 && h_noise)    // noise on a new root (raw priors)
+                apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no, pr, true);
+        }
     }
-backup:
     // levels in groups of 64, lane per level (the first group's data is in hand)
     for (int g0 = 0; g0 < depth; g0 += 64) {
         const int d = g0 + l;
@@ -1804,6 +1844,10 @@ backup:
                 pns = P.nst[pnode].ns; pqs = P.nst[pnode].qs;
             }
         }
+#if BK_PRELOAD
+        if (g0 > 0)
+#endif
+            batch_load(P.ed + V.eb, 0, l < cnt ? V.ec : 0, b0);
         // MCTS.py:169-176: level d sees the leaf value rolled (depth - d) times; the levels
         // touch distinct nodes/edges (rounds strictly increase along a path), so one lane per
         // level applies exactly the sequential update
@@ -1822,12 +1866,20 @@ backup:
         }
         // each level's arg-max under its new statistics: screened lane-serial scan, exact
         // float64 for the levels the screen leaves open
-        int maxec = V.ec;
+        int maxec = l < cnt ? V.ec : 0;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) maxec = max(maxec, __shfl_xor(maxec, o, 64));
-        int bsel = l < cnt ? lane_argmax_screen(P.ed + V.eb, V.ec, uniform(maxec), V.nns, V.nqs, C.cpuct, C.fpu,
-                                                V.off, V.nn, V.nq)
-                           : 0;
+        maxec = uniform(maxec);
+        const int lec_ = l < cnt ? V.ec : 0;
+        Screen S = screen_init(V.nns, V.nqs, C.cpuct, C.fpu);
+        screen_batch(S, b0, 0, lec_, V.off, V.nn, V.nq);
+        for (int base = BK_BATCH; base < maxec; base += BK_BATCH) {
+            EdgeStat es[BK_BATCH];
+            batch_load(P.ed + V.eb, base, lec_, es);
+            screen_batch(S, es, base, lec_, V.off, V.nn, V.nq);
+        }
+        int bsel = S.H2 < S.L1 ? S.i1 : -1;
+        if (l >= cnt) bsel = 0;
         uint64_t ex = __ballot(l < cnt && bsel < 0);
         while (ex) {
             const int j = __ffsll((unsigned long long)ex) - 1;
@@ -1846,7 +1898,7 @@ backup:
         }
     }
     if (l == 0) {
-        H->sims_done += 1;
+        H->sims_done = h_sims + 1;
         H->noise_pending = 0;
         H->leaf_kind = LEAF_NONE;
     }
