@@ -978,12 +978,14 @@ __device__ void deal_game(const Pools &P, const SearchCfg &C, int t, int8_t *b, 
 }
 
 template <int N>
-__global__ __launch_bounds__(THREADS) void k_reset_games(Pools P, SearchCfg C, int B) {
+// restart (optional): only the games with restart[t] != 0 are abandoned and re-dealt
+__global__ __launch_bounds__(THREADS) void k_reset_games(Pools P, SearchCfg C, int B,
+                                                         const uint8_t *__restrict__ restart) {
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
     __shared__ double ub[WAVES][DEAL_DRAWS];
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
-    if (t >= B) return;
+    if (t >= B || (restart && !restart[t])) return;
     int8_t *b = lds[w];
     deal_game<N>(P, C, t, b, ub[w]);
     wave_store_board<N>(P.board + (size_t)t * Lx::S, b);
@@ -2375,7 +2377,14 @@ int spl_mcts_root_priors(spl_mcts *m, float *ps, void *hs) {
 int spl_mcts_reset_games(spl_mcts *m, void *hs) {
     if (!m || !m->cfg.selfplay) return SPL_EINVAL;
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_reset_games<N>, wave_grid(m->B), dim3(THREADS), 0,
-                                          (hipStream_t)hs, m->P, m->cfg, m->B));
+                                          (hipStream_t)hs, m->P, m->cfg, m->B, nullptr));
+    return check_launch();
+}
+
+int spl_mcts_restart_games(spl_mcts *m, const uint8_t *restart, void *hs) {
+    if (!m || !m->cfg.selfplay || !restart) return SPL_EINVAL;
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_reset_games<N>, wave_grid(m->B), dim3(THREADS), 0,
+                                          (hipStream_t)hs, m->P, m->cfg, m->B, restart));
     return check_launch();
 }
 

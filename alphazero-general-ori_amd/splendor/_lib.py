@@ -10,7 +10,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("SPLENDOR_AMD_LIB") or os.path.join(PKG_ROOT, "libsplendor_amd.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 EINVAL, EDEVICE = -1, -2
 
 
@@ -69,6 +69,7 @@ _SIGS = {
     "spl_mcts_headers": ([C.c_void_p, _vp, _vp], C.c_int),
     "spl_mcts_tree_sizes": ([C.c_void_p, _vp, _vp], C.c_int),
     "spl_mcts_reset_games": ([C.c_void_p, _vp], C.c_int),
+    "spl_mcts_restart_games": ([C.c_void_p, _vp, _vp], C.c_int),
     "spl_mcts_commit": ([C.c_void_p, _vp], C.c_int),
     "spl_mcts_drain_examples": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int, _vp, _vp], C.c_int),
     "spl_nn_input": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),

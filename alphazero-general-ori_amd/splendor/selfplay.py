@@ -65,6 +65,21 @@ class SelfPlay(BatchedMCTS):
     def reset(self):
         _lib.check(self.L.spl_mcts_reset_games(self.h, self.e._s()), "spl_mcts_reset_games")
 
+    def restart(self, games):
+        """Abandon the current game of every tree with games[t] (B bools, or a list of tree
+        ids) and deal its next one; staged examples of the abandoned games are discarded.
+        Between iterations only. bench.py uses it to spread games that were dealt together
+        over the phases of a game (its `--stagger` warm-up)."""
+        if not (torch.is_tensor(games) and games.dtype == torch.bool):
+            ids = torch.as_tensor(games, dtype=torch.long)
+            games = torch.zeros(self.B, dtype=torch.bool)
+            games[ids] = True
+        mask = games.to(device=self.e.device, dtype=torch.uint8).contiguous()
+        if mask.numel() != self.B:
+            raise ValueError(f"restart mask of {mask.numel()} entries for {self.B} games")
+        _lib.check(self.L.spl_mcts_restart_games(self.h, _ptr(mask), self.e._s()), "spl_mcts_restart_games")
+        self._keep = mask                        # alive until the stream has used it
+
     def _iteration(self):
         self.simulate()
         _lib.check(self.L.spl_mcts_commit(self.h, self.e._s()), "spl_mcts_commit")

@@ -221,14 +221,22 @@ CONFIGS = {  # BASELINE.json configs: (players, games per GPU, numMCTSSims)
 
 
 def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, seed, node_boards=-1,
-                 stats_every=0):
+                 stagger=0, groups=16):
     """Self-play at one BASELINE config: B games per GPU (shard board_base = rank * B), one
     MCTS simulation per game per iteration, leaves evaluated by the fused SplendorNNet kernel
     (fp32, random init), moves committed on device. `prefill` untimed iterations bring the
     games to a steady state, `warmup` more, then exactly `steps` timed iterations (barrier +
     synchronize on both sides, max over ranks); then `window` iterations whose statistics
     (capacity events, games, moves) are reported, ending with the finished examples drained
-    and all-gathered over RCCL; symmetry expansion is timed after it."""
+    and all-gathered over RCCL; symmetry expansion is timed after it.
+
+    stagger: the B games are dealt together, so without it they share one game phase for
+    many generations and the per-iteration cost oscillates with it (config 3: 0.56-0.95 ms
+    over a ~4,800-iteration period: end-game trees reach terminal states, which need no
+    network evaluation). Within the prefill, group j of `groups` (trees t % groups == j)
+    abandons its game and is dealt a new one after j * stagger / groups iterations, so the
+    games' phases end up spread over `stagger` iterations (~ one mean game length): the
+    population a long-running self-play reaches, every phase equally represented."""
     from splendor.coach import expand_symmetries
     from splendor.env import SplendorEngine
     from splendor.nnet import LeafEvaluator, random_net
@@ -247,13 +255,19 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     done = 0
     log(f"{cfg}: {B} games, {sims} sims, pools {sp.cfg.pool_nodes} nodes / {sp.cfg.pool_edges} edges, "
         f"node boards {sp.cfg.node_boards}, {sp.device_bytes / 2**30:.1f} GiB; prefill {prefill}")
-    while done < prefill:                      # (in chunks: a sync now and then keeps the
-        k = min(2000, prefill - done)          #  host's view of progress; drained as it goes)
-        sp.run(max(k, 9), use_graph=True)
-        done += max(k, 9)
-        sp.drain(allow_drops=False)
-        torch.cuda.synchronize(dev)
-        log(f"{cfg}: prefill {done}/{prefill}")
+    stagger = min(stagger, prefill)
+    step = stagger // groups
+    marks = [(j * step, j) for j in range(1, groups)] if step else []
+    for target, j in marks + [(prefill, None)]:
+        while done < target:                   # (in chunks: a sync now and then keeps the
+            k = min(2000, target - done)       #  host's view of progress; drained as it goes)
+            sp.run(k, use_graph=True)
+            done += k
+            sp.drain(allow_drops=False)
+            torch.cuda.synchronize(dev)
+            log(f"{cfg}: prefill {done}/{prefill}")
+        if j is not None:                      # group j starts a new game (phase spreading)
+            sp.restart(torch.arange(B) % groups == j)
     prefill_s = time.perf_counter() - t_fill
     sp.run(max(warmup, 1), use_graph=True)
     sp.drain()
@@ -341,7 +355,7 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
             "pool_free_at_end": {"node_pages": pool["free_node_pages"], "of": pool["node_pages"],
                                  "edge_pages": pool["free_edge_pages"], "of_edge": pool["edge_pages"]}}
     res = {"elapsed": elapsed, "iter_ms_events": iter_ms_events, "window": delta, "tree": tree,
-           "prefill": prefill, "prefill_s": prefill_s,
+           "prefill": prefill, "prefill_s": prefill_s, "stagger": {"iterations": stagger, "groups": groups},
            "symmetry": {"examples": nsym, "variants": int(sym["board"].shape[0]) if sym else 0, "s": sym_s},
            "nn_kernel_us": nn_us}
     del sp, ev, net
@@ -357,6 +371,7 @@ def selfplay_record(cfg, r, world, steps, warmup):
             "value": world * B * steps / r["elapsed"], "unit": "rollouts/s (MCTS simulations)",
             "ms_per_iteration": r["elapsed"] / steps * 1e3, "ms_per_iteration_events": r["iter_ms_events"],
             "steps": steps, "warmup": warmup, "prefill_iterations": r["prefill"], "prefill_s": r["prefill_s"],
+            "phase_stagger": r["stagger"],
             "window": r["window"], "tree": r["tree"], "symmetry_expansion": r["symmetry"],
             "network_kernel": {"kernel": f"k_nn_forward<{n}>", "avg_us": r["nn_kernel_us"],
                                "tflops": fl / (r["nn_kernel_us"] * 1e-6) / 1e12,
@@ -512,7 +527,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000, help="timed self-play iterations (headline)")
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--prefill", type=int, default=3000, help="untimed iterations to the steady state first")
+    ap.add_argument("--prefill", type=int, default=6000, help="untimed iterations to the steady state first")
+    ap.add_argument("--stagger", type=int, default=4800, help="prefill iterations over which the games' phases "
+                    "are spread (run_selfplay; ~ the mean game length: config 3 ~4,800 iterations)")
     ap.add_argument("--window", type=int, default=10000, help="statistics window after the timed steps")
     ap.add_argument("--boards", type=int, default=32768, help="env workload: boards per GPU")
     ap.add_argument("--players", type=int, default=2, help="env workload: players")
@@ -525,8 +542,10 @@ def main():
     ap.add_argument("--chunk", type=int, default=100, help="env: moves per rollout launch")
     ap.add_argument("--env-steps", type=int, default=1000, help="config-2 object: timed moves")
     ap.add_argument("--c5-prefill", type=int, default=40000)
+    ap.add_argument("--c5-stagger", type=int, default=32000)
     ap.add_argument("--c5-window", type=int, default=6000)
     ap.add_argument("--c4-prefill", type=int, default=45000)
+    ap.add_argument("--c4-stagger", type=int, default=40000)
     ap.add_argument("--c4-window", type=int, default=4000)
     ap.add_argument("--node-boards", type=int, default=-1, help="selfplay: 1/0 force node boards on/off "
                     "(default: on unless the pools do not fit)")
@@ -563,7 +582,7 @@ def main():
     head = "config3" if args.workload in ("all", "selfplay") else args.workload
     n, B, sims = CONFIGS[head]
     r = run_selfplay(head, rank, world, dev, dist, args.steps, args.warmup, args.prefill, args.window, args.seed,
-                     args.node_boards)
+                     args.node_boards, stagger=args.stagger)
     rec = selfplay_record(head, r, world, args.steps, args.warmup)
     torch.cuda.empty_cache()
     extra = {}
@@ -573,8 +592,9 @@ def main():
         rec["cpu_baseline"] = cpu_baseline_selfplay(n, args.seed, sims)
     if secondary:
         extra["config2_env"] = run_env(args, rank, world, dev, dist, args.env_steps, 100, cpu=cpu_ok)
-        for cfg, pf, win in (("config5", args.c5_prefill, args.c5_window), ("config4", args.c4_prefill, args.c4_window)):
-            rr = run_selfplay(cfg, rank, world, dev, dist, 1000, 100, pf, win, args.seed, args.node_boards)
+        for cfg, pf, sg, win in (("config5", args.c5_prefill, args.c5_stagger, args.c5_window),
+                                 ("config4", args.c4_prefill, args.c4_stagger, args.c4_window)):
+            rr = run_selfplay(cfg, rank, world, dev, dist, 1000, 100, pf, win, args.seed, args.node_boards, stagger=sg)
             o = selfplay_record(cfg, rr, world, 1000, 100)
             if cpu_ok:
                 o["cpu_baseline"] = cpu_baseline_selfplay(CONFIGS[cfg][0], args.seed, CONFIGS[cfg][2],
@@ -592,6 +612,7 @@ def main():
                     "weights-only loader)",
             "config": {"workload": rec["workload"], "players": n, "games_per_gpu": B, "global_games": world * B,
                        "numMCTSSims": sims, "prefill_iterations": args.prefill,
+                       "phase_stagger_iterations": args.stagger,
                        "parallelism": f"dp{world} (game shards; RCCL all-gather of examples)"},
             "roofline": selfplay_roofline(rec, n, rec["tree"]["leaf_depth_mean"]),
             "cpu_baseline": cpu,

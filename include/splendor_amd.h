@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 4
+#define SPL_ABI_VERSION 5
 #define SPL_ACTIONS 409
 #define SPL_MASK_WORDS 7
 #define SPL_EINVAL (-1)
@@ -229,6 +229,13 @@ int spl_mcts_root_stats(spl_mcts *m, int64_t *counts, double *qsa, double *probs
  *   score difference (Coach.py:89-98) to the example queue and deal a new game; re-root
  *   the tree at the next canonical board (exact GC) and draw the next search type. */
 int spl_mcts_reset_games(spl_mcts *m, void *hip_stream);
+/* restart_games: like reset_games for the games with restart[t] != 0 only (restart: B u8,
+ * device): each abandons its current game (examples staged for it are discarded; nothing
+ * is written to the example queue) and is dealt its next game (game number + 1), with a
+ * fresh tree. Call between iterations. Not in the reference (its episodes run one after
+ * another): the batched driver uses it to spread B games that started together over the
+ * phases of a game (bench warm-up). */
+int spl_mcts_restart_games(spl_mcts *m, const uint8_t *restart, void *hip_stream);
 int spl_mcts_commit(spl_mcts *m, void *hip_stream);
 /* copy up to `max` finished examples to caller buffers (state E x S i8, pi E x 409 f32,
  * valid E x 7 u64, winner E x n f32, scdiff E x n i32, q E x n f32, meta E x 4 i32 =

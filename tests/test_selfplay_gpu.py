@@ -289,3 +289,43 @@ def test_compacted_leaf_evaluation_matches_full_batch():
     o0, o1 = np.lexsort(e0["meta"].T[::-1]), np.lexsort(e1["meta"].T[::-1])
     for k in e0:
         np.testing.assert_array_equal(e0[k][o0], e1[k][o1], err_msg=k)
+
+
+def test_restart_games_abandons_only_the_chosen_games():
+    """spl_mcts_restart_games (bench.py's phase stagger): the chosen trees abandon their game
+    (staged examples discarded, nothing queued) and start their next one (game number + 1,
+    a fresh tree and search); every other tree is untouched and plays on."""
+    B = 96
+    e, sp = make(2, B, 8, 4, 0.25, False, out_cap=40000)
+    sp.run(150, use_graph=False)
+    torch.cuda.synchronize()
+    before = sp.headers().copy()
+    queued = sp.drain()
+    chosen = np.arange(B) % 3 == 1
+    sp.restart(torch.from_numpy(chosen))
+    torch.cuda.synchronize()
+    after = sp.headers()
+    assert sp.drain()["board"].shape[0] == 0                 # nothing queued by a restart
+    for k in ("game_no",):
+        np.testing.assert_array_equal(after[k][chosen], before[k][chosen] + 1)
+    for k in ("episode_step", "player", "n_examples", "sims_done", "node_count"):
+        assert (after[k][chosen] == 0).all(), k
+    assert (after["budget"][chosen] > 0).all()
+    keep = ~chosen
+    for k in HDR_KEYS:
+        np.testing.assert_array_equal(after[k][keep], before[k][keep], err_msg=k)
+    sp.run(400, use_graph=False)
+    torch.cuda.synchronize()
+    h = sp.headers()
+    assert h["overflow"].max() == 0 and h["unexpanded"].max() == 0
+    ex = sp.drain()
+    meta = ex["meta"].cpu().numpy()
+    # examples of the restarted boards only come from games dealt after the restart
+    for t in np.nonzero(chosen)[0]:
+        g = meta[meta[:, 0] == t, 1]
+        assert (g > before["game_no"][t] - 1).all() or g.size == 0
+    assert queued["board"].shape[0] + ex["board"].shape[0] > 0
+
+
+HDR_KEYS = ("node_count", "edge_count", "root", "sims_done", "budget", "full", "player", "episode_step",
+            "move_no", "game_no", "n_examples", "games_done", "moves")
