@@ -84,7 +84,7 @@ __device__ __forceinline__ int px_action(int x) { return (x >> 18) & 0x1ff; }
 __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &C, int64_t eb, int ec,
                                                int ns, double qs, bool forced, int step, const Edge &first) {
     const int l = lane_id();
-    const Edge *E = P.ed + eb;
+    const EdgePtr E = P.ed + eb;
     float p[2];
     int n[2], a[2], c[2], rc[2];
     int64_t rb[2];
@@ -249,7 +249,7 @@ __device__ __forceinline__ Pick pick_edge64(const Edge &e, double cpuct, double 
 // exact pick_highest_UCB arg-max (float64, strict '>' in edge order = lowest index holding the
 // maximum) over any number of edges, the edge at offset `off` taking the statistics (on, oq)
 // (just written by this wave). Uniform.
-__device__ int ucb_argmax_wide(const Edge *E, int ec, int ns, double qs, double cpuct, double fpu, int off, int on,
+__device__ int ucb_argmax_wide(const EdgePtr E, int ec, int ns, double qs, double cpuct, double fpu, int off, int on,
                                double oq) {
     const int l = lane_id();
     const double fpu_init = fpu > 0 ? qs - fpu : fpu;
@@ -308,7 +308,7 @@ __device__ __forceinline__ float wave_np_sum409(const float *a) {
 __device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int64_t eb, int ec, uint32_t stream,
                                  float *pr, bool raw) {
     const int l = lane_id();
-    Edge *ede = P.ed + eb;
+    const EdgePtr ede = P.ed + eb;
     const uint32_t gb = C.board_base + (uint32_t)t;
     if (!raw) {
         for (int a = l; a < 416; a += 64) pr[a] = 0.f;
@@ -654,7 +654,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     {
         // edge records by new position k, batches of GCT x CR in increasing k (all reads
         // before the writes); child links and their cached ranges remapped
-        u32x4 *const ed4 = reinterpret_cast<u32x4 *>(P.ed);
+        u32x4 *const e4 = reinterpret_cast<u32x4 *>(P.ed.base);   // (EdgePool layout)
         for (int k0 = 0; k0 < run; k0 += GCT * CR) {
             u32x4 es_[CR], ek_[CR];
             int nch[CR];
@@ -668,8 +668,8 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                 es_[r] = u32x4{0, 0, 0, 0}; ek_[r] = u32x4{0, 0xFFFFFFFFu, 0, 0};
                 if (j >= 0) {
                     const int64_t src = S.ost[j] + (k - S.cs[j]);
-                    es_[r] = ed4[2 * src];
-                    ek_[r] = ed4[2 * src + 1];
+                    es_[r] = e4[EdgePool::unit(src)];
+                    ek_[r] = e4[EdgePool::unit(src) + EPG];
                 }
             }
 #pragma unroll
@@ -690,8 +690,8 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                     o.y = (uint32_t)nch[r];
                     if (nch[r] >= 0) { o.z = (uint32_t)(uint64_t)ceb[r]; o.w = (uint32_t)((uint64_t)ceb[r] >> 32); }
                     const int64_t dst = edge_g(P, t, k);
-                    ed4[2 * dst] = es_[r];
-                    ed4[2 * dst + 1] = o;
+                    e4[EdgePool::unit(dst)] = es_[r];
+                    e4[EdgePool::unit(dst) + EPG] = o;
                 }
             }
             __syncthreads();
@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     const int root = H->root, ec = P.nec[root];
     const bool forced = H->forced;
     const int sims = H->budget, cm = H->move_no;
-    const Edge *ede = P.ed + P.neb[root];
+    const EdgePtr ede = P.ed + P.neb[root];
     int best = 0;
     for (int i = l; i < ec; i += 64) best = max(best, ede[i].s.n);
     for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
@@ -1260,7 +1260,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         const uint64_t *nbrd = reinterpret_cast<const uint64_t *>(P.nbrd);
         int bnode = node;
         // pool bases and search constants of the hot loop, set up once
-        const Edge *ed_t = P.ed;
+        const EdgePool ed_t = P.ed;
         const NodeStat *nst_t = P.nst;
         const double cpuct = C.cpuct, fpu = C.fpu;
         const float cf = (float)C.cpuct;
@@ -1660,7 +1660,7 @@ __device__ __forceinline__ void screen_batch(Screen &S, const EdgeStat *es, int 
         }
     }
 }
-__device__ __forceinline__ void batch_load(const Edge *E, int base, int ec, EdgeStat *es) {
+__device__ __forceinline__ void batch_load(const EdgePtr E, int base, int ec, EdgeStat *es) {
 #pragma unroll
     for (int j = 0; j < BK_BATCH; j++) {
         es[j] = EdgeStat{0.f, 0, Q_UNSET};
@@ -1927,7 +1927,7 @@ __global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int
         if (l == 0) action[t] = (int16_t)(int)(u * (double)SPL_ACTIONS);
         return;
     }
-    const Edge *E = P.ed + P.neb[root];
+    const EdgePtr E = P.ed + P.neb[root];
     const int ec = P.nec[root];
     const int sims = H->budget;
     const bool forced = H->forced;
@@ -1985,7 +1985,7 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
     if (root < 0) return;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const Edge *E = P.ed + P.neb[root];
+    const EdgePtr E = P.ed + P.neb[root];
     const int ec = P.nec[root];
     int best = 0;
     for (int i = l; i < ec; i += 64) best = max(best, E[i].s.n);
@@ -2025,7 +2025,7 @@ __global__ __launch_bounds__(THREADS) void k_root_priors(Pools P, int B, float *
     if (root < 0) return;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const Edge *E = P.ed + P.neb[root];
+    const EdgePtr E = P.ed + P.neb[root];
     const int ec = P.nec[root];
     for (int i = l; i < ec; i += 64) o[E[i].k.a] = E[i].s.p;
 }
@@ -2158,7 +2158,7 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     size_t bytes = 0;
     auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
     acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn);
-    acc(sizeof(NodeStat) * nn); acc(nn); acc(16 * nn); acc(sizeof(Edge) * ne);
+    acc(sizeof(NodeStat) * nn); acc(nn); acc(16 * nn); acc(sizeof(EdgeStat) * 2 * ne);
     acc(4 * (size_t)B * L.nptab); acc(4 * (size_t)B * L.eptab); acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages);
     acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages); acc(64);
     acc(4 * (size_t)B * L.hcap); acc(4 * (size_t)B * L.pcap); acc(8 * (size_t)B * L.pcap); acc(4 * (size_t)B * L.pcap);
@@ -2233,7 +2233,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.neb = carve<int64_t>(p, nn); P.nec = carve<int32_t>(p, nn); P.nround = carve<int32_t>(p, nn);
     P.nst = carve<NodeStat>(p, nn); P.nterm = carve<int8_t>(p, nn);
     P.nes = carve<float>(p, 4 * nn);
-    P.ed = carve<Edge>(p, ne);
+    P.ed.base = carve<EdgeStat>(p, 2 * ne);              // EdgeStat | EdgeLink blocks per page
     P.ntab = carve<int32_t>(p, (size_t)B * P.nptab); P.etab = carve<int32_t>(p, (size_t)B * P.eptab);
     P.npidx = carve<int32_t>(p, (size_t)P.npages); P.epidx = carve<int32_t>(p, (size_t)P.epages);
     P.nfree = carve<int32_t>(p, (size_t)P.npages); P.efree = carve<int32_t>(p, (size_t)P.epages);

@@ -59,10 +59,36 @@ struct __align__(16) EdgeLink {
     int32_t child; // child node, global id (-1: not linked yet)
     int64_t ceb;   // cached child CSR base (global edge index)
 };
-// one edge = both halves in one 32-byte record (one pool pointer: fewer live SGPRs)
+// one edge's value: both halves
 struct __align__(16) Edge {
     EdgeStat s;
     EdgeLink k;
+};
+// The edge pool keeps the two halves apart, blocked by edge page: page k holds the EdgeStat
+// records of its EPG edges, then their EdgeLink records (global edge i: stat at 16-byte unit
+// i + (i & ~(EPG - 1)), link EPG units later). k_backup's per-level arg-max scans read only
+// EdgeStat (a node's statistics are contiguous: 8 edges per 128-byte line instead of 4), the
+// descent reads links from its NodeStat copy, the root scan requests both halves in one round
+// trip. A node's CSR run never straddles an edge page, so within a run E[j] is plain
+// pointer arithmetic from one base (one pointer, as the 32-byte records had).
+struct EdgeRef {
+    EdgeStat &s;
+    EdgeLink &k;
+    __device__ __forceinline__ operator Edge() const { return Edge{s, k}; }
+};
+struct EdgePtr {           // edge j of a run (within one edge page)
+    EdgeStat *p;
+    __device__ __forceinline__ EdgeRef operator[](int64_t j) const {
+        return EdgeRef{p[j], *reinterpret_cast<EdgeLink *>(p + EPG_ + j)};
+    }
+    __device__ __forceinline__ EdgePtr operator+(int64_t j) const { return EdgePtr{p + j}; }
+    static constexpr int EPG_ = 1 << 10;
+};
+struct EdgePool {          // the whole pool, by global edge index
+    EdgeStat *base;
+    __device__ __forceinline__ static int64_t unit(int64_t i) { return i + (i & ~(int64_t)(EdgePtr::EPG_ - 1)); }
+    __device__ __forceinline__ EdgePtr operator+(int64_t i) const { return EdgePtr{base + unit(i)}; }
+    __device__ __forceinline__ EdgeRef operator[](int64_t i) const { return (*this + i)[0]; }
 };
 __device__ __forceinline__ void set_cr(EdgeLink &e, int64_t eb, int ec) { e.ceb = eb; e.cec = (int16_t)ec; }
 
@@ -98,6 +124,7 @@ static_assert(sizeof(NodeStat) == 32, "NodeStat layout");
 // pops and pushes never share a launch (an array stack with one atomic top is then exact).
 constexpr int NPG_SHIFT = 6, NPG = 1 << NPG_SHIFT;     // nodes per node page
 constexpr int EPG_SHIFT = 10, EPG = 1 << EPG_SHIFT;    // edges per edge page (> 409)
+static_assert(EPG == EdgePtr::EPG_, "edge pool blocking = edge page");
 
 struct Pools {
     int nmax, emax, hcap, pcap;          // per tree: node slots, edges (page tables), hash slots, path
@@ -110,7 +137,7 @@ struct Pools {
     NodeStat *nst;                       // visit count and value of every node (one 16-byte load)
     int8_t *nterm;
     float *nes;                          // 4 terminal values per node
-    Edge *ed;                            // edge pool: UCB inputs + action, child, child's CSR range
+    EdgePool ed;                         // edge pool: UCB inputs | action, child, child's CSR range
     int32_t *ntab, *etab;                // B x nptab / B x eptab page tables
     int32_t *npidx, *epidx;              // per page: its index in the owning tree's page table
     int32_t *nfree, *efree;              // free page stacks

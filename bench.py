@@ -234,9 +234,16 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     many generations and the per-iteration cost oscillates with it (config 3: 0.56-0.95 ms
     over a ~4,800-iteration period: end-game trees reach terminal states, which need no
     network evaluation). Within the prefill, group j of `groups` (trees t % groups == j)
-    abandons its game and is dealt a new one after j * stagger / groups iterations, so the
+    abandons its game and is dealt a new one after j * (stagger // groups) iterations, so the
     games' phases end up spread over `stagger` iterations (~ one mean game length): the
-    population a long-running self-play reaches, every phase equally represented."""
+    population a long-running self-play reaches, every phase equally represented. The
+    restarts fall on multiples of the fast-search budget (numMCTSSims / ratio_fullMCTS): with
+    one simulation per tree per iteration, games dealt together keep their search boundaries
+    aligned for good (every search spends 100 or 20 simulations, so all of them end in the
+    same iterations, one in 20), and so do the restarted ones, as a self-play run whose games
+    were all dealt at once does. (Restarts off that grid spread the boundaries over all
+    iterations: config 3 then runs ~14 % slower, since every select launch then carries some
+    deep descents.)"""
     from splendor.coach import expand_symmetries
     from splendor.env import SplendorEngine
     from splendor.nnet import LeafEvaluator, random_net
@@ -256,7 +263,8 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     log(f"{cfg}: {B} games, {sims} sims, pools {sp.cfg.pool_nodes} nodes / {sp.cfg.pool_edges} edges, "
         f"node boards {sp.cfg.node_boards}, {sp.device_bytes / 2**30:.1f} GiB; prefill {prefill}")
     stagger = min(stagger, prefill)
-    step = stagger // groups
+    fast = max(1, sims // GENBU_ARGS["ratio_fullMCTS"])
+    step = stagger // groups // fast * fast
     marks = [(j * step, j) for j in range(1, groups)] if step else []
     for target, j in marks + [(prefill, None)]:
         while done < target:                   # (in chunks: a sync now and then keeps the

@@ -8,7 +8,7 @@
 set -euo pipefail
 OUT=${1:-gpurun_out/pmc_sp}
 ROUND=${2:-r03}
-WARM=${3:-3000}
+WARM=${3:-6000}
 STEPS=${4:-200}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
