@@ -39,7 +39,10 @@ def _play(rank, games, net_seed, dist_on):
     if dist_on:
         broadcast_network(net)
     ev = LeafEvaluator(eng, net, games, use_graph=False)
-    sp = SelfPlay(eng, games, ARGS, evaluator=ev, dirichlet_noise=True, seed=0x5EED, board_base=rank * games)
+    # an explicit arena budget: the default (80 % of the free HBM, read at construction)
+    # races when two processes share the GPU and both read it before either allocates
+    sp = SelfPlay(eng, games, ARGS, evaluator=ev, dirichlet_noise=True, seed=0x5EED, board_base=rank * games,
+                  mem_budget=4 << 30)
     sp.reset()
     sp.run(ITERS, use_graph=True)
     ex = sp.drain()
