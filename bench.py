@@ -220,6 +220,16 @@ CONFIGS = {  # BASELINE.json configs: (players, games per GPU, numMCTSSims)
 }
 
 
+def stagger_marks(stagger, groups, sims, ratio):
+    """(iteration, group) restart points of run_selfplay's phase stagger: group j restarts
+    after j * step iterations, step = stagger / groups rounded down to a multiple of the
+    fast-search budget sims // ratio (so the restarted games keep the search boundaries
+    every game dealt at iteration 0 has); none when the stagger is shorter than that."""
+    fast = max(1, sims // ratio)
+    step = stagger // groups // fast * fast
+    return [(j * step, j) for j in range(1, groups)] if step else []
+
+
 def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, seed, node_boards=-1,
                  stagger=0, groups=16):
     """Self-play at one BASELINE config: B games per GPU (shard board_base = rank * B), one
@@ -263,9 +273,7 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     log(f"{cfg}: {B} games, {sims} sims, pools {sp.cfg.pool_nodes} nodes / {sp.cfg.pool_edges} edges, "
         f"node boards {sp.cfg.node_boards}, {sp.device_bytes / 2**30:.1f} GiB; prefill {prefill}")
     stagger = min(stagger, prefill)
-    fast = max(1, sims // GENBU_ARGS["ratio_fullMCTS"])
-    step = stagger // groups // fast * fast
-    marks = [(j * step, j) for j in range(1, groups)] if step else []
+    marks = stagger_marks(stagger, groups, sims, GENBU_ARGS["ratio_fullMCTS"])
     for target, j in marks + [(prefill, None)]:
         while done < target:                   # (in chunks: a sync now and then keeps the
             k = min(2000, target - done)       #  host's view of progress; drained as it goes)
