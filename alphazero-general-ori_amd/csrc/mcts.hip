@@ -86,20 +86,19 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
     const int l = lane_id();
     const EdgePtr E = P.ed + eb;
     float p[2];
-    int n[2], a[2], c[2], rc[2];
-    int64_t rb[2];
+    int n[2], a[2], c[2];
     double q[2];
 #pragma unroll
     for (int j = 0; j < 2; j++) {               // first: edge l, already requested by the caller
         const int i = 64 * j + l;
         EdgeStat st{0.f, 0, Q_UNSET};
-        EdgeLink lk{0, 0, -1, 0};
+        EdgeLink lk{0, 0, -1};
         if (i < ec) {
             const Edge &ei = j == 0 ? first : E[i];
             st = ei.s; lk = ei.k;
         }
         p[j] = st.p; n[j] = st.n; q[j] = st.q;
-        a[j] = lk.a; c[j] = lk.child; rb[j] = lk.ceb; rc[j] = lk.cec;
+        a[j] = lk.a; c[j] = lk.child;
     }
 #if MCTS_TIMING
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // split load wait / compute
@@ -189,18 +188,15 @@ __device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &
         }
     }
     const int jb = bi >> 6;
-    int av = a[0], cv = c[0], rcv = rc[0];
-    int64_t rbv = rb[0];
+    int av = a[0], cv = c[0];
 #pragma unroll
     for (int j = 1; j < 2; j++)
-        if (jb == j) { av = a[j]; cv = c[j]; rbv = rb[j]; rcv = rc[j]; }
+        if (jb == j) { av = a[j]; cv = c[j]; }
     bi = uniform(bi);                           // chosen lane -> SGPRs (readlane, no LDS trip)
     av = __builtin_amdgcn_readlane(av, bi & 63);
     cv = __builtin_amdgcn_readlane(cv, bi & 63);
-    rcv = __builtin_amdgcn_readlane(rcv, bi & 63);
-    rbv = readlane64(rbv, bi & 63);
-    if (bi >= 128) { av = E[bi].k.a; cv = E[bi].k.child; rbv = E[bi].k.ceb; rcv = E[bi].k.cec; }
-    return {bi, av, cv, rcv, rbv};
+    if (bi >= 128) { av = E[bi].k.a; cv = E[bi].k.child; }
+    return {bi, av, cv, 0, 0};                  // (the child's range: child_range)
 }
 
 // pick_highest_UCB's arg-max over a node with at most 64 edges and no forced playouts at this
@@ -242,8 +238,7 @@ __device__ __forceinline__ int ucb_argmax64(const EdgeStat &e, double cpuct, dou
 __device__ __forceinline__ Pick pick_edge64(const Edge &e, double cpuct, double fpu, float cf, int ec, int ns,
                                             double qs) {
     const int bi = ucb_argmax64(e.s, cpuct, fpu, cf, ec, ns, qs);
-    return {bi, __builtin_amdgcn_readlane((int)e.k.a, bi), __builtin_amdgcn_readlane(e.k.child, bi),
-            __builtin_amdgcn_readlane((int)e.k.cec, bi), readlane64(e.k.ceb, bi)};
+    return {bi, __builtin_amdgcn_readlane((int)e.k.a, bi), __builtin_amdgcn_readlane(e.k.child, bi), 0, 0};
 }
 
 // exact pick_highest_UCB arg-max (float64, strict '>' in edge order = lowest index holding the
@@ -497,6 +492,7 @@ __device__ void mark_linked(const Pools &P, int t, int rootl, int32_t *mark, int
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 struct defeats SROA)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // k_gc collects one tree per workgroup of GCT threads (block-wide scans through LDS), so a
 // large tree's collection (config 4: ~40 K nodes, ~1 M edges) is spread over 8 waves
@@ -654,31 +650,36 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     {
         // edge records by new position k, batches of GCT x CR in increasing k (all reads
         // before the writes); child links and their cached ranges remapped
-        u32x4 *const e4 = reinterpret_cast<u32x4 *>(P.ed.base);   // (EdgePool layout)
+        // (EdgePool layout: per page 1,024 16-byte statistics, then 1,024 8-byte links)
+        u32x4 *const e4 = reinterpret_cast<u32x4 *>(P.ed.base);
+        u32x2 *const e2 = reinterpret_cast<u32x2 *>(P.ed.base);
+        constexpr int64_t PU = EdgePtr::PAGE_BYTES / 16, LU = EdgePtr::PAGE_BYTES / 8;
+        const auto su = [&](int64_t i) { return (i >> EPG_SHIFT) * PU + (i & (EPG - 1)); };
+        const auto lu = [&](int64_t i) { return (i >> EPG_SHIFT) * LU + 2 * EPG + (i & (EPG - 1)); };
         for (int k0 = 0; k0 < run; k0 += GCT * CR) {
-            u32x4 es_[CR], ek_[CR];
+            u32x4 es_[CR];
+            u32x2 ek_[CR];
             int nch[CR];
-            int64_t ceb[CR];
             bool own[CR];
 #pragma unroll
             for (int r = 0; r < CR; r++) {
                 const int k = k0 + GCT * r + tid;
                 const int j = k < run ? S.own[k] : -1;
                 own[r] = j >= 0;
-                es_[r] = u32x4{0, 0, 0, 0}; ek_[r] = u32x4{0, 0xFFFFFFFFu, 0, 0};
+                es_[r] = u32x4{0, 0, 0, 0}; ek_[r] = u32x2{0, 0xFFFFFFFFu};
                 if (j >= 0) {
                     const int64_t src = S.ost[j] + (k - S.cs[j]);
-                    es_[r] = e4[EdgePool::unit(src)];
-                    ek_[r] = e4[EdgePool::unit(src) + EPG];
+                    es_[r] = e4[su(src)];
+                    ek_[r] = e2[lu(src)];
                 }
             }
 #pragma unroll
             for (int r = 0; r < CR; r++) {
-                nch[r] = -1; ceb[r] = 0;
+                nch[r] = -1;
                 const int ch = (int)ek_[r].y;
                 if (own[r] && ch >= 0) {
                     const int nl = remap[node_l(P, ch)];
-                    if (nl >= 0) { nch[r] = node_g(P, t, nl); ceb[r] = S.cnt[nl] > 0 ? edge_g(P, t, S.cs[nl]) : 0; }
+                    if (nl >= 0) nch[r] = node_g(P, t, nl);
                 }
             }
             __syncthreads();
@@ -686,12 +687,11 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
             for (int r = 0; r < CR; r++) {
                 const int k = k0 + GCT * r + tid;
                 if (own[r]) {
-                    u32x4 o = ek_[r];
+                    u32x2 o = ek_[r];
                     o.y = (uint32_t)nch[r];
-                    if (nch[r] >= 0) { o.z = (uint32_t)(uint64_t)ceb[r]; o.w = (uint32_t)((uint64_t)ceb[r] >> 32); }
                     const int64_t dst = edge_g(P, t, k);
-                    e4[EdgePool::unit(dst)] = es_[r];
-                    e4[EdgePool::unit(dst) + EPG] = o;
+                    e4[su(dst)] = es_[r];
+                    e2[lu(dst)] = o;
                 }
             }
             __syncthreads();
@@ -1333,7 +1333,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             if (!have) nsq = nst_t[node];
             have = false;
             const bool use_cache = depth > 0 || root_cache;
-            Edge e64{EdgeStat{0.f, 0, Q_UNSET}, EdgeLink{0, 0, -1, 0}};
+            Edge e64{EdgeStat{0.f, 0, Q_UNSET}, EdgeLink{0, 0, -1}};
             if (!use_cache) e64 = ed_t[eb + (l < ec ? l : 0)];
             // the previous level's path entry is stored behind this level's loads: vmcnt counts
             // stores too, in issue order, so a store issued first would delay the loads' wait
@@ -1351,6 +1351,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                 pk = ec <= 64 && !(forced && depth == 0)
                          ? pick_edge64(e64, cpuct, fpu, cf, ec, ns, qs)
                          : pick_edge_desc(P, C, eb, ec, ns, qs, forced && depth == 0, sims, e64);
+                if (pk.child >= 0) {                     // a scanned level: the child's range
+                    pk.ceb = (int64_t)uniform64((uint64_t)P.neb[pk.child]);
+                    pk.cec = uniform(P.nterm[pk.child] ? -1 : P.nec[pk.child]);
+                }
             }
             const int64_t ge = eb + pk.e;
             pend = depth; pend_n = node; pend_e = ge; pend_x = px_pack(pk.e, ec, pk.a);
@@ -1395,7 +1399,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                     cec = P.nterm[child] ? -1 : P.nec[child];
                     if (l == 0) {
                         P.ed[ge].k.child = child;
-                        set_cr(P.ed[ge].k, ceb, cec);
                         if (cached) {
                             P.nst[node].bchild = child; P.nst[node].bcec = (int16_t)cec; P.nst[node].bceb = ceb;
                         }
@@ -1434,7 +1437,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                         for (int i = 0; i < 4; i++) P.nes[(size_t)g * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
                         hash_insert(P, t, k0, g);
                         P.ed[ge].k.child = g;
-                        set_cr(P.ed[ge].k, 0, -1);
                         if (cached) { P.nst[node].bchild = g; P.nst[node].bcec = -1; P.nst[node].bceb = 0; }
                         H->node_count = id + 1;
                     }
@@ -1819,7 +1821,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                     const int64_t pe = readlane64(pge, depth - 1 < 64 ? depth - 1 : 0);
                     const int64_t pe2 = depth - 1 < 64 ? pe : path_e[depth - 1];
                     P.ed[pe2].k.child = g;
-                    set_cr(P.ed[pe2].k, eb, ec);
                 }
                 H->node_count += 1;
             }
@@ -1892,11 +1893,19 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                                           readlane_f64(V.nq, j));
             if (l == j) bsel = b;
         }
-        // the node record: statistics, arg-max and that edge's link
+        // the node record: statistics, arg-max, that edge's link and its child's CSR range
+        // (the new leaf's, else read from the node arrays: lanes in parallel, one round trip)
         if (l < cnt) {
             EdgeLink lk = P.ed[V.eb + bsel].k;
-            if (d == depth - 1 && lg >= 0 && bsel == V.off) { lk.child = lg; lk.cec = (int16_t)lec; lk.ceb = leb; }
-            P.nst[pnode] = NodeStat{V.nqs, V.nns, (int16_t)bsel, lk.a, lk.child, lk.cec, 0, lk.ceb};
+            int64_t cb = 0;
+            int cc = 0;
+            if (d == depth - 1 && lg >= 0 && bsel == V.off) {
+                lk.child = lg; cc = lec; cb = leb;
+            } else if (lk.child >= 0) {
+                cb = P.neb[lk.child];
+                cc = P.nterm[lk.child] ? -1 : P.nec[lk.child];
+            }
+            P.nst[pnode] = NodeStat{V.nqs, V.nns, (int16_t)bsel, lk.a, lk.child, (int16_t)cc, 0, cb};
         }
     }
     if (l == 0) {
@@ -2158,7 +2167,7 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     size_t bytes = 0;
     auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
     acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn);
-    acc(sizeof(NodeStat) * nn); acc(nn); acc(16 * nn); acc(sizeof(EdgeStat) * 2 * ne);
+    acc(sizeof(NodeStat) * nn); acc(nn); acc(16 * nn); acc((ne / EPG) * EdgePtr::PAGE_BYTES);
     acc(4 * (size_t)B * L.nptab); acc(4 * (size_t)B * L.eptab); acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages);
     acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages); acc(64);
     acc(4 * (size_t)B * L.hcap); acc(4 * (size_t)B * L.pcap); acc(8 * (size_t)B * L.pcap); acc(4 * (size_t)B * L.pcap);
@@ -2233,7 +2242,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.neb = carve<int64_t>(p, nn); P.nec = carve<int32_t>(p, nn); P.nround = carve<int32_t>(p, nn);
     P.nst = carve<NodeStat>(p, nn); P.nterm = carve<int8_t>(p, nn);
     P.nes = carve<float>(p, 4 * nn);
-    P.ed.base = carve<EdgeStat>(p, 2 * ne);              // EdgeStat | EdgeLink blocks per page
+    P.ed.base = carve<char>(p, (ne / EPG) * EdgePtr::PAGE_BYTES);   // EdgeStat | EdgeLink blocks per page
     P.ntab = carve<int32_t>(p, (size_t)B * P.nptab); P.etab = carve<int32_t>(p, (size_t)B * P.eptab);
     P.npidx = carve<int32_t>(p, (size_t)P.npages); P.epidx = carve<int32_t>(p, (size_t)P.epages);
     P.nfree = carve<int32_t>(p, (size_t)P.npages); P.efree = carve<int32_t>(p, (size_t)P.epages);

@@ -46,51 +46,55 @@ static_assert(sizeof(TreeHdr) == 192, "TreeHdr layout (splendor/mcts.py HDR_DTYP
 // or pool pressure; k_gc may skip it, see GC_SHOULD_CAP)
 enum { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2 };
 
-// Edge records, two 16-byte halves: the UCB inputs and the link (both read by the scan in
-// one round trip).
+// Edge records: the UCB inputs (16 bytes) and the link (8 bytes).
 struct __align__(16) EdgeStat {
     float p;       // prior Ps[a] (float32)
     int32_t n;     // Nsa
     double q;      // Qsa (Q_UNSET = the reference's -42 sentinel)
 };
-struct __align__(16) EdgeLink {
+struct __align__(8) EdgeLink {
     int16_t a;     // action
-    int16_t cec;   // cached child CSR count (-1: terminal child); valid when child >= 0
-    int32_t child; // child node, global id (-1: not linked yet)
-    int64_t ceb;   // cached child CSR base (global edge index)
+    int16_t pad;
+    int32_t child; // child node, global id (-1: not linked yet); its CSR range is the child's
+                   // own (neb / nec / nterm) and, for the node's arg-max, cached in NodeStat
 };
+static_assert(sizeof(EdgeLink) == 8, "EdgeLink layout");
 // one edge's value: both halves
-struct __align__(16) Edge {
+struct Edge {
     EdgeStat s;
     EdgeLink k;
 };
-// The edge pool keeps the two halves apart, blocked by edge page: page k holds the EdgeStat
-// records of its EPG edges, then their EdgeLink records (global edge i: stat at 16-byte unit
-// i + (i & ~(EPG - 1)), link EPG units later). k_backup's per-level arg-max scans read only
-// EdgeStat (a node's statistics are contiguous: 8 edges per 128-byte line instead of 4), the
-// descent reads links from its NodeStat copy, the root scan requests both halves in one round
-// trip. A node's CSR run never straddles an edge page, so within a run E[j] is plain
-// pointer arithmetic from one base (one pointer, as the 32-byte records had).
+// The edge pool keeps the halves apart, blocked by edge page: page k is 24 KB — the 16-byte
+// EdgeStat records of its EPG edges, then their 8-byte EdgeLink records. k_backup's per-level
+// arg-max scans read only EdgeStat (a node's statistics are contiguous: 8 edges per 128-byte
+// line), the descent reads links from its NodeStat copy, the root scan requests both halves
+// in one round trip; 24 bytes per edge (round 2's records: 32) is what lets config 4's
+// steady-state trees fit. A node's CSR run never straddles an edge page, so a run is one
+// page base plus an offset. EdgePtr / EdgeRef give the pool the syntax of an Edge array:
+// E[i].s, E[i].k, E + i.
 struct EdgeRef {
     EdgeStat &s;
     EdgeLink &k;
     __device__ __forceinline__ operator Edge() const { return Edge{s, k}; }
 };
-struct EdgePtr {           // edge j of a run (within one edge page)
-    EdgeStat *p;
-    __device__ __forceinline__ EdgeRef operator[](int64_t j) const {
-        return EdgeRef{p[j], *reinterpret_cast<EdgeLink *>(p + EPG_ + j)};
-    }
-    __device__ __forceinline__ EdgePtr operator+(int64_t j) const { return EdgePtr{p + j}; }
+struct EdgePtr {           // edges of one run (within one edge page): page base + offset
+    char *pg;
+    int o;
     static constexpr int EPG_ = 1 << 10;
+    static constexpr int64_t PAGE_BYTES = (int64_t)EPG_ * (sizeof(EdgeStat) + sizeof(EdgeLink));
+    __device__ __forceinline__ EdgeRef operator[](int64_t j) const {
+        return EdgeRef{reinterpret_cast<EdgeStat *>(pg)[o + j],
+                       reinterpret_cast<EdgeLink *>(pg + EPG_ * sizeof(EdgeStat))[o + j]};
+    }
+    __device__ __forceinline__ EdgePtr operator+(int64_t j) const { return EdgePtr{pg, o + (int)j}; }
 };
 struct EdgePool {          // the whole pool, by global edge index
-    EdgeStat *base;
-    __device__ __forceinline__ static int64_t unit(int64_t i) { return i + (i & ~(int64_t)(EdgePtr::EPG_ - 1)); }
-    __device__ __forceinline__ EdgePtr operator+(int64_t i) const { return EdgePtr{base + unit(i)}; }
+    char *base;
+    __device__ __forceinline__ EdgePtr operator+(int64_t i) const {
+        return EdgePtr{base + (i >> 10) * EdgePtr::PAGE_BYTES, (int)(i & (EdgePtr::EPG_ - 1))};
+    }
     __device__ __forceinline__ EdgeRef operator[](int64_t i) const { return (*this + i)[0]; }
 };
-__device__ __forceinline__ void set_cr(EdgeLink &e, int64_t eb, int ec) { e.ceb = eb; e.cec = (int16_t)ec; }
 
 // a node's visit statistics (Ns, Qs) and its cached arg-max edge, one 32-byte record.
 // pick_highest_UCB (MCTS.py:199-219) at a non-root node reads only that node's Ns, Qs and its
@@ -99,7 +103,8 @@ __device__ __forceinline__ void set_cr(EdgeLink &e, int64_t eb, int ec) { e.ceb 
 // arg-max k_backup computes right after a node's update is exactly the edge the next descent
 // through the node picks: the descent follows `best` and the link copied from that edge (one
 // 32-byte load per level, no edge scan). The root level always scans. Invariant (k_backup,
-// k_select's links, k_gc's remap): {bchild, bcec, bceb} == the link of edge best.
+// k_select's links, k_gc's remap): bchild == the link of edge best, {bcec, bceb} == that
+// child's CSR range (bcec -1: terminal).
 struct __align__(16) NodeStat {
     double qs;       // Qs
     int32_t ns;      // Ns
