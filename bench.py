@@ -432,6 +432,10 @@ def selfplay_roofline(rec, n, depth):
     prof = load_json_profile("r*_selfplay_pmc.json")
     kern = (prof or {}).get("kernels", {})
     B = CONFIGS["config3"][1]
+    # the network kernel over the same full batch under rocprofv3 (duration, PMC bytes):
+    # profiles/rNN_nn_fullbatch.json (tools/nn_fullbatch.sh); the self-play PMC summary's
+    # k_nn_forward entry covers the compacted launches (~72 % of the leaves) instead
+    nnfb = load_json_profile("r*_nn_fullbatch.json") or {}
 
     def per_sim(k):
         v = kern.get(k, {}).get("hbm_bytes_per_launch")
@@ -441,9 +445,12 @@ def selfplay_roofline(rec, n, depth):
     tot = sum(v["hbm_bytes_per_sim"] or 0.0 for v in tree.values())
     return {"bound": "mfma", "achieved": nk["tflops"], "peak": FP32_MFMA_PEAK, "unit": "TFLOP/s",
             "frac": nk["frac_fp32_mfma_peak"],
-            "traffic": kern.get("k_nn_forward", {}).get("hbm_bytes_per_launch"),
+            "traffic": nnfb.get("hbm_bytes_per_launch"),
             "kernel": nk["kernel"], "kernel_avg_us": nk["avg_us"],
-            "kernel_avg_us_rocprof": kern.get("k_nn_forward", {}).get("avg_us"),
+            "kernel_avg_us_rocprof": nnfb.get("avg_us"), "rocprof_file": nnfb.get("file"),
+            "selfplay_launch": {"avg_us_rocprof": kern.get("k_nn_forward", {}).get("avg_us"),
+                                "hbm_bytes_per_launch": kern.get("k_nn_forward", {}).get("hbm_bytes_per_launch"),
+                                "note": "in self-play the kernel runs on the compacted NN-leaf list"},
             "flop_per_launch": nn_flops_per_eval(n) * B,
             "tree_kernels": {"per_kernel": tree, "hbm_bytes_per_sim_total": tot or None,
                              "algorithmic_bytes_per_sim_survey": bytes_per_rollout(n, 4.8),
