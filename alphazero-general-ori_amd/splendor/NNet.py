@@ -85,26 +85,48 @@ def _batch_generator(device):
     return g
 
 
-def _same_everywhere(E, device):
-    """True when every rank holds the same number of examples (Coach.learn all-gathers, so
-    ranks hold the same set)."""
+def _content_checksum(ex):
+    """64-bit checksum of an ExampleSet's contents (every column's bytes, position-weighted;
+    integer sums wrap identically on any device), so ranks can tell whether they hold the
+    same examples — equal counts alone do not say that."""
+    h = torch.zeros((), dtype=torch.int64, device=ex.board.device)
+    for k, col in enumerate((ex.board, ex.pi, ex.winner, ex.scdiff, ex.valids, ex.surprise)):
+        b = col.contiguous().reshape(-1).view(torch.uint8).to(torch.int64)
+        w = torch.arange(1, b.numel() + 1, dtype=torch.int64, device=b.device) * 0x9E3779B1 + (k + 1) * 0x7F4A7C15
+        h = h * 0x100000001B3 + (b * w).sum()
+    return h
+
+
+def _same_everywhere(ex, device):
+    """True when every rank holds the same examples (Coach.learn all-gathers, so ranks hold
+    the same set): the example count and a content checksum agree across ranks."""
     dist, _, world = _dist_world()
     if world == 1:
         return True
-    t = torch.tensor([E, -E], dtype=torch.int64, device=device)
+    h = _content_checksum(ex).to(device)
+    t = torch.stack([torch.tensor(len(ex), dtype=torch.int64, device=device), h])
+    t = torch.cat([t, -t])
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return int(t[0]) == -int(t[1]) == E
+    return int(t[0]) == -int(t[2]) == len(ex) and int(t[1]) == -int(t[3]) == int(h)
 
 
-def _allreduce_grads(params):
-    """Average gradients over ranks in one flat bucket (the model is ~1.25 MB of fp32)."""
+def _allreduce_grads(params, weight=None):
+    """Sum (weight given: each rank's gradients scaled by its share of the global batch) or
+    average (weight None) the gradients over ranks in one flat bucket (the model is ~1.25 MB
+    of fp32). Parameters without a gradient on this rank contribute zeros."""
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
         return
-    grads = [p.grad for p in params if p.grad is not None]
+    for p in params:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+    grads = [p.grad for p in params]
     flat = torch.cat([g.reshape(-1) for g in grads])
+    if weight is not None:
+        flat *= weight
     dist.all_reduce(flat)
-    flat /= dist.get_world_size()
+    if weight is None:
+        flat /= dist.get_world_size()
     off = 0
     for g in grads:
         g.copy_(flat[off:off + g.numel()].view_as(g))
@@ -140,7 +162,7 @@ class NNetWrapper:
         return (loss_pi(pis, out_pi), loss_v(vs, out_v), loss_scdiff_cdf(t_sd, out_sd),
                 loss_scdiff_pdf(t_sd, out_sd))
 
-    def train(self, examples, generator=None, sample_ids=None):
+    def train(self, examples, generator=None, sample_ids=None, shared=None):
         """One GenericNNetWrapper.train call over `examples` (ExampleSet, or the reference's
         list of tuples): epochs x (len // batch_size) Adam steps on batches sampled without
         replacement, total loss l_pi + vl_weight * l_v + l_cdf + l_pdf, OneCycleLR stepped
@@ -153,11 +175,17 @@ class NNetWrapper:
 
         Across ranks (torch.distributed): with the same example set on every rank (what
         Coach.learn's all-gather leaves) all ranks draw the same permutation per step and
-        rank r trains on its slice ids[r::world] of the batch, gradients averaged in one
-        all-reduce: the step count and the samples per step are the reference's (a global
-        batch of batch_size; BatchNorm statistics are per rank). Ranks holding different
-        sets sample their own batches of batch_size (the step count is the minimum over
-        ranks, so no rank waits in an all-reduce the others never enter)."""
+        rank r trains on its slice ids[r::world] of the batch; each rank's gradients are
+        scaled by its slice's share of the batch and summed in one all-reduce, i.e. the
+        gradient of the mean loss over the whole batch (slices may differ in size, an empty
+        one contributes zeros): the step count and the samples per step are the
+        reference's (a global batch of batch_size; BatchNorm statistics are per rank).
+        Ranks holding different sets sample their own batches of batch_size from a per-call
+        generator seeded by a draw from `generator` mixed with the rank (the caller's
+        generator only advances by that draw), gradients averaged; the step count is the
+        minimum over ranks, so no rank waits in an all-reduce the others never enter.
+        shared: None detects it (example count and content checksum agree on every rank);
+        True / False force a path (every rank must pass the same)."""
         if not isinstance(examples, ExampleSet):
             examples = ExampleSet.from_tuples(list(examples))
         if self.args["surprise_weight"]:
@@ -167,7 +195,9 @@ class NNetWrapper:
         ex = examples.to(self.device)
         E, bs, epochs = len(ex), int(self.args["batch_size"]), int(self.args["epochs"])
         dist, rank, world = _dist_world()
-        shared = _same_everywhere(E, self.device)
+        if shared is None:
+            shared = _same_everywhere(ex, self.device)
+        self.last_shared = bool(shared)
         batch_count = _agreed_batch_count(E // bs, self.device)
         if batch_count == 0:
             return None
@@ -181,8 +211,10 @@ class NNetWrapper:
         scheduler = optim.lr_scheduler.OneCycleLR(self.optimizer, max_lr=self.args["learn_rate"],
                                                   steps_per_epoch=batch_count, epochs=epochs)
         gen = None if sample_ids is not None else (generator or _batch_generator(self.device))
-        if gen is not None and not shared:      # different sets: decorrelate the ranks
-            gen.manual_seed(gen.initial_seed() ^ (0x9E3779B97F4A7C15 * (rank + 1) & (2 ** 63 - 1)))
+        if gen is not None and not shared and world > 1:    # different sets: decorrelate the ranks
+            s0 = int(torch.randint(0, 2 ** 62, (1,), generator=gen, device=gen.device).item())
+            gen = torch.Generator(device=self.device)
+            gen.manual_seed((s0 ^ (0x9E3779B97F4A7C15 * (rank + 1))) & (2 ** 63 - 1))
         means, step = None, 0
         for _ in range(epochs):
             self.nnet.train()
@@ -192,19 +224,26 @@ class NNetWrapper:
                     ids = sample_ids[step]
                 else:
                     ids = torch.randperm(E, generator=gen, device=self.device)[:bs]
+                weight = None
                 if shared and world > 1:
                     ids = ids[rank::world]
+                    weight = len(ids) / bs       # this slice's share of the global batch
                 step += 1
+                self.optimizer.zero_grad(set_to_none=True)
+                if len(ids) == 0:                # (batch_size < world: nothing on this rank)
+                    _allreduce_grads(params, weight)
+                    self.optimizer.step()
+                    scheduler.step()
+                    continue
                 boards = ex.board.index_select(0, ids).float()
                 valids = unpack_mask(ex.valids.index_select(0, ids))
                 pis = ex.pi.index_select(0, ids)
                 vs = ex.winner.index_select(0, ids)
                 sds = ex.scdiff.index_select(0, ids)
-                self.optimizer.zero_grad(set_to_none=True)
                 l_pi, l_v, l_c, l_p = self.losses(boards, pis, vs, sds, valids)
                 total = l_pi + self.args["vl_weight"] * l_v + l_c + l_p
                 total.backward()
-                _allreduce_grads(params)
+                _allreduce_grads(params, weight)
                 self.optimizer.step()
                 scheduler.step()
                 acc += torch.stack([l_pi.detach(), l_v.detach(), (l_c + l_p).detach()]).double()
@@ -214,6 +253,7 @@ class NNetWrapper:
         self.nnet.eval()
         return {"pi": means[0], "v": means[1], "scdiff": means[2]}
 
+    last_shared = None   # the path the last train() call took across ranks
     _loss_log = None     # list: per-step (l_pi, l_v, l_cdf, l_pdf) appended by train (tests)
 
     # ------------------------------------------------------------ checkpoints

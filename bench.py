@@ -19,10 +19,11 @@ and config 4's per-GPU shard (32,768 games, 1,600 simulations), each at steady s
 its window statistics and CPU baselines (the oracle, a scalar C port of the reference, on
 one host core and on every granted core).
 
-Contract: `python bench.py --gpus N --steps K --warmup W`; for N>1 launched by
-torch.distributed.run, one rank per GPU; games are sharded by board id (board_base =
-rank * B), examples all-gathered over RCCL at the end of the window; rank 0 prints ONE JSON
-line.
+Contract: `python bench.py --gpus N --steps K --warmup W`; for N>1 one rank per GPU, either
+launched by torch.distributed.run (WORLD_SIZE set: it must equal N) or, when started
+directly, by bench.py itself (a child torch.distributed.run of N ranks, started before
+anything touches the GPU); games are sharded by board id (board_base = rank * B), examples
+all-gathered over RCCL at the end of the window; rank 0 prints ONE JSON line.
 """
 import argparse
 import ctypes
@@ -545,6 +546,51 @@ def run_env(args, rank, world, dev, dist, K, warmup, cpu=True):
     return rec
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc, argv):
+    """`bench.py --gpus N` outside torch.distributed.run (no WORLD_SIZE in the environment):
+    start N ranks as one child torch.distributed.run on this node (127.0.0.1 rendezvous) and
+    return its exit code. Runs before anything touches the GPU: the parent only waits; rank
+    0 of the child prints the JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    log(f"launching {nproc} ranks: {' '.join(cmd[1:6])} ...")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, rank, world):
+    """--dry-run: the multi-rank plumbing of the bench line without a GPU (gloo): barrier,
+    a timed no-op interval, max over ranks, rank 0 prints the line (value null)."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "rollouts/s (MCTS simulations)",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dry_run": True,
+                          "ranks_reporting": world, "max_elapsed_s": elapsed,
+                          "config": {"parallelism": f"dp{world} (game shards; RCCL all-gather of examples)"}}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -572,11 +618,24 @@ def main():
     ap.add_argument("--c4-window", type=int, default=4000)
     ap.add_argument("--node-boards", type=int, default=-1, help="selfplay: 1/0 force node boards on/off "
                     "(default: on unless the pools do not fit)")
+    ap.add_argument("--dry-run", action="store_true", help="multi-rank plumbing only (gloo, no GPU): "
+                    "prints the line with value null")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))    # the parent never touches the GPU
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return
     dist = None
     if world > 1:
         import torch.distributed as dist

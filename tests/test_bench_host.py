@@ -37,3 +37,29 @@ def test_algorithmic_figures(bench):
     assert bench.bytes_per_board_step(2) == 846                  # SURVEY §8(d), 2 players
     assert round(bench.bytes_per_rollout(2, 4.8)) == 3698        # ~3.7 KB per simulation
     assert bench.nn_flops_per_eval(2) == 2 * 595328              # 1.19 MFLOP per leaf
+
+
+def _run_bench(argv, env_extra=None, timeout=240):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_gpus_flag_launches_that_many_ranks():
+    """`bench.py --gpus 2` without torch.distributed.run starts 2 ranks itself (gloo dry run:
+    barrier, max over ranks) and rank 0 prints ONE JSON line with n_gpus 2."""
+    import json
+    r = _run_bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["ranks_reporting"] == 2 and out["steps"] == 3 and out["dry_run"]
+
+
+def test_gpus_flag_must_match_world_size():
+    r = _run_bench(["--gpus", "2", "--dry-run"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE 1" in r.stderr

@@ -114,7 +114,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="different", bs=16):
     import sys
     sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "alphazero-general-ori_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -122,33 +122,61 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from test_train import StubGame, synthetic
     from splendor.NNet import NNetWrapper
-    w = NNetWrapper(StubGame(), dict(epochs=1, batch_size=16, dropout=0.0), device="cpu", seed=0)
-    w.train(synthetic(64, seed=10 + rank), generator=torch.Generator().manual_seed(rank))
+    w = NNetWrapper(StubGame(), dict(epochs=1, batch_size=bs, dropout=0.0), device="cpu", seed=0)
+    if mode == "different":        # own examples and generator per rank
+        gen = torch.Generator().manual_seed(rank)
+        w.train(synthetic(64, seed=10 + rank), generator=gen)
+        gen_ok = gen.initial_seed() == rank            # the caller's generator is not re-seeded
+    else:                          # the same examples and generator on every rank
+        gen = torch.Generator().manual_seed(7)
+        w.train(synthetic(64, seed=10), generator=gen)
+        gen_ok = gen.initial_seed() == 7
     flat = torch.cat([p.detach().reshape(-1) for p in w.nnet.parameters()])
     parts = [torch.zeros_like(flat) for _ in range(world)]
     dist.all_gather(parts, flat)
+    info = torch.tensor([int(w.last_shared), int(gen_ok), int(torch.isfinite(flat).all())])
+    infos = [torch.zeros_like(info) for _ in range(world)]
+    dist.all_gather(infos, info)
     if rank == 0:
-        q.put([p.numpy() for p in parts])
+        q.put(([p.numpy() for p in parts], [i.tolist() for i in infos]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_gradient_allreduce_keeps_ranks_identical():
+def _two_ranks(mode, bs=16):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode, bs)) for r in range(world)]
     for p in procs:
         p.start()
-    parts = q.get(timeout=240)
+    parts, infos = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return parts, infos
+
+
+def test_two_rank_gradient_allreduce_keeps_ranks_identical():
+    """Different example sets per rank (own generators): the different-sets path (content
+    checksums differ), the ranks stay in lockstep, the callers' generators keep their seeds."""
+    parts, infos = _two_ranks("different")
     np.testing.assert_array_equal(parts[0], parts[1])
+    assert [i[0] for i in infos] == [0, 0] and [i[1] for i in infos] == [1, 1]
     init = torch.cat([p.detach().reshape(-1) for p in
                       NNetWrapper(StubGame(), {}, device="cpu", seed=0).nnet.parameters()]).numpy()
     assert not np.array_equal(parts[0], init)          # the ranks did train
+
+
+@pytest.mark.parametrize("bs", (16, 15, 1))
+def test_two_rank_shared_set_slices_one_batch(bs):
+    """The same example set on both ranks: the shared path (one permutation, rank r trains on
+    ids[r::2]); slices of unequal size (15) or empty (batch 1) are weighted by their share,
+    so no rank's gradient turns NaN and the ranks stay identical."""
+    parts, infos = _two_ranks("shared", bs)
+    np.testing.assert_array_equal(parts[0], parts[1])
+    assert [i[0] for i in infos] == [1, 1] and all(i[2] == 1 for i in infos)
 
 
 # ------------------------------------------------------------ parity with the reference
