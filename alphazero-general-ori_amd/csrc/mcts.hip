@@ -30,6 +30,31 @@ __device__ unsigned long long g_select_timing[24];
 
 using namespace spl;
 
+// Bounds-checked diagnostic builds (-DSPL_BOUNDS_CHECK=1, tools/bounds_check.sh; never the
+// product): every node id and global edge index k_select / k_backup derive from the pools,
+// the path and the cached links is checked against the pool sizes (and a CSR run against its
+// page) before use; a violation is counted, the first one recorded (site, value, tree) and the
+// value replaced by a safe one, so the run completes and reports instead of faulting.
+#ifndef SPL_BOUNDS_CHECK
+#define SPL_BOUNDS_CHECK 0
+#endif
+#if SPL_BOUNDS_CHECK
+__device__ unsigned long long g_bounds[4];
+__device__ __noinline__ void bounds_note(int site, long long v, int t) {
+    if (atomicAdd(&g_bounds[0], 1ull) == 0) {
+        g_bounds[1] = (unsigned long long)v; g_bounds[2] = (unsigned long long)site; g_bounds[3] = (unsigned long long)t;
+    }
+}
+#define BCHK(cond, site, v, t, fix)                                   \
+    do {                                                               \
+        if (!(cond)) { bounds_note((site), (long long)(v), (t)); fix; } \
+    } while (0)
+#else
+#define BCHK(cond, site, v, t, fix) \
+    do {                            \
+    } while (0)
+#endif
+
 struct spl_ctx {  // must match splendor_env.hip
     int n;
     int token_limit;
@@ -1329,6 +1354,14 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             // below the root a level is ONE 32-byte load: the node's statistics with its cached
             // arg-max and that edge's link (NodeStat); the root's edges (first 64; lanes past
             // the range read the first edge) are requested with its statistics
+#if SPL_BOUNDS_CHECK
+            {
+                const long long NN = (long long)P.npages * NPG, NE = (long long)P.epages * EPG;
+                BCHK(node >= 0 && node < NN, 20, node, t, node = 0);
+                BCHK(eb >= 0 && eb < NE && ec <= SPL_ACTIONS && (eb & (EPG - 1)) + ec <= EPG, 21, eb, t,
+                     (eb = 0, ec = 0));
+            }
+#endif
             NodeStat nsq = hq;
             if (!have) nsq = nst_t[node];
             have = false;
@@ -1356,6 +1389,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                     pk.cec = uniform(P.nterm[pk.child] ? -1 : P.nec[pk.child]);
                 }
             }
+            BCHK(pk.e >= 0 && pk.e < ec, 22, pk.e, t, pk.e = 0);
+            BCHK(pk.child >= -1 && pk.child < (long long)P.npages * NPG, 23, pk.child, t, pk.child = -1);
             const int64_t ge = eb + pk.e;
             pend = depth; pend_n = node; pend_e = ge; pend_x = px_pack(pk.e, ec, pk.a);
             depth++;
@@ -1719,9 +1754,17 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     int pcnt = 0, pns = 0;
     double pq = 0.0, pqs = 0.0;
     EdgeStat b0[BK_BATCH];
+#if SPL_BOUNDS_CHECK
+    const long long NN = (long long)P.npages * NPG, NE = (long long)P.epages * EPG;
+#endif
     if (l < cnt) {
         V.off = px_off(px);
         V.ec = px_count(px);
+        BCHK(pnode >= 0 && pnode < NN, 1, pnode, t, pnode = 0);
+        BCHK(pge >= 0 && pge < NE, 2, pge, t, pge = 0);
+        BCHK(V.ec >= 1 && V.ec <= SPL_ACTIONS && V.off < V.ec && pge - V.off >= 0 &&
+                 ((pge - V.off) & (EPG - 1)) + V.ec <= EPG,
+             3, V.ec | (V.off << 16), t, (V.ec = 1, V.off = 0, pge = 0));
         V.eb = pge - V.off;
         const EdgeStat st = P.ed[pge].s;
         pcnt = st.n; pq = st.q;
@@ -1752,6 +1795,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                     eb = edge_run(P, H, t, ec);
                 }
             }
+        }
+        if (l == 0) {
+            BCHK(g < NN, 4, g, t, g = -1);
+            BCHK(eb < 0 || ((eb & (EPG - 1)) + ec <= EPG && eb + ec <= NE), 5, eb, t, eb = -1);
         }
         g = __shfl(g, 0, 64);
         eb = readlane64(eb, 0);
@@ -1808,6 +1855,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             bact = __builtin_amdgcn_readlane(bact, __ffsll((unsigned long long)__ballot(mine == bj)) - 1);
             __threadfence_block();
             __builtin_amdgcn_wave_barrier();
+            // the parent edge: a cross-lane read of lane depth - 1, so it is taken here, with the
+            // whole wave active — inside the lane-0 branch below a spilled `pge` is reloaded for
+            // lane 0 only and lane depth - 1 reads stale register contents (the round-3
+            // aperture violation)
+            const int64_t pe = depth > 0 ? readlane64(pge, depth - 1 < 64 ? depth - 1 : 0) : 0;
             if (l == 0) {
                 P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
                 P.neb[g] = eb; P.nec[g] = ec;
@@ -1818,8 +1870,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 else hash_insert(P, t, h_k0, g);
                 if (depth == 0) { H->root = g; H->root_eb = eb; H->root_ec = ec; }
                 else {
-                    const int64_t pe = readlane64(pge, depth - 1 < 64 ? depth - 1 : 0);
-                    const int64_t pe2 = depth - 1 < 64 ? pe : path_e[depth - 1];
+                    int64_t pe2 = depth - 1 < 64 ? pe : path_e[depth - 1];
+                    BCHK(pe2 >= 0 && pe2 < NE, 8, pe2, t, pe2 = 0);
                     P.ed[pe2].k.child = g;
                 }
                 H->node_count += 1;
@@ -1841,6 +1893,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 pnode = path_n[d]; pge = path_e[d]; px = path_x[d];
                 V.off = px_off(px);
                 V.ec = px_count(px);
+                BCHK(pnode >= 0 && pnode < NN, 9, pnode, t, pnode = 0);
+                BCHK(pge >= 0 && pge < NE, 10, pge, t, pge = 0);
+                BCHK(V.ec >= 1 && V.ec <= SPL_ACTIONS && V.off < V.ec && pge - V.off >= 0 &&
+                         ((pge - V.off) & (EPG - 1)) + V.ec <= EPG,
+                     11, V.ec | (V.off << 16), t, (V.ec = 1, V.off = 0, pge = 0));
                 V.eb = pge - V.off;
                 const EdgeStat st = P.ed[pge].s;
                 pcnt = st.n; pq = st.q;
@@ -1896,7 +1953,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         // the node record: statistics, arg-max, that edge's link and its child's CSR range
         // (the new leaf's, else read from the node arrays: lanes in parallel, one round trip)
         if (l < cnt) {
+            BCHK(bsel >= 0 && bsel < V.ec, 6, bsel, t, bsel = 0);
             EdgeLink lk = P.ed[V.eb + bsel].k;
+            BCHK(lk.child >= -1 && lk.child < NN, 7, lk.child, t, lk.child = -1);
             int64_t cb = 0;
             int cc = 0;
             if (d == depth - 1 && lg >= 0 && bsel == V.off) {
@@ -1912,6 +1971,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         H->sims_done = h_sims + 1;
         H->noise_pending = 0;
         H->leaf_kind = LEAF_NONE;
+        H->depth_max = max(H->depth_max, depth);         // leaf depth statistics (diagnostic)
+        H->depth_sum += depth;
     }
 }
 
@@ -2080,15 +2141,18 @@ __global__ __launch_bounds__(64) void k_tree_sizes(Pools P, int B, int32_t *out)
 }
 
 // deterministic hash network (oracle or_fake_predict; used for search-parity tests and
-// tree-only throughput runs)
+// tree-only throughput runs). mode 0: priors spread over (0, 1], values in [-1, 1); mode 1
+// ("peaked"): (w / max w)^256 priors and values near +-1, like the random-init SplendorNNet
+// the bench runs — leaves reach the bench's depths
 template <int N>
 __global__ __launch_bounds__(256) void k_hash_eval(int B, const int8_t *__restrict__ st,
                                                    const uint64_t *__restrict__ mask,
-                                                   float *__restrict__ pi, float *__restrict__ v) {
+                                                   float *__restrict__ pi, float *__restrict__ v, int mode) {
     const int t = blockIdx.x;
     if (t >= B) return;
     const int8_t *s = st + (size_t)t * Lay<N>::S;
     __shared__ uint64_t hsh;
+    __shared__ double wred[4];
     if (threadIdx.x == 0) {
         uint64_t h = 0xCBF29CE484222325ull;
         for (int i = 0; i < Lay<N>::S; i++) { h ^= (uint8_t)s[i]; h *= 0x100000001B3ull; }
@@ -2096,6 +2160,27 @@ __global__ __launch_bounds__(256) void k_hash_eval(int B, const int8_t *__restri
     }
     __syncthreads();
     const uint64_t h = hsh;
+    if (mode == 1) {
+        double wm = 0.0;
+        for (int a = threadIdx.x; a < SPL_ACTIONS; a += 256)
+            if ((mask[(size_t)t * 7 + a / 64] >> (a % 64)) & 1) wm = fmax(wm, (double)(1 + (mix64(h + (uint64_t)a) >> 40)));
+        for (int o = 32; o > 0; o >>= 1) wm = fmax(wm, __shfl_xor(wm, o, 64));
+        if (lane_id() == 0) wred[threadIdx.x >> 6] = wm;
+        __syncthreads();
+        wm = fmax(fmax(wred[0], wred[1]), fmax(wred[2], wred[3]));
+        for (int a = threadIdx.x; a < SPL_ACTIONS; a += 256) {
+            const bool ok = (mask[(size_t)t * 7 + a / 64] >> (a % 64)) & 1;
+            double w = (double)(1 + (mix64(h + (uint64_t)a) >> 40)) / wm;
+#pragma unroll
+            for (int k = 0; k < 8; k++) w = w * w;
+            pi[(size_t)t * SPL_ACTIONS + a] = ok ? (float)w : 0.f;
+        }
+        if (threadIdx.x < N)
+            v[(size_t)t * N + threadIdx.x] =
+                (float)((threadIdx.x == 0 ? 1.0 : -1.0) *
+                        (1.0 - (double)(mix64(h ^ (0xA5A5ull + threadIdx.x)) >> 40) * 0x1p-30));
+        return;
+    }
     for (int a = threadIdx.x; a < SPL_ACTIONS; a += 256) {
         const bool ok = (mask[(size_t)t * 7 + a / 64] >> (a % 64)) & 1;
         pi[(size_t)t * SPL_ACTIONS + a] =
@@ -2199,6 +2284,18 @@ int spl_diag_select_timing(unsigned long long *out24, int reset) {
     if (reset) {
         unsigned long long z[24] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_select_timing), z, sizeof(z)) != hipSuccess) return SPL_EDEVICE;
+    }
+    return 0;
+}
+#endif
+
+#if SPL_BOUNDS_CHECK
+// bounds-checked builds only: [0] violations, [1] first value, [2] its site, [3] its tree
+int spl_diag_bounds(unsigned long long *out4, int reset) {
+    if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_bounds), 4 * 8) != hipSuccess) return SPL_EDEVICE;
+    if (reset) {
+        unsigned long long z[4] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bounds), z, sizeof(z)) != hipSuccess) return SPL_EDEVICE;
     }
     return 0;
 }
@@ -2460,13 +2557,18 @@ int spl_nn_input(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t 
     return check_launch();
 }
 
-int spl_hash_eval(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask, float *pi,
-                  float *v, void *hs) {
-    if (!ctx || B < 0 || (B && (!state || !mask || !pi || !v))) return SPL_EINVAL;
+int spl_hash_eval_mode(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask, float *pi,
+                       float *v, int mode, void *hs) {
+    if (!ctx || B < 0 || mode < 0 || mode > 1 || (B && (!state || !mask || !pi || !v))) return SPL_EINVAL;
     if (!B) return 0;
     SPL_DISPATCH(ctx->n, hipLaunchKernelGGL(k_hash_eval<N>, dim3((unsigned)B), dim3(256), 0,
-                                            (hipStream_t)hs, B, state, mask, pi, v));
+                                            (hipStream_t)hs, B, state, mask, pi, v, mode));
     return check_launch();
+}
+
+int spl_hash_eval(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask, float *pi,
+                  float *v, void *hs) {
+    return spl_hash_eval_mode(ctx, B, state, mask, pi, v, 0, hs);
 }
 
 }  // extern "C"

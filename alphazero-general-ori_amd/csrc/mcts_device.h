@@ -36,8 +36,9 @@ struct TreeHdr {
                                          // edge page, nodes kept by the last collection
     int32_t root_round, gc_queued, withdrawals, gcs;   // root round (deferred GC), queued for
                                          // k_gc, simulations withdrawn for GC, collections run
-    int32_t leaf_hslot, leaf_slot, pad1, pad2;   // the NN leaf's empty table slot (found by the
+    int32_t leaf_hslot, leaf_slot;       // the NN leaf's empty table slot (found by the
                                          // select's lookup) and reserved node slot, or -1
+    int32_t depth_max, depth_sum;        // leaf depths of the simulations backed up: maximum, sum
 };
 static_assert(sizeof(TreeHdr) == 192, "TreeHdr layout (splendor/mcts.py HDR_DTYPE)");
 // gc_state: 0 none; 1 a leaf did not fit mid-search (withdrawn, k_gc collects, the descent

@@ -74,6 +74,7 @@ _SIGS = {
     "spl_mcts_drain_examples": ([C.c_void_p, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int, _vp, _vp], C.c_int),
     "spl_nn_input": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "spl_hash_eval": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "spl_hash_eval_mode": ([C.c_void_p, C.c_int, _vp, _vp, _vp, _vp, C.c_int, _vp], C.c_int),
 }
 
 

@@ -34,7 +34,7 @@ HDR_DTYPE = np.dtype([
     ("root_eb", "<i8"), ("enext", "<i8"),
     ("npg", "<i4"), ("epg", "<i4"), ("eleft", "<i4"), ("live_gc", "<i4"),
     ("root_round", "<i4"), ("gc_queued", "<i4"), ("withdrawals", "<i4"), ("gcs", "<i4"),
-    ("leaf_hslot", "<i4"), ("leaf_slot", "<i4"), ("hpad1", "<i4"), ("hpad2", "<i4")])
+    ("leaf_hslot", "<i4"), ("leaf_slot", "<i4"), ("depth_max", "<i4"), ("depth_sum", "<i4")])
 assert HDR_DTYPE.itemsize == 192
 
 DEFAULT_ARGS = dict(numMCTSSims=100, cpuct=1.0, fpu=0.0, prob_fullMCTS=1.0, ratio_fullMCTS=5,
@@ -52,17 +52,20 @@ def _arg(args, k):
 
 
 class HashEvaluator:
-    """Deterministic stand-in network (spl_hash_eval); identical to the oracle's."""
+    """Deterministic stand-in network (spl_hash_eval_mode); identical to the oracle's
+    or_fake_predict. mode 0: spread priors and values (shallow trees); mode 1: peaked priors
+    and values near +-1, like the random-init SplendorNNet (the bench's deep trees)."""
 
-    def __init__(self, engine):
+    def __init__(self, engine, mode=0):
         self.e = engine
+        self.mode = int(mode)
 
     def __call__(self, leaf_state, leaf_mask, leaf_valid):
         B = leaf_state.shape[0]
         pi = torch.empty((B, ACTIONS), dtype=torch.float32, device=self.e.device)
         v = torch.empty((B, self.e.n), dtype=torch.float32, device=self.e.device)
-        _lib.check(self.e.L.spl_hash_eval(self.e.ctx, B, _ptr(leaf_state), _ptr(leaf_mask), _ptr(pi),
-                                          _ptr(v), self.e._s()), "spl_hash_eval")
+        _lib.check(self.e.L.spl_hash_eval_mode(self.e.ctx, B, _ptr(leaf_state), _ptr(leaf_mask), _ptr(pi),
+                                               _ptr(v), self.mode, self.e._s()), "spl_hash_eval_mode")
         return pi, v
 
 

@@ -145,6 +145,7 @@ class SelfPlay(BatchedMCTS):
                 "overflow": int((h["overflow"] != 0).sum()),
                 "nodes_max": int(h["node_count"].max()), "edges_max": int(h["edge_count"].max()),
                 "leaf_depth_mean": float(h["depth"].mean()), "leaf_depth_max": int(h["depth"].max()),
+                "depth_sum": int(h["depth_sum"].astype("int64").sum()), "depth_max_all": int(h["depth_max"].max()),
                 **self.capacity_events(h), "examples_dropped": self.dropped_examples()}
 
 

@@ -269,9 +269,12 @@ int spl_mcts_tree_sizes(spl_mcts *m, int32_t *out, void *hip_stream);
 int spl_nn_input(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask,
                  float *x, uint8_t *valid, void *hip_stream);
 /* deterministic hash-prior network (see oracle or_fake_predict): parity tests and
- * tree-only throughput runs */
+ * tree-only throughput runs. spl_hash_eval = mode 0 (spread priors, values in [-1, 1));
+ * mode 1: peaked priors, values near +-1 (deep trees like the random-init SplendorNNet's) */
 int spl_hash_eval(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask,
                   float *pi, float *v, void *hip_stream);
+int spl_hash_eval_mode(const spl_ctx *ctx, int B, const int8_t *state, const uint64_t *mask,
+                       float *pi, float *v, int mode, void *hip_stream);
 
 /* ===================================================================== network
  * SplendorNNet inference (SplendorNNet.py:56-159 in eval mode; GenericNNetWrapper.predict

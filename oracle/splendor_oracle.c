@@ -511,12 +511,44 @@ static uint64_t splitmix64(uint64_t x) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
+/* Hash network of the search-parity tests (device: k_hash_eval). Mode 0: priors spread over
+ * (0, 1], values in [-1, 1) — shallow trees (leaf depth ~3). Mode 1 ("flat"): priors within
+ * 1.6 % of each other and values within +-1/32, like the random-init SplendorNNet the bench
+ * runs: with FPU reduction the search then keeps revisiting its first lines, and leaves
+ * reach the depths of the bench's steady state (mean > 15, max > 64). */
+static int g_fake_mode = 0;
+void or_set_fake_mode(int mode) { g_fake_mode = mode; }
 void or_fake_predict(int n, const int8_t *st, const uint8_t *va, float *pi, float *v) {
     uint64_t h = or_state_hash(st, 7 * or_rows(n));
+    if (g_fake_mode == 1) {
+        double wmax = 0.0;                                  /* like a softmax: the top legal */
+        for (int a = 0; a < 409; a++)                       /* action's weight is 1          */
+            if (va[a]) wmax = fmax(wmax, (double)(1 + (splitmix64(h + (uint64_t)a) >> 40)));
+        for (int a = 0; a < 409; a++) {
+            double w = (double)(1 + (splitmix64(h + (uint64_t)a) >> 40)) / wmax;
+            for (int k = 0; k < 8; k++) w = w * w;          /* w^256: peaked, many exact zeros */
+            pi[a] = va[a] ? (float)w : 0.f;
+        }
+        for (int i = 0; i < n; i++)
+            v[i] = (float)((i == 0 ? 1.0 : -1.0) * (1.0 - (double)(splitmix64(h ^ (0xA5A5ull + (uint64_t)i)) >> 40) * 0x1p-30));
+        return;
+    }
     for (int a = 0; a < 409; a++)
         pi[a] = va[a] ? (float)((double)(1 + (splitmix64(h + (uint64_t)a) >> 40)) * 0x1p-24) : 0.f;
     for (int i = 0; i < n; i++)
         v[i] = (float)((double)(splitmix64(h ^ (0xA5A5ull + (uint64_t)i)) >> 40) * 0x1p-23 - 1.0);
+}
+
+/* leaf depths of the searches since the last reset (edges from the root to the leaf each
+ * simulation evaluated or found terminal): sum, maximum, simulations */
+static long long g_depth_sum = 0, g_depth_max = 0, g_depth_cnt = 0;
+void or_depth_stats(long long *out3, int reset) {
+    if (out3) { out3[0] = g_depth_sum; out3[1] = g_depth_max; out3[2] = g_depth_cnt; }
+    if (reset) g_depth_sum = g_depth_max = g_depth_cnt = 0;
+}
+static void note_depth(int d) {
+    g_depth_sum += d; g_depth_cnt += 1;
+    if (d > g_depth_max) g_depth_max = d;
 }
 
 static float pw_sum(const float *a, int len) {   /* numpy pairwise_sum, float32 */
@@ -730,7 +762,7 @@ static int pick_ucb(or_mcts *m, node_t *nd, int forced) {
     return ba;
 }
 
-static void search(or_mcts *m, const int8_t *st, int forced, int noise, float *vout) {
+static void search(or_mcts *m, const int8_t *st, int forced, int noise, float *vout, int depth) {
     int n = m->n;
     node_t *nd = *lookup(m, st);
     if (!nd) {
@@ -738,9 +770,10 @@ static void search(or_mcts *m, const int8_t *st, int forced, int noise, float *v
         int any = 0; for (int i = 0; i < n; i++) any |= es[i] != 0.f;
         nd = insert(m, st);
         memcpy(nd->es, es, sizeof es);
-        if (any) { nd->terminal = 1; memcpy(vout, es, sizeof(float) * n); return; }
-    } else if (nd->terminal) { memcpy(vout, nd->es, sizeof(float) * n); return; }
+        if (any) { nd->terminal = 1; memcpy(vout, es, sizeof(float) * n); note_depth(depth); return; }
+    } else if (nd->terminal) { memcpy(vout, nd->es, sizeof(float) * n); note_depth(depth); return; }
     if (!nd->has_ps) {
+        note_depth(depth);
         or_valid_moves(n, st, 0, nd->vs);
         float v[4];
         or_fake_predict(n, st, nd->vs, nd->ps, v);
@@ -760,7 +793,7 @@ static void search(or_mcts *m, const int8_t *st, int forced, int noise, float *v
     int8_t *child = (int8_t *)malloc((size_t)m->S);
     int nxt = or_tree_step(n, st, a, child);
     float vc[4];
-    search(m, child, 0, 0, vc);
+    search(m, child, 0, 0, vc, depth + 1);
     free(child);
     nd = *lookup(m, st);                       /* table may have been rehashed */
     for (int i = 0; i < n; i++) vout[i] = vc[((i - nxt) % n + n) % n];   /* np.roll */
@@ -774,7 +807,7 @@ int or_mcts_search(or_mcts *m, const int8_t *root, int64_t *counts, double *qsa,
                    double *probs, double *q) {
     float v[4];
     for (m->step = 0; m->step < m->sims; m->step++)
-        search(m, root, m->forced, m->step == 0 && m->dir_alpha > 0, v);
+        search(m, root, m->forced, m->step == 0 && m->dir_alpha > 0, v, 0);
     node_t *nd = *lookup(m, root);
     long long c[409], best = 0;
     for (int a = 0; a < 409; a++) { c[a] = nd->nsa[a]; if (c[a] > best) best = c[a]; }
@@ -861,7 +894,7 @@ int or_selfplay_run(int n, int B, int iters, uint64_t seed, uint32_t board_base,
         for (int it = 0; it < iters; it++) {
             float v[4];
             m->step = sims_done;
-            search(m, canon, forced, sims_done == 0 && full && dir_alpha > 0, v);
+            search(m, canon, forced, sims_done == 0 && full && dir_alpha > 0, v, 0);
             sims_done++;
             if (sims_done < budget) continue;
             /* commit */

@@ -38,6 +38,8 @@ def lib():
         L.or_state_hash.argtypes = [p8, C.c_int]
         L.or_state_hash.restype = C.c_uint64
         L.or_fake_predict.argtypes = [C.c_int, p8, pu8, pf, pf]
+        L.or_set_fake_mode.argtypes = [C.c_int]
+        L.or_depth_stats.argtypes = [C.POINTER(C.c_longlong), C.c_int]
         L.or_np_sum_f32.argtypes = [pf, C.c_int]
         L.or_np_sum_f32.restype = C.c_float
         L.or_mcts_new.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, C.c_int]
@@ -225,9 +227,24 @@ def rollout_run(n, B, steps, seed, board_base=0, masks=False):
     return out
 
 
+def set_fake_mode(mode):
+    lib().or_set_fake_mode(int(mode))
+
+
+def depth_stats(reset=True):
+    """(sum, max, count) of the leaf depths of every oracle simulation since the last reset."""
+    out = (C.c_longlong * 3)()
+    lib().or_depth_stats(out, int(reset))
+    return tuple(int(x) for x in out)
+
+
 def selfplay_run(n, B, iters, seed, num_sims, ratio_full, prob_full, cpuct, fpu, forced, temp_threshold,
-                 board_base=0, max_ex=20000, dir_alpha=0.0, dir_temp=1.25):
-    """Oracle of the device self-play loop (spl_mcts_commit semantics)."""
+                 board_base=0, max_ex=20000, dir_alpha=0.0, dir_temp=1.25, fake_mode=0):
+    """Oracle of the device self-play loop (spl_mcts_commit semantics). fake_mode: the hash
+    network's mode (0 spread, 1 flat); the result's "depth" = (sum, max, count) of its
+    simulations' leaf depths."""
+    set_fake_mode(fake_mode)
+    depth_stats(reset=True)
     R = rows(n)
     board = np.zeros((B, R, 7), np.int8)
     hdr = np.zeros((B, 8), np.int32)
@@ -243,8 +260,10 @@ def selfplay_run(n, B, iters, seed, num_sims, ratio_full, prob_full, cpuct, fpu,
                               _p(st, C.c_int8), _p(pi, C.c_float), _p(va, C.c_uint64), _p(win, C.c_float),
                               _p(sd, C.c_int32), _p(q, C.c_float), _p(meta, C.c_int32))
     k = min(k, max_ex)
+    depth = depth_stats(reset=True)
+    set_fake_mode(0)
     return {"board": board, "hdr": hdr, "ex_board": st[:k], "pi": pi[:k], "valids": va[:k],
-            "winner": win[:k], "scdiff": sd[:k], "surprise": q[:k], "meta": meta[:k]}
+            "winner": win[:k], "scdiff": sd[:k], "surprise": q[:k], "meta": meta[:k], "depth": depth}
 
 
 ST_FULL, ST_DIR, ST_PICK, ST_MOVE, ST_DEAL, ST_BEST = (1 << 24), (2 << 24), (3 << 24), (4 << 24), (5 << 24), (6 << 24)

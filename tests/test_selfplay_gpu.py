@@ -329,3 +329,105 @@ def test_restart_games_abandons_only_the_chosen_games():
 
 HDR_KEYS = ("node_count", "edge_count", "root", "sims_done", "budget", "full", "player", "episode_step",
             "move_no", "game_no", "n_examples", "games_done", "moves")
+
+
+GENBU = dict(cpuct=2.5, fpu=0.3, prob_full=0.25, ratio=5, noise=True)
+
+
+def _deep_device(n, B, iters, sims=100, seed=11, **kw):
+    from splendor.env import SplendorEngine
+    from splendor.mcts import HashEvaluator
+    from splendor.selfplay import SelfPlay
+    args = dict(numMCTSSims=sims, cpuct=GENBU["cpuct"], fpu=GENBU["fpu"], prob_fullMCTS=GENBU["prob_full"],
+                ratio_fullMCTS=GENBU["ratio"], forced_playouts=False, dirichletAlpha=0.3, temperature=[1.25, 0.8],
+                tempThreshold=10)
+    e = SplendorEngine(n)
+    sp = SelfPlay(e, B, args, evaluator=HashEvaluator(e, mode=1), dirichlet_noise=True, seed=seed,
+                  out_cap=60000, **kw)
+    sp.reset()
+    sp.run(iters, use_graph=True)
+    torch.cuda.synchronize()
+    hdr = sp.headers()
+    st = sp.stats()
+    ex = {k: v.cpu().numpy() for k, v in sp.drain().items()}
+    print(f"deep self-play n={n} B={B} iters={iters} {kw}: {st}", flush=True)
+    del sp
+    return hdr, st, ex
+
+
+def _deep_selfplay(n, B, iters, sims=100, seed=11, device_run=None, **kw):
+    """Self-play with the peaked hash network (mode 1: the random-init SplendorNNet's regime:
+    deep trees, long terminal lines) against the oracle's sequential loop, bit for bit."""
+    hdr, st, ex = device_run or _deep_device(n, B, iters, sims, seed, **kw)
+    ref = O.selfplay_run(n, B, iters, seed, sims, GENBU["ratio"], GENBU["prob_full"], GENBU["cpuct"], GENBU["fpu"],
+                         False, 10, max_ex=60000, dir_alpha=0.3, dir_temp=1.25, fake_mode=1)
+    rh = ref["hdr"]
+    for k, j in (("player", 0), ("episode_step", 1), ("move_no", 2), ("game_no", 3), ("games_done", 4),
+                 ("moves", 5), ("sims_done", 6)):
+        np.testing.assert_array_equal(hdr[k], rh[:, j], err_msg=k)
+    dsum, dmax, dcnt = ref["depth"]
+    assert st["depth_sum"] == dsum and st["depth_max_all"] == dmax     # every simulation's leaf depth
+    assert len(ex["pi"]) == len(ref["pi"])
+    if not len(ex["pi"]):
+        return st, dsum / dcnt, dmax
+    ex = sort_examples(ex, ex["meta"])
+    rf = sort_examples(ref, ref["meta"])
+    for k, rk in (("meta", "meta"), ("board", "ex_board"), ("pi", "pi"), ("winner", "winner"),
+                  ("scdiff", "scdiff"), ("surprise", "surprise")):
+        np.testing.assert_array_equal(ex[k], rf[rk], err_msg=k)
+    np.testing.assert_array_equal(ex["valids"].view(np.uint64), rf["valids"])
+    return st, dsum / dcnt, dmax
+
+
+@pytest.mark.parametrize("n,B,iters", [(2, 128, 3000), (4, 64, 2000)])    # (4p games outlast 2,000)
+def test_deep_selfplay_matches_oracle(n, B, iters):
+    """The bench's regime: genbu search arguments, Dirichlet noise, 100
+    simulations, the peaked hash network — leaves at mean depth > 15 and beyond 64 levels, so
+    k_backup's later 64-level groups and the descent's path reuse past 64 levels run — bit
+    for bit against the oracle (headers, every leaf depth, every finished example)."""
+    st, mean, mx = _deep_selfplay(n, B, iters)
+    assert mean > 15 and mx > 64, (mean, mx)
+    assert st["prunes"] == st["resets"] == st["unexpanded"] == 0
+
+
+def test_withdrawals_repeat_the_same_simulation():
+    """Shared pools sized so searches run out of pages mid-search: the leaf is withdrawn,
+    k_gc collects the tree's garbage and the descent repeats — the games stay bit-exact with
+    the oracle's (which never runs out), with withdrawals > 0 and no other capacity event.
+    The pools shrink step by step (device only) until a run withdraws without any other
+    event; that run is compared with the oracle."""
+    from splendor.mcts import BatchedMCTS
+    n, B, iters = 2, 64, 2000
+    nc = BatchedMCTS.default_node_cap(100)
+    ratio = BatchedMCTS.EDGES_PER_NODE
+
+    def run(per_tree):
+        return _deep_device(n, B, iters, pool_nodes=B * per_tree, pool_edges=B * per_tree * ratio,
+                            node_cap=nc, edge_cap=32 * nc)
+
+    def events(r):
+        return r[1]["withdrawals"], r[1]["prunes"] + r[1]["resets"] + r[1]["unexpanded"]
+    hi, lo, found = 4096, None, None        # hi: no withdrawals; lo: withdrawals with other events
+    for per_tree in (2048, 1024, 512, 256):
+        r = run(per_tree)
+        w, other = events(r)
+        if w and not other:
+            found = r
+            break
+        if w:
+            lo = per_tree
+            break
+        hi = per_tree
+    while found is None and lo is not None and hi - lo > 4:
+        mid = (hi + lo) // 2
+        r = run(mid)
+        w, other = events(r)
+        if w and not other:
+            found = r
+        elif w:
+            lo = mid
+        else:
+            hi = mid
+    assert found is not None, "no pool size gave withdrawals without other capacity events"
+    st, _, _ = _deep_selfplay(n, B, iters, device_run=found)
+    assert st["withdrawals"] > 0
