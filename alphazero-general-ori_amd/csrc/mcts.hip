@@ -82,14 +82,10 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 }
 
 // ------------------------------------------------------------ edge selection
-// pick_edge for the descent: every edge's (P, N, Q, action, child) is requested in one go
-// (up to 2 x 64 edges in registers — more would cost occupancy; wider nodes loop over the
-// rest), so a tree level costs one round trip for the edges; the chosen edge's action and
-// child come from its lane by shuffle.
+// A pick: the edge's rank in its node's run, its action, its child (global id, -1: not linked)
+// and whether that child is terminal.
 struct Pick {
-    int e, a, child;
-    int cec;                                    // child's cached CSR count (valid when child >= 0)
-    int64_t ceb;                                // and base (global edge index)
+    int e, a, child, cterm;
 };
 __device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
     const int lo = __builtin_amdgcn_readlane((int)(uint64_t)x, l);
@@ -99,195 +95,95 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
 __device__ __forceinline__ double readlane_f64(double x, int l) {
     return __longlong_as_double(readlane64(__double_as_longlong(x), l));
 }
+__device__ __forceinline__ int wave_min_i32(int x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
+    return uniform(x);
+}
+__device__ __forceinline__ int wave_max_i32(int x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
+    return uniform(x);
+}
 
-// path_x: a path level's edge offset in its node's CSR run, the run's count and the action
-__device__ __forceinline__ int px_pack(int off, int ec, int a) { return off | (ec << 9) | (a << 18); }
+// path_x: a path level's edge: its rank in the node's run and its action
+__device__ __forceinline__ int px_pack(int off, int a) { return off | (a << 9); }
 __device__ __forceinline__ int px_off(int x) { return x & 0x1ff; }
-__device__ __forceinline__ int px_count(int x) { return (x >> 9) & 0x1ff; }
-__device__ __forceinline__ int px_action(int x) { return (x >> 18) & 0x1ff; }
+__device__ __forceinline__ int px_action(int x) { return (x >> 9) & 0x1ff; }
 
-__device__ __forceinline__ Pick pick_edge_desc(const Pools &P, const SearchCfg &C, int64_t eb, int ec,
-                                               int ns, double qs, bool forced, int step, const Edge &first) {
-    const int l = lane_id();
-    const EdgePtr E = P.ed + eb;
-    float p[2];
-    int n[2], a[2], c[2];
-    double q[2];
-#pragma unroll
-    for (int j = 0; j < 2; j++) {               // first: edge l, already requested by the caller
-        const int i = 64 * j + l;
-        EdgeStat st{0.f, 0, Q_UNSET};
-        EdgeLink lk{0, 0, -1};
-        if (i < ec) {
-            const Edge &ei = j == 0 ? first : E[i];
-            st = ei.s; lk = ei.k;
-        }
-        p[j] = st.p; n[j] = st.n; q[j] = st.q;
-        a[j] = lk.a; c[j] = lk.child;
-    }
-#if MCTS_TIMING
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // split load wait / compute
-    SPL_PROBE(8)
-#endif
-    int bi = -1;
-    if (forced) {                               // MCTS.py:208-213: first under-visited edge
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int i = 64 * j + l;
-            const bool f = i < ec && (long long)n[j] < (long long)sqrt(0.5 * (double)p[j] * (double)step);
-            const uint64_t b = __ballot(f);
-            if (bi < 0 && b) bi = 64 * j + __ffsll((unsigned long long)b) - 1;
-        }
-        for (int base = 128; bi < 0 && base < ec; base += 64) {
-            const int i = base + l;
-            bool f = false;
-            if (i < ec) f = (long long)E[i].s.n < (long long)sqrt(0.5 * (double)E[i].s.p * (double)step);
-            const uint64_t b = __ballot(f);
-            if (b) bi = base + __ffsll((unsigned long long)b) - 1;
-        }
-    }
-    const double fpu_init = C.fpu > 0 ? qs - C.fpu : C.fpu;
-    if (bi < 0 && ec <= 128) {
-        // pick_highest_UCB screened in float32: each edge's UCB u (the float64 value the
-        // reference computes) lies in [uf - e, uf + e] for its float32 estimate uf (relative
-        // error of the estimate <= 7e-7 of |uf| + |q|; e is 3x that). With L = max(uf - e),
-        // every edge that can hold the maximum has uf + e >= L; when that is one edge, it is
-        // the strict-'>' arg-max and the exact float64 evaluation is skipped. Ties and near
-        // ties (several candidates) fall through to the exact path below.
-        const float cf = (float)C.cpuct, sqf = sqrtf((float)ns), sqef = sqrtf((float)ns + 1e-8f);
-        const float ff = (float)fpu_init;
-        float lo[2], hi[2];
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            lo[j] = -INFINITY; hi[j] = -INFINITY;
-            if (64 * j + l < ec) {
-                const bool vis = q[j] != Q_UNSET;
-                const float qf = vis ? (float)q[j] : ff;
-                const float tf = vis ? cf * p[j] * sqf * __builtin_amdgcn_rcpf(1.f + (float)n[j]) : cf * p[j] * sqef;
-                const float uf = qf + tf;
-                const float e = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
-                lo[j] = uf - e; hi[j] = uf + e;
-            }
-        }
-        const float L = wave_max_f32(fmaxf(lo[0], lo[1]));
-        const uint64_t c0 = __ballot(hi[0] >= L), c1 = __ballot(hi[1] >= L);
-        if (__popcll(c0) + __popcll(c1) == 1)
-            bi = uniform(c0 ? __ffsll((unsigned long long)c0) - 1 : 64 + __ffsll((unsigned long long)c1) - 1);
-    }
-    if (bi < 0) {                               // pick_highest_UCB (MCTS.py:199-219)
-        const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
-        double bu = -INFINITY, uj[2];
-        int bj = 0x7fffffff;
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int i = 64 * j + l;
-            uj[j] = -INFINITY;
-            if (i < ec) {
-                const double u = q[j] != Q_UNSET ? q[j] + C.cpuct * (double)p[j] * sq / (double)(1 + n[j])
-                                                 : fpu_init + C.cpuct * (double)p[j] * sq_eps;
-                uj[j] = u;
-                if (u > bu) { bu = u; bj = i; }
-            }
-        }
-        if (ec <= 128) {
-            // strict '>' scan in action order = the lowest edge index holding the maximum:
-            // DPP wave max, then the first lane of the first half that holds it
-            const double m = wave_max_f64(bu);
-            const uint64_t b0 = __ballot(uj[0] == m);
-            bi = b0 ? __ffsll((unsigned long long)b0) - 1
-                    : 64 + __ffsll((unsigned long long)__ballot(uj[1] == m)) - 1;
-            bi = uniform(bi);
-        }
-        for (int base = 128; bi < 0 && base < ec; base += 64) {
-            const int i = base + l;
-            if (i < ec) {
-                const double qq = E[i].s.q, pp = (double)E[i].s.p;
-                const double u = qq != Q_UNSET ? qq + C.cpuct * pp * sq / (double)(1 + E[i].s.n)
-                                               : fpu_init + C.cpuct * pp * sq_eps;
-                if (u > bu) { bu = u; bj = i; }
-            }
-        }
-        if (bi < 0) {
-            wave_argmax(bu, bj);
-            bi = bj;
-        }
-    }
-    const int jb = bi >> 6;
-    int av = a[0], cv = c[0];
-#pragma unroll
-    for (int j = 1; j < 2; j++)
-        if (jb == j) { av = a[j]; cv = c[j]; }
-    bi = uniform(bi);                           // chosen lane -> SGPRs (readlane, no LDS trip)
-    av = __builtin_amdgcn_readlane(av, bi & 63);
-    cv = __builtin_amdgcn_readlane(cv, bi & 63);
-    if (bi >= 128) { av = E[bi].k.a; cv = E[bi].k.child; }
-    return {bi, av, cv, 0, 0};                  // (the child's range: child_range)
+// pick_highest_UCB's two expressions (MCTS.py:214-216) in float64, evaluated in the
+// reference's order
+__device__ __forceinline__ double ucb_visited(double q, int n, float p, double cpuct, double sq) {
+    return q + cpuct * (double)p * sq / (double)(1 + n);
 }
-
-// pick_highest_UCB's arg-max over a node with at most 64 edges and no forced playouts at this
-// level, one edge per lane (lanes >= ec hold anything and take no part), straight-line: the
-// float32 screen of pick_edge_desc with the exact float64 arg-max as the fallback. Uniform.
-__device__ __forceinline__ int ucb_argmax64(const EdgeStat &e, double cpuct, double fpu, float cf, int ec, int ns,
-                                            double qs) {
-    const int l = lane_id();
-    const bool in = l < ec;
-    const double fpu_init = fpu > 0 ? qs - fpu : fpu;
-    const bool vis = e.q != Q_UNSET;
-    int bi;
-    {
-        // branch-free estimate; v_sqrt_f32 / v_rcp_f32 (1 ulp) are inside the error bound
-        const float nf = (float)ns;
-        const float sq = vis ? __builtin_amdgcn_sqrtf(nf) : __builtin_amdgcn_sqrtf(nf + 1e-8f);
-        const float rc = vis ? __builtin_amdgcn_rcpf(1.f + (float)e.n) : 1.f;
-        const float qf = vis ? (float)e.q : (float)fpu_init;
-        const float uf = qf + cf * e.p * sq * rc;
-        const float er = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
-        const float L = wave_max_f32(in ? uf - er : -INFINITY);
-        const uint64_t c = __ballot(in && uf + er >= L);
-        bi = __popcll(c) == 1 ? __ffsll((unsigned long long)c) - 1 : -1;
-    }
-    if (bi < 0) {
-        const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
-        double u = -INFINITY;
-        if (in)
-            u = vis ? e.q + cpuct * (double)e.p * sq / (double)(1 + e.n)
-                    : fpu_init + cpuct * (double)e.p * sq_eps;
-        const double m = wave_max_f64(u);
-        bi = __ffsll((unsigned long long)__ballot(u == m)) - 1;
-    }
-    return uniform(bi);
+__device__ __forceinline__ double ucb_unvisited(float p, double cpuct, double fpu_init, double sq_eps) {
+    return fpu_init + cpuct * (double)p * sq_eps;
 }
+__device__ __forceinline__ double fpu_base(double fpu, double qs) { return fpu > 0 ? qs - fpu : fpu; }
 
-// the descent's root level in the common case (<= 64 edges, no forced playouts): the arg-max
-// and the chosen edge's link by readlane. Same result as pick_edge_desc.
-__device__ __forceinline__ Pick pick_edge64(const Edge &e, double cpuct, double fpu, float cf, int ec, int ns,
-                                            double qs) {
-    const int bi = ucb_argmax64(e.s, cpuct, fpu, cf, ec, ns, qs);
-    return {bi, __builtin_amdgcn_readlane((int)e.k.a, bi), __builtin_amdgcn_readlane(e.k.child, bi), 0, 0};
-}
-
-// exact pick_highest_UCB arg-max (float64, strict '>' in edge order = lowest index holding the
-// maximum) over any number of edges, the edge at offset `off` taking the statistics (on, oq)
-// (just written by this wave). Uniform.
-__device__ int ucb_argmax_wide(const EdgePtr E, int ec, int ns, double qs, double cpuct, double fpu, int off, int on,
-                               double oq) {
+// exact pick_highest_UCB over a whole run (MCTS.py:199-219), wave-wide: lane per edge in
+// chunks of 64, statistics from the node's visit block; the reference scans actions in order
+// with a strict '>', so ties go to the lowest action. forced (a root with forced playouts,
+// :208-213): the lowest action with Nsa < int(sqrt(0.5 P step)) wins outright. Uniform.
+__device__ Pick scan_run(const Pools &P, const NodeRun &r, int ns, double qs, double cpuct, double fpu, bool forced,
+                         int step) {
     const int l = lane_id();
-    const double fpu_init = fpu > 0 ? qs - fpu : fpu;
+    const double fpu_init = fpu_base(fpu, qs);
     const double sq = sqrt((double)ns), sq_eps = sqrt((double)ns + 1e-8);
     double bu = -INFINITY;
-    int bj = 0x7fffffff;
-    for (int base = 0; base < ec; base += 64) {
+    int ba = 0x7fffffff, bi = 0, bc = -1;
+    int fa = 0x7fffffff, fi = 0, fc = -1;
+    for (int base = 0; base < r.ec; base += 64) {
         const int i = base + l;
-        if (i < ec) {
-            EdgeStat e = E[i].s;
-            if (i == off) { e.n = on; e.q = oq; }
-            const double u = e.q != Q_UNSET ? e.q + cpuct * (double)e.p * sq / (double)(1 + e.n)
-                                            : fpu_init + cpuct * (double)e.p * sq_eps;
-            if (u > bu) { bu = u; bj = i; }
+        if (i < r.ec) {
+            const EdgeP e = *P.ep(r.eb + i);
+            int n = 0, c = -1;
+            double q = Q_UNSET;
+            if (e.vi >= 0) {
+                const VisitRec v = *P.vr(r.vb + REC_UNITS * e.vi);
+                n = v.n; q = v.q; c = v.child;
+            }
+            if (forced && (long long)n < (long long)sqrt(0.5 * (double)e.p * (double)step) && e.a < fa) {
+                fa = e.a; fi = i; fc = c;
+            }
+            const double u = q != Q_UNSET ? ucb_visited(q, n, e.p, cpuct, sq) : ucb_unvisited(e.p, cpuct, fpu_init, sq_eps);
+            if (u > bu || (u == bu && e.a < ba)) { bu = u; ba = e.a; bi = i; bc = c; }
         }
     }
-    wave_argmax(bu, bj);
-    return uniform(bj);
+    if (forced) {
+        const int m = wave_min_i32(fa);
+        if (m != 0x7fffffff) {
+            const int ln = __ffsll((unsigned long long)__ballot(fa == m)) - 1;
+            return {__builtin_amdgcn_readlane(fi, ln), m, __builtin_amdgcn_readlane(fc, ln), 0};
+        }
+    }
+    const double mu = wave_max_f64(bu);
+    const int am = wave_min_i32(bu == mu ? ba : 0x7fffffff);
+    const int ln = __ffsll((unsigned long long)__ballot(bu == mu && ba == am)) - 1;
+    return {__builtin_amdgcn_readlane(bi, ln), am, __builtin_amdgcn_readlane(bc, ln), 0};
+}
+
+// The best unvisited edge of a run, exactly: the candidate (lowest rank without statistics:
+// the largest prior, lowest action among equal priors) unless a later unvisited edge with a
+// smaller prior rounds to the same float64 u and has a lower action (strict '>' in action
+// order). Walks from the candidate while u stays equal (edges of the candidate's prior are
+// passed over: their actions are larger); usually one step. One lane; cand < ec.
+__device__ __forceinline__ int best_unvisited(const Pools &P, int64_t eb, int ec, int cand, double cpuct,
+                                              double fpu_init, double sq_eps, double &u_out, int &a_out) {
+    const EdgeP c = *P.ep(eb + cand);
+    const double uc = ucb_unvisited(c.p, cpuct, fpu_init, sq_eps);
+    int bi = cand, ba = c.a;
+    if (c.p > 0.f) {
+        for (int j = cand + 1; j < ec; j++) {
+            const EdgeP e = *P.ep(eb + j);
+            if (e.vi >= 0 || e.p == c.p) continue;
+            if (ucb_unvisited(e.p, cpuct, fpu_init, sq_eps) < uc) break;
+            if (e.a < ba) { ba = e.a; bi = j; }
+        }
+    }
+    u_out = uc;
+    a_out = ba;
+    return bi;
 }
 
 // ------------------------------------------------------------ prior sums
@@ -314,6 +210,68 @@ __device__ __forceinline__ float wave_np_sum409(const float *a) {
     return (b0 + b1) + (b2 + b3);
 }
 
+// ------------------------------------------------------------ runs in action order
+__device__ __forceinline__ void wave_lds_fence() {
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+}
+// index of action a among the legal actions `bits` (the reference's array order)
+__device__ __forceinline__ int order_of(const uint64_t *bits, int a) {
+    const int w = a >> 6;
+    int k = 0;
+#pragma unroll
+    for (int j = 0; j < 6; j++) k += j < w ? __popcll(bits[j]) : 0;
+    return k + __popcll(bits[w] & ((1ull << (a & 63)) - 1));
+}
+// the i-th legal action (i < count)
+__device__ __forceinline__ int action_at(const uint64_t *bits, int i) {
+#pragma unroll 1
+    for (int j = 0; j < 7; j++) {
+        const int c = __popcll(bits[j]);
+        if (i < c) return 64 * j + kth_bit64(bits[j], i);
+        i -= c;
+    }
+    return 408;
+}
+// the legal-action set of a run into LDS bits[7]. Wave-collective.
+__device__ __forceinline__ void run_bits(const Pools &P, const NodeRun &r, uint64_t *bits) {
+    const int l = lane_id();
+    if (l < 7) bits[l] = 0;
+    wave_lds_fence();
+    for (int i = l; i < r.ec; i += 64) {
+        const int a = P.ep(r.eb + i)->a;
+        atomicOr(reinterpret_cast<unsigned long long *>(bits + (a >> 6)), 1ull << (a & 63));
+    }
+    wave_lds_fence();
+}
+
+// A run written sorted by (prior descending, action ascending) from the LDS list cp / ca /
+// cvi of its ec edges in ACTION order (cvi: visit record index, nullptr = none yet); visit
+// records get their edge's new rank and prior. Returns the lowest rank without a visit
+// record (ec: none). Wave-collective.
+__device__ int write_sorted_run(const Pools &P, int64_t eb, int64_t vb, int ec, const float *cp, const int16_t *ca,
+                                const int16_t *cvi) {
+    int cmin = ec;
+    for (int i = lane_id(); i < ec; i += 64) {
+        const float pi = cp[i];
+        int r = 0;
+        for (int j = 0; j < ec; j++) {
+            const float pj = cp[j];
+            r += (pj > pi) || (pj == pi && j < i);
+        }
+        const int vi = cvi ? cvi[i] : -1;
+        *P.ep(eb + r) = EdgeP{pi, ca[i], (int16_t)vi};
+        if (vi >= 0) {
+            VisitRec *R = P.vr(vb + REC_UNITS * vi);
+            R->p = pi;
+            R->off = (int16_t)r;
+        } else {
+            cmin = min(cmin, r);
+        }
+    }
+    return wave_min_i32(cmin);
+}
+
 // ------------------------------------------------------------ Dirichlet root noise
 // softmax(Ps, T0) (MCTS.py:245-250) -> applyDirNoise (:180-186) -> normalise (:239-242) on
 // the root's priors, for any number of legal actions. Types and orders as the oracle pins
@@ -323,29 +281,17 @@ __device__ __forceinline__ float wave_np_sum409(const float *a) {
 // The Dirichlet vector replaces the reference's unseeded Generator.dirichlet: det_gamma on
 // the Philox sequence (seed, board, stream), counters 4096*i for the i-th legal action,
 // normalised like numpy's dirichlet (sequential sum, times its reciprocal).
-// pr: LDS scratch of 416 floats for this wave; raw: pr already holds the network's priors
-// (a new root, :141-144), else the stored priors of an expanded root are used (:150-154).
-__device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int64_t eb, int ec, uint32_t stream,
-                                 float *pr, bool raw) {
+// pr: LDS, the priors by action (0 for illegal actions; 416 floats), replaced by the noised
+// ones; bits: the legal actions (LDS), ec of them. Wave-collective.
+__device__ void root_noise_lds(const SearchCfg &C, int t, uint32_t stream, float *pr, const uint64_t *bits, int ec) {
     const int l = lane_id();
-    const EdgePtr ede = P.ed + eb;
     const uint32_t gb = C.board_base + (uint32_t)t;
-    if (!raw) {
-        for (int a = l; a < 416; a += 64) pr[a] = 0.f;
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        for (int i = l; i < ec; i += 64) pr[ede[i].k.a] = ede[i].s.p;
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-    }
     if (C.dir_temp != 1.0) {
         const double e = 1.0 / C.dir_temp;
         const double s = wave_np_sum409_f64(pr, [e](float x) { return det_pow((double)x, e); });
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_fence();
         for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = (float)(det_pow((double)pr[a], e) / s);
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_fence();
     }
     // Dirichlet: gammas lane-parallel, their sum sequential in action order; the gammas
     // are drawn again for the mix (deterministic) instead of being kept in registers
@@ -365,18 +311,49 @@ __device__ void apply_root_noise(const Pools &P, const SearchCfg &C, int t, int6
     for (int j = 0; j < (ec + 63) / 64; j++) {
         const int i = 64 * j + l;
         if (i < ec) {
-            const int a = ede[i].k.a;
+            const int a = action_at(bits, i);
             const double d = ok ? det_gamma(C.dir_alpha, C.seed, gb, stream, (uint32_t)i * 4096u) * inv
                                 : 1.0 / (double)ec;
             pr[a] = (float)(0.75 * (double)pr[a] + 0.25 * d);
         }
     }
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_fence();
     const float nsum = wave_np_sum409(pr);
-    for (int i = l; i < ec; i += 64) ede[i].s.p = pr[ede[i].k.a] / nsum;
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
+    for (int a = l; a < SPL_ACTIONS; a += 64)
+        if ((bits[a >> 6] >> (a & 63)) & 1) pr[a] = pr[a] / nsum;
+    wave_lds_fence();
+}
+
+// LDS scratch of a wave that re-sorts or stages a run (root noise, move sampling)
+struct RunScr {
+    uint64_t bits[7];
+    float pr[416];                 // priors by action
+    float cp[SPL_ACTIONS];         // the run in action order: prior, action, visit record
+    int16_t ca[SPL_ACTIONS];
+    int16_t cvi[SPL_ACTIONS];
+};
+
+// root noise on an expanded root (MCTS.py:150-154, the stored priors): its run re-noised,
+// re-sorted, its visit records' priors and ranks updated; returns the new candidate rank.
+// Wave-collective.
+__device__ int noise_kept_root(const Pools &P, const SearchCfg &C, int t, const NodeRun &r, uint32_t stream,
+                               RunScr &S) {
+    const int l = lane_id();
+    run_bits(P, r, S.bits);
+    for (int a = l; a < 416; a += 64) S.pr[a] = 0.f;
+    wave_lds_fence();
+    for (int i = l; i < r.ec; i += 64) {
+        const EdgeP e = *P.ep(r.eb + i);
+        S.pr[e.a] = e.p;
+        const int k = order_of(S.bits, e.a);
+        S.ca[k] = e.a;
+        S.cvi[k] = e.vi;
+    }
+    wave_lds_fence();
+    root_noise_lds(C, t, stream, S.pr, S.bits, r.ec);
+    for (int k = l; k < r.ec; k += 64) S.cp[k] = S.pr[S.ca[k]];
+    wave_lds_fence();
+    return write_sorted_run(P, r.eb, r.vb, r.ec, S.cp, S.ca, S.cvi);
 }
 
 // ------------------------------------------------------------ page allocation
@@ -407,25 +384,25 @@ __device__ int node_slot(const Pools &P, TreeHdr *H, int t, int id) {
     return tab[pi] * NPG + (id & (NPG - 1));
 }
 
-// a CSR run of ec edges for a new node (global base), from the tree's current edge page or a
-// fresh one (runs never straddle pages); -1 when the tree's edge pages are at their maximum
-// or the pool is empty. One lane.
-__device__ int64_t edge_run(const Pools &P, TreeHdr *H, int t, int ec) {
-    if (H->eleft < ec) {
+// n contiguous edge units for tree t (a run or a visit block: global base), from the tree's
+// current edge page or a fresh one (allocations never straddle pages); -1 when the tree's
+// edge pages are at their maximum or the pool is empty. One lane.
+__device__ int64_t unit_alloc(const Pools &P, TreeHdr *H, int t, int n) {
+    if (H->eleft < n) {
         if (H->epg >= P.eptab) return -1;
         const int pg = pop_page(P.efree, P.alloc + 1);
         if (pg < 0) { atomicAdd(P.alloc + 3, 1); return -1; }
         P.etab[(size_t)t * P.eptab + H->epg] = pg;
         P.epidx[pg] = H->epg;
         H->epg += 1;
-        H->enext = (int64_t)pg * EPG;
-        H->eleft = EPG;
+        H->enext = (int64_t)pg * UPG;
+        H->eleft = UPG;
     }
-    const int64_t eb = H->enext;
-    H->enext = eb + ec;
-    H->eleft -= ec;
-    H->edge_count += ec;
-    return eb;
+    const int64_t b = H->enext;
+    H->enext = b + n;
+    H->eleft -= n;
+    H->edge_count += n;
+    return b;
 }
 
 // push n page ids (src[0..n)) back to a free stack, wave-collective
@@ -442,85 +419,95 @@ __device__ __forceinline__ void push_pages(int32_t *stack, int32_t *top, int cap
 // Keep the root and every node whose round counter exceeds the root's: rounds strictly
 // increase along every move (SplendorLogicNumba.py:287), so no other node is reachable from
 // this root or any later one — an exact subset of the reference's table (which only
-// evicts rounds < R-5, MCTS.py:80-85). Compacts the tree's nodes and CSR edges in place (in
-// its own page order), remaps child links and their cached ranges, rebuilds the
-// transposition table and returns the pages it no longer needs to the pools.
+// evicts rounds < R-5, MCTS.py:80-85). Compacts the tree's nodes (in place, in its own page
+// order) and their edge units (each kept node's run followed by its visit records, staged
+// through a scratch buffer: runs and visit blocks were allocated in different orders),
+// remaps child links, rebuilds the transposition table and returns the pages it no longer
+// needs to the pools.
 // linked = true (capacity pressure, see begin_search): keep only the root and the nodes
 // reachable from it through child links, dropping nodes that only a transposition lookup
-// could reach. Wave-collective; runs in k_gc (one wave per tree) with a scratch area of
-// gc_ints(nmax) ints.
+// could reach. Runs in k_gc (one workgroup per tree) with a scratch area of gc_ints ints.
 struct GcScr {
+    int64_t *ost;       // new local -> its old run base (global unit)
+    int64_t *ovb;       // new local -> its old visit block base
+    uint64_t *buf;      // new unit position -> the unit's value (staging)
     int32_t *remap;     // old local -> new local (-1: dropped); prune: reachability marks first
-    int32_t *nvs;       // old local -> new local edge position of its CSR run
-    int32_t *cs;        // new local -> new edge position
-    int32_t *cnt;       // new local -> edge count
+    int32_t *nvs;       // old local -> new local unit position of its allocation
+    int32_t *cs;        // new local -> new unit position
+    int32_t *cnt;       // new local -> units
     int32_t *inv;       // new local -> old local
-    int32_t *queue;     // prune: breadth-first queue (old locals)
-    int32_t *own;       // new edge position -> new local of its node (-1: page-end gap)
-    int64_t *ost;       // new local -> old global edge base
+    int32_t *queue;     // prune: breadth-first queue (old locals); then the cached links
+    int32_t *oec;       // new local -> its run length (edges)
+    int32_t *own;       // new unit position -> new local of its node (-1: page-end gap)
 };
-__host__ __device__ inline size_t gc_ints(int nmax, int emax) { return 8 * (size_t)(nmax + 2) + (size_t)emax + 64; }
-__device__ __forceinline__ GcScr gc_scr(int32_t *base, int nmax) {
-    const size_t m = (size_t)nmax + 2;
+__host__ __device__ inline size_t gc_ints(int nmax, int emax) {
+    return 11 * (size_t)(nmax + 2) + 3 * (size_t)emax + 64;
+}
+__device__ __forceinline__ GcScr gc_scr(int32_t *base, int nmax, int emax) {
+    const size_t m = (size_t)nmax + 2;                       // (even: nmax is a multiple of 64)
     GcScr S;
-    S.ost = reinterpret_cast<int64_t *>(base);                 // 2m ints, 8-byte aligned
-    S.remap = base + 2 * m; S.nvs = S.remap + m; S.cs = S.nvs + m; S.cnt = S.cs + m;
-    S.inv = S.cnt + m; S.queue = S.inv + m; S.own = S.queue + m;
+    S.ost = reinterpret_cast<int64_t *>(base);
+    S.ovb = reinterpret_cast<int64_t *>(base + 2 * m);
+    S.buf = reinterpret_cast<uint64_t *>(base + 4 * m);
+    int32_t *q = base + 4 * m + 2 * (size_t)emax;
+    S.remap = q; S.nvs = q + m; S.cs = q + 2 * m; S.cnt = q + 3 * m;
+    S.inv = q + 4 * m; S.queue = q + 5 * m; S.oec = q + 6 * m; S.own = q + 7 * m;
     return S;
 }
 
 // mark[i] = 1 for the root (local rootl) and every node reachable from it through child
-// links, 0 else (breadth-first in batches of up to 64 queued nodes, their edges 64 at a time)
+// links, 0 else (breadth-first in batches of up to 64 queued nodes, their visit records —
+// the only linked edges — 64 at a time)
 __device__ void mark_linked(const Pools &P, int t, int rootl, int32_t *mark, int32_t *q) {
     const int l = lane_id();
     const int nc = P.hdr[t].node_count;
     for (int i = l; i < nc; i += 64) mark[i] = i == rootl ? 1 : 0;
     if (l == 0) q[0] = rootl;
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_fence();
     int head = 0, tail = 1;
     while (head < tail) {
         const int nbt = min(64, tail - head);
-        int64_t eb = 0;
-        int ec = 0;
+        int64_t vb = 0;
+        int cnt = 0;
         if (l < nbt) {
             const int g = node_g(P, t, q[head + l]);
-            eb = P.neb[g];
-            ec = P.nterm[g] ? 0 : P.nec[g];
+            if (!P.nterm[g]) {
+                const NodeRun r = P.nrun[g];
+                vb = r.vb;
+                cnt = r.vcnt;
+            }
         }
         head += nbt;
-        int incl = ec;
+        int incl = cnt;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int y = __shfl_up(incl, o, 64);
             if (l >= o) incl += y;
         }
-        const int tot = __shfl(incl, 63, 64), excl = incl - ec;
+        const int tot = __shfl(incl, 63, 64), excl = incl - cnt;
         for (int c0 = 0; c0 < tot; c0 += 64) {
             const int e = c0 + l;
             int lo = 0;                                  // last lane with excl <= e
 #pragma unroll
             for (int step = 32; step > 0; step >>= 1)
                 if (__shfl(excl, lo + step, 64) <= e) lo += step;
-            const int64_t ebo = __shfl(eb, lo, 64);
+            const int64_t vbo = __shfl(vb, lo, 64);
             const int exo = __shfl(excl, lo, 64);
-            const int c = e < tot ? P.ed[ebo + (e - exo)].k.child : -1;
+            const int c = e < tot ? P.vr(vbo + REC_UNITS * (e - exo))->child : -1;
             const int cl = c >= 0 ? node_l(P, c) : -1;
             const bool fresh = cl >= 0 && atomicCAS(&mark[cl], 0, 1) == 0;
             const uint64_t bm = __ballot(fresh);
             if (fresh) q[tail + __popcll(bm & lanemask_lt())] = cl;
             tail += __popcll(bm);
-            __threadfence_block();
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_fence();
         }
     }
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 struct defeats SROA)
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // k_gc collects one tree per workgroup of GCT threads (block-wide scans through LDS), so a
-// large tree's collection (config 4: ~40 K nodes, ~1 M edges) is spread over 8 waves
+// large tree's collection (config 4: ~40 K nodes, ~0.5 M edge units) is spread over 8 waves
 constexpr int GCT = 512, GCW8 = GCT / 64;
 struct GcLds {
     int32_t wsum[GCW8];
@@ -560,7 +547,7 @@ __device__ __forceinline__ int block_min(int x, GcLds &L) {
     return m;
 }
 
-template <int CR = 4>   // edges per thread per round trip of the edge move (boards: 2 CR units)
+template <int CR = 4>   // board units per thread per round trip of the node-board move (x2)
 __device__ int compact_tree(const Pools &P, int t, int root, int root_round, const GcScr &S, GcLds &L,
                             int bunits, bool linked = false) {
     const int tid = threadIdx.x;
@@ -583,26 +570,28 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         kept += tot;
     }
     __syncthreads();
-    // new edge position of every kept node's CSR run: packed in local order, a run that would
-    // straddle an edge page starts the next page (the nodes before the first straddler of a
-    // chunk are placed, the rest retried from that page's start). Positions never exceed the
-    // old ones, so the in-place moves below read every record before it is overwritten.
+    // new unit position of every kept node's allocation (run + visit records): packed in local
+    // order, an allocation that would straddle an edge page starts the next page (the nodes
+    // before the first straddler of a chunk are placed, the rest retried from that page's start)
     int run = 0;
     for (int base = 0; base < nc; base += GCT) {
         const int i = base + tid;
-        int ec = 0;
+        int sz = 0;
         if (i < nc && remap[i] >= 0) {
             const int g = node_g(P, t, i);
-            ec = P.nterm[g] ? 0 : P.nec[g];
+            if (!P.nterm[g]) {
+                const NodeRun r = P.nrun[g];
+                sz = r.ec + REC_UNITS * r.vcnt;
+            }
         }
-        bool pending = ec > 0;
+        bool pending = sz > 0;
         int start = run;
         for (;;) {
-            const int x = pending ? ec : 0;
+            const int x = pending ? sz : 0;
             int tot;
             const int ex = block_scan(x, tot, L);
             const int st = run + ex;
-            const bool strad = pending && (st & (EPG - 1)) + ec > EPG;
+            const bool strad = pending && (st & (UPG - 1)) + sz > UPG;
             const int f = block_min(strad ? tid : GCT, L);
             if (f == GCT) {
                 if (pending) start = st;
@@ -610,7 +599,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                 break;
             }
             if (pending && tid < f) { start = st; pending = false; }
-            if (tid == f) L.bc[0] = (st & ~(EPG - 1)) + EPG;
+            if (tid == f) L.bc[0] = (st & ~(UPG - 1)) + UPG;
             __syncthreads();
             run = L.bc[0];
             __syncthreads();
@@ -619,52 +608,52 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     }
     __syncthreads();
     // node records, chunk by chunk in local order (new slot <= old slot): reads, then writes
-    int my_edges = 0;
+    int my_units = 0;
     for (int base = 0; base < nc; base += GCT) {
         const int i = base + tid;
         const int ni = i < nc ? remap[i] : -1;
         uint64_t k0 = 0, k1 = 0;
-        int64_t oeb = 0;
-        int ec = 0, rd = 0, vs = 0;
-        NodeStat nst{0.0, 0, -1, 0, -1, 0, 0, 0};
+        NodeRun nr{0, 0, 0, 0, 0, 0};
+        NodeStat nst{0.0, 0, -1, 0, -1, 0, 0};
+        int rd = 0, vs = 0;
         int8_t term = 0;
-        float es[4] = {0, 0, 0, 0};
         if (ni >= 0) {
             const int g = node_g(P, t, i);
             k0 = P.nkey0[g]; k1 = P.nkey1[g];
-            oeb = P.neb[g]; ec = P.nec[g]; nst = P.nst[g]; rd = P.nround[g];
+            nr = P.nrun[g]; nst = P.nst[g]; rd = P.nround[g];
             term = P.nterm[g];
-#pragma unroll
-            for (int j = 0; j < 4; j++) es[j] = P.nes[(size_t)g * 4 + j];
             vs = S.nvs[i];
         }
         __syncthreads();
         if (ni >= 0) {
             const int ng = node_g(P, t, ni);
-            const int run_ec = term ? 0 : ec;
+            const int sz = term ? 0 : nr.ec + REC_UNITS * nr.vcnt;
+            NodeRun w = nr;                              // (a terminal node's values as they are)
+            if (!term) {
+                w.eb = nr.ec > 0 ? unit_g(P, t, vs) : 0;
+                w.vb = nr.vcnt > 0 ? unit_g(P, t, vs + nr.ec) : 0;
+                w.vcap = nr.vcnt;
+            }
             P.nkey0[ng] = k0; P.nkey1[ng] = k1;
-            P.neb[ng] = run_ec > 0 ? edge_g(P, t, vs) : 0; P.nec[ng] = ec; P.nround[ng] = rd;
+            P.nrun[ng] = w; P.nround[ng] = rd;
             P.nst[ng] = nst; P.nterm[ng] = term;
-            S.queue[ni] = nst.bchild;                    // (the arg-max's link, remapped below)
-#pragma unroll
-            for (int j = 0; j < 4; j++) P.nes[(size_t)ng * 4 + j] = es[j];
-            S.cs[ni] = vs; S.cnt[ni] = run_ec; S.inv[ni] = i; S.ost[ni] = oeb;
-            my_edges += run_ec;
+            S.queue[ni] = term ? -1 : nst.bchild;        // (the arg-max's link, remapped below)
+            S.cs[ni] = vs; S.cnt[ni] = sz; S.inv[ni] = i;
+            S.ost[ni] = nr.eb; S.ovb[ni] = nr.vb; S.oec[ni] = term ? 0 : nr.ec;
+            my_units += sz;
         }
     }
-    int edges;
-    (void)block_scan(my_edges, edges, L);
-    // the cached arg-max's link (NodeStat) remapped like the edges' links below
+    int units;
+    (void)block_scan(my_units, units, L);
+    // the cached arg-max's link (NodeStat) remapped like the visit records' links below
     for (int ni = tid; ni < kept; ni += GCT) {
         const int ch = S.queue[ni];
         if (ch >= 0) {
             const int nl = remap[node_l(P, ch)];
-            NodeStat *ns = P.nst + node_g(P, t, ni);
-            ns->bchild = nl >= 0 ? node_g(P, t, nl) : -1;
-            if (nl >= 0) ns->bceb = S.cnt[nl] > 0 ? edge_g(P, t, S.cs[nl]) : 0;
+            P.nst[node_g(P, t, ni)].bchild = nl >= 0 ? node_g(P, t, nl) : -1;
         }
     }
-    // the owner of every new edge position (gaps before a page start: -1)
+    // the owner of every new unit position (gaps before a page start: -1)
     for (int k = tid; k < run; k += GCT) S.own[k] = -1;
     __syncthreads();
     for (int ni = tid; ni < kept; ni += GCT) {
@@ -672,63 +661,41 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         for (int e = 0; e < c; e++) S.own[c0 + e] = ni;
     }
     __syncthreads();
-    {
-        // edge records by new position k, batches of GCT x CR in increasing k (all reads
-        // before the writes); child links and their cached ranges remapped
-        // (EdgePool layout: per page 1,024 16-byte statistics, then 1,024 8-byte links)
-        u32x4 *const e4 = reinterpret_cast<u32x4 *>(P.ed.base);
-        u32x2 *const e2 = reinterpret_cast<u32x2 *>(P.ed.base);
-        constexpr int64_t PU = EdgePtr::PAGE_BYTES / 16, LU = EdgePtr::PAGE_BYTES / 8;
-        const auto su = [&](int64_t i) { return (i >> EPG_SHIFT) * PU + (i & (EPG - 1)); };
-        const auto lu = [&](int64_t i) { return (i >> EPG_SHIFT) * LU + 2 * EPG + (i & (EPG - 1)); };
-        for (int k0 = 0; k0 < run; k0 += GCT * CR) {
-            u32x4 es_[CR];
-            u32x2 ek_[CR];
-            int nch[CR];
-            bool own[CR];
-#pragma unroll
-            for (int r = 0; r < CR; r++) {
-                const int k = k0 + GCT * r + tid;
-                const int j = k < run ? S.own[k] : -1;
-                own[r] = j >= 0;
-                es_[r] = u32x4{0, 0, 0, 0}; ek_[r] = u32x2{0, 0xFFFFFFFFu};
-                if (j >= 0) {
-                    const int64_t src = S.ost[j] + (k - S.cs[j]);
-                    es_[r] = e4[su(src)];
-                    ek_[r] = e2[lu(src)];
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < CR; r++) {
-                nch[r] = -1;
-                const int ch = (int)ek_[r].y;
-                if (own[r] && ch >= 0) {
+    // units staged by new position (a run's EdgeP units verbatim, visit records with their
+    // links remapped), then written back; every thread writes back exactly the positions it
+    // staged, so only the workgroup barrier between the two passes is needed
+    for (int k = tid; k < run; k += GCT) {
+        const int j = S.own[k];
+        if (j < 0) continue;
+        const int rel = k - S.cs[j], ec = S.oec[j];
+        uint64_t v;
+        if (rel < ec) {
+            v = P.eu[S.ost[j] + rel];
+        } else {
+            const int rr = rel - ec;
+            v = P.eu[S.ovb[j] + rr];
+            if (rr % REC_UNITS == 1) {                   // {n, child}: the link remapped
+                const int ch = (int)(v >> 32);
+                int nch = -1;
+                if (ch >= 0) {
                     const int nl = remap[node_l(P, ch)];
-                    if (nl >= 0) nch[r] = node_g(P, t, nl);
+                    if (nl >= 0) nch = node_g(P, t, nl);
                 }
+                v = (v & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)nch << 32);
             }
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < CR; r++) {
-                const int k = k0 + GCT * r + tid;
-                if (own[r]) {
-                    u32x2 o = ek_[r];
-                    o.y = (uint32_t)nch[r];
-                    const int64_t dst = edge_g(P, t, k);
-                    e4[su(dst)] = es_[r];
-                    e2[lu(dst)] = o;
-                }
-            }
-            __syncthreads();
         }
+        S.buf[k] = v;
     }
+    __syncthreads();
+    for (int k = tid; k < run; k += GCT)
+        if (S.own[k] >= 0) P.eu[unit_g(P, t, k)] = S.buf[k];
     if (P.nbrd) {
         // node boards (bunits 16-byte units each) of new slot nn come from old slot inv[nn]
         // (>= nn), batches in increasing unit with all reads before the writes
         u32x4 *bb = reinterpret_cast<u32x4 *>(P.nbrd);
-        const int units = kept * bunits;
+        const int bu = kept * bunits;
         constexpr int R = 2 * CR;
-        for (int k0 = 0; k0 < units; k0 += GCT * R) {
+        for (int k0 = 0; k0 < bu; k0 += GCT * R) {
             u32x4 d[R];
             size_t dst[R];
             bool mv[R];
@@ -736,7 +703,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
             for (int r = 0; r < R; r++) {
                 const int k = k0 + GCT * r + tid;
                 mv[r] = false; dst[r] = 0; d[r] = u32x4{0, 0, 0, 0};
-                if (k < units) {
+                if (k < bu) {
                     const int nn = k / bunits, u = k - nn * bunits, on = S.inv[nn];
                     if (on != nn) {
                         mv[r] = true;
@@ -763,31 +730,32 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         while (atomicCAS(&hs[h], -1, g) != -1) h = (h + 1) & (uint32_t)(P.hcap - 1);
     }
     // pages past the compacted tree go back to the pools
-    const int npg = (kept + NPG - 1) >> NPG_SHIFT, epg = (run + EPG - 1) >> EPG_SHIFT;
+    const int npg = (kept + NPG - 1) >> NPG_SHIFT, epg = (run + UPG - 1) >> UPG_SHIFT;
     const int onpg = H->npg, oepg = H->epg;
     const int nroot = rootl >= 0 && remap[rootl] >= 0 ? node_g(P, t, remap[rootl]) : -1;
-    const int eleft = epg * EPG - run;
-    const int64_t enext = eleft > 0 ? edge_g(P, t, run) : 0;
+    const int eleft = epg * UPG - run;
+    const int64_t enext = eleft > 0 ? unit_g(P, t, run) : 0;
     __syncthreads();
     if (tid < 64) {
         push_pages(P.nfree, P.alloc + 0, P.npages, P.ntab + (size_t)t * P.nptab + npg, onpg - npg);
         push_pages(P.efree, P.alloc + 1, P.epages, P.etab + (size_t)t * P.eptab + epg, oepg - epg);
     }
     if (tid == 0) {
-        H->node_count = kept; H->edge_count = edges;
+        H->node_count = kept; H->edge_count = units;
         H->npg = npg; H->epg = epg; H->eleft = eleft; H->enext = enext;
-        H->live_gc = kept; H->gcs += 1;
+        H->live_gc = kept; H->units_gc = units; H->gcs += 1;
     }
     __syncthreads();
     return nroot;
 }
 
-// does the next search fit tree t's maxima (budget nodes; 409 root edges plus edge_reserve
-// per simulation, in edge positions counting the tail of the current page)
+// edge units of tree t in use (counting the unused tail of its current page)
+__device__ __forceinline__ long long units_used(const TreeHdr *H) { return (long long)H->epg * UPG - H->eleft; }
+// does the next search fit tree t's maxima (budget nodes; a root's run and visit block plus
+// edge_reserve units per simulation)
 __device__ __forceinline__ bool tree_fits(const Pools &P, const SearchCfg &C, const TreeHdr *H) {
-    const long long used = (long long)H->epg * EPG - H->eleft;
     return H->node_count + H->budget + 1 <= P.nmax &&
-           used + SPL_ACTIONS + (long long)H->budget * C.edge_reserve <= (long long)P.eptab * EPG;
+           units_used(H) + 4 * SPL_ACTIONS + (long long)H->budget * C.edge_reserve <= (long long)P.eptab * UPG;
 }
 // every page of tree t back to the pools, empty table. Wave-collective.
 __device__ void empty_tree(const Pools &P, int t) {
@@ -801,7 +769,7 @@ __device__ void empty_tree(const Pools &P, int t) {
     __builtin_amdgcn_wave_barrier();
     if (lane_id() == 0) {
         H->node_count = 0; H->edge_count = 0; H->npg = 0; H->epg = 0; H->eleft = 0; H->enext = 0;
-        H->live_gc = 0;
+        H->live_gc = 0; H->units_gc = 0;
     }
     __builtin_amdgcn_wave_barrier();
 }
@@ -818,16 +786,17 @@ __device__ __forceinline__ void gc_push(const Pools &P, TreeHdr *H, int t) {
 // Re-root tree t at the canonical board staged in LDS `s` (MCTS.getActionProb entry,
 // :45-56): look the root up in the persistent table (keep) or start empty; draw the
 // full/fast search decision (ST_FULL) and arm root noise. Wave-collective.
-// Garbage (nodes with rounds <= the root's: unreachable, and no lookup can match them) is
-// collected by k_gc, queued here:
+// Garbage (nodes with rounds <= the root's: unreachable, and no lookup can match them; runs
+// and visit blocks of collected nodes, outgrown visit blocks) is collected by k_gc, queued
+// here:
 //   must (gc_state 3): the search would not fit the tree's maxima (node slots, edge page
 //     table), or the arena has no self-play commit (search-only arenas never withdraw a
 //     simulation, so every search starts compacted); after compaction k_gc prunes the tree
 //     to the nodes linked from the root (prunes++) and empties it if that is still too
 //     large (resets++);
-//   should (gc_state 5): a tree whose garbage exceeds alpha x its live size, alpha from 4
-//     (pools at most half full) down to 1/8 as they fill; k_gc may defer these
-//     (GC_SHOULD_CAP per launch).
+//   should (gc_state 5): a tree whose garbage (nodes or edge units) exceeds alpha x its live
+//     size, alpha from 4 (pools at most half full) down to 1/8 as they fill; k_gc may defer
+//     these (GC_SHOULD_CAP per launch).
 // Without an event the kept table is exactly the reference's reachable table.
 template <int N>
 __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const int8_t *s, bool keep,
@@ -846,28 +815,25 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         wave_fingerprint<N>(s, k0, k1);
         root = hash_lookup(P, t, k0, k1);
         const int nc = H->node_count;
-        const long long used = (long long)H->epg * EPG - H->eleft;
+        const long long used = units_used(H);
         const bool must = nc + budget + 1 > P.nmax ||
-                          used + SPL_ACTIONS + (long long)budget * C.edge_reserve > (long long)P.eptab * EPG;
+                          used + 4 * SPL_ACTIONS + (long long)budget * C.edge_reserve > (long long)P.eptab * UPG;
         // garbage allowance alpha x the live size (at the last collection): a collection
         // copies the live tree to free its garbage, so a large alpha is cheap per freed node;
         // it shrinks as the shared pools fill (free share f: alpha = 4 down to 1/8)
         const float f = fminf((float)P.alloc[0] / (float)P.npages, (float)P.alloc[1] / (float)P.epages);
         const float alpha = f >= 0.5f ? 4.f : fmaxf(0.125f, 8.f * f);
-        const bool should = nc > (int)((1.f + alpha) * (float)H->live_gc) + budget + NPG;
+        const bool should = nc > (int)((1.f + alpha) * (float)H->live_gc) + budget + NPG ||
+                            used > (long long)((1.f + alpha) * (float)H->units_gc) +
+                                       (long long)budget * C.edge_reserve + UPG;
         gcs = must || !C.selfplay ? 3 : (should ? 5 : 0);   // search-only arenas: every search
                                                            // starts compacted (no withdrawals there)
     } else {
         empty_tree(P, t);
     }
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
-    const int64_t reb = root >= 0 ? P.neb[root] : 0;
-    const int rec = root >= 0 ? P.nec[root] : 0;
+    wave_lds_fence();
     if (l == 0) {
         H->root = root;                                  // (a queued GC moves it)
-        H->root_eb = reb;
-        H->root_ec = rec;
         H->sims_done = 0;
         H->full = full;
         H->budget = budget;
@@ -878,40 +844,52 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         H->gc_state = gcs;
         H->root_round = rr;
         H->move_no = mv + 1;
+        H->depth = 0;                                    // (a new search: no path reuse)
         if (gcs) gc_push(P, H, t);
     }
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_fence();
 }
 
 // Garbage collection queued by k_backup (a leaf did not fit mid-search: gc_state 1) and by
 // search starts (3 must, 5 should), one workgroup of GCT threads per queued tree, GC_WG
 // workgroups sharing the queue (a workgroup's scratch: gc_stride ints of P.gscr). Exactly
 // begin_search's policy: compact (rounds > the root's), prune to the linked nodes, empty.
-// Queued trees come in bursts (games start together, so trees fill up together): entries
-// past GC_SHOULD_CAP that only "should" be collected are skipped this time (their search
-// fits; the next search start queues them again), so no launch carries a whole burst.
+// Queued trees come in bursts (games start together and commit together, so trees fill up
+// together): "should" collections beyond GC_SHOULD_CAP per launch stay queued for the next
+// launches (k_gc runs behind every self-play backup and commit), so the burst of a commit
+// iteration is spread over the following iterations. That is exact: a deferred tree searches
+// on as it is (its search fits), and if a leaf finds no room meanwhile the simulation is
+// withdrawn (gc_state 5 -> 1) and the tree collected in the next launch.
 constexpr int GC_WG = 256;      // one per CU
 #ifndef GC_SHOULD_CAP
-#define GC_SHOULD_CAP 256
+#define GC_SHOULD_CAP 16
 #endif
 template <int N>
 __global__ __launch_bounds__(GCT) void k_gc(Pools P, SearchCfg C) {
     __shared__ GcLds L;
+    __shared__ int keep_s;
     const int tid = threadIdx.x;
     const int tail = P.counters[2];                      // no pushes while k_gc runs
     const int ftail = P.counters[5];
     if (tail == 0 && ftail == 0) return;                 // (the usual case)
-    const GcScr S = gc_scr(P.gscr + (size_t)blockIdx.x * P.gc_stride, P.nmax);
+    const GcScr S = gc_scr(P.gscr + (size_t)blockIdx.x * P.gc_stride, P.nmax, P.emax);
     for (int k = blockIdx.x; k < tail; k += gridDim.x) {     // garbage collection
         const int t = P.gcq[k];
         TreeHdr *H = P.hdr + t;
         const int st = H->gc_state;
+        if (tid == 0) {
+            int keep = 0;
+            if (st == 5 && atomicAdd(&P.counters[8], 1) >= GC_SHOULD_CAP) {
+                keep = 1;                                // deferred: stays queued
+                P.gcq2[atomicAdd(&P.counters[9], 1)] = t;
+            }
+            keep_s = keep;
+        }
+        __syncthreads();
+        if (keep_s) continue;
         int root = H->root;
         const int nst = st == 1 ? 2 : 0;
-        if (st == 5 && k >= GC_SHOULD_CAP) {
-            // deferred (its search fits as it is)
-        } else if (st == 1) {                            // the descent then repeats
+        if (st == 1) {                                   // the descent then repeats
             root = compact_tree<4>(P, t, root, P.nround[root], S, L, NodeBoard<N>::UNITS);
         } else if (st == 3 || st == 5) {
             const int rr = H->root_round;
@@ -928,19 +906,17 @@ __global__ __launch_bounds__(GCT) void k_gc(Pools P, SearchCfg C) {
             }
         }
         __syncthreads();
-        const int64_t reb = root >= 0 ? P.neb[root] : 0;
-        const int rec = root >= 0 ? P.nec[root] : 0;
         if (tid == 0) {
-            H->root = root;
-            H->root_eb = reb;
-            H->root_ec = rec;
-            H->gc_state = nst;                           // (2: once per search)
             H->gc_queued = 0;
-            H->depth = 0;                                // (node ids moved: no path reuse)
+            if (st == 1 || st == 3 || st == 5) {
+                H->root = root;
+                H->gc_state = nst;                       // (2: once per search)
+                H->depth = 0;                            // (node ids moved: no path reuse)
+            }
         }
         __syncthreads();
     }
-    // finished games' example rows (k_commit): the staging rows stay untouched until the
+// finished games' example rows (k_commit): the staging rows stay untouched until the
     // tree's next commit, a later iteration
     for (int k = blockIdx.x; k < ftail; k += gridDim.x) {
         const int2 e = P.flq[k];
@@ -952,10 +928,24 @@ __global__ __launch_bounds__(GCT) void k_gc(Pools P, SearchCfg C) {
         for (int i = tid; i < SPL_ACTIONS; i += GCT) dst[i] = src[i];
     }
     __syncthreads();
-    if (tid == 0 && atomicAdd(&P.counters[4], 1) == (int)gridDim.x - 1) {
-        P.counters[2] = 0;                               // the last workgroup out resets the queues
-        P.counters[5] = 0;
-        P.counters[4] = 0;
+    if (tid == 0) {
+        __threadfence();                                 // (deferred entries before the count)
+        keep_s = atomicAdd(&P.counters[4], 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (keep_s) {                                        // the last workgroup out: the deferred
+        __threadfence();                                 // entries become the queue
+        const int nk = __hip_atomic_load(&P.counters[9], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = tid; i < nk; i += GCT)
+            P.gcq[i] = __hip_atomic_load(&P.gcq2[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (tid == 0) {
+            P.counters[2] = nk;
+            P.counters[5] = 0;
+            P.counters[4] = 0;
+            P.counters[8] = 0;
+            P.counters[9] = 0;
+        }
     }
 }
 
@@ -1033,7 +1023,10 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     __shared__ __align__(16) int8_t lds[WAVES][2][Lx::LS];
     __shared__ double ub[WAVES][DEAL_DRAWS];
     __shared__ double pterm[WAVES][SPL_ACTIONS];         // random_pick's per-edge terms
-    __shared__ int16_t pact[WAVES][SPL_ACTIONS];
+    __shared__ int16_t pact[WAVES][SPL_ACTIONS];         // the root's edges in action order:
+    __shared__ int32_t pcnt[WAVES][SPL_ACTIONS];         // action, visit count, prior
+    __shared__ float pprior[WAVES][SPL_ACTIONS];
+    __shared__ uint64_t pbits[WAVES][7];
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
@@ -1042,13 +1035,24 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     // search is not done)
     if (H->gc_state == 1 || H->sims_done < H->budget || H->overflow || H->root < 0) return;
     const uint32_t gb = C.board_base + (uint32_t)t;
-    const int root = H->root, ec = P.nec[root];
+    const int root = H->root;
+    const NodeRun rr = P.nrun[root];
+    const int ec = rr.ec;
     const bool forced = H->forced;
     const int sims = H->budget, cm = H->move_no;
-    const EdgePtr ede = P.ed + P.neb[root];
+    // the root's edges staged in action order (the reference's array order, which the
+    // sequential sums of random_pick follow)
+    run_bits(P, rr, pbits[w]);
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, ede[i].s.n);
-    for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
+    for (int i = l; i < ec; i += 64) {
+        const EdgeP e = *P.ep(rr.eb + i);
+        const int n = e.vi >= 0 ? P.vr(rr.vb + REC_UNITS * e.vi)->n : 0;
+        const int k = order_of(pbits[w], e.a);
+        pact[w][k] = e.a; pcnt[w][k] = n; pprior[w][k] = e.p;
+        best = max(best, n);
+    }
+    best = wave_max_i32(best);
+    wave_lds_fence();
     // policy counts: pruned (MCTS.py:69-74); where the reference would divide 0/0
     // (Coach.py:83 raises) fall back to raw counts, then to uniform
     int mode = forced ? 0 : 1;
@@ -1056,11 +1060,11 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     for (; mode < 3; mode++) {
         tot = 0;
         for (int i = l; i < ec; i += 64)
-            tot += mode == 0 ? pruned_count(ede[i].s.n, best, true, ede[i].s.p, sims) : (mode == 1 ? ede[i].s.n : 1);
+            tot += mode == 0 ? pruned_count(pcnt[w][i], best, true, pprior[w][i], sims) : (mode == 1 ? pcnt[w][i] : 1);
         for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
         if (tot > 0) break;
     }
-#define POLICY_COUNT(i) (mode == 0 ? pruned_count(ede[i].s.n, best, true, ede[i].s.p, sims) : (mode == 1 ? (long long)ede[i].s.n : 1ll))
+#define POLICY_COUNT(i) (mode == 0 ? pruned_count(pcnt[w][i], best, true, pprior[w][i], sims) : (mode == 1 ? (long long)pcnt[w][i] : 1ll))
     const int step = H->episode_step + 1;
     const int player = H->player;
     int8_t *s = lds[w][0], *b = lds[w][1];
@@ -1075,7 +1079,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         for (int i = l; i < ec; i += 64)   // getSymmetries stores pi as float32 (SplendorGame.py:59-61)
-            pi[ede[i].k.a] = (float)((double)POLICY_COUNT(i) / (double)tot);
+            pi[pact[w][i]] = (float)((double)POLICY_COUNT(i) / (double)tot);
         uint64_t m[7];
         wave_valid_moves<N>(s, 0, lim, m);
         store_mask(P.ex_valid + x * 7, m);
@@ -1091,10 +1095,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     // (the per-edge terms lane-parallel into LDS, the order-dependent sums on lane 0)
     int action = 408;
     const double T = C.temp_threshold > 0 ? (step < C.temp_threshold ? 2.0 : 0.2) : 1.0;
-    for (int i = l; i < ec; i += 64) {
-        pterm[w][i] = temp_pow((double)POLICY_COUNT(i) / (double)tot, T);
-        pact[w][i] = ede[i].k.a;
-    }
+    for (int i = l; i < ec; i += 64) pterm[w][i] = temp_pow((double)POLICY_COUNT(i) / (double)tot, T);
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     if (l == 0) {
@@ -1220,6 +1221,20 @@ __global__ void k_drain_reset(Pools P, int max, int32_t *n_out) {
 }
 
 // ------------------------------------------------------------ select
+// a terminal node's end values (NodeRun of a terminal node: es[4] in its first 16 bytes)
+__device__ __forceinline__ void term_values(const Pools &P, int g, float v[4]) {
+    const NodeRun r = P.nrun[g];
+    v[0] = __int_as_float((int)(uint32_t)(uint64_t)r.eb); v[1] = __int_as_float((int)(uint32_t)((uint64_t)r.eb >> 32));
+    v[2] = __int_as_float((int)(uint32_t)(uint64_t)r.vb); v[3] = __int_as_float((int)(uint32_t)((uint64_t)r.vb >> 32));
+}
+__device__ __forceinline__ NodeRun term_run(const float v[4]) {
+    NodeRun r;
+    r.eb = (int64_t)(((uint64_t)(uint32_t)__float_as_int(v[1]) << 32) | (uint32_t)__float_as_int(v[0]));
+    r.vb = (int64_t)(((uint64_t)(uint32_t)__float_as_int(v[3]) << 32) | (uint32_t)__float_as_int(v[2]));
+    r.ec = 0; r.vcnt = 0; r.vcap = 0; r.cand = 0;
+    return r;
+}
+
 template <int N>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_WAVES))) void k_select(Pools P, SearchCfg C, int B, int lim,
                                                     int8_t *__restrict__ leaf_state,
@@ -1228,7 +1243,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                                                     int32_t *__restrict__ leaf_count) {
     using Lx = Lay<N>;
     __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
-    __shared__ __align__(16) float lpr[WAVES][416];         // root-noise scratch
+    __shared__ RunScr scr[WAVES];                           // root noise on a kept root
     // trees start in P.order (deep descents first: the launch ends with its deepest descent)
     const int w = uniform(threadIdx.x >> 6), slot = blockIdx.x * WAVES + w;
     if (slot >= B) return;
@@ -1251,29 +1266,30 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         spl_probe_last = clock64();
     }
 #endif
-    int32_t *path_n = P.path_n + (size_t)t * P.pcap;
-    int64_t *path_e = P.path_e + (size_t)t * P.pcap;
+    int32_t *path_n = P.path_n + (size_t)t * (P.pcap + 1);
     int32_t *path_x = P.path_x + (size_t)t * P.pcap;
     // the previous simulation's path, first 64 levels (lane per level), requested with the header
     int ppn = -1, ppx = 0;
-    int64_t ppe = 0;
-    if (l < P.pcap) { ppn = path_n[l]; ppx = path_x[l]; ppe = path_e[l]; }
+    if (l < P.pcap) { ppn = path_n[l]; ppx = path_x[l]; }
     SPL_PROBE(0)
     int node = H->root, depth = 0, kind = LEAF_NN;
     int miss = -1;                                       // the NN leaf's empty table slot
+    int leaf_node = -1;                                  // a terminal leaf's node
     uint64_t k0 = 0, k1 = 0;
     float val[4] = {0, 0, 0, 0};
     if (node < 0) {
         wave_fingerprint<N>(s, k0, k1);                  // the root itself is the leaf
     } else {
-        // CSR range of the current node: the root's from the header, every child's from the
-        // link cached with its parent's arg-max (NodeStat) or on the edge that led to it
-        int64_t eb = H->root_eb;
-        int ec = H->root_ec;
         const bool noised = sims == 0 && H->noise_pending;
-        if (noised) {
-            apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no, lpr[w], false);
-            if (l == 0) H->noise_pending = 0;           // (a withdrawn simulation must not re-noise)
+        if (noised) {                                    // the stored priors re-noised (:150-154)
+            const NodeRun r = P.nrun[node];
+            const int cand = noise_kept_root(P, C, t, r, ST_DIR | (uint32_t)H->move_no, scr[w]);
+            if (l == 0) {
+                H->noise_pending = 0;                    // (a withdrawn simulation must not re-noise)
+                P.nrun[node].cand = (int16_t)cand;
+                P.nst[node].best = -1;                   // ranks moved: the root scans
+            }
+            wave_lds_fence();
         }
         const bool forced = H->forced;
         // the root's cached arg-max holds unless its priors were just noised or forced
@@ -1284,13 +1300,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         // expand); `bnode` is the node whose board is in LDS (the root's, from root_state)
         const uint64_t *nbrd = reinterpret_cast<const uint64_t *>(P.nbrd);
         int bnode = node;
-        // pool bases and search constants of the hot loop, set up once
-        const EdgePool ed_t = P.ed;
         const NodeStat *nst_t = P.nst;
         const double cpuct = C.cpuct, fpu = C.fpu;
-        const float cf = (float)C.cpuct;
         int pend = -1, pend_n = 0, pend_x = 0;               // path entry not yet stored
-        int64_t pend_e = 0;
         // The previous simulation's path (this search's, same root; k_gc clears H->depth when
         // it moves nodes) is this descent's as far as its nodes' cached arg-maxes still pick
         // its edges: k_backup rewrote exactly those nodes' records, so one round trip for the
@@ -1298,29 +1310,25 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         // dependent loads. The descent resumes at level q = the first level whose node now
         // picks another edge (or the previous leaf's parent), with that node's record in hand.
         bool have = false;
-        NodeStat hq{0.0, 0, -1, 0, -1, 0, 0, 0};
+        NodeStat hq{0.0, 0, -1, 0, -1, 0, 0};
         {
             const int pd = min(H->depth, 64);
             const bool ok = sims > 0 && pd > 0 && __builtin_amdgcn_readfirstlane(ppn) == node;
             if (ok) {
-                NodeStat h{0.0, 0, -1, 0, -1, 0, 0, 0};
+                NodeStat h{0.0, 0, -1, 0, -1, 0, 0};
                 if (l < pd) h = nst_t[ppn];
                 const bool agree = l < pd && h.best == px_off(ppx) && (l > 0 || root_cache);
                 const uint64_t dis = ~__ballot(agree) & (pd < 64 ? (1ull << pd) - 1 : ~0ull);
                 const int p = dis ? __ffsll((unsigned long long)dis) - 1 : pd;
                 const int q = uniform(min(p, pd - 1));
-                const int xq = __builtin_amdgcn_readlane(ppx, q);
                 node = __builtin_amdgcn_readlane(ppn, q);
-                ec = px_count(xq);
-                eb = readlane64(ppe, q) - px_off(xq);
                 depth = q;
                 hq.qs = readlane_f64(h.qs, q);
                 hq.ns = __builtin_amdgcn_readlane(h.ns, q);
                 hq.best = (int16_t)__builtin_amdgcn_readlane((int)h.best, q);
                 hq.ba = (int16_t)__builtin_amdgcn_readlane((int)h.ba, q);
                 hq.bchild = __builtin_amdgcn_readlane(h.bchild, q);
-                hq.bcec = (int16_t)__builtin_amdgcn_readlane((int)h.bcec, q);
-                hq.bceb = readlane64(h.bceb, q);
+                hq.bterm = __builtin_amdgcn_readlane(h.bterm, q);
                 have = true;
                 if (!nbrd) {
                     // no node boards: the board of the resume node is the root's with the
@@ -1344,64 +1352,45 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
         }
         for (;;) {
             SPL_PROBE(1)
-            if (depth > 0 && ec < 0) {
-                kind = LEAF_TERMINAL;
-#pragma unroll
-                for (int i = 0; i < 4; i++) val[i] = P.nes[(size_t)node * 4 + i];
-                break;
-            }
             if (depth >= P.pcap) { kind = LEAF_NONE; if (l == 0) H->overflow = 2; break; }
-            // below the root a level is ONE 32-byte load: the node's statistics with its cached
-            // arg-max and that edge's link (NodeStat); the root's edges (first 64; lanes past
-            // the range read the first edge) are requested with its statistics
 #if SPL_BOUNDS_CHECK
-            {
-                const long long NN = (long long)P.npages * NPG, NE = (long long)P.epages * EPG;
-                BCHK(node >= 0 && node < NN, 20, node, t, node = 0);
-                BCHK(eb >= 0 && eb < NE && ec <= SPL_ACTIONS && (eb & (EPG - 1)) + ec <= EPG, 21, eb, t,
-                     (eb = 0, ec = 0));
-            }
+            BCHK(node >= 0 && node < (long long)P.npages * NPG, 20, node, t, node = 0);
 #endif
+            // a level is ONE 32-byte load: the node's statistics with its cached arg-max and
+            // that edge's link (NodeStat)
             NodeStat nsq = hq;
             if (!have) nsq = nst_t[node];
             have = false;
             const bool use_cache = depth > 0 || root_cache;
-            Edge e64{EdgeStat{0.f, 0, Q_UNSET}, EdgeLink{0, 0, -1}};
-            if (!use_cache) e64 = ed_t[eb + (l < ec ? l : 0)];
             // the previous level's path entry is stored behind this level's loads: vmcnt counts
             // stores too, in issue order, so a store issued first would delay the loads' wait
-            if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_e[pend] = pend_e; path_x[pend] = pend_x; }
+            if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_x[pend] = pend_x; }
             pend = -1;
             const int cbest = uniform(nsq.best);
             Pick pk;
             if (use_cache && cbest >= 0) {
-                pk = Pick{cbest, uniform(nsq.ba), uniform(nsq.bchild), uniform(nsq.bcec),
-                          (int64_t)uniform64((uint64_t)nsq.bceb)};
-            } else {
-                if (use_cache) e64 = ed_t[eb + (l < ec ? l : 0)];   // (no cached arg-max)
-                const int ns = nsq.ns;
-                const double qs = nsq.qs;
-                pk = ec <= 64 && !(forced && depth == 0)
-                         ? pick_edge64(e64, cpuct, fpu, cf, ec, ns, qs)
-                         : pick_edge_desc(P, C, eb, ec, ns, qs, forced && depth == 0, sims, e64);
-                if (pk.child >= 0) {                     // a scanned level: the child's range
-                    pk.ceb = (int64_t)uniform64((uint64_t)P.neb[pk.child]);
-                    pk.cec = uniform(P.nterm[pk.child] ? -1 : P.nec[pk.child]);
-                }
+                pk = Pick{cbest, uniform(nsq.ba), uniform(nsq.bchild), uniform(nsq.bterm)};
+            } else {                                     // the root scans (noise, forced playouts)
+                NodeRun r = P.nrun[node];
+                r.eb = (int64_t)uniform64((uint64_t)r.eb); r.vb = (int64_t)uniform64((uint64_t)r.vb);
+                r.ec = (int16_t)uniform(r.ec);
+                pk = scan_run(P, r, nsq.ns, nsq.qs, cpuct, fpu, forced && depth == 0, sims);
+                if (pk.child < 0 && pk.e == cbest && !noised) { pk.child = uniform(nsq.bchild); pk.cterm = uniform(nsq.bterm); }
+                else pk.cterm = pk.child >= 0 ? uniform((int)P.nterm[pk.child]) : 0;
             }
-            BCHK(pk.e >= 0 && pk.e < ec, 22, pk.e, t, pk.e = 0);
             BCHK(pk.child >= -1 && pk.child < (long long)P.npages * NPG, 23, pk.child, t, pk.child = -1);
-            const int64_t ge = eb + pk.e;
-            pend = depth; pend_n = node; pend_e = ge; pend_x = px_pack(pk.e, ec, pk.a);
+            pend = depth; pend_n = node; pend_x = px_pack(pk.e, pk.a);
             depth++;
             int child = uniform(pk.child);
-            int64_t ceb = pk.ceb;
-            int cec = uniform(pk.cec);
             SPL_PROBE(2)
+            if (child >= 0 && pk.cterm) {                    // a terminal child (MCTS.py:125-132)
+                kind = LEAF_TERMINAL;
+                term_values(P, child, val);
+                leaf_node = child;
+                break;
+            }
             if (child >= 0 && nbrd) {                        // linked: no transition needed
                 node = child;
-                eb = ceb;
-                ec = cec;
                 continue;
             }
             if (bnode != node) {                             // stage this node's stored board
@@ -1421,22 +1410,23 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             __builtin_amdgcn_wave_barrier();
             if (nxt) wave_roll_players<N>(s, s, nxt);
             SPL_PROBE(3)
-            // a link written here is copied into the node's cached arg-max when that is the edge
-            // (k_backup rewrites it anyway; this keeps it exact when the simulation is withdrawn)
-            const bool cached = uniform(nsq.best) == pk.e;
+            // a link found here is copied into the node's cached arg-max when that is the edge
+            // (k_backup links the edge's visit record; the copy keeps a withdrawn simulation's
+            // link for the next descent)
+            const bool cached = cbest == pk.e;
             if (child < 0) {
                 wave_fingerprint<N>(s, k0, k1);
                 k0 = uniform64(k0); k1 = uniform64(k1);
                 child = uniform(hash_lookup(P, t, k0, k1, &miss));
                 miss = uniform(miss);
-                if (child >= 0) {                            // transposition: link + cache
-                    ceb = P.neb[child];
-                    cec = P.nterm[child] ? -1 : P.nec[child];
-                    if (l == 0) {
-                        P.ed[ge].k.child = child;
-                        if (cached) {
-                            P.nst[node].bchild = child; P.nst[node].bcec = (int16_t)cec; P.nst[node].bceb = ceb;
-                        }
+                if (child >= 0) {                            // transposition
+                    const int ct = uniform((int)P.nterm[child]);
+                    if (l == 0 && cached) { P.nst[node].bchild = child; P.nst[node].bterm = ct; }
+                    if (ct) {
+                        kind = LEAF_TERMINAL;
+                        term_values(P, child, val);
+                        leaf_node = child;
+                        break;
                     }
                 }
             }
@@ -1444,8 +1434,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
             if (child >= 0) {
                 node = child;
                 bnode = child;
-                eb = ceb;
-                ec = cec;
                 continue;
             }
             float es[N];
@@ -1458,29 +1446,28 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
 #pragma unroll
                 for (int i = 0; i < N; i++) val[i] = es[i];
                 __builtin_amdgcn_wave_barrier();
+                int g = -1;
                 if (l == 0) {
                     const int id = H->node_count;
-                    const int g = node_slot(P, H, t, id);
+                    g = node_slot(P, H, t, id);
                     if (g < 0) {                             // no room: back up, do not store
                         H->unexpanded += 1;
                     } else {
-                        P.nkey0[g] = k0; P.nkey1[g] = k1; P.neb[g] = 0;
-                        P.nec[g] = 0;
-                        P.nst[g] = NodeStat{0.0, 0, -1, 0, -1, 0, 0, 0};
+                        P.nkey0[g] = k0; P.nkey1[g] = k1;
+                        P.nrun[g] = term_run(val);
+                        P.nst[g] = NodeStat{0.0, 0, -1, 0, -1, 0, 0};
                         P.nround[g] = (uint8_t)bt(row(s, 0), 6); P.nterm[g] = 1;
-#pragma unroll
-                        for (int i = 0; i < 4; i++) P.nes[(size_t)g * 4 + i] = i < N ? es[i < N ? i : 0] : 0.f;
                         hash_insert(P, t, k0, g);
-                        P.ed[ge].k.child = g;
-                        if (cached) { P.nst[node].bchild = g; P.nst[node].bcec = -1; P.nst[node].bceb = 0; }
+                        if (cached) { P.nst[node].bchild = g; P.nst[node].bterm = 1; }
                         H->node_count = id + 1;
                     }
                 }
+                leaf_node = __shfl(g, 0, 64);
                 break;
             }
             break;                                           // new NN leaf
         }
-        if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_e[pend] = pend_e; path_x[pend] = pend_x; }
+        if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_x[pend] = pend_x; }
     }
     __builtin_amdgcn_wave_barrier();
     SPL_PROBE(5)
@@ -1508,6 +1495,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
 #pragma unroll
         for (int i = 0; i < 4; i++) H->leaf_v[i] = val[i];
         leaf_valid[t] = kind == LEAF_NN;
+        path_n[depth] = kind == LEAF_TERMINAL ? leaf_node : -1;   // the leaf's node (k_backup links it)
     }
 #if MCTS_TIMING
     SPL_PROBE(7)
@@ -1635,73 +1623,119 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
 
 // k_backup: expansion of the NN leaf, the path backup (MCTS.py:169-176) and every path node's
 // cached arg-max (NodeStat), so the next descent through the node reads its pick instead of
-// scanning. Lane per level: each lane scans its node's edges (batches of BK_BATCH requested
-// together) in one pass of pick_edge_desc's float32 screen — the running maximum L of u - e
-// with its edge, and the largest u + e of every other edge; that is below L exactly when one
-// edge can hold the maximum, which is then the strict-'>' arg-max. Otherwise (ties, near
-// ties) the wave evaluates that level exactly in float64 (ucb_argmax_wide).
+// scanning. Lane per level. A level's arg-max needs only its visited edges (the visit block)
+// and its best unvisited edge (the run's candidate: MCTS.py:214 is monotone in P), plus the
+// next unvisited edge of a smaller prior so the float32 screen can rule out a float64
+// rounding tie: each lane screens its level's records (batches of BK_BATCH requested
+// together) in one pass — the running maximum L of u - e with its edge, and the largest u + e
+// of every other item; that is below L exactly when one edge can hold the maximum, which is
+// then the strict-'>' arg-max. Otherwise (ties, near ties) and for levels with more than
+// BK_WIDE records (roots) the wave evaluates the level exactly in float64.
 #ifndef BK_BATCH
-#define BK_BATCH 8
+#define BK_BATCH 2
 #endif
-#ifndef BK_PRELOAD
-#define BK_PRELOAD 0       // first batch of every level requested before the expansion
+#ifndef BK_WIDE
+#define BK_WIDE 12
 #endif
 #ifndef BACKUP_WAVES
 #define BACKUP_WAVES 5
 #endif
 
-// per-level view of a group of path levels after their update (lane j = level j)
-struct LevelV {
-    int64_t eb;       // CSR base of the level's node
-    int ec, off;      // its edge count, the offset of the edge taken
-    int nn, nns;      // the taken edge's and the node's new visit counts
-    double nq, nqs;   // their new values
-};
-
-// lane-serial screened arg-max of one node, one batch of edges at a time: the running
-// maximum L1 of u - e with its edge i1 and its u + e (H1), and the largest u + e of all other
-// edges (H2). One edge can hold the maximum exactly when H2 < L1.
 struct Screen {
     float L1, H1, H2, cf, ff, sqv, sqe;
-    int i1;
+    int off, a, child;        // the leading item: rank, action, link
 };
 __device__ __forceinline__ Screen screen_init(int ns, double qs, double cpuct, double fpu) {
     Screen S;
     S.cf = (float)cpuct;
-    S.ff = (float)(fpu > 0 ? qs - fpu : fpu);
+    S.ff = (float)fpu_base(fpu, qs);
     const float nf = (float)ns;
     S.sqv = __builtin_amdgcn_sqrtf(nf);
     S.sqe = __builtin_amdgcn_sqrtf(nf + 1e-8f);
     S.L1 = -INFINITY; S.H1 = -INFINITY; S.H2 = -INFINITY;
-    S.i1 = 0;
+    S.off = 0; S.a = 0; S.child = -1;
     return S;
 }
-// edges base .. base + BK_BATCH - 1 (those < ec) in es[]; the edge at `off` takes (on, oq)
-// (just written by this wave)
-__device__ __forceinline__ void screen_batch(Screen &S, const EdgeStat *es, int base, int ec, int off, int on,
-                                             double oq) {
-#pragma unroll
-    for (int j = 0; j < BK_BATCH; j++) {
-        const int i = base + j;
-        if (i < ec) {
-            EdgeStat st = es[j];
-            if (i == off) { st.n = on; st.q = oq; }
-            const bool vis = st.q != Q_UNSET;
-            const float rc = vis ? __builtin_amdgcn_rcpf(1.f + (float)st.n) : 1.f;
-            const float qf = vis ? (float)st.q : S.ff;
-            const float uf = qf + S.cf * st.p * (vis ? S.sqv : S.sqe) * rc;
-            const float er = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
-            const float lo = uf - er, hi = uf + er;
-            if (lo > S.L1) { S.H2 = fmaxf(S.H2, S.H1); S.L1 = lo; S.H1 = hi; S.i1 = i; }
-            else S.H2 = fmaxf(S.H2, hi);
-        }
+// one edge's float32 UCB estimate with its error bound (|estimate - the reference's float64
+// value| <= e = 2.1e-6 (|u| + |q|), tests/test_ucb_screen.py)
+__device__ __forceinline__ void screen_item(Screen &S, bool vis, float p, int n, double q, int off, int a, int child) {
+    const float rc = vis ? __builtin_amdgcn_rcpf(1.f + (float)n) : 1.f;
+    const float qf = vis ? (float)q : S.ff;
+    const float uf = qf + S.cf * p * (vis ? S.sqv : S.sqe) * rc;
+    const float er = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
+    const float lo = uf - er, hi = uf + er;
+    if (lo > S.L1) {
+        S.H2 = fmaxf(S.H2, S.H1); S.L1 = lo; S.H1 = hi;
+        S.off = off; S.a = a; S.child = child;
+    } else {
+        S.H2 = fmaxf(S.H2, hi);
     }
 }
-__device__ __forceinline__ void batch_load(const EdgePtr E, int base, int ec, EdgeStat *es) {
-#pragma unroll
-    for (int j = 0; j < BK_BATCH; j++) {
-        es[j] = EdgeStat{0.f, 0, Q_UNSET};
-        if (base + j < ec) es[j] = E[base + j].s;
+
+// exact arg-max of one level (wave-uniform arguments): its visit records lane-parallel, the
+// record `vidx` taking (n1, q1) (just written by the level's lane), and its best unvisited
+// edge (uc, ac, rc; has_c) as computed by that lane. Ties: lowest action.
+__device__ void exact_level(const Pools &P, int64_t vb, int vcnt, int ns, double cpuct, int vidx, int n1, double q1,
+                            bool has_c, double uc, int ac, int rc, int &rank, int &act, int &child) {
+    const int l = lane_id();
+    const double sq = sqrt((double)ns);
+    double bu = -INFINITY;
+    int ba = 0x7fffffff, bo = 0, bc = -1;
+    if (l == 0 && has_c) { bu = uc; ba = ac; bo = rc; }
+    for (int base = 0; base < vcnt; base += 64) {
+        const int k = base + l;
+        if (k < vcnt) {
+            const VisitRec v = *P.vr(vb + REC_UNITS * k);
+            const int n = k == vidx ? n1 : v.n;
+            const double q = k == vidx ? q1 : v.q;
+            const double u = ucb_visited(q, n, v.p, cpuct, sq);
+            if (u > bu || (u == bu && v.a < ba)) { bu = u; ba = v.a; bo = v.off; bc = v.child; }
+        }
+    }
+    const double mu = wave_max_f64(bu);
+    const int am = wave_min_i32(bu == mu ? ba : 0x7fffffff);
+    const int ln = __ffsll((unsigned long long)__ballot(bu == mu && ba == am)) - 1;
+    rank = __builtin_amdgcn_readlane(bo, ln);
+    act = am;
+    child = __builtin_amdgcn_readlane(bc, ln);
+}
+
+// per-level state of a group of path levels (lane j = level g0 + j)
+struct Level {
+    int node, off, act, child;  // the node, the edge taken (rank, action), the node it led to
+    int ns;                     // Ns before the update
+    double qs;
+    NodeRun r;                  // the node's run / visit block
+    EdgeP e;                    // the edge taken
+    int n;                      // its Nsa (0 without a visit record)
+    double q;                   // its Qsa
+    int rchild;                 // its record's link
+    int grow;                   // new visit-block capacity (0: no new block needed)
+    int64_t nb;                 // the new block (grow)
+};
+
+// the loads of one group: path entries, node records, the edges taken and their records
+__device__ __forceinline__ void load_levels(const Pools &P, int t, int g0, int depth, int lid, Level &V, bool in) {
+    const int32_t *path_n = P.path_n + (size_t)t * (P.pcap + 1);
+    const int32_t *path_x = P.path_x + (size_t)t * P.pcap;
+    const int d = g0 + lane_id();
+    V.node = 0; V.off = 0; V.act = 0; V.child = -1; V.ns = 0; V.qs = 0.0;
+    V.r = NodeRun{0, 0, 0, 0, 0, 0}; V.e = EdgeP{0.f, 0, -1}; V.n = 0; V.q = Q_UNSET; V.rchild = -1;
+    V.grow = 0; V.nb = -1;
+    if (!in) return;
+    V.node = path_n[d];
+    const int px = path_x[d];
+    V.child = d + 1 < depth ? path_n[d + 1] : lid;
+    V.off = px_off(px); V.act = px_action(px);
+    const NodeStat st = P.nst[V.node];
+    V.ns = st.ns; V.qs = st.qs;
+    V.r = P.nrun[V.node];
+    V.e = *P.ep(V.r.eb + V.off);
+    if (V.e.vi >= 0) {
+        const VisitRec v = *P.vr(V.r.vb + REC_UNITS * V.e.vi);
+        V.n = v.n; V.q = v.q; V.rchild = v.child;
+    } else if (V.r.vcnt == V.r.vcap) {
+        V.grow = V.r.vcap == 0 ? 1 : min(2 * (int)V.r.vcap, (int)V.r.ec);
     }
 }
 
@@ -1711,260 +1745,278 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                                                     const uint64_t *__restrict__ leaf_mask,
                                                     const float *__restrict__ pi,
                                                     const float *__restrict__ v) {
-    __shared__ __align__(16) float lpi[WAVES][(KINDS & 1) ? 416 : 4];
+    __shared__ RunScr scr[WAVES];
     const int w = uniform(threadIdx.x >> 6), t = blockIdx.x * WAVES + w;
     if (t >= B) return;
     const int l = lane_id();
     TreeHdr *H = P.hdr + t;
-    const int32_t *path_n = P.path_n + (size_t)t * P.pcap;
-    const int64_t *path_e = P.path_e + (size_t)t * P.pcap;
-    const int32_t *path_x = P.path_x + (size_t)t * P.pcap;
-    // every input that depends on nothing else is requested at once: the header fields, the
-    // path's first 64 levels (lane per level), and for an NN leaf its mask, value and policy
-    int pnode = path_n[l], px = path_x[l];               // (pcap >= 256)
-    int64_t pge = path_e[l];
     const int kind = H->leaf_kind;
     if (kind == LEAF_NONE || !((KINDS >> (kind - 1)) & 1)) return;
     const int depth = H->depth;
     const int h_slot = H->leaf_slot, h_hslot = H->leaf_hslot, h_round = H->leaf_round;
     const uint64_t h_k0 = H->leaf_k0, h_k1 = H->leaf_k1;
     const int h_sims = H->sims_done, h_noise = H->noise_pending, h_gc = H->gc_state;
-    const int h_eleft = H->eleft;
-    const int64_t h_enext = H->enext;
+    const int32_t *path_n = P.path_n + (size_t)t * (P.pcap + 1);
+    int64_t *path_b = P.path_b + (size_t)t * P.pcap;
     float val[4] = {0, 0, 0, 0};
-    float piv[7] = {0, 0, 0, 0, 0, 0, 0};
-    uint64_t mw[7] = {0, 0, 0, 0, 0, 0, 0};
-    if (kind == LEAF_NN) {
+    int lid = -1;                                        // the leaf's node (terminal: stored by select)
+    RunScr &S = scr[w];
+    if (kind == LEAF_NN) {                               // the leaf's policy and mask, staged in LDS
         const float *gp = pi + (size_t)t * SPL_ACTIONS;
 #pragma unroll
-        for (int k = 0; k < 7; k++) {
-            mw[k] = leaf_mask[(size_t)t * 7 + k];
-            if (64 * k + l < SPL_ACTIONS) piv[k] = gp[64 * k + l];
-        }
+        for (int k = 0; k < 7; k++)
+            if (64 * k + l < SPL_ACTIONS) S.pr[64 * k + l] = gp[64 * k + l];
+        if (l < 7) S.bits[l] = leaf_mask[(size_t)t * 7 + l];
 #pragma unroll
         for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
     } else {
 #pragma unroll
         for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
+        lid = path_n[depth];
     }
-    // the first group's statistics and the first batch of every level's edges, requested
-    // before the expansion (which never touches them: the new node is not on its own path)
-    int cnt = min(depth, 64);
-    LevelV V{0, 0, 0, 0, 0, 0.0, 0.0};
-    int pcnt = 0, pns = 0;
-    double pq = 0.0, pqs = 0.0;
-    EdgeStat b0[BK_BATCH];
-#if SPL_BOUNDS_CHECK
-    const long long NN = (long long)P.npages * NPG, NE = (long long)P.epages * EPG;
-#endif
-    if (l < cnt) {
-        V.off = px_off(px);
-        V.ec = px_count(px);
-        BCHK(pnode >= 0 && pnode < NN, 1, pnode, t, pnode = 0);
-        BCHK(pge >= 0 && pge < NE, 2, pge, t, pge = 0);
-        BCHK(V.ec >= 1 && V.ec <= SPL_ACTIONS && V.off < V.ec && pge - V.off >= 0 &&
-                 ((pge - V.off) & (EPG - 1)) + V.ec <= EPG,
-             3, V.ec | (V.off << 16), t, (V.ec = 1, V.off = 0, pge = 0));
-        V.eb = pge - V.off;
-        const EdgeStat st = P.ed[pge].s;
-        pcnt = st.n; pq = st.q;
-        pns = P.nst[pnode].ns; pqs = P.nst[pnode].qs;
-    }
-#if BK_PRELOAD
-    batch_load(P.ed + V.eb, 0, l < cnt ? V.ec : 0, b0);
-#endif
-    int lg = -1, lec = 0;                                // the new leaf, linked to the last path edge
-    int64_t leb = 0;
-    if (kind == LEAF_NN) {
-        int ec = 0;
-#pragma unroll
-        for (int k = 0; k < 7; k++) ec += __popcll(mw[k]);
-        // the new node's slot (reserved by k_select with node boards) and CSR run (from the
-        // tree's current edge page or a fresh one from the shared pool)
-        int g = -1;
-        int64_t eb = -1;
-        if (l == 0) {
-            g = h_slot >= 0 ? h_slot : node_slot(P, H, t, H->node_count);
-            if (g >= 0) {
-                if (h_eleft >= ec) {
-                    eb = h_enext;
-                    H->enext = eb + ec;
-                    H->eleft = h_eleft - ec;
-                    H->edge_count += ec;
-                } else {
-                    eb = edge_run(P, H, t, ec);
-                }
-            }
+    // ---- pass A: the first group's levels in registers; every visit block that must grow and
+    // the NN leaf's run allocated before anything changes, so a simulation that finds no room
+    // can still be withdrawn
+    const int cnt0 = min(depth, 64);
+    Level V;
+    load_levels(P, t, 0, depth, lid, V, l < cnt0);
+    bool fail = false;
+    for (int g0 = 0; g0 < depth && !fail; g0 += 64) {
+        Level Vg;
+        if (g0 > 0) load_levels(P, t, g0, depth, lid, Vg, g0 + l < depth);
+        const int grow = g0 == 0 ? V.grow : Vg.grow;
+        uint64_t gm = __ballot(grow > 0);
+        int64_t nb = -1;
+        while (gm) {
+            const int j = __ffsll((unsigned long long)gm) - 1;
+            gm &= gm - 1;
+            const int units = REC_UNITS * __builtin_amdgcn_readlane(grow, j);
+            int64_t b = -1;
+            if (l == 0) b = unit_alloc(P, H, t, units);
+            b = readlane64(b, 0);
+            if (b < 0) { fail = true; break; }
+            if (l == j) nb = b;
         }
-        if (l == 0) {
-            BCHK(g < NN, 4, g, t, g = -1);
-            BCHK(eb < 0 || ((eb & (EPG - 1)) + ec <= EPG && eb + ec <= NE), 5, eb, t, eb = -1);
+        if (g0 == 0) V.nb = nb;
+        else if (grow > 0 && nb >= 0) path_b[g0 + l] = nb;
+    }
+    int g = -1, ec = 0;
+    int64_t eb = -1;
+    if (kind == LEAF_NN) {
+        wave_lds_fence();
+#pragma unroll
+        for (int k = 0; k < 7; k++) ec += __popcll(S.bits[k]);
+        if (!fail && l == 0) {
+            // the new node's slot (reserved by k_select with node boards) and run
+            g = h_slot >= 0 ? h_slot : node_slot(P, H, t, H->node_count);
+            if (g >= 0) eb = unit_alloc(P, H, t, ec);
         }
         g = __shfl(g, 0, 64);
         eb = readlane64(eb, 0);
-        if (eb < 0 && C.selfplay && depth > 0 && h_gc == 0) {
-            // garbage is collected lazily (begin_search), so a self-play search may run out
-            // of room with dead nodes still held: this simulation is withdrawn (no backup,
-            // not counted), k_gc (launched behind every backup of a self-play arena) collects
-            // the garbage (exact: nodes with rounds <= the root's) and the next select repeats
-            // the same descent. Search-only arenas never withdraw.
-            if (l == 0) {
-                H->gc_state = 1;
-                H->leaf_kind = LEAF_NONE;
-                H->withdrawals += 1;
-                gc_push(P, H, t);
-            }
-            return;
+    }
+    if ((fail || (kind == LEAF_NN && eb < 0)) && C.selfplay && depth > 0 && (h_gc == 0 || h_gc == 5)) {
+        // garbage is collected lazily (begin_search), so a self-play search may run out
+        // of room with dead nodes still held: this simulation is withdrawn (no backup,
+        // not counted), k_gc (launched behind every backup of a self-play arena) collects
+        // the garbage (exact: nodes with rounds <= the root's) and the next select repeats
+        // the same descent. Search-only arenas never withdraw.
+        if (l == 0) {
+            H->gc_state = 1;
+            H->leaf_kind = LEAF_NONE;
+            H->withdrawals += 1;
+            gc_push(P, H, t);
         }
+        return;
+    }
+    if (fail) {                                          // a visit block found no room: the
+        if (l == 0) {                                    // simulation is lost (counted)
+            H->unexpanded += 1;
+            H->sims_done = h_sims + 1;
+            H->noise_pending = 0;
+            H->leaf_kind = LEAF_NONE;
+        }
+        return;
+    }
+    if (kind == LEAF_NN) {
         if (eb < 0) {                                    // no room: back up v, do not store
             if (l == 0) H->unexpanded += 1;
         } else {
-            float *pr = lpi[w];
-#pragma unroll
-            for (int k = 0; k < 7; k++)
-                if (64 * k + l < SPL_ACTIONS) pr[64 * k + l] = piv[k];
-            __builtin_amdgcn_wave_barrier();
-            const float sum = wave_np_sum409(pr);                    // normalise (MCTS.py:144)
-            // the new node's arg-max: every edge unvisited (Ns = 0, Qs = v), so u = fpu_init +
-            // cpuct * P * sqrt(0 + EPS) (MCTS.py:214), evaluated exactly, lowest index on ties
-            const double fpu_init = C.fpu > 0 ? (double)val[0] - C.fpu : C.fpu;
-            const double sq_eps = sqrt(1e-8);
-            double bu = -INFINITY;
-            int bj = 0x7fffffff, bact = 0;
+            // the run, sorted by (prior desc, action asc): priors normalised in NumPy's
+            // pairwise order (MCTS.py:144), or a new root's noised (:141-143)
+            float *pr = S.pr;
+            const bool noise = depth == 0 && h_sims == 0 && h_noise;
+            if (noise) {
+                root_noise_lds(C, t, ST_DIR | (uint32_t)H->move_no, pr, S.bits, ec);
+            } else {
+                const float sum = wave_np_sum409(pr);
+                wave_lds_fence();
+                for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = pr[a] / sum;
+                wave_lds_fence();
+            }
             int run = 0;
 #pragma unroll
             for (int k = 0; k < 7; k++) {
-                const uint64_t wd = mw[k];
+                const uint64_t wd = S.bits[k];
                 if ((wd >> l) & 1) {
                     const int r = run + __popcll(wd & lanemask_lt());
-                    const int a = 64 * k + l;
-                    const float p = piv[k] / sum;
-                    P.ed[eb + r].k.a = (int16_t)a;
-                    P.ed[eb + r].s.p = p;
-                    P.ed[eb + r].s.n = 0;
-                    P.ed[eb + r].s.q = Q_UNSET;
-                    P.ed[eb + r].k.child = -1;
-                    const double u = fpu_init + C.cpuct * (double)p * sq_eps;
-                    if (u > bu) { bu = u; bj = r; bact = a; }
+                    S.cp[r] = pr[64 * k + l];
+                    S.ca[r] = (int16_t)(64 * k + l);
                 }
                 run += __popcll(wd);
             }
-            const int mine = bj;
-            wave_argmax(bu, bj);
-            bj = uniform(bj);
-            bact = __builtin_amdgcn_readlane(bact, __ffsll((unsigned long long)__ballot(mine == bj)) - 1);
-            __threadfence_block();
-            __builtin_amdgcn_wave_barrier();
-            // the parent edge: a cross-lane read of lane depth - 1, so it is taken here, with the
-            // whole wave active — inside the lane-0 branch below a spilled `pge` is reloaded for
-            // lane 0 only and lane depth - 1 reads stale register contents (the round-3
-            // aperture violation)
-            const int64_t pe = depth > 0 ? readlane64(pge, depth - 1 < 64 ? depth - 1 : 0) : 0;
+            wave_lds_fence();
+            (void)write_sorted_run(P, eb, 0, ec, S.cp, S.ca, nullptr);
+            // the new node's arg-max: every edge unvisited (Ns = 0, Qs = v), u = fpu_init +
+            // cpuct * P * sqrt(0 + EPS) (MCTS.py:214): the top-ranked edge unless a smaller
+            // prior rounds to the same u with a lower action (from the LDS list, action order)
+            int bsel = -1, bact = 0;
+            if (depth > 0) {
+                const double fpu_init = fpu_base(C.fpu, (double)val[0]), sq_eps = sqrt(1e-8);
+                double bu = -INFINITY;
+                int ba = 0x7fffffff;
+                for (int i = l; i < ec; i += 64) {
+                    const double u = ucb_unvisited(S.cp[i], C.cpuct, fpu_init, sq_eps);
+                    if (u > bu || (u == bu && S.ca[i] < ba)) { bu = u; ba = S.ca[i]; }
+                }
+                const double mu = wave_max_f64(bu);
+                bact = wave_min_i32(bu == mu ? ba : 0x7fffffff);
+                // its rank: edges of a larger prior, or of the same prior and a lower action
+                const float pb = S.pr[bact];
+                int r = 0;
+                for (int i = l; i < ec; i += 64) r += (S.cp[i] > pb) || (S.cp[i] == pb && S.ca[i] < bact);
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+                bsel = uniform(r);
+            }
             if (l == 0) {
                 P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
-                P.neb[g] = eb; P.nec[g] = ec;
-                // (a new root: its priors may still be noised below, and a root always scans)
-                P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)(depth == 0 ? -1 : bj), (int16_t)bact, -1, 0, 0, 0};
+                P.nrun[g] = NodeRun{eb, 0, (int16_t)ec, 0, 0, 0};
+                // (a new root: its priors may still be noised, and a root scans)
+                P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)bsel, (int16_t)bact, -1, 0, 0};
                 P.nround[g] = h_round; P.nterm[g] = 0;
                 if (h_hslot >= 0) P.hslot[(size_t)t * P.hcap + h_hslot] = g;   // the select's lookup ended there
                 else hash_insert(P, t, h_k0, g);
-                if (depth == 0) { H->root = g; H->root_eb = eb; H->root_ec = ec; }
-                else {
-                    int64_t pe2 = depth - 1 < 64 ? pe : path_e[depth - 1];
-                    BCHK(pe2 >= 0 && pe2 < NE, 8, pe2, t, pe2 = 0);
-                    P.ed[pe2].k.child = g;
-                }
+                if (depth == 0) H->root = g;
                 H->node_count += 1;
             }
-            lg = g; leb = eb; lec = ec;
-            __threadfence_block();
-            __builtin_amdgcn_wave_barrier();
-            if (depth == 0 && h_sims == 0 && h_noise)    // noise on a new root (raw priors)
-                apply_root_noise(P, C, t, eb, ec, ST_DIR | (uint32_t)H->move_no, pr, true);
+            lid = g;
         }
     }
-    // levels in groups of 64, lane per level (the first group's data is in hand)
+    if (depth > 0 && kind == LEAF_NN && l == (depth - 1 < 64 ? depth - 1 : 64)) V.child = lid;
+    // ---- pass B: levels in groups of 64, lane per level (the first group's data is in hand)
     for (int g0 = 0; g0 < depth; g0 += 64) {
         const int d = g0 + l;
+        const int cnt = min(64, depth - g0);
+        const bool in = l < cnt;
         if (g0 > 0) {
-            cnt = min(64, depth - g0);
-            V = LevelV{0, 0, 0, 0, 0, 0.0, 0.0};
-            if (l < cnt) {
-                pnode = path_n[d]; pge = path_e[d]; px = path_x[d];
-                V.off = px_off(px);
-                V.ec = px_count(px);
-                BCHK(pnode >= 0 && pnode < NN, 9, pnode, t, pnode = 0);
-                BCHK(pge >= 0 && pge < NE, 10, pge, t, pge = 0);
-                BCHK(V.ec >= 1 && V.ec <= SPL_ACTIONS && V.off < V.ec && pge - V.off >= 0 &&
-                         ((pge - V.off) & (EPG - 1)) + V.ec <= EPG,
-                     11, V.ec | (V.off << 16), t, (V.ec = 1, V.off = 0, pge = 0));
-                V.eb = pge - V.off;
-                const EdgeStat st = P.ed[pge].s;
-                pcnt = st.n; pq = st.q;
-                pns = P.nst[pnode].ns; pqs = P.nst[pnode].qs;
-            }
+            load_levels(P, t, g0, depth, lid, V, in);
+            if (in && V.grow > 0) V.nb = path_b[d];
         }
-#if BK_PRELOAD
-        if (g0 > 0)
-#endif
-            batch_load(P.ed + V.eb, 0, l < cnt ? V.ec : 0, b0);
         // MCTS.py:169-176: level d sees the leaf value rolled (depth - d) times; the levels
-        // touch distinct nodes/edges (rounds strictly increase along a path), so one lane per
+        // touch distinct nodes (rounds strictly increase along a path), so one lane per
         // level applies exactly the sequential update
-        if (l < cnt) {
+        int n1 = 0, vidx = -1, nns = 0;
+        double q1 = 0.0, nqs = 0.0;
+        if (in) {
             const int rot = (depth - d) % N, vi = (N - rot) % N;
             float vr = val[0];
 #pragma unroll
             for (int i = 1; i < N; i++) vr = vi == i ? val[i] : vr;   // (no dynamic index: scratch)
             const double v0 = (double)vr;
-            V.nq = ((double)pcnt * pq + v0) / (double)(pcnt + 1);
-            V.nqs = ((double)(pns + 1) * pqs + v0) / (double)(pns + 2);
-            V.nn = pcnt + 1;
-            V.nns = pns + 1;
-            P.ed[pge].s.q = V.nq;
-            P.ed[pge].s.n = V.nn;
+            nqs = ((double)(V.ns + 1) * V.qs + v0) / (double)(V.ns + 2);
+            nns = V.ns + 1;
+            q1 = ((double)V.n * V.q + v0) / (double)(V.n + 1);
+            n1 = V.n + 1;
+            if (V.e.vi >= 0) {                           // Qsa, Nsa (+ the link, if new)
+                vidx = V.e.vi;
+                VisitRec *R = P.vr(V.r.vb + REC_UNITS * vidx);
+                R->q = q1;
+                R->n = n1;
+                if (V.rchild < 0 && V.child >= 0) R->child = V.child;
+            } else {                                     // the edge's first visit: a record
+                if (V.grow > 0) {                        // (the block outgrown: moved)
+                    for (int k = 0; k < REC_UNITS * V.r.vcnt; k++) P.eu[V.nb + k] = P.eu[V.r.vb + k];
+                    V.r.vb = V.nb;
+                    V.r.vcap = (int16_t)V.grow;
+                }
+                vidx = V.r.vcnt;
+                *P.vr(V.r.vb + REC_UNITS * vidx) = VisitRec{q1, n1, V.child, V.e.p, (int16_t)V.off, (int16_t)V.act};
+                P.ep(V.r.eb + V.off)->vi = (int16_t)vidx;
+                V.r.vcnt = (int16_t)(vidx + 1);
+                if (V.off == V.r.cand) {                 // the next candidate: next rank without
+                    int j = V.off + 1;                   // a record (usually the next one)
+                    while (j < V.r.ec && P.ep(V.r.eb + j)->vi >= 0) j++;
+                    V.r.cand = (int16_t)j;
+                }
+                P.nrun[V.node] = V.r;
+            }
+            V.rchild = V.rchild >= 0 ? V.rchild : V.child;
         }
-        // each level's arg-max under its new statistics: screened lane-serial scan, exact
-        // float64 for the levels the screen leaves open
-        int maxec = l < cnt ? V.ec : 0;
+        // each level's arg-max under its new statistics
+        const bool wide = in && V.r.vcnt > BK_WIDE;
+        Screen S = screen_init(nns, nqs, C.cpuct, C.fpu);
+        bool has_c = false;
+        double uc = 0.0;
+        int ac = 0, rc = 0;
+        if (in && V.r.cand < V.r.ec) {                   // the best unvisited edge + the next
+            has_c = true;                                // unvisited one of a smaller prior
+            const EdgeP c = *P.ep(V.r.eb + V.r.cand);
+            rc = V.r.cand; ac = c.a;
+            screen_item(S, false, c.p, 0, 0.0, rc, c.a, -1);
+            if (c.p > 0.f) {
+                for (int j = V.r.cand + 1; j < V.r.ec; j++) {
+                    const EdgeP e = *P.ep(V.r.eb + j);
+                    if (e.vi >= 0 || e.p == c.p) continue;
+                    screen_item(S, false, e.p, 0, 0.0, j, e.a, -1);
+                    break;
+                }
+            }
+        }
+        int maxv = in && !wide ? V.r.vcnt : 0;
+        maxv = wave_max_i32(maxv);
+        const int myv = in && !wide ? V.r.vcnt : 0;
+        for (int base = 0; base < maxv; base += BK_BATCH) {
+            VisitRec rb[BK_BATCH];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) maxec = max(maxec, __shfl_xor(maxec, o, 64));
-        maxec = uniform(maxec);
-        const int lec_ = l < cnt ? V.ec : 0;
-        Screen S = screen_init(V.nns, V.nqs, C.cpuct, C.fpu);
-        screen_batch(S, b0, 0, lec_, V.off, V.nn, V.nq);
-        for (int base = BK_BATCH; base < maxec; base += BK_BATCH) {
-            EdgeStat es[BK_BATCH];
-            batch_load(P.ed + V.eb, base, lec_, es);
-            screen_batch(S, es, base, lec_, V.off, V.nn, V.nq);
+            for (int k = 0; k < BK_BATCH; k++)
+                if (base + k < myv) rb[k] = *P.vr(V.r.vb + REC_UNITS * (base + k));
+#pragma unroll
+            for (int k = 0; k < BK_BATCH; k++) {
+                const int i = base + k;
+                if (i < myv) {
+                    const VisitRec &R = rb[k];
+                    const bool mine = i == vidx;
+                    screen_item(S, true, R.p, mine ? n1 : R.n, mine ? q1 : R.q, R.off, R.a,
+                                mine ? V.rchild : R.child);
+                }
+            }
         }
-        int bsel = S.H2 < S.L1 ? S.i1 : -1;
-        if (l >= cnt) bsel = 0;
-        uint64_t ex = __ballot(l < cnt && bsel < 0);
+        bool open = in && (wide || !(S.H2 < S.L1));
+        int bsel = S.off, bact = S.a, bch = S.child;
+        if (open && has_c) {                             // exact best unvisited edge (own lane)
+            double u;
+            rc = best_unvisited(P, V.r.eb, V.r.ec, V.r.cand, C.cpuct, fpu_base(C.fpu, nqs), sqrt((double)nns + 1e-8),
+                                u, ac);
+            uc = u;
+        }
+        wave_lds_fence();                                // records written above, read across lanes
+        uint64_t ex = __ballot(open);
         while (ex) {
             const int j = __ffsll((unsigned long long)ex) - 1;
             ex &= ex - 1;
-            const int b = ucb_argmax_wide(P.ed + readlane64(V.eb, j), __builtin_amdgcn_readlane(V.ec, j),
-                                          __builtin_amdgcn_readlane(V.nns, j), readlane_f64(V.nqs, j), C.cpuct, C.fpu,
-                                          __builtin_amdgcn_readlane(V.off, j), __builtin_amdgcn_readlane(V.nn, j),
-                                          readlane_f64(V.nq, j));
-            if (l == j) bsel = b;
+            int rk, ak, ck;
+            exact_level(P, readlane64(V.r.vb, j), __builtin_amdgcn_readlane((int)V.r.vcnt, j),
+                        __builtin_amdgcn_readlane(nns, j), C.cpuct, __builtin_amdgcn_readlane(vidx, j),
+                        __builtin_amdgcn_readlane(n1, j), readlane_f64(q1, j),
+                        __builtin_amdgcn_readlane((int)has_c, j) != 0, readlane_f64(uc, j),
+                        __builtin_amdgcn_readlane(ac, j), __builtin_amdgcn_readlane(rc, j), rk, ak, ck);
+            if (l == j) { bsel = rk; bact = ak; bch = ck; }
         }
-        // the node record: statistics, arg-max, that edge's link and its child's CSR range
-        // (the new leaf's, else read from the node arrays: lanes in parallel, one round trip)
-        if (l < cnt) {
-            BCHK(bsel >= 0 && bsel < V.ec, 6, bsel, t, bsel = 0);
-            EdgeLink lk = P.ed[V.eb + bsel].k;
-            BCHK(lk.child >= -1 && lk.child < NN, 7, lk.child, t, lk.child = -1);
-            int64_t cb = 0;
-            int cc = 0;
-            if (d == depth - 1 && lg >= 0 && bsel == V.off) {
-                lk.child = lg; cc = lec; cb = leb;
-            } else if (lk.child >= 0) {
-                cb = P.neb[lk.child];
-                cc = P.nterm[lk.child] ? -1 : P.nec[lk.child];
-            }
-            P.nst[pnode] = NodeStat{V.nqs, V.nns, (int16_t)bsel, lk.a, lk.child, (int16_t)cc, 0, cb};
+        // the node record: statistics, arg-max and its link (the path edge's link as just set)
+        if (in) {
+            if (bsel == V.off) bch = V.rchild;
+            const int bt_ = bch >= 0 ? (int)P.nterm[bch] : 0;
+            P.nst[V.node] = NodeStat{nqs, nns, (int16_t)bsel, (int16_t)bact, bch, bt_, 0};
         }
     }
     if (l == 0) {
@@ -1987,6 +2039,7 @@ __global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int
                                                        const uint8_t *__restrict__ active,
                                                        uint32_t board_base, uint32_t stream,
                                                        int16_t *__restrict__ action) {
+    __shared__ uint64_t hb[WAVES][7];                    // the best actions (bitmap, action order)
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B || (active && !active[t])) return;
     const int l = lane_id();
@@ -1997,42 +2050,42 @@ __global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int
         if (l == 0) action[t] = (int16_t)(int)(u * (double)SPL_ACTIONS);
         return;
     }
-    const EdgePtr E = P.ed + P.neb[root];
-    const int ec = P.nec[root];
+    const NodeRun r = P.nrun[root];
     const int sims = H->budget;
     const bool forced = H->forced;
+    auto count = [&](int i, float &p, int &a) {
+        const EdgeP e = *P.ep(r.eb + i);
+        p = e.p; a = e.a;
+        return e.vi >= 0 ? P.vr(r.vb + REC_UNITS * e.vi)->n : 0;
+    };
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, E[i].s.n);
-    for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
+    for (int i = l; i < r.ec; i += 64) { float p; int a; best = max(best, count(i, p, a)); }
+    best = wave_max_i32(best);
     long long top = 0;
-    for (int i = l; i < ec; i += 64)
-        top = max(top, pruned_count(E[i].s.n, best, forced, E[i].s.p, sims));
+    for (int i = l; i < r.ec; i += 64) {
+        float p; int a;
+        const int n = count(i, p, a);
+        top = max(top, pruned_count(n, best, forced, p, sims));
+    }
     for (int o = 32; o > 0; o >>= 1) top = max(top, (long long)__shfl_xor(top, o, 64));
     if (top == 0) {
         if (l == 0) action[t] = (int16_t)(int)(u * (double)SPL_ACTIONS);
         return;
     }
+    if (l < 7) hb[w][l] = 0;
+    wave_lds_fence();
+    for (int i = l; i < r.ec; i += 64) {
+        float p; int a;
+        const int n = count(i, p, a);
+        if (pruned_count(n, best, forced, p, sims) == top)
+            atomicOr(reinterpret_cast<unsigned long long *>(&hb[w][a >> 6]), 1ull << (a & 63));
+    }
+    wave_lds_fence();
     int nbest = 0;
-    for (int base = 0; base < ec; base += 64) {
-        const int i = base + l;
-        const bool hit = i < ec && pruned_count(E[i].s.n, best, forced, E[i].s.p, sims) == top;
-        nbest += __popcll(__ballot(hit));
-    }
-    int k = (int)(u * (double)nbest);                    // k-th best in action order
-    for (int base = 0; base < ec; base += 64) {
-        const int i = base + l;
-        const bool hit = i < ec && pruned_count(E[i].s.n, best, forced, E[i].s.p, sims) == top;
-        const uint64_t b = __ballot(hit);
-        const int c = __popcll(b);
-        if (k < c) {
-            uint64_t x = b;
-            for (int j = 0; j < k; j++) x &= x - 1;
-            const int pos = __ffsll((unsigned long long)x) - 1;
-            if (l == 0) action[t] = E[base + pos].k.a;
-            return;
-        }
-        k -= c;
-    }
+#pragma unroll
+    for (int j = 0; j < 7; j++) nbest += __popcll(hb[w][j]);
+    const int k = (int)(u * (double)nbest);              // k-th best in action order
+    if (l == 0) action[t] = (int16_t)action_at(hb[w], k);
 }
 
 // ------------------------------------------------------------ results
@@ -2055,27 +2108,36 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
     if (root < 0) return;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const EdgePtr E = P.ed + P.neb[root];
-    const int ec = P.nec[root];
+    const NodeRun r = P.nrun[root];
     int best = 0;
-    for (int i = l; i < ec; i += 64) best = max(best, E[i].s.n);
-    for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
+    for (int i = l; i < r.ec; i += 64) {
+        const EdgeP e = *P.ep(r.eb + i);
+        best = max(best, e.vi >= 0 ? P.vr(r.vb + REC_UNITS * e.vi)->n : 0);
+    }
+    best = wave_max_i32(best);
     const int sims = H->budget;
     const bool forced = H->forced;
     long long tot = 0;
-    for (int i = l; i < ec; i += 64) {
-        const int a = E[i].k.a;
-        const long long c = pruned_count(E[i].s.n, best, forced, E[i].s.p, sims);
-        if (counts) counts[(size_t)t * SPL_ACTIONS + a] = E[i].s.n;
-        if (adjusted) adjusted[(size_t)t * SPL_ACTIONS + a] = c;
-        if (qsa) qsa[(size_t)t * SPL_ACTIONS + a] = E[i].s.q;
+    for (int i = l; i < r.ec; i += 64) {
+        const EdgeP e = *P.ep(r.eb + i);
+        int cn = 0;
+        double cq = Q_UNSET;
+        if (e.vi >= 0) {
+            const VisitRec v = *P.vr(r.vb + REC_UNITS * e.vi);
+            cn = v.n; cq = v.q;
+        }
+        const long long c = pruned_count(cn, best, forced, e.p, sims);
+        if (counts) counts[(size_t)t * SPL_ACTIONS + e.a] = cn;
+        if (adjusted) adjusted[(size_t)t * SPL_ACTIONS + e.a] = c;
+        if (qsa) qsa[(size_t)t * SPL_ACTIONS + e.a] = cq;
         tot += c;
     }
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-    for (int i = l; i < ec; i += 64) {
-        const int a = E[i].k.a;
-        const long long c = pruned_count(E[i].s.n, best, forced, E[i].s.p, sims);
-        if (probs) probs[(size_t)t * SPL_ACTIONS + a] = (double)c / (double)tot;
+    for (int i = l; i < r.ec; i += 64) {
+        const EdgeP e = *P.ep(r.eb + i);
+        const int cn = e.vi >= 0 ? P.vr(r.vb + REC_UNITS * e.vi)->n : 0;
+        const long long c = pruned_count(cn, best, forced, e.p, sims);
+        if (probs) probs[(size_t)t * SPL_ACTIONS + e.a] = (double)c / (double)tot;
     }
     if (q && l == 0) {
         const double q0 = P.nst[root].qs;
@@ -2095,9 +2157,11 @@ __global__ __launch_bounds__(THREADS) void k_root_priors(Pools P, int B, float *
     if (root < 0) return;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const EdgePtr E = P.ed + P.neb[root];
-    const int ec = P.nec[root];
-    for (int i = l; i < ec; i += 64) o[E[i].k.a] = E[i].s.p;
+    const NodeRun r = P.nrun[root];
+    for (int i = l; i < r.ec; i += 64) {
+        const EdgeP e = *P.ep(r.eb + i);
+        o[e.a] = e.p;
+    }
 }
 
 // leaf int8 [B,R,7] + packed mask -> float32 board and bool mask (predict, :160-161).
@@ -2120,7 +2184,7 @@ __global__ __launch_bounds__(256) void k_nn_input(int B, int R, const int8_t *__
 
 // tree sizes (spl_mcts_tree_sizes): slots in use and the live part of each tree — the root
 // and the nodes whose round exceeds the root's (what garbage collection keeps), with their
-// CSR edges. Diagnostic (capacity planning), one wave per tree.
+// edge units (runs and visit blocks). Diagnostic (capacity planning), one wave per tree.
 __global__ __launch_bounds__(64) void k_tree_sizes(Pools P, int B, int32_t *out) {
     const int t = blockIdx.x;
     if (t >= B) return;
@@ -2131,7 +2195,13 @@ __global__ __launch_bounds__(64) void k_tree_sizes(Pools P, int B, int32_t *out)
     int ln = 0, le = 0;
     for (int i = l; i < nc; i += 64) {
         const int g = node_g(P, t, i);
-        if (g == root || P.nround[g] > rr) { ln++; le += P.nterm[g] ? 0 : P.nec[g]; }
+        if (g == root || P.nround[g] > rr) {
+            ln++;
+            if (!P.nterm[g]) {
+                const NodeRun r = P.nrun[g];
+                le += r.ec + REC_UNITS * r.vcap;
+            }
+        }
     }
     for (int o = 32; o > 0; o >>= 1) { ln += __shfl_xor(ln, o, 64); le += __shfl_xor(le, o, 64); }
     if (l == 0) {
@@ -2231,8 +2301,8 @@ struct Plan {
 static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     Plan L;
     L.nptab = (cfg->node_cap + NPG - 1) / NPG;
-    L.eptab = (cfg->edge_cap + EPG - 1) / EPG;
-    L.nmax = L.nptab * NPG; L.emax = L.eptab * EPG;
+    L.eptab = (cfg->edge_cap + UPG - 1) / UPG;
+    L.nmax = L.nptab * NPG; L.emax = L.eptab * UPG;
     // transposition table: power of two with load <= 0.7 at the tree's maximum
     int h = 64;
     while ((long long)h * 7 < (long long)L.nmax * 10) h <<= 1;
@@ -2245,21 +2315,22 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     const long long pn = cfg->pool_nodes > 0 ? cfg->pool_nodes : (long long)B * L.nmax;
     const long long pe = cfg->pool_edges > 0 ? cfg->pool_edges : (long long)B * L.emax;
     L.npages = (pn + NPG - 1) / NPG;
-    L.epages = (pe + EPG - 1) / EPG;
-    const size_t nn = (size_t)L.npages * NPG, ne = (size_t)L.epages * EPG;
+    L.epages = (pe + UPG - 1) / UPG;
+    const size_t nn = (size_t)L.npages * NPG, ne = (size_t)L.epages * UPG;
     const size_t nx = (size_t)B * L.excap, no = (size_t)L.out_cap;
     const int gcw = B < GC_WG ? B : GC_WG;
     size_t bytes = 0;
     auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
-    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(8 * nn); acc(4 * nn); acc(4 * nn);
-    acc(sizeof(NodeStat) * nn); acc(nn); acc(16 * nn); acc((ne / EPG) * EdgePtr::PAGE_BYTES);
+    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn);
+    acc(sizeof(NodeStat) * nn); acc(sizeof(NodeRun) * nn); acc(nn); acc(8 * ne);
     acc(4 * (size_t)B * L.nptab); acc(4 * (size_t)B * L.eptab); acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages);
     acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages); acc(64);
-    acc(4 * (size_t)B * L.hcap); acc(4 * (size_t)B * L.pcap); acc(8 * (size_t)B * L.pcap); acc(4 * (size_t)B * L.pcap);
+    acc(4 * (size_t)B * L.hcap); acc(4 * (size_t)B * (L.pcap + 1)); acc(4 * (size_t)B * L.pcap); acc(8 * (size_t)B * L.pcap);
     acc(4 * (size_t)gcw * gc_ints(L.nmax, L.emax)); acc((size_t)B * L.S);
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
     acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
-    acc(16 * no); acc(64); acc((size_t)L.nbb * nn); acc(4 * (size_t)B); acc(8 * no); acc(4 * (size_t)B);
+    acc(16 * no); acc(64); acc((size_t)L.nbb * nn); acc(4 * (size_t)B); acc(4 * (size_t)B); acc(8 * no);
+    acc(4 * (size_t)B);
     L.bytes = bytes;
     return L;
 }
@@ -2270,11 +2341,11 @@ static bool valid_cfg(const spl_ctx *ctx, int B, const spl_mcts_config *cfg) {
         return false;
     // global node ids are int32; page ids too
     const long long nmax = (long long)((cfg->node_cap + NPG - 1) / NPG) * NPG;
-    const long long emax = (long long)((cfg->edge_cap + EPG - 1) / EPG) * EPG;
+    const long long emax = (long long)((cfg->edge_cap + UPG - 1) / UPG) * UPG;
     const long long pn = cfg->pool_nodes > 0 ? cfg->pool_nodes : (long long)B * nmax;
     const long long pe = cfg->pool_edges > 0 ? cfg->pool_edges : (long long)B * emax;
     return cfg->node_cap <= (1 << 24) && cfg->edge_cap <= (1 << 28) && pn + NPG < (1LL << 31) &&
-           pe / EPG + 1 < (1LL << 31);
+           pe / UPG + 1 < (1LL << 31);
 }
 
 #if MCTS_TIMING
@@ -2319,13 +2390,14 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     C.forced_playouts = cfg->forced_playouts; C.dirichlet = cfg->dirichlet_alpha > 0;
     C.temp_threshold = cfg->temp_threshold; C.seed = cfg->seed; C.board_base = cfg->board_base;
     C.selfplay = cfg->selfplay;
-    C.edge_reserve = 32;
+    C.edge_reserve = 48;                                  // units: a new node's run (~20 edges) +
+                                                          // visit records and their growth
     Pools &P = m->P;
     const Plan L = plan_pools(ctx->n, B, cfg);
     P.nmax = L.nmax; P.emax = L.emax; P.hcap = L.hcap; P.pcap = L.pcap;
     P.nptab = L.nptab; P.eptab = L.eptab;
     P.npages = (int)L.npages; P.epages = (int)L.epages;
-    const size_t nn = (size_t)L.npages * NPG, ne = (size_t)L.epages * EPG;
+    const size_t nn = (size_t)L.npages * NPG, ne = (size_t)L.epages * UPG;
     const int excap = L.excap;
     const size_t nx = (size_t)B * excap, no = (size_t)L.out_cap;
     const int gcw = B < GC_WG ? B : GC_WG;
@@ -2336,19 +2408,18 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     char *p = (char *)arena;
     P.hdr = carve<TreeHdr>(p, B);
     P.nkey0 = carve<uint64_t>(p, nn); P.nkey1 = carve<uint64_t>(p, nn);
-    P.neb = carve<int64_t>(p, nn); P.nec = carve<int32_t>(p, nn); P.nround = carve<int32_t>(p, nn);
-    P.nst = carve<NodeStat>(p, nn); P.nterm = carve<int8_t>(p, nn);
-    P.nes = carve<float>(p, 4 * nn);
-    P.ed.base = carve<char>(p, (ne / EPG) * EdgePtr::PAGE_BYTES);   // EdgeStat | EdgeLink blocks per page
+    P.nround = carve<int32_t>(p, nn);
+    P.nst = carve<NodeStat>(p, nn); P.nrun = carve<NodeRun>(p, nn); P.nterm = carve<int8_t>(p, nn);
+    P.eu = carve<uint64_t>(p, ne);                                   // EdgeP runs, VisitRec blocks
     P.ntab = carve<int32_t>(p, (size_t)B * P.nptab); P.etab = carve<int32_t>(p, (size_t)B * P.eptab);
     P.npidx = carve<int32_t>(p, (size_t)P.npages); P.epidx = carve<int32_t>(p, (size_t)P.epages);
     P.nfree = carve<int32_t>(p, (size_t)P.npages); P.efree = carve<int32_t>(p, (size_t)P.epages);
     P.alloc = carve<int32_t>(p, 16);
     P.hslot = carve<int32_t>(p, (size_t)B * P.hcap);
-    P.path_n = carve<int32_t>(p, (size_t)B * P.pcap);
-    P.path_e = carve<int64_t>(p, (size_t)B * P.pcap);
+    P.path_n = carve<int32_t>(p, (size_t)B * (P.pcap + 1));
     P.path_x = carve<int32_t>(p, (size_t)B * P.pcap);
-    P.gc_stride = gc_ints(P.nmax, P.eptab * EPG);
+    P.path_b = carve<int64_t>(p, (size_t)B * P.pcap);
+    P.gc_stride = gc_ints(P.nmax, P.emax);
     P.gscr = carve<int32_t>(p, (size_t)gcw * P.gc_stride);
     P.root_state = carve<int8_t>(p, (size_t)B * m->S);
     P.excap = excap; P.out_cap = (int)no;
@@ -2362,6 +2433,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.out_meta = carve<int32_t>(p, 4 * no); P.counters = carve<int32_t>(p, 16);
     P.nbrd = L.nbb ? carve<int8_t>(p, (size_t)L.nbb * nn) : nullptr;
     P.gcq = carve<int32_t>(p, (size_t)B);
+    P.gcq2 = carve<int32_t>(p, (size_t)B);
     P.flq = carve<int2>(p, no);
     P.order = carve<int32_t>(p, (size_t)B);
     // zero the small state (headers, counters); the pools need no initialisation (a slot
@@ -2524,7 +2596,7 @@ int spl_mcts_pool_state(spl_mcts *m, int32_t *out, void *hs) {
 
 int spl_mcts_pool_pages(const spl_mcts *m, long long *out4) {
     if (!m || !out4) return SPL_EINVAL;
-    out4[0] = m->P.npages; out4[1] = m->P.epages; out4[2] = NPG; out4[3] = EPG;
+    out4[0] = m->P.npages; out4[1] = m->P.epages; out4[2] = NPG; out4[3] = UPG;
     return 0;
 }
 

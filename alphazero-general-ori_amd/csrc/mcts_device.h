@@ -19,20 +19,19 @@ constexpr double Q_UNSET = -42.0;   // MCTS.py:9 NAN sentinel
 
 struct TreeHdr {
     int32_t node_count, edge_count, root, sims_done;   // node_count: the tree's node slots in use
-    int32_t budget, full, noise_pending, depth;         // (local order), edge_count: edges in use
-    int32_t leaf_kind, player, episode_step, move_no;
+    int32_t budget, full, noise_pending, depth;         // (local order), edge_count: edge units in
+    int32_t leaf_kind, player, episode_step, move_no;   // use (runs, visit blocks, garbage)
     int32_t game_no, overflow, n_examples, leaf_round;
     uint64_t leaf_k0, leaf_k1;
     float leaf_v[4];
-    int32_t games_done, forced, moves, root_ec;
+    int32_t games_done, forced, moves, pad0;
     // capacity events: searches that started on a tree pruned to the nodes
     // linked from the root / on an emptied tree, and simulations whose leaf did not fit
     // (evaluated and backed up without being stored)
     int32_t prunes, resets, unexpanded, gc_state;
-    int64_t root_eb;                     // the root's CSR range (global edge index, count root_ec):
-                                         // the descent's first level needs no node load
-    int64_t enext;                       // next free edge of the tree's current edge page
-    int32_t npg, epg, eleft, live_gc;    // node / edge pages held, edges left in the current
+    int64_t units_gc;                    // edge units kept by the last collection
+    int64_t enext;                       // next free unit of the tree's current edge page
+    int32_t npg, epg, eleft, live_gc;    // node / edge pages held, units left in the current
                                          // edge page, nodes kept by the last collection
     int32_t root_round, gc_queued, withdrawals, gcs;   // root round (deferred GC), queued for
                                          // k_gc, simulations withdrawn for GC, collections run
@@ -47,112 +46,103 @@ static_assert(sizeof(TreeHdr) == 192, "TreeHdr layout (splendor/mcts.py HDR_DTYP
 // or pool pressure; k_gc may skip it, see GC_SHOULD_CAP)
 enum { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2 };
 
-// Edge records: the UCB inputs (16 bytes) and the link (8 bytes).
-struct __align__(16) EdgeStat {
+// ---------------------------------------------------------------- two-tier edges
+// The edge pool is a pool of 8-byte units handed out in pages of UPG units. A node owns
+//   a run: one EdgeP (8 B) per legal action — what an unvisited edge needs, the prior and the
+//     action — sorted by (prior descending, action ascending), so the best unvisited edge of
+//     a node is its lowest-ranked edge without statistics (pick_highest_UCB, MCTS.py:214:
+//     an unvisited edge's u = fpu_init + cpuct P sqrt(Ns + EPS) is monotone in P);
+//   a visit block: one VisitRec (24 B = 3 units) per edge with statistics (Nsa, Qsa, the
+//     link), appended on the edge's first backup; the block grows by doubling (relocated;
+//     the old one is garbage until the tree's next collection).
+// Measured live trees keep statistics on ~6 % of their edges, so an edge costs ~9 bytes
+// instead of a full 24-byte record (what lets BASELINE config 4's trees fit).
+struct EdgeP {
     float p;       // prior Ps[a] (float32)
-    int32_t n;     // Nsa
-    double q;      // Qsa (Q_UNSET = the reference's -42 sentinel)
-};
-struct __align__(8) EdgeLink {
     int16_t a;     // action
-    int16_t pad;
-    int32_t child; // child node, global id (-1: not linked yet); its CSR range is the child's
-                   // own (neb / nec / nterm) and, for the node's arg-max, cached in NodeStat
+    int16_t vi;    // its VisitRec in the node's block, -1: none (Nsa = 0, Qsa = -42)
 };
-static_assert(sizeof(EdgeLink) == 8, "EdgeLink layout");
-// one edge's value: both halves
-struct Edge {
-    EdgeStat s;
-    EdgeLink k;
+static_assert(sizeof(EdgeP) == 8, "EdgeP layout");
+struct VisitRec {
+    double q;      // Qsa
+    int32_t n;     // Nsa
+    int32_t child; // link: child node (global id), -1: not linked
+    float p;       // the edge's prior (copy of its EdgeP)
+    int16_t off;   // its rank in the run
+    int16_t a;     // its action
 };
-// The edge pool keeps the halves apart, blocked by edge page: page k is 24 KB — the 16-byte
-// EdgeStat records of its EPG edges, then their 8-byte EdgeLink records. k_backup's per-level
-// arg-max scans read only EdgeStat (a node's statistics are contiguous: 8 edges per 128-byte
-// line), the descent reads links from its NodeStat copy, the root scan requests both halves
-// in one round trip; 24 bytes per edge (round 2's records: 32) is what lets config 4's
-// steady-state trees fit. A node's CSR run never straddles an edge page, so a run is one
-// page base plus an offset. EdgePtr / EdgeRef give the pool the syntax of an Edge array:
-// E[i].s, E[i].k, E + i.
-struct EdgeRef {
-    EdgeStat &s;
-    EdgeLink &k;
-    __device__ __forceinline__ operator Edge() const { return Edge{s, k}; }
-};
-struct EdgePtr {           // edges of one run (within one edge page): page base + offset
-    char *pg;
-    int o;
-    static constexpr int EPG_ = 1 << 10;
-    static constexpr int64_t PAGE_BYTES = (int64_t)EPG_ * (sizeof(EdgeStat) + sizeof(EdgeLink));
-    __device__ __forceinline__ EdgeRef operator[](int64_t j) const {
-        return EdgeRef{reinterpret_cast<EdgeStat *>(pg)[o + j],
-                       reinterpret_cast<EdgeLink *>(pg + EPG_ * sizeof(EdgeStat))[o + j]};
-    }
-    __device__ __forceinline__ EdgePtr operator+(int64_t j) const { return EdgePtr{pg, o + (int)j}; }
-};
-struct EdgePool {          // the whole pool, by global edge index
-    char *base;
-    __device__ __forceinline__ EdgePtr operator+(int64_t i) const {
-        return EdgePtr{base + (i >> 10) * EdgePtr::PAGE_BYTES, (int)(i & (EdgePtr::EPG_ - 1))};
-    }
-    __device__ __forceinline__ EdgeRef operator[](int64_t i) const { return (*this + i)[0]; }
-};
+static_assert(sizeof(VisitRec) == 24, "VisitRec layout");
+constexpr int REC_UNITS = 3;
 
-// a node's visit statistics (Ns, Qs) and its cached arg-max edge, one 32-byte record.
+// a node's allocation: its run and visit block (global unit indices), or, for a terminal
+// node, its end values (the first 16 bytes hold es[4])
+struct NodeRun {
+    int64_t eb;      // run base
+    int64_t vb;      // visit block base
+    int16_t ec;      // edges (legal actions; 0: terminal)
+    int16_t vcnt;    // visit records in use
+    int16_t vcap;    // visit block capacity (records)
+    int16_t cand;    // lowest rank without a visit record (ec: none) = the best unvisited edge
+};
+static_assert(sizeof(NodeRun) == 24, "NodeRun layout");
+
+// a node's visit statistics (Ns, Qs) and its cached arg-max, one 32-byte record.
 // pick_highest_UCB (MCTS.py:199-219) at a non-root node reads only that node's Ns, Qs and its
 // edges' P, N, Q; all of them change only when a simulation backs up through the node (priors
 // change only at a root: Dirichlet noise, :150-154; forced playouts are root-only, :157). So the
 // arg-max k_backup computes right after a node's update is exactly the edge the next descent
-// through the node picks: the descent follows `best` and the link copied from that edge (one
-// 32-byte load per level, no edge scan). The root level always scans. Invariant (k_backup,
-// k_select's links, k_gc's remap): bchild == the link of edge best, {bcec, bceb} == that
-// child's CSR range (bcec -1: terminal).
+// through the node picks: the descent follows `best` and its link (one 32-byte load per level,
+// no edge scan). The root level scans when its priors were just noised or forced playouts are
+// on. Invariant (k_backup, k_select's links, k_gc's remap): bchild is the child of edge `best`
+// (-1: not linked), bterm whether that child is terminal.
 struct __align__(16) NodeStat {
     double qs;       // Qs
     int32_t ns;      // Ns
-    int16_t best;    // cached arg-max: edge offset in the CSR run (-1: unknown, scan)
+    int16_t best;    // cached arg-max: rank of the edge in the run (-1: unknown, scan)
     int16_t ba;      // its action
     int32_t bchild;  // its child (global id, -1: not linked)
-    int16_t bcec;    // the child's CSR count (-1: terminal)
-    int16_t pad;
-    int64_t bceb;    // the child's CSR base (global edge index)
+    int32_t bterm;   // 1: that child is terminal (its values in nrun)
+    int64_t pad;
 };
 static_assert(sizeof(NodeStat) == 32, "NodeStat layout");
 
-// Per-GPU shared arena. Nodes and edges live in pools shared by all trees and
-// are handed out in pages: node page = NPG consecutive global node ids, edge page = EPG
-// consecutive global edge indices. A tree holds a list of node pages and a list of edge
-// pages (its page tables, in allocation order) and addresses everything by GLOBAL id: child
-// links, cached child CSR ranges, the path, the root and the transposition table hold global
-// ids, so the descent never translates. A tree's "local" node index (0 .. node_count) is its
-// allocation order (slot i = page ntab[i / NPG], offset i % NPG); its edges are contiguous per
-// node and never straddle an edge page. Pages are popped from the free stacks by k_select /
-// k_backup only and pushed back by k_gc / k_commit / k_set_roots / k_reset_games only, so
-// pops and pushes never share a launch (an array stack with one atomic top is then exact).
+// Per-GPU shared arena. Nodes and edge units live in pools shared by all trees
+// and are handed out in pages: node page = NPG consecutive global node ids, edge page = UPG
+// consecutive global unit indices. A tree holds a list of node pages and a list of edge pages
+// (its page tables, in allocation order) and addresses everything by GLOBAL id: child links,
+// the path, the root and the transposition table hold global ids, so the descent never
+// translates. A tree's "local" node index (0 .. node_count) is its allocation order (slot i =
+// page ntab[i / NPG], offset i % NPG). Runs and visit blocks never straddle an edge page. Pages
+// are popped from the free stacks by k_select / k_backup only and pushed back by k_gc /
+// k_commit / k_set_roots / k_reset_games only, so pops and pushes never share a launch (an
+// array stack with one atomic top is then exact).
 constexpr int NPG_SHIFT = 6, NPG = 1 << NPG_SHIFT;     // nodes per node page
-constexpr int EPG_SHIFT = 10, EPG = 1 << EPG_SHIFT;    // edges per edge page (> 409)
-static_assert(EPG == EdgePtr::EPG_, "edge pool blocking = edge page");
+constexpr int UPG_SHIFT = 11, UPG = 1 << UPG_SHIFT;    // units per edge page (16 KB): a node's
+                                                       // run + block is at most 409 x (1 + 3)
+static_assert(UPG >= 4 * 409, "a node's allocation fits one edge page");
 
 struct Pools {
-    int nmax, emax, hcap, pcap;          // per tree: node slots, edges (page tables), hash slots, path
-    int nptab, eptab;                    // page-table entries per tree (nmax / NPG, emax / EPG)
+    int nmax, emax, hcap, pcap;          // per tree: node slots, edge units (page tables), hash
+                                         // slots, path levels
+    int nptab, eptab;                    // page-table entries per tree (nmax / NPG, emax / UPG)
     int npages, epages;                  // pages in the pools
     TreeHdr *hdr;
     uint64_t *nkey0, *nkey1;             // node pool, indexed by global node id
-    int64_t *neb;
-    int32_t *nec, *nround;
-    NodeStat *nst;                       // visit count and value of every node (one 16-byte load)
+    int32_t *nround;
+    NodeStat *nst;                       // statistics + cached arg-max of every node
+    NodeRun *nrun;                       // its run / visit block (terminal: end values)
     int8_t *nterm;
-    float *nes;                          // 4 terminal values per node
-    EdgePool ed;                         // edge pool: UCB inputs | action, child, child's CSR range
+    uint64_t *eu;                        // edge unit pool (EdgeP runs, VisitRec blocks)
     int32_t *ntab, *etab;                // B x nptab / B x eptab page tables
     int32_t *npidx, *epidx;              // per page: its index in the owning tree's page table
     int32_t *nfree, *efree;              // free page stacks
     int32_t *alloc;                      // [0] / [1] free node / edge pages (stack tops),
                                          // [2] / [3] failed node / edge page requests
     int32_t *hslot;                      // B x hcap transposition table (global node ids)
-    int32_t *path_n;                     // B x pcap descent path: node (global id)
-    int64_t *path_e;                     // B x pcap and the edge taken (global index)
-    int32_t *path_x;                     // B x pcap its offset in the node's CSR run | count << 16
+    int32_t *path_n;                     // B x (pcap + 1) descent path: node (global id); entry
+                                         // `depth` = the leaf's node when it is stored
+    int32_t *path_x;                     // B x pcap the edge taken: rank | action << 9
+    int64_t *path_b;                     // B x pcap k_backup scratch: a level's new visit block
     int32_t *gscr;                       // k_gc scratch, GC_WG x gc_stride ints
     size_t gc_stride;
     int8_t *nbrd;                        // per node slot its canonical board (LDS row format), or
@@ -172,20 +162,26 @@ struct Pools {
     int32_t *counters;                   // [0] queued examples [1] dropped [2] GC queue
                                          // [5] example-row queue [4] k_gc workgroups done
                                          // [6] [7] deep / other trees filed by k_leaf_mask
+                                         // [8] should-collections taken by this k_gc launch
+                                         // [9] deferred entries (gcq2)
     int32_t *gcq;                        // B: trees whose garbage collection k_gc runs
+    int32_t *gcq2;                       // B: entries deferred to the next k_gc launch
     int2 *flq;                           // out_cap: (staging row, queue slot) rows k_gc copies
     int32_t *order;                      // B: the trees in k_select's launch order (deep first)
+
+    __device__ __forceinline__ EdgeP *ep(int64_t u) const { return reinterpret_cast<EdgeP *>(eu + u); }
+    __device__ __forceinline__ VisitRec *vr(int64_t u) const { return reinterpret_cast<VisitRec *>(eu + u); }
 };
 
-// tree t's local node slot i / local (virtual) edge position v -> global
+// tree t's local node slot i / local (virtual) unit position v -> global
 __device__ __forceinline__ int node_g(const Pools &P, int t, int i) {
     return P.ntab[(size_t)t * P.nptab + (i >> NPG_SHIFT)] * NPG + (i & (NPG - 1));
 }
 __device__ __forceinline__ int node_l(const Pools &P, int g) {
     return P.npidx[g >> NPG_SHIFT] * NPG + (g & (NPG - 1));
 }
-__device__ __forceinline__ int64_t edge_g(const Pools &P, int t, int v) {
-    return (int64_t)P.etab[(size_t)t * P.eptab + (v >> EPG_SHIFT)] * EPG + (v & (EPG - 1));
+__device__ __forceinline__ int64_t unit_g(const Pools &P, int t, int v) {
+    return (int64_t)P.etab[(size_t)t * P.eptab + (v >> UPG_SHIFT)] * UPG + (v & (UPG - 1));
 }
 
 // per-node board slot (Pools::nbrd): the LDS row format padded to 16 bytes
@@ -199,7 +195,7 @@ struct SearchCfg {
     double cpuct, fpu, dir_alpha, dir_temp, prob_full;
     int num_sims, ratio_full, forced_playouts, dirichlet;
     int temp_threshold, selfplay;
-    int edge_reserve;                    // edges reserved per simulation at search start
+    int edge_reserve;                    // edge units reserved per simulation at search start
     uint64_t seed;
     uint32_t board_base;
 };

@@ -29,9 +29,9 @@ HDR_DTYPE = np.dtype([
     ("leaf_kind", "<i4"), ("player", "<i4"), ("episode_step", "<i4"), ("move_no", "<i4"),
     ("game_no", "<i4"), ("overflow", "<i4"), ("n_examples", "<i4"), ("leaf_round", "<i4"),
     ("leaf_k0", "<u8"), ("leaf_k1", "<u8"), ("leaf_v", "<f4", (4,)),
-    ("games_done", "<i4"), ("forced", "<i4"), ("moves", "<i4"), ("root_ec", "<i4"),
+    ("games_done", "<i4"), ("forced", "<i4"), ("moves", "<i4"), ("pad0", "<i4"),
     ("prunes", "<i4"), ("resets", "<i4"), ("unexpanded", "<i4"), ("gc_state", "<i4"),
-    ("root_eb", "<i8"), ("enext", "<i8"),
+    ("units_gc", "<i8"), ("enext", "<i8"),
     ("npg", "<i4"), ("epg", "<i4"), ("eleft", "<i4"), ("live_gc", "<i4"),
     ("root_round", "<i4"), ("gc_queued", "<i4"), ("withdrawals", "<i4"), ("gcs", "<i4"),
     ("leaf_hslot", "<i4"), ("leaf_slot", "<i4"), ("depth_max", "<i4"), ("depth_sum", "<i4")])
@@ -109,8 +109,10 @@ class BatchedMCTS:
         self._hdr = torch.empty((B, HDR_DTYPE.itemsize // 4), dtype=torch.int32, device=dev)
 
     MEM_FRACTION = 0.8      # of the device's free memory a default-sized arena may take
-    EDGES_PER_NODE = 15     # pool edge:node ratio (live trees: 15-19 edges per node, profiles/r03_tree_sizes_*;
-                            # node slots are ~65 B, so erring towards nodes is cheap)
+    UNITS_PER_NODE = 20     # pool edge-unit : node-slot ratio (8-byte units: one per edge, three per
+                            # edge with statistics; live trees ~16 edges + ~4 units of visit records
+                            # per node, profiles/r04_tree_sizes_*); node slots are ~85 B, so erring
+                            # towards nodes is cheap
     NODE_MAX = 45056        # per-tree node maximum (transposition table 64 K slots at most)
 
     @staticmethod
@@ -123,12 +125,13 @@ class BatchedMCTS:
 
     def _plan(self, engine, B, sims, cfg, node_cap, edge_cap, pool_nodes, pool_edges, auto_boards, mem_budget):
         """Tree maxima and the shared pools. node_cap / edge_cap: the largest
-        single tree (transposition table, page tables); pool_nodes / pool_edges: node slots
-        and edges shared by all B trees. Explicit caps without pools keep the static
-        layout (pool = B x cap). Default: pools fill MEM_FRACTION of the free HBM (or
-        mem_budget bytes) at EDGES_PER_NODE edges per node slot; node boards (a speed
-        option) are kept when the pools then still hold 8 x sims + 512 node slots per tree,
-        else dropped first: capacity (the reference's exact table) wins over descent speed."""
+        single tree (transposition table, page tables; edge_cap in 8-byte edge units);
+        pool_nodes / pool_edges: node slots and edge units shared by all B trees. Explicit caps
+        without pools keep the static layout (pool = B x cap). Default: pools fill
+        MEM_FRACTION of the free HBM (or mem_budget bytes) at UNITS_PER_NODE units per node
+        slot; node boards (a speed option) are kept when the pools then still hold 8 x sims +
+        512 node slots per tree, else dropped first: capacity (the reference's exact table)
+        wins over descent speed."""
         nc = int(node_cap or self.default_node_cap(sims))
         ec = int(edge_cap or 32 * nc)
         cfg.node_cap, cfg.edge_cap = nc, ec
@@ -142,7 +145,7 @@ class BatchedMCTS:
             cfg.pool_edges = cfg.pool_edges or B * ec
             return
         budget = int(mem_budget) if mem_budget else int(self.MEM_FRACTION * torch.cuda.mem_get_info(engine.device)[0])
-        R = self.EDGES_PER_NODE
+        R = self.UNITS_PER_NODE
 
         def plan(pn):
             cfg.pool_nodes, cfg.pool_edges = int(pn), int(pn) * R
@@ -170,7 +173,7 @@ class BatchedMCTS:
         f = out.tolist()
         return {"free_node_pages": f[0], "free_edge_pages": f[1], "node_page_misses": f[2],
                 "edge_page_misses": f[3], "node_pages": int(pages[0]), "edge_pages": int(pages[1]),
-                "nodes_per_page": int(pages[2]), "edges_per_page": int(pages[3])}
+                "nodes_per_page": int(pages[2]), "units_per_page": int(pages[3])}
 
     def __del__(self):
         if getattr(self, "h", None) is not None:

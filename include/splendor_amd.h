@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 5
+#define SPL_ABI_VERSION 6
 #define SPL_ACTIONS 409
 #define SPL_MASK_WORDS 7
 #define SPL_EINVAL (-1)
@@ -150,7 +150,10 @@ typedef struct {
     int temp_threshold;      /* tempThreshold (Coach.py:82-83), self-play only */
     int node_cap;            /* maximum node slots of one tree (its transposition table and
                                 node page table are sized for it) */
-    int edge_cap;            /* maximum CSR edges of one tree (its edge page table) */
+    int edge_cap;            /* maximum edge units of one tree (its edge page table). Edges are
+                                stored in two tiers of 8-byte units: every edge one unit (prior,
+                                action) in its node's run, and an edge with statistics (Nsa,
+                                Qsa, child link) 3 more in its node's visit block */
     uint64_t seed;           /* Philox key for search/self-play randomness */
     uint32_t board_base;     /* global id of tree 0 (multi-GPU sharding) */
     int selfplay;            /* 1: trees play games (spl_mcts_reset_games / spl_mcts_commit) */
@@ -160,10 +163,10 @@ typedef struct {
                                 transition (getNextState, MCTS.py:155-157) — the descent then
                                 runs one transition per simulation instead of one per level */
     long long pool_nodes;    /* node slots shared by all B trees (0: B x node_cap) */
-    long long pool_edges;    /* edges shared by all B trees (0: B x edge_cap). Trees draw node
-                                pages (64 slots) and edge pages (1024 edges) from these pools
-                                on demand and return them when garbage is collected, so memory
-                                follows the sum of the live trees, not B x the largest one */
+    long long pool_edges;    /* edge units shared by all B trees (0: B x edge_cap). Trees draw
+                                node pages (64 slots) and edge pages (2048 units) from these
+                                pools on demand and return them when garbage is collected, so
+                                memory follows the sum of the live trees, not B x the largest */
 } spl_mcts_config;
 
 int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_mcts **out);
@@ -251,7 +254,7 @@ int spl_mcts_counters(spl_mcts *m, int32_t *out, void *hip_stream);
  * unexpanded in its tree's header). pool_pages (host): pages in the node / edge pools and
  * their sizes (node slots / edges per page). */
 int spl_mcts_pool_state(spl_mcts *m, int32_t *out, void *hip_stream);
-int spl_mcts_pool_pages(const spl_mcts *m, long long *out4);
+int spl_mcts_pool_pages(const spl_mcts *m, long long *out4);   /* pages, pages, NPG, units/page */
 int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *valid,
                             float *winner, int32_t *scdiff, float *q, int32_t *meta, int max,
                             int32_t *n_out, void *hip_stream);

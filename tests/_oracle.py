@@ -241,7 +241,7 @@ def depth_stats(reset=True):
 def selfplay_run(n, B, iters, seed, num_sims, ratio_full, prob_full, cpuct, fpu, forced, temp_threshold,
                  board_base=0, max_ex=20000, dir_alpha=0.0, dir_temp=1.25, fake_mode=0):
     """Oracle of the device self-play loop (spl_mcts_commit semantics). fake_mode: the hash
-    network's mode (0 spread, 1 flat); the result's "depth" = (sum, max, count) of its
+    network's mode (0 spread, 1 peaked); the result's "depth" = (sum, max, count) of its
     simulations' leaf depths."""
     set_fake_mode(fake_mode)
     depth_stats(reset=True)

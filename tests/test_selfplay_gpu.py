@@ -355,12 +355,32 @@ def _deep_device(n, B, iters, sims=100, seed=11, **kw):
     return hdr, st, ex
 
 
+def _oracle_lagged(n, B, iters, seed, sims, lag):
+    """The oracle's self-play loop (peaked hash network, genbu arguments) where tree t runs
+    iters - lag[t] iterations: a withdrawn simulation repeats in the next iteration, so a tree
+    that withdrew w times is exactly w simulations behind. Runs of trees with equal lag go
+    together (every draw is keyed by the global board id)."""
+    args = (sims, GENBU["ratio"], GENBU["prob_full"], GENBU["cpuct"], GENBU["fpu"], False, 10)
+    kw = dict(max_ex=60000, dir_alpha=0.3, dir_temp=1.25, fake_mode=1)
+    lag = np.asarray(lag, np.int64)
+    parts, t0 = [], 0
+    while t0 < B:
+        t1 = t0 + 1
+        while t1 < B and lag[t1] == lag[t0]:
+            t1 += 1
+        parts.append(O.selfplay_run(n, t1 - t0, iters - int(lag[t0]), seed, *args, board_base=t0, **kw))
+        t0 = t1
+    ref = {k: np.concatenate([p[k] for p in parts]) for k in parts[0] if k != "depth"}
+    d = [p["depth"] for p in parts]
+    ref["depth"] = (sum(x[0] for x in d), max(x[1] for x in d), sum(x[2] for x in d))
+    return ref
+
+
 def _deep_selfplay(n, B, iters, sims=100, seed=11, device_run=None, **kw):
     """Self-play with the peaked hash network (mode 1: the random-init SplendorNNet's regime:
     deep trees, long terminal lines) against the oracle's sequential loop, bit for bit."""
     hdr, st, ex = device_run or _deep_device(n, B, iters, sims, seed, **kw)
-    ref = O.selfplay_run(n, B, iters, seed, sims, GENBU["ratio"], GENBU["prob_full"], GENBU["cpuct"], GENBU["fpu"],
-                         False, 10, max_ex=60000, dir_alpha=0.3, dir_temp=1.25, fake_mode=1)
+    ref = _oracle_lagged(n, B, iters, seed, sims, hdr["withdrawals"])
     rh = ref["hdr"]
     for k, j in (("player", 0), ("episode_step", 1), ("move_no", 2), ("game_no", 3), ("games_done", 4),
                  ("moves", 5), ("sims_done", 6)):
@@ -399,7 +419,7 @@ def test_withdrawals_repeat_the_same_simulation():
     from splendor.mcts import BatchedMCTS
     n, B, iters = 2, 64, 2000
     nc = BatchedMCTS.default_node_cap(100)
-    ratio = BatchedMCTS.EDGES_PER_NODE
+    ratio = BatchedMCTS.UNITS_PER_NODE
 
     def run(per_tree):
         return _deep_device(n, B, iters, pool_nodes=B * per_tree, pool_edges=B * per_tree * ratio,
