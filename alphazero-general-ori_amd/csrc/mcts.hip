@@ -1506,6 +1506,292 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
 #endif
 }
 
+// ------------------------------------------------------------ select, lane per tree
+// k_select_lanes: the same descent as k_select with one LANE per tree (64 trees per wave).
+// Below the root a level is one 32-byte NodeStat load (the cached arg-max and its link), work
+// for a single lane, so a wave per tree leaves 63 lanes idle and the launch is bound by wave
+// slots x the chain latency; lane per tree keeps 64 chains in flight per wave. The steps that
+// need a board — the in-tree transition at the edge to expand (MCTS.py:227-235), the
+// fingerprint lookup (:119-120), the end check (:125) and the new leaf's board — run per lane
+// on the lane's own LDS board. Root scans (a root whose priors were just noised, forced
+// playouts, a new root) and root noise stay wave-collective, one tree at a time (rare).
+// Results are identical to k_select's (same picks, paths, leaves, links).
+
+// swap_players on a lane's own LDS board, in place: every player block rotated left by its
+// stride (gems k, nobles 3k — hard-coded 3, SplendorLogicNumba.py:345 —, cards k, reserved
+// 6k rows; wave_roll_players' mapping) by three reversals
+template <int N>
+__device__ __forceinline__ void lane_roll_players(int8_t *s, int k) {
+    using Lx = Lay<N>;
+    auto rev = [&](int a, int b) {
+        for (--b; a < b; a++, b--) {
+            const uint64_t x = row(s, a);
+            row(s, a) = row(s, b);
+            row(s, b) = x;
+        }
+    };
+    auto rot = [&](int base, int m, int sh) {
+        sh %= m;
+        if (!sh) return;
+        rev(base, base + sh);
+        rev(base + sh, base + m);
+        rev(base, base + m);
+    };
+    rot(Lx::GEMS, N, k);
+    rot(Lx::GEMS + N, N * Lx::NN, 3 * k);
+    rot(Lx::GEMS + N + N * Lx::NN, N, k);
+    rot(Lx::GEMS + 2 * N + N * Lx::NN, 6 * N, 6 * k);
+}
+// the wave_fingerprint of a lane's own board
+template <int N>
+__device__ __forceinline__ void lane_fingerprint(const int8_t *s, uint64_t &k0, uint64_t &k1) {
+    uint64_t a = 0, b = 0;
+    for (int i = 0; i < Lay<N>::ROWS; i++) {
+        const uint64_t x = row(s, i) | ((uint64_t)i << 56);
+        a ^= mix64(x ^ 0x243F6A8885A308D3ull);
+        b ^= mix64(x ^ 0x13198A2E03707344ull);
+    }
+    k0 = a;
+    k1 = b | 1ull;
+}
+// the in-tree transition of one lane's board (MCTS.py:227-235): make_move(a, 0, det) + roll
+template <int N>
+__device__ __forceinline__ void lane_tree_step(int8_t *s, int a) {
+    Chance ch{nullptr, 0, 0, 0, 0};
+    int nxt;
+    switch (move_kind_of(a)) {
+        case MK_GEMS: nxt = make_move<N, MK_GEMS>(s, a, 0, true, ch); break;
+        case MK_BUY: nxt = make_move<N, MK_BUY>(s, a, 0, true, ch); break;
+        case MK_RESERVE: nxt = make_move<N, MK_RESERVE>(s, a, 0, true, ch); break;
+        default: nxt = make_move<N, MK_BUY_RESERVED>(s, a, 0, true, ch); break;
+    }
+    if (nxt) lane_roll_players<N>(s, nxt);
+}
+
+#ifndef PATH_CHUNK
+#define PATH_CHUNK 8       // previous-path levels a lane checks per round trip
+#endif
+enum { LS_DESCEND = 0, LS_EXPAND = 1, LS_DONE = 2 };
+
+template <int N>
+__global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B, int lim,
+                                                     int8_t *__restrict__ leaf_state,
+                                                     uint8_t *__restrict__ leaf_valid,
+                                                     int32_t *__restrict__ leaf_count) {
+    using Lx = Lay<N>;
+    constexpr int ST = (Lx::ROWS % 2 ? Lx::ROWS : Lx::ROWS + 1) * 8;   // odd row count per board:
+    __shared__ __align__(16) int8_t boards[64 * ST];                    // lanes on distinct banks
+    __shared__ RunScr scr;                                              // root noise (one tree)
+    const int l = lane_id();
+    const int slot = blockIdx.x * 64 + l;
+    if (blockIdx.x == 0 && l < 2) P.counters[6 + l] = 0;     // k_leaf_mask's filing counters
+    if (blockIdx.x == 0 && l == 2 && leaf_count) *leaf_count = 0;
+    const bool live = slot < B;
+    const int t = live ? P.order[slot] : 0;
+    TreeHdr *H = P.hdr + t;
+    int8_t *s = boards + l * ST;
+    int sims = 0, root = -1, hdepth = 0, mv = 0;
+    bool act = false, noise = false, forced = false;
+    if (live) {
+        sims = H->sims_done;
+        act = sims < H->budget && !H->overflow;
+        root = H->root; hdepth = H->depth; mv = H->move_no;
+        noise = H->noise_pending != 0; forced = H->forced != 0;
+        if (!act) { leaf_valid[t] = 0; H->leaf_kind = LEAF_NONE; }
+    }
+    const uint64_t *nbrd = reinterpret_cast<const uint64_t *>(P.nbrd);
+    const int32_t pstride = P.pcap + 1;
+    int32_t *path_n = P.path_n + (size_t)t * pstride;
+    int32_t *path_x = P.path_x + (size_t)t * P.pcap;
+    // boards the lane needs from the start: the root's when it is the leaf, or without node
+    // boards (the transition then runs at every level, from the root)
+    if (act && (root < 0 || !nbrd))
+        for (int u = 0; u < Conv<N>::UNITS; u++) Conv<N>::load(s, P.root_state + (size_t)t * Lx::S, u);
+    // root noise on kept roots (:150-154), wave-collective one tree at a time
+    const bool noised = act && root >= 0 && sims == 0 && noise;
+    for (uint64_t m = __ballot(noised); m; m &= m - 1) {
+        const int j = __ffsll((unsigned long long)m) - 1;
+        const int tj = __builtin_amdgcn_readlane(t, j), rj = __builtin_amdgcn_readlane(root, j);
+        NodeRun r = P.nrun[rj];
+        r.eb = (int64_t)uniform64((uint64_t)r.eb); r.vb = (int64_t)uniform64((uint64_t)r.vb);
+        r.ec = (int16_t)uniform(r.ec);
+        const int cand = noise_kept_root(P, C, tj, r, ST_DIR | (uint32_t)__builtin_amdgcn_readlane(mv, j), scr);
+        if (l == 0) {
+            P.hdr[tj].noise_pending = 0;                 // (a withdrawn simulation must not re-noise)
+            P.nrun[rj].cand = (int16_t)cand;
+            P.nst[rj].best = -1;                         // ranks moved: the root scans
+        }
+        wave_lds_fence();
+    }
+    __threadfence_block();
+    const bool root_cache = !forced && !noised;
+    int node = root, depth = 0, state = act && root >= 0 ? LS_DESCEND : LS_DONE;
+    int kind = act ? LEAF_NN : LEAF_NONE;
+    // resume on the previous simulation's path (same search: sims > 0; k_gc clears H->depth
+    // when it moves nodes) at the first level whose node's cached pick no longer is the path's
+    // edge, or the previous leaf's parent; PATH_CHUNK levels per round trip
+    if (state == LS_DESCEND && sims > 0 && hdepth > 0) {
+        int q = hdepth - 1;
+        bool found = false;
+        for (int d0 = 0; d0 < hdepth && !found; d0 += PATH_CHUNK) {
+            int pn[PATH_CHUNK], px[PATH_CHUNK];
+#pragma unroll
+            for (int k = 0; k < PATH_CHUNK; k++) {
+                pn[k] = 0; px[k] = -1;
+                if (d0 + k < hdepth) { pn[k] = path_n[d0 + k]; px[k] = path_x[d0 + k]; }
+            }
+            int bk[PATH_CHUNK];
+#pragma unroll
+            for (int k = 0; k < PATH_CHUNK; k++) bk[k] = d0 + k < hdepth ? P.nst[pn[k]].best : -2;
+#pragma unroll
+            for (int k = 0; k < PATH_CHUNK; k++) {
+                const int d = d0 + k;
+                if (!found && d < hdepth && (bk[k] != px_off(px[k]) || (d == 0 && !root_cache))) { q = d; found = true; }
+            }
+        }
+        node = path_n[q];
+        depth = q;
+        if (!nbrd)                                       // the resume node's board: the path's moves
+            for (int d = 0; d < q; d++) lane_tree_step<N>(s, px_action(path_x[d]));
+    }
+    // the root level scans when its cached pick does not hold (noise, forced playouts, a new
+    // root): wave-collective, one tree at a time, before the lanes descend
+    Pick pk{0, 0, -1, 0};
+    bool have_pk = false;
+    NodeStat nsq{0.0, 0, -1, 0, -1, 0, 0};
+    if (state == LS_DESCEND) nsq = P.nst[node];
+    const bool scan = state == LS_DESCEND && depth == 0 && (!root_cache || nsq.best < 0);
+    for (uint64_t m = __ballot(scan); m; m &= m - 1) {
+        const int j = __ffsll((unsigned long long)m) - 1;
+        const int nj = __builtin_amdgcn_readlane(node, j);
+        NodeRun r = P.nrun[nj];
+        r.eb = (int64_t)uniform64((uint64_t)r.eb); r.vb = (int64_t)uniform64((uint64_t)r.vb);
+        r.ec = (int16_t)uniform(r.ec);
+        const Pick p = scan_run(P, r, __builtin_amdgcn_readlane(nsq.ns, j), readlane_f64(nsq.qs, j), C.cpuct, C.fpu,
+                                __builtin_amdgcn_readlane((int)forced, j) != 0, __builtin_amdgcn_readlane(sims, j));
+        if (l == j) { pk = p; have_pk = true; }
+    }
+    if (have_pk) {                                       // the scanned edge's link and whether terminal
+        if (pk.child < 0 && pk.e == nsq.best && !noised) { pk.child = nsq.bchild; pk.cterm = nsq.bterm; }
+        else pk.cterm = pk.child >= 0 ? (int)P.nterm[pk.child] : 0;
+    }
+    bool have_nsq = state == LS_DESCEND;
+    int bnode = nbrd ? -1 : node;                        // the node whose board the lane holds
+    int miss = -1, leaf_node = -1, cbest = -1;
+    uint64_t k0 = 0, k1 = 0;
+    float val[4] = {0, 0, 0, 0};
+    int pend = -1, pend_n = 0, pend_x = 0;
+    while (__ballot(state != LS_DONE)) {
+        if (state == LS_DESCEND) {
+            if (depth >= P.pcap) {
+                state = LS_DONE; kind = LEAF_NONE; H->overflow = 2;
+            } else {
+                if (!have_pk) {                          // ONE 32-byte load per level
+                    if (!have_nsq) nsq = P.nst[node];
+                    pk = Pick{nsq.best, nsq.ba, nsq.bchild, nsq.bterm};
+                }
+                have_pk = false; have_nsq = false;
+                cbest = nsq.best;
+                if (pend >= 0) { path_n[pend] = pend_n; path_x[pend] = pend_x; }
+                pend = depth; pend_n = node; pend_x = px_pack(pk.e, pk.a);
+                depth++;
+                if (pk.child >= 0 && pk.cterm) {         // a terminal child (MCTS.py:125-132)
+                    kind = LEAF_TERMINAL;
+                    term_values(P, pk.child, val);
+                    leaf_node = pk.child;
+                    state = LS_DONE;
+                } else if (pk.child >= 0 && nbrd) {      // linked: no transition needed
+                    node = pk.child;
+                } else {
+                    state = LS_EXPAND;
+                }
+            }
+        }
+        if (state == LS_EXPAND) {
+            if (nbrd && bnode != node) {                 // stage this node's stored board
+                const uint64_t *src = nbrd + (size_t)node * (NodeBoard<N>::BYTES / 8);
+                for (int r = 0; r < Lx::ROWS; r++) row(s, r) = src[r];
+            }
+            lane_tree_step<N>(s, pk.a);
+            int child = pk.child;
+            const bool cached = cbest == pk.e;
+            if (child < 0) {
+                lane_fingerprint<N>(s, k0, k1);
+                child = hash_lookup(P, t, k0, k1, &miss);
+                if (child >= 0) {                        // transposition: link the cached pick
+                    const int ct = P.nterm[child];
+                    if (cached) { P.nst[node].bchild = child; P.nst[node].bterm = ct; }
+                    if (ct) {
+                        kind = LEAF_TERMINAL;
+                        term_values(P, child, val);
+                        leaf_node = child;
+                        state = LS_DONE;
+                    }
+                }
+            }
+            if (state == LS_EXPAND) {
+                if (child >= 0) {                        // continue below the linked node
+                    node = child;
+                    bnode = child;
+                    state = LS_DESCEND;
+                } else {
+                    float es[N];
+                    check_end<N>(s, es);                 // MCTS.py:125
+                    bool any = false;
+#pragma unroll
+                    for (int i = 0; i < N; i++) any |= es[i] != 0.f;
+                    if (any) {
+                        kind = LEAF_TERMINAL;
+#pragma unroll
+                        for (int i = 0; i < N; i++) val[i] = es[i];
+                        const int id = H->node_count;
+                        const int g = node_slot(P, H, t, id);
+                        if (g < 0) {                     // no room: back up, do not store
+                            H->unexpanded += 1;
+                        } else {
+                            P.nkey0[g] = k0; P.nkey1[g] = k1;
+                            P.nrun[g] = term_run(val);
+                            P.nst[g] = NodeStat{0.0, 0, -1, 0, -1, 0, 0};
+                            P.nround[g] = (uint8_t)bt(row(s, 0), 6); P.nterm[g] = 1;
+                            hash_insert(P, t, k0, g);
+                            if (cached) { P.nst[node].bchild = g; P.nst[node].bterm = 1; }
+                            H->node_count = id + 1;
+                        }
+                        leaf_node = g;
+                    }
+                    state = LS_DONE;                     // terminal, or a new NN leaf
+                }
+            }
+        }
+    }
+    if (pend >= 0) { path_n[pend] = pend_n; path_x[pend] = pend_x; }
+    if (act && root < 0) lane_fingerprint<N>(s, k0, k1);   // the root itself is the leaf
+    if (act && kind == LEAF_NN) {                        // its board for k_leaf_mask / the network
+        for (int u = 0; u < Conv<N>::UNITS; u++) Conv<N>::store(leaf_state + (size_t)t * Lx::S, s, u);
+        int g = -1;
+        if (P.nbrd) {                                    // the slot k_backup will insert it at
+            g = node_slot(P, H, t, H->node_count);
+            if (g >= 0) {
+                uint64_t *dst = reinterpret_cast<uint64_t *>(P.nbrd + (size_t)g * NodeBoard<N>::BYTES);
+                for (int r = 0; r < Lx::ROWS; r++) dst[r] = row(s, r);
+            }
+        }
+        H->leaf_slot = g;
+    }
+    if (act) {
+        H->depth = depth;
+        H->leaf_kind = kind;
+        H->leaf_hslot = kind == LEAF_NN ? miss : -1;
+        if (kind != LEAF_NN) H->leaf_slot = -1;
+        H->leaf_k0 = k0; H->leaf_k1 = k1;
+        H->leaf_round = (uint8_t)bt(row(s, 0), 6);
+#pragma unroll
+        for (int i = 0; i < 4; i++) H->leaf_v[i] = val[i];
+        leaf_valid[t] = kind == LEAF_NN;
+        path_n[depth] = kind == LEAF_TERMINAL ? leaf_node : -1;
+    }
+}
+
 // ------------------------------------------------------------ leaf masks
 // getValidMoves(leaf, 0) (MCTS.py:136) for every NN leaf of a select, lane per leaf, 64
 // leaves per workgroup: the rollout kernel's factorised predicate and mask-word phases
@@ -1735,7 +2021,9 @@ __device__ __forceinline__ void load_levels(const Pools &P, int t, int g0, int d
         const VisitRec v = *P.vr(V.r.vb + REC_UNITS * V.e.vi);
         V.n = v.n; V.q = v.q; V.rchild = v.child;
     } else if (V.r.vcnt == V.r.vcap) {
-        V.grow = V.r.vcap == 0 ? 1 : min(2 * (int)V.r.vcap, (int)V.r.ec);
+        // blocks double; a root's takes room for every edge at once (a root gains visited
+        // edges fastest, and its block then never moves again during the search)
+        V.grow = d == 0 ? (int)V.r.ec : (V.r.vcap == 0 ? 1 : min(2 * (int)V.r.vcap, (int)V.r.ec));
     }
 }
 
@@ -1780,8 +2068,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     const int cnt0 = min(depth, 64);
     Level V;
     load_levels(P, t, 0, depth, lid, V, l < cnt0);
-    bool fail = false;
-    for (int g0 = 0; g0 < depth && !fail; g0 += 64) {
+    bool fail = false;                                   // a visit block found no room
+    for (int g0 = 0; g0 < depth; g0 += 64) {
         Level Vg;
         if (g0 > 0) load_levels(P, t, g0, depth, lid, Vg, g0 + l < depth);
         const int grow = g0 == 0 ? V.grow : Vg.grow;
@@ -1792,13 +2080,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             gm &= gm - 1;
             const int units = REC_UNITS * __builtin_amdgcn_readlane(grow, j);
             int64_t b = -1;
-            if (l == 0) b = unit_alloc(P, H, t, units);
+            if (l == 0 && !fail) b = unit_alloc(P, H, t, units);
             b = readlane64(b, 0);
-            if (b < 0) { fail = true; break; }
+            if (b < 0) fail = true;
             if (l == j) nb = b;
         }
         if (g0 == 0) V.nb = nb;
-        else if (grow > 0 && nb >= 0) path_b[g0 + l] = nb;
+        else if (grow > 0) path_b[g0 + l] = nb;
     }
     int g = -1, ec = 0;
     int64_t eb = -1;
@@ -1828,15 +2116,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         }
         return;
     }
-    if (fail) {                                          // a visit block found no room: the
-        if (l == 0) {                                    // simulation is lost (counted)
-            H->unexpanded += 1;
-            H->sims_done = h_sims + 1;
-            H->noise_pending = 0;
-            H->leaf_kind = LEAF_NONE;
-        }
-        return;
-    }
+    // (no withdrawal possible: a level whose visit block found no room backs up its node
+    // but leaves the edge without statistics — counted, like an unstored leaf)
+    if (fail && l == 0) H->unexpanded += 1;
     if (kind == LEAF_NN) {
         if (eb < 0) {                                    // no room: back up v, do not store
             if (l == 0) H->unexpanded += 1;
@@ -1933,6 +2215,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 R->q = q1;
                 R->n = n1;
                 if (V.rchild < 0 && V.child >= 0) R->child = V.child;
+            } else if (V.grow > 0 && V.nb < 0) {         // no room for the record (counted)
+                vidx = -1;
             } else {                                     // the edge's first visit: a record
                 if (V.grow > 0) {                        // (the block outgrown: moved)
                     for (int k = 0; k < REC_UNITS * V.r.vcnt; k++) P.eu[V.nb + k] = P.eu[V.r.vb + k];
@@ -2184,7 +2468,7 @@ __global__ __launch_bounds__(256) void k_nn_input(int B, int R, const int8_t *__
 
 // tree sizes (spl_mcts_tree_sizes): slots in use and the live part of each tree — the root
 // and the nodes whose round exceeds the root's (what garbage collection keeps), with their
-// edge units (runs and visit blocks). Diagnostic (capacity planning), one wave per tree.
+// edge units (runs and visit records). Diagnostic (capacity planning), one wave per tree.
 __global__ __launch_bounds__(64) void k_tree_sizes(Pools P, int B, int32_t *out) {
     const int t = blockIdx.x;
     if (t >= B) return;
@@ -2199,7 +2483,8 @@ __global__ __launch_bounds__(64) void k_tree_sizes(Pools P, int B, int32_t *out)
             ln++;
             if (!P.nterm[g]) {
                 const NodeRun r = P.nrun[g];
-                le += r.ec + REC_UNITS * r.vcap;
+                le += r.ec + REC_UNITS * r.vcnt;         // (content: block slack depends on the
+                                                         //  collection history)
             }
         }
     }
@@ -2491,11 +2776,20 @@ int spl_mcts_pick_best(spl_mcts *m, const uint8_t *active, uint32_t board_base, 
     return check_launch();
 }
 
+#ifndef SELECT_LANES
+#define SELECT_LANES 1     // k_select_lanes (lane per tree); 0: k_select (wave per tree)
+#endif
 static int launch_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
                          int32_t *leaf_index, int32_t *leaf_count, void *hs) {
-    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select<N>, wave_grid(m->B), dim3(THREADS), 0,
-                                          (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
-                                          leaf_state, leaf_mask, leaf_valid, leaf_count));
+    if (SELECT_LANES) {
+        SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select_lanes<N>, dim3((unsigned)((m->B + 63) / 64)), dim3(64), 0,
+                                              (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
+                                              leaf_state, leaf_valid, leaf_count));
+    } else {
+        SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select<N>, wave_grid(m->B), dim3(THREADS), 0,
+                                              (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
+                                              leaf_state, leaf_mask, leaf_valid, leaf_count));
+    }
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_leaf_mask<N>, dim3((unsigned)((m->B + 63) / 64)), dim3(256), 0,
                                           (hipStream_t)hs, m->P, m->B, m->token_limit, leaf_state, leaf_valid,
                                           leaf_mask, leaf_index, leaf_count));
