@@ -1701,6 +1701,8 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                     leaf_node = pk.child;
                     state = LS_DONE;
                 } else if (pk.child >= 0 && nbrd) {      // linked: no transition needed
+                    BCHK(P.nround[pk.child] == P.nround[node] + 1, 30, ((long long)node << 32) | (uint32_t)pk.child, t,
+                         pk.child = pk.child);
                     node = pk.child;
                 } else {
                     state = LS_EXPAND;
@@ -1730,6 +1732,8 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                 }
             }
             if (state == LS_EXPAND) {
+                BCHK(child < 0 || P.nround[child] == (uint8_t)bt(row(s, 0), 6), 31,
+                     ((long long)node << 32) | (uint32_t)child, t, child = child);
                 if (child >= 0) {                        // continue below the linked node
                     node = child;
                     bnode = child;
@@ -2215,6 +2219,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 R->q = q1;
                 R->n = n1;
                 if (V.rchild < 0 && V.child >= 0) R->child = V.child;
+                BCHK(V.child < 0 || P.nround[V.child] == P.nround[V.node] + 1, 32,
+                     ((long long)V.node << 32) | (uint32_t)V.child, t, V.child = V.child);
+                BCHK(V.rchild < 0 || V.child < 0 || V.rchild == V.child, 33,
+                     ((long long)V.rchild << 32) | (uint32_t)V.child, t, V.child = V.child);
             } else if (V.grow > 0 && V.nb < 0) {         // no room for the record (counted)
                 vidx = -1;
             } else {                                     // the edge's first visit: a record
@@ -2224,6 +2232,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                     V.r.vcap = (int16_t)V.grow;
                 }
                 vidx = V.r.vcnt;
+                BCHK(V.child < 0 || P.nround[V.child] == P.nround[V.node] + 1, 34,
+                     ((long long)V.node << 32) | (uint32_t)V.child, t, V.child = V.child);
                 *P.vr(V.r.vb + REC_UNITS * vidx) = VisitRec{q1, n1, V.child, V.e.p, (int16_t)V.off, (int16_t)V.act};
                 P.ep(V.r.eb + V.off)->vi = (int16_t)vidx;
                 V.r.vcnt = (int16_t)(vidx + 1);
@@ -2299,6 +2309,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         // the node record: statistics, arg-max and its link (the path edge's link as just set)
         if (in) {
             if (bsel == V.off) bch = V.rchild;
+            BCHK(bch < 0 || P.nround[bch] == P.nround[V.node] + 1, 35, ((long long)V.node << 32) | (uint32_t)bch, t,
+                 bch = bch);
             const int bt_ = bch >= 0 ? (int)P.nterm[bch] : 0;
             P.nst[V.node] = NodeStat{nqs, nns, (int16_t)bsel, (int16_t)bact, bch, bt_, 0};
         }

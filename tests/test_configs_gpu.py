@@ -8,10 +8,12 @@
   with SplendorNNet leaves (property checks), and the slice equality plus the oracle on a
   64-game slice with the hash network (bit-exact, noise included).
 * Config 4 per-GPU shard (2 players, 32,768 games, numMCTSSims=1600): full size with pools
-  planned against the device's memory; searches keep running under capacity pressure
-  (events counted, never a frozen tree), and the slice equality with the hash network.
+  planned against the device's memory, run past its steady state (phase-spread, as the
+  bench) with zero capacity events; searches keep running under capacity pressure (events
+  counted, never a frozen tree), and the slice equality with the hash network.
 """
 import gc
+import os
 
 import numpy as np
 import pytest
@@ -21,6 +23,7 @@ torch = pytest.importorskip("torch")
 import _oracle as O  # noqa: E402
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 GENBU = dict(cpuct=2.5, fpu=0.3, prob_fullMCTS=0.25, ratio_fullMCTS=5, forced_playouts=False,
              dirichletAlpha=0.3, temperature=[1.25, 0.8], tempThreshold=10)
@@ -164,10 +167,12 @@ def test_capacity_pressure_is_graceful():
     assert st["overflow"] == 0 and st["games_done"] > 0
     assert st["prunes"] > 0 and st["withdrawals"] > 0 and st["collections"] > 0
     h = sp.headers()
-    nmax, emax = 128, 3 * 1024                                   # caps rounded up to whole pages
-    assert (h["node_count"] <= nmax).all() and (h["epg"] <= emax // 1024).all()
+    nmax, epages = 128, 2                                        # caps rounded up to whole pages
+    assert (h["node_count"] <= nmax).all() and (h["epg"] <= epages).all()   # (2,048-unit pages)
     assert h["moves"].min() > 10                                 # every tree kept committing moves
-    assert (h["gc_queued"] == 0).all()                           # the GC queue drains
+    # the GC queue drains: what stays queued is only "should" collections deferred to later
+    # launches (GC_SHOULD_CAP per launch)
+    assert ((h["gc_queued"] == 0) | (h["gc_state"] == 5)).all()
 
 
 def test_search_arena_spends_whole_budget_under_pressure():
@@ -191,16 +196,23 @@ def test_search_arena_spends_whole_budget_under_pressure():
     assert bool((counts.sum(1) == sims - 1).all())
 
 
-@pytest.mark.parametrize("n,B,sims,prefill,window", [(2, 32768, 100, 3000, 3000), (4, 16384, 400, 30000, 8000)])
-def test_steady_state_search_is_reference_exact(n, B, sims, prefill, window):
-    """Configs 3 and 5 at full size with SplendorNNet leaves on the default shared pools, run
-    to their steady state (config 3: games finish from ~2,400 iterations on; config 5: the
-    first games end near 16,000 and the trees that all started together peak around 20,000)
-    and then through a window: no search in the window ran on a pruned or emptied tree and
-    every leaf was stored (prunes == resets == unexpanded == 0), so each tree is the
-    reference's table. Events during the synchronised start-up transient are printed."""
+@pytest.mark.parametrize("n,B,sims,prefill,window,stagger", [(2, 32768, 100, 3000, 3000, 0),
+                                                             (4, 16384, 400, 30000, 8000, 0),
+                                                             (2, 32768, 1600, 45000, 4000, 40000)])
+def test_steady_state_search_is_reference_exact(n, B, sims, prefill, window, stagger):
+    """Configs 3, 5 and 4's per-GPU shard at full size with SplendorNNet leaves on the default
+    shared pools, run to their steady state (config 3: games finish from ~2,400 iterations
+    on; config 5: the first games end near 16,000 and the trees that all started together
+    peak around 20,000; config 4: games spread over the phases of a game as in bench.py,
+    `stagger`) and then through a window: no search in the window ran on a pruned or emptied
+    tree and every leaf was stored (prunes == resets == unexpanded == 0), so each tree is the
+    reference's table. Events during the start-up transient are printed."""
+    import importlib.util
     from splendor.nnet import LeafEvaluator, random_net
     from splendor.env import SplendorEngine
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
     e = SplendorEngine(n)
     ev = LeafEvaluator(e, random_net(n, seed=0), B, use_graph=False)
     _, sp = selfplay(n, B, sims, evaluator=ev)
@@ -211,7 +223,12 @@ def test_steady_state_search_is_reference_exact(n, B, sims, prefill, window):
             sp.run(min(4000, k - done), use_graph=True)
             done += min(4000, k - done)
             sp.drain()
-    run(prefill)
+    done = 0
+    for target, j in bench.stagger_marks(stagger, 16, sims, GENBU["ratio_fullMCTS"]) + [(prefill, None)]:
+        run(target - done)                      # (phase stagger as bench.run_selfplay)
+        done = target
+        if j is not None:
+            sp.restart(torch.arange(B) % 16 == j)
     ev0 = sp.check_capacity(allow=True)
     g0 = sp.stats()["games_done"]
     run(window)

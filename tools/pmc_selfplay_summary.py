@@ -14,15 +14,20 @@ import sys
 KERNELS = ("k_select", "k_leaf_mask", "k_nn_forward", "k_backup", "k_commit", "k_gc")
 
 
+
+def _kname(k):
+    """k_select_lanes (lane per tree) is the select kernel: reported as k_select."""
+    return "k_select" if k == "k_select_lanes" else k
+
 def per_kernel(d, last=None):
     """Counter averages per dispatch of each kernel, over its last `last` dispatches."""
     acc = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             m = re.search(r"k_\w+", r.get("Kernel_Name", ""))
-            if not m or m.group(0) not in KERNELS:
+            if not m or _kname(m.group(0)) not in KERNELS:
                 continue
-            k, disp = m.group(0), int(r["Dispatch_Id"])
+            k, disp = _kname(m.group(0)), int(r["Dispatch_Id"])
             acc.setdefault(k, {}).setdefault(disp, {})
             c = r["Counter_Name"]
             acc[k][disp][c] = acc[k][disp].get(c, 0.0) + float(r["Counter_Value"])
@@ -39,8 +44,8 @@ def durations(d):
     for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             m = re.search(r"k_\w+", r["Name"])
-            if m and m.group(0) in KERNELS:
-                out[m.group(0)] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
+            if m and _kname(m.group(0)) in KERNELS:
+                out[_kname(m.group(0))] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
     return out
 
 
