@@ -39,8 +39,9 @@ using namespace spl;
 #define SPL_BOUNDS_CHECK 0
 #endif
 #if SPL_BOUNDS_CHECK
-__device__ unsigned long long g_bounds[4];
+__device__ unsigned long long g_bounds[4 + 64];   // count, first (value, site, tree), per-site counts
 __device__ __noinline__ void bounds_note(int site, long long v, int t) {
+    atomicAdd(&g_bounds[4 + (site & 63)], 1ull);
     if (atomicAdd(&g_bounds[0], 1ull) == 0) {
         g_bounds[1] = (unsigned long long)v; g_bounds[2] = (unsigned long long)site; g_bounds[3] = (unsigned long long)t;
     }
@@ -49,6 +50,11 @@ __device__ __noinline__ void bounds_note(int site, long long v, int t) {
     do {                                                               \
         if (!(cond)) { bounds_note((site), (long long)(v), (t)); fix; } \
     } while (0)
+// is global node id g one of tree t's first `lim` node slots (its own page)
+#define IN_TREE(P, t, g, lim)                                                                          \
+    ((g) >= 0 && (g) < (P).npages * NPG && (P).npidx[(g) >> NPG_SHIFT] < (P).hdr[t].npg &&             \
+     (P).ntab[(size_t)(t) * (P).nptab + (P).npidx[(g) >> NPG_SHIFT]] == ((g) >> NPG_SHIFT) &&          \
+     node_l((P), (g)) < (lim))
 #else
 #define BCHK(cond, site, v, t, fix) \
     do {                            \
@@ -494,6 +500,7 @@ __device__ void mark_linked(const Pools &P, int t, int rootl, int32_t *mark, int
             const int64_t vbo = __shfl(vb, lo, 64);
             const int exo = __shfl(excl, lo, 64);
             const int c = e < tot ? P.vr(vbo + REC_UNITS * (e - exo))->child : -1;
+            BCHK(c < 0 || IN_TREE(P, t, c, nc), 58, c, t, (void)0);
             const int cl = c >= 0 ? node_l(P, c) : -1;
             const bool fresh = cl >= 0 && atomicCAS(&mark[cl], 0, 1) == 0;
             const uint64_t bm = __ballot(fresh);
@@ -547,6 +554,7 @@ __device__ __forceinline__ int block_min(int x, GcLds &L) {
     return m;
 }
 
+constexpr int GC_NOFIT = -2;   // compact_tree: the compacted tree would not fit its page table
 template <int CR = 4>   // board units per thread per round trip of the node-board move (x2)
 __device__ int compact_tree(const Pools &P, int t, int root, int root_round, const GcScr &S, GcLds &L,
                             int bunits, bool linked = false) {
@@ -606,6 +614,10 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         }
         if (i < nc && remap[i] >= 0) S.nvs[i] = start;
     }
+    // packed with page-end gaps in an order other than the allocation order, the kept units
+    // may need more pages than the tree's page table holds (only near its maximum): nothing is
+    // written yet, the caller falls back to pruning / emptying
+    if (run > P.emax) return GC_NOFIT;
     __syncthreads();
     // node records, chunk by chunk in local order (new slot <= old slot): reads, then writes
     int my_units = 0;
@@ -649,8 +661,11 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     for (int ni = tid; ni < kept; ni += GCT) {
         const int ch = S.queue[ni];
         if (ch >= 0) {
+            BCHK(IN_TREE(P, t, ch, nc), 56, ((long long)ni << 32) | (uint32_t)ch, t, (void)0);
             const int nl = remap[node_l(P, ch)];
             P.nst[node_g(P, t, ni)].bchild = nl >= 0 ? node_g(P, t, nl) : -1;
+            BCHK(nl < 0 || P.nround[node_g(P, t, nl)] == P.nround[node_g(P, t, ni)] + 1, 40,
+                 ((long long)ni << 32) | (uint32_t)nl, t, (void)0);
         }
     }
     // the owner of every new unit position (gaps before a page start: -1)
@@ -678,8 +693,11 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                 const int ch = (int)(v >> 32);
                 int nch = -1;
                 if (ch >= 0) {
+                    BCHK(IN_TREE(P, t, ch, nc), 57, ((long long)j << 32) | (uint32_t)ch, t, (void)0);
                     const int nl = remap[node_l(P, ch)];
                     if (nl >= 0) nch = node_g(P, t, nl);
+                    BCHK(nl < 0 || P.nround[nch] == P.nround[node_g(P, t, j)] + 1, 41,
+                         ((long long)j << 32) | (uint32_t)nl, t, (void)0);
                 }
                 v = (v & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)nch << 32);
             }
@@ -814,6 +832,7 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         uint64_t k0, k1;
         wave_fingerprint<N>(s, k0, k1);
         root = hash_lookup(P, t, k0, k1);
+        BCHK(root < 0 || IN_TREE(P, t, root, H->node_count), 54, root, t, (void)0);
         const int nc = H->node_count;
         const long long used = units_used(H);
         const bool must = nc + budget + 1 > P.nmax ||
@@ -889,17 +908,22 @@ __global__ __launch_bounds__(GCT) void k_gc(Pools P, SearchCfg C) {
         if (keep_s) continue;
         int root = H->root;
         const int nst = st == 1 ? 2 : 0;
-        if (st == 1) {                                   // the descent then repeats
-            root = compact_tree<4>(P, t, root, P.nround[root], S, L, NodeBoard<N>::UNITS);
-        } else if (st == 3 || st == 5) {
-            const int rr = H->root_round;
-            root = compact_tree<4>(P, t, root, rr, S, L, NodeBoard<N>::UNITS);
-            if (!tree_fits(P, C, H) && root >= 0) {
-                root = compact_tree<4>(P, t, root, rr, S, L, NodeBoard<N>::UNITS, true);
+        if (st == 1 || st == 3 || st == 5) {
+            // mid-search (1: the descent then repeats): rounds above the root's; search start:
+            // above the root round
+            const int rr = st == 1 && root >= 0 ? P.nround[root] : H->root_round;
+            const int r0 = root;
+            root = compact_tree<4>(P, t, r0, rr, S, L, NodeBoard<N>::UNITS);
+            // capacity pressure (search start: the search would not fit; any: the compacted
+            // layout would not fit the page table): prune to the linked nodes, else empty
+            bool prune = root == GC_NOFIT;
+            if (!prune && st != 1) prune = !tree_fits(P, C, H) && root >= 0;
+            if (prune) {
+                root = compact_tree<4>(P, t, root == GC_NOFIT ? r0 : root, rr, S, L, NodeBoard<N>::UNITS, true);
                 if (tid == 0) H->prunes += 1;
             }
             __syncthreads();
-            if (!tree_fits(P, C, H)) {
+            if (root == GC_NOFIT || (st != 1 && !tree_fits(P, C, H))) {
                 root = -1;
                 if (tid < 64) empty_tree(P, t);
                 if (tid == 0) H->resets += 1;
@@ -1701,6 +1725,7 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                     leaf_node = pk.child;
                     state = LS_DONE;
                 } else if (pk.child >= 0 && nbrd) {      // linked: no transition needed
+                    BCHK(IN_TREE(P, t, pk.child, H->node_count), 52, pk.child, t, (void)0);
                     BCHK(P.nround[pk.child] == P.nround[node] + 1, 30, ((long long)node << 32) | (uint32_t)pk.child, t,
                          pk.child = pk.child);
                     node = pk.child;
@@ -1713,6 +1738,11 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
             if (nbrd && bnode != node) {                 // stage this node's stored board
                 const uint64_t *src = nbrd + (size_t)node * (NodeBoard<N>::BYTES / 8);
                 for (int r = 0; r < Lx::ROWS; r++) row(s, r) = src[r];
+#if SPL_BOUNDS_CHECK
+                uint64_t f0, f1;
+                lane_fingerprint<N>(s, f0, f1);
+                BCHK(f0 == P.nkey0[node] && f1 == P.nkey1[node], 36, node, t, (void)0);
+#endif
             }
             lane_tree_step<N>(s, pk.a);
             int child = pk.child;
@@ -1722,6 +1752,8 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                 child = hash_lookup(P, t, k0, k1, &miss);
                 if (child >= 0) {                        // transposition: link the cached pick
                     const int ct = P.nterm[child];
+                    BCHK(IN_TREE(P, t, child, H->node_count), 53, child, t, (void)0);
+                    BCHK(P.nround[child] == P.nround[node] + 1, 37, ((long long)node << 32) | (uint32_t)child, t, (void)0);
                     if (cached) { P.nst[node].bchild = child; P.nst[node].bterm = ct; }
                     if (ct) {
                         kind = LEAF_TERMINAL;
@@ -2175,6 +2207,16 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 bsel = uniform(r);
             }
             if (l == 0) {
+#if SPL_BOUNDS_CHECK
+                if (P.nbrd) {                            // the board select stored at the slot
+                    uint64_t bw[Lay<N>::ROWS];
+                    const uint64_t *src = reinterpret_cast<const uint64_t *>(P.nbrd) + (size_t)g * (NodeBoard<N>::BYTES / 8);
+                    for (int r = 0; r < Lay<N>::ROWS; r++) bw[r] = src[r];
+                    uint64_t f0, f1;
+                    lane_fingerprint<N>(reinterpret_cast<const int8_t *>(bw), f0, f1);
+                    BCHK(f0 == h_k0 && f1 == h_k1, 43, g, t, (void)0);
+                }
+#endif
                 P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
                 P.nrun[g] = NodeRun{eb, 0, (int16_t)ec, 0, 0, 0};
                 // (a new root: its priors may still be noised, and a root scans)
@@ -2219,6 +2261,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 R->q = q1;
                 R->n = n1;
                 if (V.rchild < 0 && V.child >= 0) R->child = V.child;
+                BCHK(V.child < 0 || IN_TREE(P, t, V.child, P.nmax), 50, V.child, t, (void)0);
                 BCHK(V.child < 0 || P.nround[V.child] == P.nround[V.node] + 1, 32,
                      ((long long)V.node << 32) | (uint32_t)V.child, t, V.child = V.child);
                 BCHK(V.rchild < 0 || V.child < 0 || V.rchild == V.child, 33,
@@ -2232,6 +2275,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                     V.r.vcap = (int16_t)V.grow;
                 }
                 vidx = V.r.vcnt;
+                BCHK(V.child < 0 || IN_TREE(P, t, V.child, P.nmax), 50, V.child, t, (void)0);
+                BCHK(IN_TREE(P, t, V.node, P.nmax), 55, V.node, t, (void)0);
                 BCHK(V.child < 0 || P.nround[V.child] == P.nround[V.node] + 1, 34,
                      ((long long)V.node << 32) | (uint32_t)V.child, t, V.child = V.child);
                 *P.vr(V.r.vb + REC_UNITS * vidx) = VisitRec{q1, n1, V.child, V.e.p, (int16_t)V.off, (int16_t)V.act};
@@ -2309,6 +2354,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         // the node record: statistics, arg-max and its link (the path edge's link as just set)
         if (in) {
             if (bsel == V.off) bch = V.rchild;
+            BCHK(bch < 0 || IN_TREE(P, t, bch, P.nmax), 51, bch, t, (void)0);
             BCHK(bch < 0 || P.nround[bch] == P.nround[V.node] + 1, 35, ((long long)V.node << 32) | (uint32_t)bch, t,
                  bch = bch);
             const int bt_ = bch >= 0 ? (int)P.nterm[bch] : 0;
@@ -2660,9 +2706,9 @@ int spl_diag_select_timing(unsigned long long *out24, int reset) {
 #if SPL_BOUNDS_CHECK
 // bounds-checked builds only: [0] violations, [1] first value, [2] its site, [3] its tree
 int spl_diag_bounds(unsigned long long *out4, int reset) {
-    if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_bounds), 4 * 8) != hipSuccess) return SPL_EDEVICE;
+    if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_bounds), 68 * 8) != hipSuccess) return SPL_EDEVICE;
     if (reset) {
-        unsigned long long z[4] = {0};
+        unsigned long long z[68] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_bounds), z, sizeof(z)) != hipSuccess) return SPL_EDEVICE;
     }
     return 0;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic (bounds-checked library, SPLENDOR_AMD_LIB=ablib/libchk.so): the capacity-pressure
 self-play of tests/test_configs_gpu.py::test_capacity_pressure_is_graceful, then the bounds /
-link-consistency counter of spl_diag_bounds: [count, first value, site, tree]."""
+link-consistency counter of spl_diag_bounds: [count, first value, site, tree] + per-site counts."""
 import ctypes
 import json
 import os
@@ -19,7 +19,7 @@ def main():
     from splendor.selfplay import SelfPlay
     L = _lib.lib()
     L.spl_diag_bounds.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    out = (ctypes.c_ulonglong * 4)()
+    out = (ctypes.c_ulonglong * 68)()
     L.spl_diag_bounds(out, 1)
     genbu = dict(cpuct=2.5, fpu=0.3, prob_fullMCTS=0.25, ratio_fullMCTS=5, forced_playouts=False,
                  dirichletAlpha=0.3, temperature=[1.25, 0.8], tempThreshold=10)
@@ -36,6 +36,7 @@ def main():
         st = sp.stats()
         print(json.dumps({"round": r, "violations": int(out[0]), "value": int(out[1]), "node": int(out[1]) >> 32,
                           "child": int(out[1]) & 0xFFFFFFFF, "site": int(out[2]), "tree": int(out[3]),
+                          "sites": {k: int(out[4 + k]) for k in range(64) if out[4 + k]},
                           "overflow": st["overflow"], "prunes": st["prunes"], "resets": st["resets"],
                           "withdrawals": st["withdrawals"], "unexpanded": st["unexpanded"]}), flush=True)
 
