@@ -1,14 +1,16 @@
-// mcts_device.h — device-resident batched PUCT tree (one tree per game, one wave per tree).
+// mcts_device.h — device-resident batched PUCT trees (one tree per game) in a shared arena.
 //
 // Restates MCTS.py (search :99-177, pick_highest_UCB :199-219, backup :171-176,
-// getActionProb :45-97) as three stream-ordered kernels per simulation wave:
-//   select  : descend from the root with a wave arg-max over the node's CSR edges, apply
-//             the deterministic in-tree transition in LDS, resolve the child through the
-//             per-tree transposition table; emit one leaf per tree (NN leaf or terminal).
-//   backup  : expand the NN leaf (CSR edges over legal actions, priors normalised in NumPy's
-//             pairwise order), insert it, then walk the path updating Q/N with the
-//             per-level value rotation (np.roll, :169).
-//   commit  : (self-play) play the move, record the example, re-root, collect garbage.
+// getActionProb :45-97) as stream-ordered kernels per simulation wave:
+//   select  : (k_select_lanes, lane per tree) descend from the root along each node's cached
+//             arg-max (one 32-byte NodeStat per level), apply the deterministic in-tree
+//             transition at the expanded edge, resolve the child through the per-tree
+//             transposition table; emit one leaf per tree (NN leaf or terminal).
+//   backup  : (k_backup, wave per tree, lane per level) expand the NN leaf (its run of edges
+//             sorted by prior, priors normalised in NumPy's pairwise order), insert it, then
+//             update every path level (visit record, Ns / Qs, with the per-level value
+//             rotation, np.roll :169) and recompute its cached arg-max.
+//   commit  : (self-play) play the move, record the example, re-root; k_gc collects garbage.
 // Arithmetic types follow the deployed reference: Q, Qs, UCB in float64; P float32.
 #pragma once
 #include "splendor_device.h"
