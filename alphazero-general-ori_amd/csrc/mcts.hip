@@ -864,6 +864,7 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         H->root_round = rr;
         H->move_no = mv + 1;
         H->depth = 0;                                    // (a new search: no path reuse)
+        H->wd_search = 0;
         if (gcs) gc_push(P, H, t);
     }
     wave_lds_fence();
@@ -934,7 +935,7 @@ __global__ __launch_bounds__(GCT) void k_gc(Pools P, SearchCfg C) {
             H->gc_queued = 0;
             if (st == 1 || st == 3 || st == 5) {
                 H->root = root;
-                H->gc_state = nst;                       // (2: once per search)
+                H->gc_state = nst;                       // (2: collected mid-search)
                 H->depth = 0;                            // (node ids moved: no path reuse)
             }
         }
@@ -2063,6 +2064,9 @@ __device__ __forceinline__ void load_levels(const Pools &P, int t, int g0, int d
     }
 }
 
+#ifndef WD_MAX
+#define WD_MAX 4           // withdrawals per search (k_backup)
+#endif
 // KINDS: the leaf kinds this launch backs up (bit 0 NN, bit 1 terminal; spl_mcts_backup_kind)
 template <int N, int KINDS>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_WAVES))) void k_backup(Pools P, SearchCfg C, int B,
@@ -2138,16 +2142,21 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         g = __shfl(g, 0, 64);
         eb = readlane64(eb, 0);
     }
-    if ((fail || (kind == LEAF_NN && eb < 0)) && C.selfplay && depth > 0 && (h_gc == 0 || h_gc == 5)) {
+    if ((fail || (kind == LEAF_NN && eb < 0)) && C.selfplay && depth > 0 &&
+        (h_gc == 0 || h_gc == 5 || (h_gc == 2 && H->wd_search < WD_MAX))) {
         // garbage is collected lazily (begin_search), so a self-play search may run out
         // of room with dead nodes still held: this simulation is withdrawn (no backup,
         // not counted), k_gc (launched behind every backup of a self-play arena) collects
         // the garbage (exact: nodes with rounds <= the root's) and the next select repeats
-        // the same descent. Search-only arenas never withdraw.
+        // the same descent. With the shared pools nearly empty the repeat can fail again
+        // (its own garbage is gone, other trees' collections refill the pools meanwhile):
+        // up to WD_MAX withdrawals per search, then the leaf is backed up unstored.
+        // Search-only arenas never withdraw.
         if (l == 0) {
             H->gc_state = 1;
             H->leaf_kind = LEAF_NONE;
             H->withdrawals += 1;
+            H->wd_search += 1;
             gc_push(P, H, t);
         }
         return;

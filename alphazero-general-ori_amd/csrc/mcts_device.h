@@ -26,7 +26,7 @@ struct TreeHdr {
     int32_t game_no, overflow, n_examples, leaf_round;
     uint64_t leaf_k0, leaf_k1;
     float leaf_v[4];
-    int32_t games_done, forced, moves, pad0;
+    int32_t games_done, forced, moves, wd_search;   // wd_search: withdrawals in this search
     // capacity events: searches that started on a tree pruned to the nodes
     // linked from the root / on an emptied tree, and simulations whose leaf did not fit
     // (evaluated and backed up without being stored)
@@ -43,7 +43,7 @@ struct TreeHdr {
 };
 static_assert(sizeof(TreeHdr) == 192, "TreeHdr layout (splendor/mcts.py HDR_DTYPE)");
 // gc_state: 0 none; 1 a leaf did not fit mid-search (withdrawn, k_gc collects, the descent
-// repeats); 2 collected once this search; 3 collection before this search (must: the
+// repeats); 2 collected mid-search (a further withdrawal is allowed while wd_search < WD_MAX); 3 collection before this search (must: the
 // search does not fit the tree's maxima); 5 collection before this search (should: garbage
 // or pool pressure; k_gc may skip it, see GC_SHOULD_CAP)
 enum { LEAF_NONE = 0, LEAF_NN = 1, LEAF_TERMINAL = 2 };

@@ -68,6 +68,10 @@ __host__ __device__ constexpr int ntiles16(int N) { return (N + 15) / 16; }
 __host__ __device__ constexpr bool f16(int l) { return l >= 4; }
 __host__ __device__ constexpr int colpad(int l, int N) { return f16(l) ? ntiles16(N) * 16 : ntiles(N) * 32; }
 __host__ __device__ constexpr int wfloats(int l, int N, int K) { return colpad(l, N) * kpad(K); }
+// the split copy of a per-column layer: [4][Kp16/16][3][64][8] bf16 (hi, mid, lo parts of
+// W[32 nt + l % 32][16 c + 8 (l / 32) + j]), as floats
+__host__ __device__ constexpr int kp16(int K) { return (K + 15) / 16 * 16; }
+__host__ __device__ constexpr int sfloats(int K) { return 4 * (kp16(K) / 16) * 3 * 64 * 8 / 2; }
 
 // layer order of the packed weights: dense2d_1, dense2d_1[3], partialgpool_1 dense,
 // dense2d_3, dense1d_4, partialgpool_4 dense, dense1d_5[0], dense1d_5[3], partialgpool_5
@@ -85,7 +89,14 @@ struct Net {
     }
     static constexpr int boff(int l) { return woff(l) + wfloats(l, Ns[l], Ks[l]); }
     static constexpr int AFF = woff(NL);
-    static constexpr int TOTAL = AFF + 28;
+    // bf16 x 3 copies of the 4 per-column layers (NN_SPLIT), 16-byte aligned after the affines
+    static constexpr int SBASE = (AFF + 28 + 3) / 4 * 4;
+    static constexpr int soff(int l) {
+        int o = SBASE;
+        for (int j = 0; j < l; j++) o += sfloats(Ks[j]);
+        return o;
+    }
+    static constexpr int TOTAL = soff(4);
     static constexpr int X0S = (kpad(R) / 4) % 2 ? kpad(R) : kpad(R) + 4;   // int8 input stride (odd dwords)
 };
 
@@ -149,6 +160,127 @@ __device__ __forceinline__ void gemm_tiles(const float *__restrict__ wp, int nt,
     }
     next();
     __builtin_amdgcn_sched_barrier(0);
+}
+
+
+#ifndef NN_SPLIT
+#define NN_SPLIT 0      // 1: per-column layers on bf16 MFMAs with operands split in three parts
+#endif
+// Split per-column GEMMs (NN_SPLIT): an f32 x is exactly hi + mid + lo, three bf16 parts
+// taken by truncation (hi: the top 8 significant bits, mid: the top 8 of the residual, lo: the
+// rest, at most 8 significant bits), and x y = Σ over the parts' products minus the three
+// smallest (mid lo, lo mid, lo lo: < 2^-22 |x y| together, ~2^-24 typically). v_mfma_f32_32x32x16_bf16 takes 16 k per instruction at 16 times the f32
+// MFMA's rate, so the six products of a 16-k chunk cost 6 x 32 cycles against 8 x 64 for
+// v_mfma_f32_32x32x2_f32. Each bf16 product is exact in f32; hi hi goes into the layer's
+// accumulator and the five smaller products into a second one (added in the epilogue), so
+// the large accumulator rounds once per MFMA (16 k) instead of once per k, and the small one's
+// roundings are ~2^-8 smaller: measured against float64 the split layer's error is below the
+// f32 MFMA's (tools/nn_split_probe.hip). The int8 boards of dense2d_1 are exact
+// in bf16: three products (the weight's parts) into one accumulator.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int PFS = 2;                 // chunks of weight parts in flight
+struct RingS {
+    bf16x8 b[PFS][3];
+};
+struct F8 {
+    float4 lo, hi;                     // 8 consecutive k of one lane's A row
+};
+
+[[maybe_unused]] __device__ __forceinline__ void split8(const F8 &x, bf16x8 &hi, bf16x8 &mid, bf16x8 &lo) {
+    const float xs[8] = {x.lo.x, x.lo.y, x.lo.z, x.lo.w, x.hi.x, x.hi.y, x.hi.z, x.hi.w};
+    uint32_t h[8], m[8], l[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        h[j] = __float_as_uint(xs[j]) & 0xFFFF0000u;
+        const float r1 = xs[j] - __uint_as_float(h[j]);
+        m[j] = __float_as_uint(r1) & 0xFFFF0000u;
+        l[j] = __float_as_uint(r1 - __uint_as_float(m[j]));
+    }
+    u32x4 H, M, L;
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        H[p] = (h[2 * p] >> 16) | h[2 * p + 1];
+        M[p] = (m[2 * p] >> 16) | m[2 * p + 1];
+        L[p] = (l[2 * p] >> 16) | (l[2 * p + 1] & 0xFFFF0000u);
+    }
+    hi = __builtin_bit_cast(bf16x8, H);
+    mid = __builtin_bit_cast(bf16x8, M);
+    lo = __builtin_bit_cast(bf16x8, L);
+}
+// 8 int8 (two dwords) -> 8 bf16, exact
+[[maybe_unused]] __device__ __forceinline__ bf16x8 i8_to_bf16x8(int v0, int v1) {
+    u32x4 r;
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const int v = p < 2 ? v0 : v1, sh = 16 * (p & 1);
+        const uint32_t e0 = __float_as_uint((float)(int8_t)(v >> sh)) >> 16;
+        const uint32_t e1 = __float_as_uint((float)(int8_t)(v >> (sh + 8))) & 0xFFFF0000u;
+        r[p] = e0 | e1;
+    }
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+// first PFS chunks of column block nt of a split layer (C chunks of 16 k) into the ring
+template <int C>
+__device__ __forceinline__ void rings_load(const float *__restrict__ ws, int nt, RingS &r) {
+    const bf16x8 *w = reinterpret_cast<const bf16x8 *>(ws) + (size_t)nt * C * 3 * 64 + (threadIdx.x & 63);
+#pragma unroll
+    for (int p = 0; p < PFS; p++)
+#pragma unroll
+        for (int q = 0; q < 3; q++) r.b[p][q] = w[((p < C ? p : C - 1) * 3 + q) * 64];
+}
+
+// gemm_tiles on split operands: token tiles t0 .. t0+T-1 x column block nt over C chunks of
+// 16 k. INT8: afetch(t, k) -> bf16x8 (exact A, three products); else afetch(t, k) -> F8
+// (A split here, six products). Lane l: A[row l % 32][k = 16 c + 8 (l / 32) + j].
+template <int T, int C, bool INT8, class AF, class NX>
+__device__ __forceinline__ void gemm_split(const float *__restrict__ ws, int nt, int t0, RingS &r, AF afetch,
+                                           f32x16 *acc, NX next) {
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const bf16x8 *w = reinterpret_cast<const bf16x8 *>(ws) + (size_t)nt * C * 3 * 64 + lane;
+    f32x16 acl[T];                                       // the five smaller products
+#pragma unroll
+    for (int t = 0; t < T; t++) { acc[t] = zero16(); acl[t] = zero16(); }
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+        const bf16x8 b0 = r.b[c % PFS][0], b1 = r.b[c % PFS][1], b2 = r.b[c % PFS][2];
+        if (c + PFS < C)
+#pragma unroll
+            for (int q = 0; q < 3; q++) r.b[c % PFS][q] = w[((c + PFS) * 3 + q) * 64];
+        if constexpr (INT8) {
+            bf16x8 a[T];
+#pragma unroll
+            for (int t = 0; t < T; t++) a[t] = afetch(t0 + t, 16 * c + 8 * h);
+#pragma unroll
+            for (int t = 0; t < T; t++) {
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b2, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b1, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b0, acc[t], 0, 0, 0);
+            }
+        } else {
+            F8 x[T];
+#pragma unroll
+            for (int t = 0; t < T; t++) x[t] = afetch(t0 + t, 16 * c + 8 * h);
+#pragma unroll
+            for (int t = 0; t < T; t++) {
+                bf16x8 a0, a1, a2;
+                split8(x[t], a0, a1, a2);
+                acl[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acl[t], 0, 0, 0);
+                acl[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acl[t], 0, 0, 0);
+                acl[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acl[t], 0, 0, 0);
+                acl[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acl[t], 0, 0, 0);
+                acl[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acl[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[t], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    next();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!INT8)
+#pragma unroll
+        for (int t = 0; t < T; t++) acc[t] += acl[t];
 }
 
 
@@ -314,8 +446,14 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float *aff = W + Nt::AFF;                        // s1, t1, sp1, tp1
     const int t0 = 4 * wg, ntok = wg ? 3 : 4;              // this wave's token tiles (per-column layers)
     constexpr int S1 = kpad(R) / 2;
+#if NN_SPLIT
+    constexpr int C1 = kp16(R) / 16;
+    RingS rings;                                           // per-column weight parts, one layer ahead
+    rings_load<C1>(W + Nt::soff(0), wc, rings);
+#else
     RingC ringc;                                           // per-column weight fragments, one layer ahead
     ringc_load<S1>(W + Nt::woff(0), wc, ringc);
+#endif
 
     // ---- input: x[column c][leaf i][row r] = state[leaf][r][c] as int8 (token c*32+i)
     int8_t *x0 = reinterpret_cast<int8_t *>(bufA);
@@ -357,6 +495,23 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     f32x16 acc[4];
     const int col = 32 * wc + acc_col();
     // this wave's 4 (group 0) or 3 (group 1) token tiles of column block wc
+#if NN_SPLIT
+    // (s_const: chunks of 16 k; i8_const: A is the int8 input)
+    auto gemm_cols = [&](auto c_const, auto i8_const, const float *ws, auto afetch, auto next) {
+        constexpr int C = decltype(c_const)::value;
+        constexpr bool I8 = decltype(i8_const)::value != 0;
+        if (wg == 0)
+            gemm_split<4, C, I8>(ws, wc, 0, rings, afetch, acc, next);
+        else
+            gemm_split<3, C, I8>(ws, wc, 4, rings, afetch, acc, next);
+    };
+    auto fetchA8 = [&](int col0) {
+        return [&, col0](int t, int c) {
+            const float *p = bufA + (t * ML + li) * XS + col0 + c;
+            return F8{ld4(p), ld4(p + 4)};
+        };
+    };
+#else
     auto gemm_col = [&](auto s_const, const float *wp, auto afetch, auto next) {
         constexpr int S = decltype(s_const)::value;
         if (wg == 0)
@@ -364,6 +519,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         else
             gemm_tiles<3, S>(wp, wc, 4, ringc, afetch, acc, next);
     };
+#endif
     // per-column epilogue over this wave's token tiles: dst = f(acc, t, n)
     auto store_tiles = [&](int coloff, auto f) {
 #pragma unroll
@@ -382,10 +538,18 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // retires loads in order)
     {
         const float bias = W[Nt::boff(0) + col];
+#if NN_SPLIT
+        // (k past R reads zero padding or the next row's bytes: their weights are 0)
+        gemm_cols(IntC<C1>(), IntC<1>(), W + Nt::soff(0), [&](int t, int c) {
+            const int32_t *p = reinterpret_cast<const int32_t *>(x0 + (t * ML + li) * X0S + c);
+            return i8_to_bf16x8(p[0], p[1]);
+        }, [&] { rings_load<8>(W + Nt::soff(1), wc, rings); });
+#else
         gemm_col(IntC<S1>(), W + Nt::woff(0), [&](int t, int c) {
             const int v = *reinterpret_cast<const int32_t *>(x0 + (t * ML + li) * X0S + c);
             return make_float4((float)(int8_t)v, (float)(int8_t)(v >> 8), (float)(int8_t)(v >> 16), (float)(v >> 24));
         }, [&] { ringc_load<64>(W + Nt::woff(1), wc, ringc); });
+#endif
         lds_barrier();
         store_tiles(col, [&](float x, int t) { return fmaxf((x + bias) * aff[t] + aff[7 + t], 0.f); });
         lds_barrier();
@@ -394,7 +558,11 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // ---- dense2d_1[3]: relu(W2 x + b2)
     {
         const float bias = W[Nt::boff(1) + col];
+#if NN_SPLIT
+        gemm_cols(IntC<8>(), IntC<0>(), W + Nt::soff(1), fetchA8(0), [&] { rings_load<6>(W + Nt::soff(2), wc, rings); });
+#else
         gemm_col(IntC<64>(), W + Nt::woff(1), fetchA(0), [&] { ringc_load<48>(W + Nt::woff(2), wc, ringc); });
+#endif
         lds_barrier();
         store_tiles(col, [&](float x, int) { return fmaxf(x + bias, 0.f); });
         lds_barrier();
@@ -403,7 +571,11 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // ---- partialgpool_1: [max, mean over 4 groups of 8 of x[0:32]] ++ relu(BN(Wp1 x[32:] + bp1))
     {
         const float bias = W[Nt::boff(2) + col];  // 0-padded to 128 columns
+#if NN_SPLIT
+        gemm_cols(IntC<6>(), IntC<0>(), W + Nt::soff(2), fetchA8(32), [&] { rings_load<8>(W + Nt::soff(3), wc, rings); });
+#else
         gemm_col(IntC<48>(), W + Nt::woff(2), fetchA(32), [&] { ringc_load<64>(W + Nt::woff(3), wc, ringc); });
+#endif
         constexpr int NQ = (7 * ML * 8 + NNT - 1) / NNT;
         float pv[NQ];
 #pragma unroll
@@ -436,7 +608,11 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     Ring16 ring;                           // per-leaf weight fragments, one layer ahead
     {
         const float bias = W[Nt::boff(3) + col];
+#if NN_SPLIT
+        gemm_cols(IntC<8>(), IntC<0>(), W + Nt::soff(3), fetchA8(0), [&] { ring_load<1, 44>(W + Nt::woff(4), w, 8, 8, ring); });
+#else
         gemm_col(IntC<64>(), W + Nt::woff(3), fetchA(0), [&] { ring_load<1, 44>(W + Nt::woff(4), w, 8, 8, ring); });
+#endif
         lds_barrier();
 #pragma unroll
         for (int t = 0; t < 4; t++)

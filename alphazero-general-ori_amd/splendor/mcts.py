@@ -29,7 +29,7 @@ HDR_DTYPE = np.dtype([
     ("leaf_kind", "<i4"), ("player", "<i4"), ("episode_step", "<i4"), ("move_no", "<i4"),
     ("game_no", "<i4"), ("overflow", "<i4"), ("n_examples", "<i4"), ("leaf_round", "<i4"),
     ("leaf_k0", "<u8"), ("leaf_k1", "<u8"), ("leaf_v", "<f4", (4,)),
-    ("games_done", "<i4"), ("forced", "<i4"), ("moves", "<i4"), ("pad0", "<i4"),
+    ("games_done", "<i4"), ("forced", "<i4"), ("moves", "<i4"), ("wd_search", "<i4"),
     ("prunes", "<i4"), ("resets", "<i4"), ("unexpanded", "<i4"), ("gc_state", "<i4"),
     ("units_gc", "<i8"), ("enext", "<i8"),
     ("npg", "<i4"), ("epg", "<i4"), ("eleft", "<i4"), ("live_gc", "<i4"),

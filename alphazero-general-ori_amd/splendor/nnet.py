@@ -189,13 +189,40 @@ class FoldedNet(nn.Module):
         return pi, v
 
 
+def _bf16_parts(w):
+    """f32 w -> (hi, mid, lo) bf16 bit patterns (int32 holding 16 bits) by truncation, as the
+    kernel splits activations; hi + mid + lo == w exactly (lo keeps at most 8 significant bits)."""
+    u = w.contiguous().view(torch.int32)
+    hi = u & -65536
+    r1 = w - hi.view(torch.float32)
+    mid = r1.contiguous().view(torch.int32) & -65536
+    r2 = (r1 - mid.view(torch.float32)).contiguous().view(torch.int32)
+    return [(x >> 16) & 0xFFFF for x in (hi, mid, r2)]
+
+
+def _split_layer(w):
+    """The bf16 x 3 copy of a per-column layer (NN_SPLIT kernels): [4][Kp16/16][3][64][8]
+    bf16, element (nt, c, p, l, j) = part p of W[32 nt + l % 32][16 c + 8 (l / 32) + j], as
+    float32 storage (two bf16 per float, little-endian)."""
+    N, K = w.shape
+    k16 = (K + 15) // 16 * 16
+    wp = torch.zeros((128, k16), dtype=torch.float32, device=w.device)
+    wp[:N, :K] = w
+    parts = torch.stack(_bf16_parts(wp))                           # [3][128][k16]
+    # [p][nt][col][c][g][j] -> [nt][c][p][g][col][j]; lane = 32 g + col
+    t = parts.view(3, 4, 32, k16 // 16, 2, 8).permute(1, 3, 0, 4, 2, 5).reshape(-1, 2)
+    packed = (t[:, 0] | (t[:, 1] << 16)).to(torch.int32)
+    return packed.view(torch.float32)
+
+
 def pack_weights(folded, n_players):
     """Pack a FoldedNet into the layout k_nn_forward reads (include/splendor_amd.h,
     spl_nn_forward): per layer the MFMA B-fragment order — layers 0-3 (32x32x2):
     [NT][S/4][64][4], element (nt, q, l, j) = W[32 nt + (l & 31)][4 q + j + (l >> 5) S],
     S = Kp/2; layers 4-12 (16x16x4, Kp % 16 == 0): [NT][Kp/16][64][4], element (nt, q, l, j)
-    = W[16 nt + (l & 15)][16 q + 4 (l >> 4) + j] — then the 0-padded bias; finally the
-    per-column BN affines."""
+    = W[16 nt + (l & 15)][16 q + 4 (l >> 4) + j] — then the 0-padded bias; then the
+    per-column BN affines; then (16-byte aligned) the bf16 x 3 copies of layers 0-3 that
+    NN_SPLIT kernels read (_split_layer)."""
     f = folded
     layers = [(f.w1, f.b1), (f.w2, f.b2), (f.wp1, f.bp1), (f.w3, f.b3), (f.w4, f.b4), (f.wp4, f.bp4),
               (f.w5a, f.b5a), (f.w5b, f.b5b), (f.wp5, f.bp5), (f.wpi1, f.bpi1), (f.wpi2, f.bpi2),
@@ -222,6 +249,9 @@ def pack_weights(folded, n_players):
             bp[:N] = b
             parts.append(bp)
         parts += [f.s1.reshape(7), f.t1.reshape(7), f.sp1.reshape(7), f.tp1.reshape(7)]
+        pad = -sum(p.numel() for p in parts) % 4                    # 16-byte aligned split copies
+        parts.append(torch.zeros(pad, dtype=torch.float32, device=f.w1.device))
+        parts += [_split_layer(w) for w, _ in layers[:4]]
         out = torch.cat([p.float() for p in parts]).contiguous()
     want = _lib.lib().spl_nn_packed_floats(n_players)
     if out.numel() != want:
