@@ -554,7 +554,7 @@ __device__ __forceinline__ int block_min(int x, GcLds &L) {
     return m;
 }
 
-constexpr int GC_NOFIT = -2;   // compact_tree: the compacted tree would not fit its page table
+constexpr int GC_NOFIT = -2;   // compact_tree: the compacted tree would not fit the edge pages it holds
 template <int CR = 4>   // board units per thread per round trip of the node-board move (x2)
 __device__ int compact_tree(const Pools &P, int t, int root, int root_round, const GcScr &S, GcLds &L,
                             int bunits, bool linked = false) {
@@ -614,10 +614,12 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         }
         if (i < nc && remap[i] >= 0) S.nvs[i] = start;
     }
-    // packed with page-end gaps in an order other than the allocation order, the kept units
-    // may need more pages than the tree's page table holds (only near its maximum): nothing is
-    // written yet, the caller falls back to pruning / emptying
-    if (run > P.emax) return GC_NOFIT;
+    // packed with page-end gaps in an order other than the allocation order (a node's run and
+    // visit block together, by local index), the kept units may need more edge pages than the
+    // tree holds (the compaction moves units within its own pages and takes none from the
+    // pool: k_gc only pushes pages). Only with almost no garbage: nothing is written yet, the
+    // caller falls back to pruning / emptying.
+    if (run > H->epg * UPG) return GC_NOFIT;
     __syncthreads();
     // node records, chunk by chunk in local order (new slot <= old slot): reads, then writes
     int my_units = 0;
