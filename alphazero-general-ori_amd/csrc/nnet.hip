@@ -107,7 +107,7 @@ __device__ __forceinline__ f32x16 zero16() {
     return z;
 }
 
-__device__ __forceinline__ void mfma4(const float4 &a, const float4 &b, f32x16 &acc) {
+[[maybe_unused]] __device__ __forceinline__ void mfma4(const float4 &a, const float4 &b, f32x16 &acc) {
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
@@ -164,7 +164,7 @@ __device__ __forceinline__ void gemm_tiles(const float *__restrict__ wp, int nt,
 
 
 #ifndef NN_SPLIT
-#define NN_SPLIT 0      // 1: per-column layers on bf16 MFMAs with operands split in three parts
+#define NN_SPLIT 1      // per-column layers on bf16 MFMAs with operands split in three parts (0: f32 MFMA)
 #endif
 // Split per-column GEMMs (NN_SPLIT): an f32 x is exactly hi + mid + lo, three bf16 parts
 // taken by truncation (hi: the top 8 significant bits, mid: the top 8 of the residual, lo: the
@@ -445,12 +445,12 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const auto rowof = [&](int i) -> size_t { return idx ? (size_t)idx[b0 + i] : (size_t)(b0 + i); };
     const float *aff = W + Nt::AFF;                        // s1, t1, sp1, tp1
     const int t0 = 4 * wg, ntok = wg ? 3 : 4;              // this wave's token tiles (per-column layers)
-    constexpr int S1 = kpad(R) / 2;
 #if NN_SPLIT
     constexpr int C1 = kp16(R) / 16;
     RingS rings;                                           // per-column weight parts, one layer ahead
     rings_load<C1>(W + Nt::soff(0), wc, rings);
 #else
+    constexpr int S1 = kpad(R) / 2;
     RingC ringc;                                           // per-column weight fragments, one layer ahead
     ringc_load<S1>(W + Nt::woff(0), wc, ringc);
 #endif
@@ -529,9 +529,11 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 for (int r = 0; r < 16; r++)
                     bufA[((t0 + t) * ML + acc_row(r)) * XS + coloff] = f(acc[t][r], t0 + t);
     };
+#if !NN_SPLIT
     auto fetchA = [&](int col0) {
         return [&, col0](int t, int c) { return ld4(bufA + (t * ML + li) * XS + col0 + c); };
     };
+#endif
     NN_PROBE(0)
     // ---- dense2d_1: relu(s1[c] * (W1 x + b1) + t1[c])
     // (each layer's bias is read before its GEMM, ahead of the next layer's ring: vmcnt

@@ -424,7 +424,8 @@ def load_traffic(path, B, moves):
 
 
 def selfplay_roofline(rec, n, depth):
-    """Roofline block of the headline: the dominant kernel is k_nn_forward (MFMA-bound, fp32):
+    """Roofline block of the headline: the dominant kernel is k_nn_forward (MFMA-bound, f32
+    arithmetic; per-column layers on split-bf16 MFMAs, see mfma_mix):
     achieved = 1.19 MFLOP per leaf x B leaves / its HIP-event launch time. traffic = its HBM
     bytes per launch from the newest committed PMC summary (profiles/rNN_selfplay_pmc.json,
     tools/pmc_selfplay.sh); the tree kernels' measured bytes per simulation are set beside
@@ -446,6 +447,11 @@ def selfplay_roofline(rec, n, depth):
     tot = sum(v["hbm_bytes_per_sim"] or 0.0 for v in tree.values())
     return {"bound": "mfma", "achieved": nk["tflops"], "peak": FP32_MFMA_PEAK, "unit": "TFLOP/s",
             "frac": nk["frac_fp32_mfma_peak"],
+            "mfma_mix": "f32 arithmetic (the reference's precision): the 4 per-column layers (61 % of the "
+                        "FLOPs) on v_mfma_f32_32x32x16_bf16 with each f32 operand split exactly into three "
+                        "bf16 parts (six products per 16-k chunk, DESIGN.md §4), the 9 per-leaf layers on "
+                        "v_mfma_f32_16x16x4_f32; achieved counts the network's f32 FLOPs only, against "
+                        "the dense f32 MFMA peak",
             "traffic": nnfb.get("hbm_bytes_per_launch"),
             "kernel": nk["kernel"], "kernel_avg_us": nk["avg_us"],
             "kernel_avg_us_rocprof": nnfb.get("avg_us"), "rocprof_file": nnfb.get("file"),
