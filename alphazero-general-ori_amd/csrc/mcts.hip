@@ -541,18 +541,6 @@ __device__ __forceinline__ int block_scan(int x, int &total, GcLds &L) {   // ex
     total = tot;
     return off + incl - x;
 }
-__device__ __forceinline__ int block_min(int x, GcLds &L) {
-    const int l = lane_id(), w = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
-    if (l == 0) L.wsum[w] = x;
-    __syncthreads();
-    int m = L.wsum[0];
-#pragma unroll
-    for (int i = 1; i < GCW8; i++) m = min(m, L.wsum[i]);
-    __syncthreads();
-    return m;
-}
 
 constexpr int GC_NOFIT = -2;   // compact_tree: the compacted tree would not fit the edge pages it holds
 template <int CR = 4>   // board units per thread per round trip of the node-board move (x2)
@@ -579,41 +567,58 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     }
     __syncthreads();
     // new unit position of every kept node's allocation (run + visit records): packed in local
-    // order, an allocation that would straddle an edge page starts the next page (the nodes
-    // before the first straddler of a chunk are placed, the rest retried from that page's start)
-    int run = 0;
-    for (int base = 0; base < nc; base += GCT) {
-        const int i = base + tid;
+    // order, an allocation that would straddle an edge page starts the next page. The sizes
+    // are staged (all threads), then ONE wave walks the nodes 64 at a time with wave prefix
+    // sums, placing the lanes before the first straddler and retrying the rest from the next
+    // page — a few instructions per page boundary instead of block-wide scans (round 4: the
+    // block-scan version cost ~6 workgroup barriers per page boundary, most of a collection)
+    for (int i = tid; i < nc; i += GCT) {
         int sz = 0;
-        if (i < nc && remap[i] >= 0) {
+        if (remap[i] >= 0) {
             const int g = node_g(P, t, i);
             if (!P.nterm[g]) {
                 const NodeRun r = P.nrun[g];
                 sz = r.ec + REC_UNITS * r.vcnt;
             }
         }
-        bool pending = sz > 0;
-        int start = run;
-        for (;;) {
-            const int x = pending ? sz : 0;
-            int tot;
-            const int ex = block_scan(x, tot, L);
-            const int st = run + ex;
-            const bool strad = pending && (st & (UPG - 1)) + sz > UPG;
-            const int f = block_min(strad ? tid : GCT, L);
-            if (f == GCT) {
-                if (pending) start = st;
-                run += tot;
-                break;
-            }
-            if (pending && tid < f) { start = st; pending = false; }
-            if (tid == f) L.bc[0] = (st & ~(UPG - 1)) + UPG;
-            __syncthreads();
-            run = L.bc[0];
-            __syncthreads();
-        }
-        if (i < nc && remap[i] >= 0) S.nvs[i] = start;
+        S.nvs[i] = sz;
     }
+    __syncthreads();
+    if (tid < 64) {
+        const int l = tid;
+        int run = 0;
+        for (int base = 0; base < nc; base += 64) {
+            const int i = base + l;
+            const bool kept = i < nc && remap[i] >= 0;
+            const int sz = kept ? S.nvs[i] : 0;
+            bool pending = sz > 0;
+            int start = run;
+            for (;;) {
+                const int x = pending ? sz : 0;
+                int incl = x;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(incl, o, 64);
+                    if (l >= o) incl += y;
+                }
+                const int st = run + incl - x;
+                const bool strad = pending && (st & (UPG - 1)) + sz > UPG;
+                const uint64_t m = __ballot(strad);
+                if (!m) {
+                    if (pending) start = st;
+                    run += __shfl(incl, 63, 64);
+                    break;
+                }
+                const int f = __ffsll((unsigned long long)m) - 1;
+                if (pending && l < f) { start = st; pending = false; }
+                run = (__builtin_amdgcn_readlane(st, f) & ~(UPG - 1)) + UPG;
+            }
+            if (kept) S.nvs[i] = start;
+        }
+        if (l == 0) L.bc[0] = run;
+    }
+    __syncthreads();
+    const int run = L.bc[0];
     // packed with page-end gaps in an order other than the allocation order (a node's run and
     // visit block together, by local index), the kept units may need more edge pages than the
     // tree holds (the compaction moves units within its own pages and takes none from the
@@ -878,13 +883,16 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
 // begin_search's policy: compact (rounds > the root's), prune to the linked nodes, empty.
 // Queued trees come in bursts (games start together and commit together, so trees fill up
 // together): "should" collections beyond GC_SHOULD_CAP per launch stay queued for the next
-// launches (k_gc runs behind every self-play backup and commit), so the burst of a commit
-// iteration is spread over the following iterations. That is exact: a deferred tree searches
-// on as it is (its search fits), and if a leaf finds no room meanwhile the simulation is
-// withdrawn (gc_state 5 -> 1) and the tree collected in the next launch.
+// launches (k_gc runs behind every self-play backup and commit). That is exact: a deferred
+// tree searches on as it is (its search fits), and if a leaf finds no room meanwhile the
+// simulation is withdrawn (gc_state 5 -> 1) and the tree collected in the next launch. A
+// collection is a chain of dependent phases in one workgroup, so a launch costs about its
+// slowest collection however many run beside it: the cap is one round of workgroups (a
+// smaller cap spreads a burst over more launches that each pay that latency — round 4
+// measured 16 per launch at 195 us per launch, ~390 us per iteration at config 3).
 constexpr int GC_WG = 256;      // one per CU
 #ifndef GC_SHOULD_CAP
-#define GC_SHOULD_CAP 16
+#define GC_SHOULD_CAP GC_WG
 #endif
 template <int N>
 __global__ __launch_bounds__(GCT) void k_gc(Pools P, SearchCfg C) {
@@ -1708,7 +1716,13 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
     uint64_t k0 = 0, k1 = 0;
     float val[4] = {0, 0, 0, 0};
     int pend = -1, pend_n = 0, pend_x = 0;
+    // descend phase: every lane in DESCEND takes one level per round trip until it reaches the
+    // edge it expands (or a terminal child); then the expansions of all lanes run together —
+    // the expansion (board staging, transition, fingerprint, lookup) is long, and lanes
+    // reaching it at different levels would otherwise run it once per level in turn
+    // (measured: 342 us per select at config 3 with the two phases interleaved)
     while (__ballot(state != LS_DONE)) {
+      while (__ballot(state == LS_DESCEND)) {
         if (state == LS_DESCEND) {
             if (depth >= P.pcap) {
                 state = LS_DONE; kind = LEAF_NONE; H->overflow = 2;
@@ -1737,6 +1751,7 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                 }
             }
         }
+      }
         if (state == LS_EXPAND) {
             if (nbrd && bnode != node) {                 // stage this node's stored board
                 const uint64_t *src = nbrd + (size_t)node * (NodeBoard<N>::BYTES / 8);
