@@ -573,8 +573,9 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     // page — a few instructions per page boundary instead of block-wide scans (round 4: the
     // block-scan version cost ~6 workgroup barriers per page boundary, most of a collection)
     for (int i = tid; i < nc; i += GCT) {
-        int sz = 0;
+        int sz = -1;                                     // (-1: dropped)
         if (remap[i] >= 0) {
+            sz = 0;
             const int g = node_g(P, t, i);
             if (!P.nterm[g]) {
                 const NodeRun r = P.nrun[g];
@@ -587,10 +588,18 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     if (tid < 64) {
         const int l = tid;
         int run = 0;
+        constexpr int PD = 4;                            // chunks of sizes loaded ahead
+        int pre[PD];
+#pragma unroll
+        for (int d = 0; d < PD; d++) pre[d] = 64 * d + l < nc ? S.nvs[64 * d + l] : -1;
         for (int base = 0; base < nc; base += 64) {
             const int i = base + l;
-            const bool kept = i < nc && remap[i] >= 0;
-            const int sz = kept ? S.nvs[i] : 0;
+            const int szk = pre[0];
+#pragma unroll
+            for (int d = 0; d + 1 < PD; d++) pre[d] = pre[d + 1];
+            pre[PD - 1] = base + 64 * PD + l < nc ? S.nvs[base + 64 * PD + l] : -1;
+            const bool kept = szk >= 0;
+            const int sz = kept ? szk : 0;
             bool pending = sz > 0;
             int start = run;
             for (;;) {
@@ -685,35 +694,68 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     __syncthreads();
     // units staged by new position (a run's EdgeP units verbatim, visit records with their
     // links remapped), then written back; every thread writes back exactly the positions it
-    // staged, so only the workgroup barrier between the two passes is needed
-    for (int k = tid; k < run; k += GCT) {
-        const int j = S.own[k];
-        if (j < 0) continue;
-        const int rel = k - S.cs[j], ec = S.oec[j];
-        uint64_t v;
-        if (rel < ec) {
-            v = P.eu[S.ost[j] + rel];
-        } else {
-            const int rr = rel - ec;
-            v = P.eu[S.ovb[j] + rr];
-            if (rr % REC_UNITS == 1) {                   // {n, child}: the link remapped
-                const int ch = (int)(v >> 32);
-                int nch = -1;
-                if (ch >= 0) {
-                    BCHK(IN_TREE(P, t, ch, nc), 57, ((long long)j << 32) | (uint32_t)ch, t, (void)0);
-                    const int nl = remap[node_l(P, ch)];
-                    if (nl >= 0) nch = node_g(P, t, nl);
-                    BCHK(nl < 0 || P.nround[nch] == P.nround[node_g(P, t, j)] + 1, 41,
-                         ((long long)j << 32) | (uint32_t)nl, t, (void)0);
+    // staged, so only the workgroup barrier between the two passes is needed. SR positions
+    // per thread per batch with each stage's loads issued together (owner -> its old bases ->
+    // the unit -> the link's remap: four dependent round trips per batch, not per unit)
+    constexpr int SR = 8;
+    for (int k0 = 0; k0 < run; k0 += GCT * SR) {
+        int j[SR];
+#pragma unroll
+        for (int r = 0; r < SR; r++) {
+            const int k = k0 + GCT * r + tid;
+            j[r] = k < run ? S.own[k] : -1;
+        }
+        int64_t src[SR];
+        bool link[SR];
+#pragma unroll
+        for (int r = 0; r < SR; r++) {
+            src[r] = 0; link[r] = false;
+            if (j[r] >= 0) {
+                const int rel = k0 + GCT * r + tid - S.cs[j[r]], ec = S.oec[j[r]];
+                if (rel < ec) {
+                    src[r] = S.ost[j[r]] + rel;
+                } else {
+                    const int rr = rel - ec;
+                    src[r] = S.ovb[j[r]] + rr;
+                    link[r] = rr % REC_UNITS == 1;       // {n, child}: the link remapped
                 }
-                v = (v & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)nch << 32);
             }
         }
-        S.buf[k] = v;
+        uint64_t v[SR];
+#pragma unroll
+        for (int r = 0; r < SR; r++) v[r] = j[r] >= 0 ? P.eu[src[r]] : 0;
+#pragma unroll
+        for (int r = 0; r < SR; r++) {
+            if (!link[r]) continue;
+            const int ch = (int)(v[r] >> 32);
+            int nch = -1;
+            if (ch >= 0) {
+                BCHK(IN_TREE(P, t, ch, nc), 57, ((long long)j[r] << 32) | (uint32_t)ch, t, (void)0);
+                const int nl = remap[node_l(P, ch)];
+                if (nl >= 0) nch = node_g(P, t, nl);
+                BCHK(nl < 0 || P.nround[nch] == P.nround[node_g(P, t, j[r])] + 1, 41,
+                     ((long long)j[r] << 32) | (uint32_t)nl, t, (void)0);
+            }
+            v[r] = (v[r] & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)nch << 32);
+        }
+#pragma unroll
+        for (int r = 0; r < SR; r++)
+            if (j[r] >= 0) S.buf[k0 + GCT * r + tid] = v[r];
     }
     __syncthreads();
-    for (int k = tid; k < run; k += GCT)
-        if (S.own[k] >= 0) P.eu[unit_g(P, t, k)] = S.buf[k];
+    for (int k0 = 0; k0 < run; k0 += GCT * SR) {
+        int j[SR];
+        uint64_t v[SR];
+#pragma unroll
+        for (int r = 0; r < SR; r++) {
+            const int k = k0 + GCT * r + tid;
+            j[r] = k < run ? S.own[k] : -1;
+            v[r] = k < run ? S.buf[k] : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < SR; r++)
+            if (j[r] >= 0) P.eu[unit_g(P, t, k0 + GCT * r + tid)] = v[r];
+    }
     if (P.nbrd) {
         // node boards (bunits 16-byte units each) of new slot nn come from old slot inv[nn]
         // (>= nn), batches in increasing unit with all reads before the writes
