@@ -1706,26 +1706,10 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
     int kind = act ? LEAF_NN : LEAF_NONE;
     // resume on the previous simulation's path (same search: sims > 0; k_gc clears H->depth
     // when it moves nodes) at the first level whose node's cached pick no longer is the path's
-    // edge, or the previous leaf's parent; PATH_CHUNK levels per round trip
+    // edge, or the previous leaf's parent — k_backup, which moved those picks, recorded that
+    // level (H->resume); only a backup changes a cached pick between two selects of a search
     if (state == LS_DESCEND && sims > 0 && hdepth > 0) {
-        int q = hdepth - 1;
-        bool found = false;
-        for (int d0 = 0; d0 < hdepth && !found; d0 += PATH_CHUNK) {
-            int pn[PATH_CHUNK], px[PATH_CHUNK];
-#pragma unroll
-            for (int k = 0; k < PATH_CHUNK; k++) {
-                pn[k] = 0; px[k] = -1;
-                if (d0 + k < hdepth) { pn[k] = path_n[d0 + k]; px[k] = path_x[d0 + k]; }
-            }
-            int bk[PATH_CHUNK];
-#pragma unroll
-            for (int k = 0; k < PATH_CHUNK; k++) bk[k] = d0 + k < hdepth ? P.nst[pn[k]].best : -2;
-#pragma unroll
-            for (int k = 0; k < PATH_CHUNK; k++) {
-                const int d = d0 + k;
-                if (!found && d < hdepth && (bk[k] != px_off(px[k]) || (d == 0 && !root_cache))) { q = d; found = true; }
-            }
-        }
+        const int q = root_cache ? min(H->resume, hdepth - 1) : 0;
         node = path_n[q];
         depth = q;
         if (!nbrd)                                       // the resume node's board: the path's moves
@@ -2300,6 +2284,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     }
     if (depth > 0 && kind == LEAF_NN && l == (depth - 1 < 64 ? depth - 1 : 64)) V.child = lid;
     // ---- pass B: levels in groups of 64, lane per level (the first group's data is in hand)
+    int moved = 0x7fffffff;                              // the first level whose cached pick moved
     for (int g0 = 0; g0 < depth; g0 += 64) {
         const int d = g0 + l;
         const int cnt = min(64, depth - g0);
@@ -2308,6 +2293,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             load_levels(P, t, g0, depth, lid, V, in);
             if (in && V.grow > 0) V.nb = path_b[d];
         }
+        // visit blocks that move (a new record in a full block): every lane copies, level by
+        // level (one round trip per moving block instead of one per unit on its level's lane)
+        for (uint64_t gm = __ballot(in && V.e.vi < 0 && V.grow > 0 && V.nb >= 0 && V.r.vcnt > 0); gm; gm &= gm - 1) {
+            const int j = __ffsll((unsigned long long)gm) - 1;
+            const int64_t ob = readlane64(V.r.vb, j), nb = readlane64(V.nb, j);
+            const int nu = REC_UNITS * __builtin_amdgcn_readlane((int)V.r.vcnt, j);
+            for (int k = l; k < nu; k += 64) P.eu[nb + k] = P.eu[ob + k];
+        }
+        wave_lds_fence();                                // (copies by other lanes, read below)
         // MCTS.py:169-176: level d sees the leaf value rolled (depth - d) times; the levels
         // touch distinct nodes (rounds strictly increase along a path), so one lane per
         // level applies exactly the sequential update
@@ -2337,8 +2331,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             } else if (V.grow > 0 && V.nb < 0) {         // no room for the record (counted)
                 vidx = -1;
             } else {                                     // the edge's first visit: a record
-                if (V.grow > 0) {                        // (the block outgrown: moved)
-                    for (int k = 0; k < REC_UNITS * V.r.vcnt; k++) P.eu[V.nb + k] = P.eu[V.r.vb + k];
+                if (V.grow > 0) {                        // (the block outgrown: moved above)
                     V.r.vb = V.nb;
                     V.r.vcap = (int16_t)V.grow;
                 }
@@ -2428,6 +2421,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             const int bt_ = bch >= 0 ? (int)P.nterm[bch] : 0;
             P.nst[V.node] = NodeStat{nqs, nns, (int16_t)bsel, (int16_t)bact, bch, bt_, 0};
         }
+        moved = min(moved, wave_min_i32(in && bsel != V.off ? d : 0x7fffffff));
     }
     if (l == 0) {
         H->sims_done = h_sims + 1;
@@ -2435,6 +2429,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         H->leaf_kind = LEAF_NONE;
         H->depth_max = max(H->depth_max, depth);         // leaf depth statistics (diagnostic)
         H->depth_sum += depth;
+        H->resume = min(moved, max(depth - 1, 0));
     }
 }
 

@@ -40,8 +40,11 @@ struct TreeHdr {
     int32_t leaf_hslot, leaf_slot;       // the NN leaf's empty table slot (found by the
                                          // select's lookup) and reserved node slot, or -1
     int32_t depth_max, depth_sum;        // leaf depths of the simulations backed up: maximum, sum
+    int32_t resume;                      // the next descent's first new level (k_backup: the first
+                                         // path level whose cached pick moved, else the leaf's parent)
+    int32_t pad1, pad2, pad3;
 };
-static_assert(sizeof(TreeHdr) == 192, "TreeHdr layout (splendor/mcts.py HDR_DTYPE)");
+static_assert(sizeof(TreeHdr) == 208, "TreeHdr layout (splendor/mcts.py HDR_DTYPE)");
 // gc_state: 0 none; 1 a leaf did not fit mid-search (withdrawn, k_gc collects, the descent
 // repeats); 2 collected mid-search (a further withdrawal is allowed while wd_search < WD_MAX); 3 collection before this search (must: the
 // search does not fit the tree's maxima); 5 collection before this search (should: garbage

@@ -22,7 +22,7 @@ import torch
 from . import _lib
 from .env import ACTIONS, MASK_WORDS, _ptr
 
-# TreeHdr (csrc/mcts_device.h), 192 bytes
+# TreeHdr (csrc/mcts_device.h), 208 bytes
 HDR_DTYPE = np.dtype([
     ("node_count", "<i4"), ("edge_count", "<i4"), ("root", "<i4"), ("sims_done", "<i4"),
     ("budget", "<i4"), ("full", "<i4"), ("noise_pending", "<i4"), ("depth", "<i4"),
@@ -34,8 +34,9 @@ HDR_DTYPE = np.dtype([
     ("units_gc", "<i8"), ("enext", "<i8"),
     ("npg", "<i4"), ("epg", "<i4"), ("eleft", "<i4"), ("live_gc", "<i4"),
     ("root_round", "<i4"), ("gc_queued", "<i4"), ("withdrawals", "<i4"), ("gcs", "<i4"),
-    ("leaf_hslot", "<i4"), ("leaf_slot", "<i4"), ("depth_max", "<i4"), ("depth_sum", "<i4")])
-assert HDR_DTYPE.itemsize == 192
+    ("leaf_hslot", "<i4"), ("leaf_slot", "<i4"), ("depth_max", "<i4"), ("depth_sum", "<i4"),
+    ("resume", "<i4"), ("pad1", "<i4"), ("pad2", "<i4"), ("pad3", "<i4")])
+assert HDR_DTYPE.itemsize == 208
 
 DEFAULT_ARGS = dict(numMCTSSims=100, cpuct=1.0, fpu=0.0, prob_fullMCTS=1.0, ratio_fullMCTS=5,
                     forced_playouts=False, dirichletAlpha=0.0, temperature=[1.25, 0.8],

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 6
+#define SPL_ABI_VERSION 7
 #define SPL_ACTIONS 409
 #define SPL_MASK_WORDS 7
 #define SPL_EINVAL (-1)
@@ -258,7 +258,7 @@ int spl_mcts_pool_pages(const spl_mcts *m, long long *out4);   /* pages, pages, 
 int spl_mcts_drain_examples(spl_mcts *m, int8_t *state, float *pi, uint64_t *valid,
                             float *winner, int32_t *scdiff, float *q, int32_t *meta, int max,
                             int32_t *n_out, void *hip_stream);
-/* copies the B per-tree headers (192 bytes each, layout in splendor/mcts.py) to `out` */
+/* copies the B per-tree headers (208 bytes each, layout in splendor/mcts.py) to `out` */
 int spl_mcts_headers(spl_mcts *m, int32_t *out, void *hip_stream);
 
 /* out B x 4 i32 per tree: node slots used, edge slots used, live nodes (the root and every
