@@ -2004,7 +2004,7 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
 #define BK_WIDE 12
 #endif
 #ifndef BACKUP_WAVES
-#define BACKUP_WAVES 5
+#define BACKUP_WAVES 4
 #endif
 
 struct Screen {
