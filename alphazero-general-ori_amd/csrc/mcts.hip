@@ -2081,10 +2081,10 @@ struct Level {
 };
 
 // the loads of one group: path entries, node records, the edges taken and their records
-__device__ __forceinline__ void load_levels(const Pools &P, int t, int g0, int depth, int lid, Level &V, bool in) {
+// (level d of tree t on this lane)
+__device__ __forceinline__ void load_levels_at(const Pools &P, int t, int d, int depth, int lid, Level &V, bool in) {
     const int32_t *path_n = P.path_n + (size_t)t * (P.pcap + 1);
     const int32_t *path_x = P.path_x + (size_t)t * P.pcap;
-    const int d = g0 + lane_id();
     V.node = 0; V.off = 0; V.act = 0; V.child = -1; V.ns = 0; V.qs = 0.0;
     V.r = NodeRun{0, 0, 0, 0, 0, 0}; V.e = EdgeP{0.f, 0, -1}; V.n = 0; V.q = Q_UNSET; V.rchild = -1;
     V.grow = 0; V.nb = -1;
@@ -2105,6 +2105,9 @@ __device__ __forceinline__ void load_levels(const Pools &P, int t, int g0, int d
         // edges fastest, and its block then never moves again during the search)
         V.grow = d == 0 ? (int)V.r.ec : (V.r.vcap == 0 ? 1 : min(2 * (int)V.r.vcap, (int)V.r.ec));
     }
+}
+__device__ __forceinline__ void load_levels(const Pools &P, int t, int g0, int depth, int lid, Level &V, bool in) {
+    load_levels_at(P, t, g0 + lane_id(), depth, lid, V, in);
 }
 
 #ifndef WD_MAX
@@ -2428,6 +2431,361 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         H->noise_pending = 0;
         H->leaf_kind = LEAF_NONE;
         H->depth_max = max(H->depth_max, depth);         // leaf depth statistics (diagnostic)
+        H->depth_sum += depth;
+        H->resume = min(moved, max(depth - 1, 0));
+    }
+}
+
+// ------------------------------------------------------------ backup, two trees per wave
+// k_backup_h: k_backup with each wave's halves on two trees (lanes [32h, 32h + 32) on tree
+// 2 w + h, lane per path level, levels in groups of 32). k_backup's time scales with the
+// number of trees at a fixed occupancy (latency of ~15-20 dependent round trips per tree,
+// 4 waves per SIMD by registers); two trees per wave double the trees in flight. Per-tree
+// collective steps (the policy staging and prior sums, the sorted run, the new node's
+// arg-max, allocations, the resume level) run on 32-lane halves; steps that need the whole
+// wave (root noise, the exact evaluation of a level, block copies) take the two trees' items
+// in turn. Same arithmetic, same order of every sum: bit-identical to k_backup.
+__device__ __forceinline__ int hbase() { return lane_id() & 32; }
+__device__ __forceinline__ int half_min_i32(int x) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
+    return x;
+}
+__device__ __forceinline__ int half_sum_i32(int x) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+__device__ __forceinline__ double half_max_f64(double x) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        const int lo = __shfl_xor(__double2loint(x), o, 64), hi = __shfl_xor(__double2hiint(x), o, 64);
+        x = fmax(x, __hiloint2double(hi, lo));
+    }
+    return x;
+}
+__device__ __forceinline__ int64_t shfl64(int64_t x, int src) {
+    const int lo = __shfl((int)(uint32_t)(uint64_t)x, src, 64), hi = __shfl((int)((uint64_t)x >> 32), src, 64);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// wave_np_sum409 on a half: the same blocks and combining order, lanes hbase() + 0 .. 31
+__device__ __forceinline__ float half_np_sum409(const float *a) {
+    const int l = lane_id() & 31, hb = hbase();
+    const int blk = (l >> 3) & 3, j = l & 7;
+    const int off = blk == 0 ? 0 : (blk == 1 ? 96 : (blk == 2 ? 200 : 304));
+    const int len = blk == 0 ? 96 : (blk == 3 ? 105 : 104);
+    float r = a[off + j];
+    for (int i = 8; i < len - (len % 8); i += 8) r += a[off + i + j];
+    float r1 = __shfl_xor(r, 1, 64);
+    float p01 = (j & 1) ? r1 + r : r + r1;
+    float p23 = __shfl_xor(p01, 2, 64);
+    float q = (j & 2) ? p23 + p01 : p01 + p23;
+    float q2 = __shfl_xor(q, 4, 64);
+    float res = (j & 4) ? q2 + q : q + q2;
+    float blockv = __shfl(res, hb + 8 * blk, 64);
+    if (blk == 3) blockv = blockv + a[off + 104];
+    const float b0 = __shfl(blockv, hb, 64), b1 = __shfl(blockv, hb + 8, 64);
+    const float b2 = __shfl(blockv, hb + 16, 64), b3 = __shfl(blockv, hb + 24, 64);
+    return (b0 + b1) + (b2 + b3);
+}
+// write_sorted_run of a new node (no visit records yet) on a half
+__device__ __forceinline__ void half_write_new_run(const Pools &P, int64_t eb, int ec, const float *cp,
+                                                   const int16_t *ca) {
+    for (int i = lane_id() & 31; i < ec; i += 32) {
+        const float pi = cp[i];
+        int r = 0;
+        for (int j = 0; j < ec; j++) {
+            const float pj = cp[j];
+            r += (pj > pi) || (pj == pi && j < i);
+        }
+        *P.ep(eb + r) = EdgeP{pi, ca[i], (int16_t)-1};
+    }
+}
+struct BkScr {                         // a half's scratch: the leaf's policy and mask, its run
+    uint64_t bits[7];
+    float pr[416];
+    float cp[SPL_ACTIONS];
+    int16_t ca[SPL_ACTIONS];
+};
+
+template <int N, int KINDS>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_WAVES))) void k_backup_h(
+    Pools P, SearchCfg C, int B, const uint64_t *__restrict__ leaf_mask, const float *__restrict__ pi,
+    const float *__restrict__ v) {
+    __shared__ BkScr scr[2 * WAVES];
+    const int w = uniform(threadIdx.x >> 6), l = lane_id(), hl = l & 31, hb = l & 32, half = l >> 5;
+    const int t = 2 * (blockIdx.x * WAVES + w) + half;
+    const bool tv = t < B;
+    TreeHdr *H = P.hdr + (tv ? t : 0);
+    const int kind0 = tv ? H->leaf_kind : LEAF_NONE;
+    const bool act = kind0 != LEAF_NONE && ((KINDS >> (kind0 - 1)) & 1);
+    if (!__ballot(act)) return;
+    bool done = !act;                                    // this half's tree has nothing (more) to do
+    const int kind = act ? kind0 : LEAF_NONE;
+    const int depth = act ? H->depth : 0;
+    const int h_slot = H->leaf_slot, h_hslot = H->leaf_hslot, h_round = H->leaf_round;
+    const uint64_t h_k0 = H->leaf_k0, h_k1 = H->leaf_k1;
+    const int h_sims = H->sims_done, h_noise = H->noise_pending, h_gc = H->gc_state;
+    const int32_t *path_n = P.path_n + (size_t)(tv ? t : 0) * (P.pcap + 1);
+    int64_t *path_b = P.path_b + (size_t)(tv ? t : 0) * P.pcap;
+    float val[4] = {0, 0, 0, 0};
+    int lid = -1;
+    BkScr &S = scr[2 * w + half];
+    if (kind == LEAF_NN) {
+        const float *gp = pi + (size_t)t * SPL_ACTIONS;
+#pragma unroll
+        for (int k = 0; k < 13; k++)
+            if (32 * k + hl < SPL_ACTIONS) S.pr[32 * k + hl] = gp[32 * k + hl];
+        if (hl < 7) S.bits[hl] = leaf_mask[(size_t)t * 7 + hl];
+#pragma unroll
+        for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
+    } else if (kind == LEAF_TERMINAL) {
+#pragma unroll
+        for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
+        lid = path_n[depth];
+    }
+    const int dmax = max(__shfl(depth, 0, 64), __shfl(depth, 32, 64));   // (uniform group loops)
+    // ---- pass A (as k_backup)
+    Level V;
+    load_levels_at(P, t, hl, depth, lid, V, act && hl < min(depth, 32));
+    bool fail = false;
+    for (int g0 = 0; g0 < dmax; g0 += 32) {
+        Level Vg;
+        if (g0 > 0) load_levels_at(P, t, g0 + hl, depth, lid, Vg, act && g0 + hl < depth);
+        const int grow = g0 == 0 ? V.grow : Vg.grow;
+        uint64_t gm = __ballot(grow > 0);
+        int64_t nb = -1;
+        while (gm) {                                     // (both halves' blocks in turn)
+            const int j = __ffsll((unsigned long long)gm) - 1;
+            gm &= gm - 1;
+            const int units = REC_UNITS * __builtin_amdgcn_readlane(grow, j);
+            const bool mine = hb == (j & 32);
+            int64_t b = -1;
+            if (l == (j & 32) && !fail) b = unit_alloc(P, H, t, units);
+            b = readlane64(b, j & 32);
+            if (mine && b < 0) fail = true;
+            if (l == j) nb = b;
+        }
+        if (g0 == 0) V.nb = nb;
+        else if (grow > 0) path_b[g0 + hl] = nb;
+    }
+    int g = -1, ec = 0;
+    int64_t eb = -1;
+    if (kind == LEAF_NN) {
+        wave_lds_fence();
+#pragma unroll
+        for (int k = 0; k < 7; k++) ec += __popcll(S.bits[k]);
+        if (!fail && hl == 0) {
+            g = h_slot >= 0 ? h_slot : node_slot(P, H, t, H->node_count);
+            if (g >= 0) eb = unit_alloc(P, H, t, ec);
+        }
+    }
+    g = __shfl(g, hb, 64);
+    eb = shfl64(eb, hb);
+    if (act && (fail || (kind == LEAF_NN && eb < 0)) && C.selfplay && depth > 0 &&
+        (h_gc == 0 || h_gc == 5 || (h_gc == 2 && H->wd_search < WD_MAX))) {
+        if (hl == 0) {                                   // withdrawn (see k_backup)
+            H->gc_state = 1;
+            H->leaf_kind = LEAF_NONE;
+            H->withdrawals += 1;
+            H->wd_search += 1;
+            gc_push(P, H, t);
+        }
+        done = true;
+    }
+    if (!done && fail && hl == 0) H->unexpanded += 1;
+    const bool expand = !done && kind == LEAF_NN && eb >= 0;
+    if (!done && kind == LEAF_NN && eb < 0 && hl == 0) H->unexpanded += 1;
+    // root noise on a new root (whole wave, one tree at a time)
+    const bool noise = expand && depth == 0 && h_sims == 0 && h_noise;
+    for (uint64_t nm = __ballot(noise && hl == 0); nm; nm &= nm - 1) {
+        const int j = __ffsll((unsigned long long)nm) - 1;
+        BkScr &Sj = scr[2 * w + (j >> 5)];
+        root_noise_lds(C, __builtin_amdgcn_readlane(t, j), ST_DIR | (uint32_t)__builtin_amdgcn_readlane(H->move_no, j),
+                       Sj.pr, Sj.bits, __builtin_amdgcn_readlane(ec, j));
+    }
+    if (expand) {
+        float *pr = S.pr;
+        if (!noise) {
+            const float sum = half_np_sum409(pr);
+            wave_lds_fence();
+            for (int a = hl; a < SPL_ACTIONS; a += 32) pr[a] = pr[a] / sum;
+            wave_lds_fence();
+        }
+        int run = 0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const uint64_t wd = S.bits[k];
+#pragma unroll
+            for (int hh = 0; hh < 2; hh++) {
+                const int bit = 32 * hh + hl;
+                if ((wd >> bit) & 1) {
+                    const int r = run + __popcll(wd & ((1ull << bit) - 1));
+                    S.cp[r] = pr[64 * k + bit];
+                    S.ca[r] = (int16_t)(64 * k + bit);
+                }
+            }
+            run += __popcll(wd);
+        }
+        wave_lds_fence();
+        half_write_new_run(P, eb, ec, S.cp, S.ca);
+    }
+    {                                                    // the new node's arg-max (see k_backup)
+        int bsel = -1, bact = 0;
+        double bu = -INFINITY;
+        int ba = 0x7fffffff;
+        const bool narg = expand && depth > 0;
+        if (narg) {
+            const double fpu_init = fpu_base(C.fpu, (double)val[0]), sq_eps = sqrt(1e-8);
+            for (int i = hl; i < ec; i += 32) {
+                const double u = ucb_unvisited(S.cp[i], C.cpuct, fpu_init, sq_eps);
+                if (u > bu || (u == bu && S.ca[i] < ba)) { bu = u; ba = S.ca[i]; }
+            }
+        }
+        const double mu = half_max_f64(bu);
+        bact = half_min_i32(bu == mu ? ba : 0x7fffffff);
+        int r = 0;
+        if (narg) {
+            const float pb = S.pr[bact];
+            for (int i = hl; i < ec; i += 32) r += (S.cp[i] > pb) || (S.cp[i] == pb && S.ca[i] < bact);
+        }
+        r = half_sum_i32(r);
+        if (narg) bsel = r;
+        else bact = 0;
+        if (expand && hl == 0) {
+            P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
+            P.nrun[g] = NodeRun{eb, 0, (int16_t)ec, 0, 0, 0};
+            P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)bsel, (int16_t)bact, -1, 0, 0};
+            P.nround[g] = h_round; P.nterm[g] = 0;
+            if (h_hslot >= 0) P.hslot[(size_t)t * P.hcap + h_hslot] = g;
+            else hash_insert(P, t, h_k0, g);
+            if (depth == 0) H->root = g;
+            H->node_count += 1;
+        }
+        if (expand) lid = g;
+    }
+    if (!done && depth > 0 && kind == LEAF_NN && hl == (depth - 1 < 32 ? depth - 1 : 32)) V.child = lid;
+    // ---- pass B (as k_backup), levels in groups of 32 per half
+    int moved = 0x7fffffff;
+    for (int g0 = 0; g0 < dmax; g0 += 32) {
+        const int d = g0 + hl;
+        const bool in = !done && d < depth;
+        if (g0 > 0) {
+            load_levels_at(P, t, d, depth, lid, V, in);
+            if (in && V.grow > 0) V.nb = path_b[d];
+        }
+        for (uint64_t gm = __ballot(in && V.e.vi < 0 && V.grow > 0 && V.nb >= 0 && V.r.vcnt > 0); gm; gm &= gm - 1) {
+            const int j = __ffsll((unsigned long long)gm) - 1;
+            const int64_t ob = readlane64(V.r.vb, j), nb = readlane64(V.nb, j);
+            const int nu = REC_UNITS * __builtin_amdgcn_readlane((int)V.r.vcnt, j);
+            for (int k = l; k < nu; k += 64) P.eu[nb + k] = P.eu[ob + k];
+        }
+        wave_lds_fence();
+        int n1 = 0, vidx = -1, nns = 0;
+        double q1 = 0.0, nqs = 0.0;
+        if (in) {
+            const int rot = (depth - d) % N, vi = (N - rot) % N;
+            float vr = val[0];
+#pragma unroll
+            for (int i = 1; i < N; i++) vr = vi == i ? val[i] : vr;
+            const double v0 = (double)vr;
+            nqs = ((double)(V.ns + 1) * V.qs + v0) / (double)(V.ns + 2);
+            nns = V.ns + 1;
+            q1 = ((double)V.n * V.q + v0) / (double)(V.n + 1);
+            n1 = V.n + 1;
+            if (V.e.vi >= 0) {
+                vidx = V.e.vi;
+                VisitRec *R = P.vr(V.r.vb + REC_UNITS * vidx);
+                R->q = q1;
+                R->n = n1;
+                if (V.rchild < 0 && V.child >= 0) R->child = V.child;
+            } else if (V.grow > 0 && V.nb < 0) {
+                vidx = -1;
+            } else {
+                if (V.grow > 0) {
+                    V.r.vb = V.nb;
+                    V.r.vcap = (int16_t)V.grow;
+                }
+                vidx = V.r.vcnt;
+                *P.vr(V.r.vb + REC_UNITS * vidx) = VisitRec{q1, n1, V.child, V.e.p, (int16_t)V.off, (int16_t)V.act};
+                P.ep(V.r.eb + V.off)->vi = (int16_t)vidx;
+                V.r.vcnt = (int16_t)(vidx + 1);
+                if (V.off == V.r.cand) {
+                    int j = V.off + 1;
+                    while (j < V.r.ec && P.ep(V.r.eb + j)->vi >= 0) j++;
+                    V.r.cand = (int16_t)j;
+                }
+                P.nrun[V.node] = V.r;
+            }
+            V.rchild = V.rchild >= 0 ? V.rchild : V.child;
+        }
+        const bool wide = in && V.r.vcnt > BK_WIDE;
+        Screen Sc = screen_init(nns, nqs, C.cpuct, C.fpu);
+        bool has_c = false;
+        double uc = 0.0;
+        int ac = 0, rc = 0;
+        if (in && V.r.cand < V.r.ec) {
+            has_c = true;
+            const EdgeP c = *P.ep(V.r.eb + V.r.cand);
+            rc = V.r.cand; ac = c.a;
+            screen_item(Sc, false, c.p, 0, 0.0, rc, c.a, -1);
+            if (c.p > 0.f) {
+                for (int j = V.r.cand + 1; j < V.r.ec; j++) {
+                    const EdgeP e = *P.ep(V.r.eb + j);
+                    if (e.vi >= 0 || e.p == c.p) continue;
+                    screen_item(Sc, false, e.p, 0, 0.0, j, e.a, -1);
+                    break;
+                }
+            }
+        }
+        const int myv = in && !wide ? V.r.vcnt : 0;
+        const int maxv = wave_max_i32(myv);
+        for (int base = 0; base < maxv; base += BK_BATCH) {
+            VisitRec rb[BK_BATCH];
+#pragma unroll
+            for (int k = 0; k < BK_BATCH; k++)
+                if (base + k < myv) rb[k] = *P.vr(V.r.vb + REC_UNITS * (base + k));
+#pragma unroll
+            for (int k = 0; k < BK_BATCH; k++) {
+                const int i = base + k;
+                if (i < myv) {
+                    const VisitRec &R = rb[k];
+                    const bool mine = i == vidx;
+                    screen_item(Sc, true, R.p, mine ? n1 : R.n, mine ? q1 : R.q, R.off, R.a, mine ? V.rchild : R.child);
+                }
+            }
+        }
+        bool open = in && (wide || !(Sc.H2 < Sc.L1));
+        int bsel = Sc.off, bact = Sc.a, bch = Sc.child;
+        if (open && has_c) {
+            double u;
+            rc = best_unvisited(P, V.r.eb, V.r.ec, V.r.cand, C.cpuct, fpu_base(C.fpu, nqs), sqrt((double)nns + 1e-8),
+                                u, ac);
+            uc = u;
+        }
+        wave_lds_fence();
+        for (uint64_t ex = __ballot(open); ex; ex &= ex - 1) {
+            const int j = __ffsll((unsigned long long)ex) - 1;
+            int rk, ak, ck;
+            exact_level(P, readlane64(V.r.vb, j), __builtin_amdgcn_readlane((int)V.r.vcnt, j),
+                        __builtin_amdgcn_readlane(nns, j), C.cpuct, __builtin_amdgcn_readlane(vidx, j),
+                        __builtin_amdgcn_readlane(n1, j), readlane_f64(q1, j),
+                        __builtin_amdgcn_readlane((int)has_c, j) != 0, readlane_f64(uc, j),
+                        __builtin_amdgcn_readlane(ac, j), __builtin_amdgcn_readlane(rc, j), rk, ak, ck);
+            if (l == j) { bsel = rk; bact = ak; bch = ck; }
+        }
+        if (in) {
+            if (bsel == V.off) bch = V.rchild;
+            const int bt_ = bch >= 0 ? (int)P.nterm[bch] : 0;
+            P.nst[V.node] = NodeStat{nqs, nns, (int16_t)bsel, (int16_t)bact, bch, bt_, 0};
+        }
+        moved = min(moved, half_min_i32(in && bsel != V.off ? d : 0x7fffffff));
+    }
+    if (!done && hl == 0) {
+        H->sims_done = h_sims + 1;
+        H->noise_pending = 0;
+        H->leaf_kind = LEAF_NONE;
+        H->depth_max = max(H->depth_max, depth);
         H->depth_sum += depth;
         H->resume = min(moved, max(depth - 1, 0));
     }
@@ -2929,10 +3287,25 @@ int spl_mcts_select_compact(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask
     return launch_select(m, leaf_state, leaf_mask, leaf_valid, leaf_index, leaf_count, hs);
 }
 
+#ifndef BACKUP_HALF
+#define BACKUP_HALF 1      // k_backup_h (two trees per wave); 0: k_backup (one tree per wave)
+#endif
 int spl_mcts_backup_kind(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v, int kinds,
                          void *hs) {
     if (!m || kinds < 1 || kinds > 3 || ((kinds & SPL_LEAF_NN) && (!leaf_mask || !pi || !v))) return SPL_EINVAL;
-    if (kinds == 3) {
+    if (BACKUP_HALF) {
+        const dim3 grid = wave_grid((m->B + 1) / 2);
+        if (kinds == 3) {
+            SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup_h<N, 3>), grid, dim3(THREADS), 0, (hipStream_t)hs, m->P,
+                                                  m->cfg, m->B, leaf_mask, pi, v));
+        } else if (kinds == SPL_LEAF_NN) {
+            SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup_h<N, 1>), grid, dim3(THREADS), 0, (hipStream_t)hs, m->P,
+                                                  m->cfg, m->B, leaf_mask, pi, v));
+        } else {
+            SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup_h<N, 2>), grid, dim3(THREADS), 0, (hipStream_t)hs, m->P,
+                                                  m->cfg, m->B, leaf_mask, pi, v));
+        }
+    } else if (kinds == 3) {
         SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup<N, 3>), wave_grid(m->B), dim3(THREADS), 0,
                                               (hipStream_t)hs, m->P, m->cfg, m->B, leaf_mask, pi, v));
     } else if (kinds == SPL_LEAF_NN) {
