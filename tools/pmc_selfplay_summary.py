@@ -16,8 +16,9 @@ KERNELS = ("k_select", "k_leaf_mask", "k_nn_forward", "k_backup", "k_commit", "k
 
 
 def _kname(k):
-    """k_select_lanes (lane per tree) is the select kernel: reported as k_select."""
-    return "k_select" if k == "k_select_lanes" else k
+    """k_select_lanes (lane per tree) is the select kernel, k_backup_h (two trees per wave) the
+    backup kernel: reported as k_select / k_backup."""
+    return {"k_select_lanes": "k_select", "k_backup_h": "k_backup"}.get(k, k)
 
 def per_kernel(d, last=None):
     """Counter averages per dispatch of each kernel, over its last `last` dispatches."""
