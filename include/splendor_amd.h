@@ -283,7 +283,9 @@ int spl_hash_eval_mode(const spl_ctx *ctx, int B, const int8_t *state, const uin
  * SplendorNNet inference (SplendorNNet.py:56-159 in eval mode; GenericNNetWrapper.predict
  * :141-168 minus the host round trip) as one fused kernel: int8 boards [B][R][7] + packed
  * masks [B][7] -> pi [B][409] = softmax(masked logits, invalid -> -1e8) and v [B][n] =
- * tanh(value head). fp32 throughout (products and accumulation in f32, MFMA).
+ * tanh(value head). f32 arithmetic: the per-column layers on bf16 MFMAs with every f32
+ * operand split exactly into three bf16 parts (six products per 16-k chunk, the largest in its
+ * own f32 accumulator), the per-leaf layers on f32 MFMA.
  *
  * packed_weights: spl_nn_packed_floats(n) floats, 16-byte aligned, the eval-mode network
  * with BatchNorms folded (splendor/nnet.py pack_weights). For each of the 13 linear layers
@@ -298,7 +300,11 @@ int spl_hash_eval_mode(const spl_ctx *ctx, int B, const int8_t *state, const uin
  *     (0 outside N x K)
  *     bias    [T NT] (0-padded)
  * then the per-board-column BatchNorm affines of dense2d_1 and partialgpool_1:
- * s1[7], t1[7], sp1[7], tp1[7] (y = x * s + t). Returns the float count or SPL_EINVAL. */
+ * s1[7], t1[7], sp1[7], tp1[7] (y = x * s + t); then, from the next 16-byte boundary, the
+ * first 4 layers again as exact three-part bf16 splits (w = hi + mid + lo by truncation) for
+ * the bf16-MFMA form of those layers: per layer [4][Kp16/16][3][64][8] bf16 (Kp16 = K rounded
+ * up to 16), element (nt, c, p, l, j) = part p of W[32 nt + l % 32][16 c + 8 (l / 32) + j],
+ * two bf16 per float slot. Returns the float count or SPL_EINVAL. */
 int spl_nn_packed_floats(int n_players);
 int spl_nn_forward(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
                    const float *packed_weights, float *pi, float *v, void *hip_stream);
