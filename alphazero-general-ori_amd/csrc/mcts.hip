@@ -642,7 +642,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         const int ni = i < nc ? remap[i] : -1;
         uint64_t k0 = 0, k1 = 0;
         NodeRun nr{0, 0, 0, 0, 0, 0};
-        NodeStat nst{0.0, 0, -1, 0, -1, 0, 0};
+        NodeStat nst{0.0, 0, -1, 0, -1, 0, -1};
         int rd = 0, vs = 0;
         int8_t term = 0;
         if (ni >= 0) {
@@ -1532,7 +1532,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_
                     } else {
                         P.nkey0[g] = k0; P.nkey1[g] = k1;
                         P.nrun[g] = term_run(val);
-                        P.nst[g] = NodeStat{0.0, 0, -1, 0, -1, 0, 0};
+                        P.nst[g] = NodeStat{0.0, 0, -1, 0, -1, 0, -1};
                         P.nround[g] = (uint8_t)bt(row(s, 0), 6); P.nterm[g] = 1;
                         hash_insert(P, t, k0, g);
                         if (cached) { P.nst[node].bchild = g; P.nst[node].bterm = 1; }
@@ -1719,7 +1719,7 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
     // root): wave-collective, one tree at a time, before the lanes descend
     Pick pk{0, 0, -1, 0};
     bool have_pk = false;
-    NodeStat nsq{0.0, 0, -1, 0, -1, 0, 0};
+    NodeStat nsq{0.0, 0, -1, 0, -1, 0, -1};
     if (state == LS_DESCEND) nsq = P.nst[node];
     const bool scan = state == LS_DESCEND && depth == 0 && (!root_cache || nsq.best < 0);
     for (uint64_t m = __ballot(scan); m; m &= m - 1) {
@@ -1831,7 +1831,7 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                         } else {
                             P.nkey0[g] = k0; P.nkey1[g] = k1;
                             P.nrun[g] = term_run(val);
-                            P.nst[g] = NodeStat{0.0, 0, -1, 0, -1, 0, 0};
+                            P.nst[g] = NodeStat{0.0, 0, -1, 0, -1, 0, -1};
                             P.nround[g] = (uint8_t)bt(row(s, 0), 6); P.nterm[g] = 1;
                             hash_insert(P, t, k0, g);
                             if (cached) { P.nst[node].bchild = g; P.nst[node].bterm = 1; }
@@ -2009,7 +2009,7 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
 
 struct Screen {
     float L1, H1, H2, cf, ff, sqv, sqe;
-    int off, a, child;        // the leading item: rank, action, link
+    int off, a, child, vi;    // the leading item: rank, action, link, visit record (-1: none)
 };
 __device__ __forceinline__ Screen screen_init(int ns, double qs, double cpuct, double fpu) {
     Screen S;
@@ -2019,12 +2019,13 @@ __device__ __forceinline__ Screen screen_init(int ns, double qs, double cpuct, d
     S.sqv = __builtin_amdgcn_sqrtf(nf);
     S.sqe = __builtin_amdgcn_sqrtf(nf + 1e-8f);
     S.L1 = -INFINITY; S.H1 = -INFINITY; S.H2 = -INFINITY;
-    S.off = 0; S.a = 0; S.child = -1;
+    S.off = 0; S.a = 0; S.child = -1; S.vi = -1;
     return S;
 }
 // one edge's float32 UCB estimate with its error bound (|estimate - the reference's float64
 // value| <= e = 2.1e-6 (|u| + |q|), tests/test_ucb_screen.py)
-__device__ __forceinline__ void screen_item(Screen &S, bool vis, float p, int n, double q, int off, int a, int child) {
+__device__ __forceinline__ void screen_item(Screen &S, bool vis, float p, int n, double q, int off, int a, int child,
+                                            int vi = -1) {
     const float rc = vis ? __builtin_amdgcn_rcpf(1.f + (float)n) : 1.f;
     const float qf = vis ? (float)q : S.ff;
     const float uf = qf + S.cf * p * (vis ? S.sqv : S.sqe) * rc;
@@ -2032,7 +2033,7 @@ __device__ __forceinline__ void screen_item(Screen &S, bool vis, float p, int n,
     const float lo = uf - er, hi = uf + er;
     if (lo > S.L1) {
         S.H2 = fmaxf(S.H2, S.H1); S.L1 = lo; S.H1 = hi;
-        S.off = off; S.a = a; S.child = child;
+        S.off = off; S.a = a; S.child = child; S.vi = vi;
     } else {
         S.H2 = fmaxf(S.H2, hi);
     }
@@ -2042,11 +2043,11 @@ __device__ __forceinline__ void screen_item(Screen &S, bool vis, float p, int n,
 // record `vidx` taking (n1, q1) (just written by the level's lane), and its best unvisited
 // edge (uc, ac, rc; has_c) as computed by that lane. Ties: lowest action.
 __device__ void exact_level(const Pools &P, int64_t vb, int vcnt, int ns, double cpuct, int vidx, int n1, double q1,
-                            bool has_c, double uc, int ac, int rc, int &rank, int &act, int &child) {
+                            bool has_c, double uc, int ac, int rc, int &rank, int &act, int &child, int &rvi) {
     const int l = lane_id();
     const double sq = sqrt((double)ns);
     double bu = -INFINITY;
-    int ba = 0x7fffffff, bo = 0, bc = -1;
+    int ba = 0x7fffffff, bo = 0, bc = -1, bv = -1;
     if (l == 0 && has_c) { bu = uc; ba = ac; bo = rc; }
     for (int base = 0; base < vcnt; base += 64) {
         const int k = base + l;
@@ -2055,7 +2056,7 @@ __device__ void exact_level(const Pools &P, int64_t vb, int vcnt, int ns, double
             const int n = k == vidx ? n1 : v.n;
             const double q = k == vidx ? q1 : v.q;
             const double u = ucb_visited(q, n, v.p, cpuct, sq);
-            if (u > bu || (u == bu && v.a < ba)) { bu = u; ba = v.a; bo = v.off; bc = v.child; }
+            if (u > bu || (u == bu && v.a < ba)) { bu = u; ba = v.a; bo = v.off; bc = v.child; bv = k; }
         }
     }
     const double mu = wave_max_f64(bu);
@@ -2064,6 +2065,7 @@ __device__ void exact_level(const Pools &P, int64_t vb, int vcnt, int ns, double
     rank = __builtin_amdgcn_readlane(bo, ln);
     act = am;
     child = __builtin_amdgcn_readlane(bc, ln);
+    rvi = __builtin_amdgcn_readlane(bv, ln);
 }
 
 // per-level state of a group of path levels (lane j = level g0 + j)
@@ -2096,7 +2098,11 @@ __device__ __forceinline__ void load_levels_at(const Pools &P, int t, int d, int
     const NodeStat st = P.nst[V.node];
     V.ns = st.ns; V.qs = st.qs;
     V.r = P.nrun[V.node];
-    V.e = *P.ep(V.r.eb + V.off);
+    // the path edge is the node's cached pick (the descent followed it) unless the root
+    // level scanned: its visit record is then known without the EdgeP (whose prior only a
+    // new record needs)
+    if (st.best == V.off && st.bvi >= 0) V.e = EdgeP{0.f, (int16_t)V.act, st.bvi};
+    else V.e = *P.ep(V.r.eb + V.off);
     if (V.e.vi >= 0) {
         const VisitRec v = *P.vr(V.r.vb + REC_UNITS * V.e.vi);
         V.n = v.n; V.q = v.q; V.rchild = v.child;
@@ -2275,7 +2281,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
                 P.nrun[g] = NodeRun{eb, 0, (int16_t)ec, 0, 0, 0};
                 // (a new root: its priors may still be noised, and a root scans)
-                P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)bsel, (int16_t)bact, -1, 0, 0};
+                P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)bsel, (int16_t)bact, -1, 0, -1};
                 P.nround[g] = h_round; P.nterm[g] = 0;
                 if (h_hslot >= 0) P.hslot[(size_t)t * P.hcap + h_hslot] = g;   // the select's lookup ended there
                 else hash_insert(P, t, h_k0, g);
@@ -2390,12 +2396,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                     const VisitRec &R = rb[k];
                     const bool mine = i == vidx;
                     screen_item(S, true, R.p, mine ? n1 : R.n, mine ? q1 : R.q, R.off, R.a,
-                                mine ? V.rchild : R.child);
+                                mine ? V.rchild : R.child, i);
                 }
             }
         }
         bool open = in && (wide || !(S.H2 < S.L1));
-        int bsel = S.off, bact = S.a, bch = S.child;
+        int bsel = S.off, bact = S.a, bch = S.child, bvi = S.vi;
         if (open && has_c) {                             // exact best unvisited edge (own lane)
             double u;
             rc = best_unvisited(P, V.r.eb, V.r.ec, V.r.cand, C.cpuct, fpu_base(C.fpu, nqs), sqrt((double)nns + 1e-8),
@@ -2407,22 +2413,22 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         while (ex) {
             const int j = __ffsll((unsigned long long)ex) - 1;
             ex &= ex - 1;
-            int rk, ak, ck;
+            int rk, ak, ck, vk;
             exact_level(P, readlane64(V.r.vb, j), __builtin_amdgcn_readlane((int)V.r.vcnt, j),
                         __builtin_amdgcn_readlane(nns, j), C.cpuct, __builtin_amdgcn_readlane(vidx, j),
                         __builtin_amdgcn_readlane(n1, j), readlane_f64(q1, j),
                         __builtin_amdgcn_readlane((int)has_c, j) != 0, readlane_f64(uc, j),
-                        __builtin_amdgcn_readlane(ac, j), __builtin_amdgcn_readlane(rc, j), rk, ak, ck);
-            if (l == j) { bsel = rk; bact = ak; bch = ck; }
+                        __builtin_amdgcn_readlane(ac, j), __builtin_amdgcn_readlane(rc, j), rk, ak, ck, vk);
+            if (l == j) { bsel = rk; bact = ak; bch = ck; bvi = vk; }
         }
         // the node record: statistics, arg-max and its link (the path edge's link as just set)
         if (in) {
-            if (bsel == V.off) bch = V.rchild;
+            if (bsel == V.off) { bch = V.rchild; bvi = vidx; }
             BCHK(bch < 0 || IN_TREE(P, t, bch, P.nmax), 51, bch, t, (void)0);
             BCHK(bch < 0 || P.nround[bch] == P.nround[V.node] + 1, 35, ((long long)V.node << 32) | (uint32_t)bch, t,
                  bch = bch);
             const int bt_ = bch >= 0 ? (int)P.nterm[bch] : 0;
-            P.nst[V.node] = NodeStat{nqs, nns, (int16_t)bsel, (int16_t)bact, bch, bt_, 0};
+            P.nst[V.node] = NodeStat{nqs, nns, (int16_t)bsel, (int16_t)bact, bch, bt_, (int16_t)bvi};
         }
         moved = min(moved, wave_min_i32(in && bsel != V.off ? d : 0x7fffffff));
     }
@@ -2655,7 +2661,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         if (expand && hl == 0) {
             P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
             P.nrun[g] = NodeRun{eb, 0, (int16_t)ec, 0, 0, 0};
-            P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)bsel, (int16_t)bact, -1, 0, 0};
+            P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)bsel, (int16_t)bact, -1, 0, -1};
             P.nround[g] = h_round; P.nterm[g] = 0;
             if (h_hslot >= 0) P.hslot[(size_t)t * P.hcap + h_hslot] = g;
             else hash_insert(P, t, h_k0, g);
@@ -2751,12 +2757,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 if (i < myv) {
                     const VisitRec &R = rb[k];
                     const bool mine = i == vidx;
-                    screen_item(Sc, true, R.p, mine ? n1 : R.n, mine ? q1 : R.q, R.off, R.a, mine ? V.rchild : R.child);
+                    screen_item(Sc, true, R.p, mine ? n1 : R.n, mine ? q1 : R.q, R.off, R.a, mine ? V.rchild : R.child, i);
                 }
             }
         }
         bool open = in && (wide || !(Sc.H2 < Sc.L1));
-        int bsel = Sc.off, bact = Sc.a, bch = Sc.child;
+        int bsel = Sc.off, bact = Sc.a, bch = Sc.child, bvi = Sc.vi;
         if (open && has_c) {
             double u;
             rc = best_unvisited(P, V.r.eb, V.r.ec, V.r.cand, C.cpuct, fpu_base(C.fpu, nqs), sqrt((double)nns + 1e-8),
@@ -2766,18 +2772,18 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         wave_lds_fence();
         for (uint64_t ex = __ballot(open); ex; ex &= ex - 1) {
             const int j = __ffsll((unsigned long long)ex) - 1;
-            int rk, ak, ck;
+            int rk, ak, ck, vk;
             exact_level(P, readlane64(V.r.vb, j), __builtin_amdgcn_readlane((int)V.r.vcnt, j),
                         __builtin_amdgcn_readlane(nns, j), C.cpuct, __builtin_amdgcn_readlane(vidx, j),
                         __builtin_amdgcn_readlane(n1, j), readlane_f64(q1, j),
                         __builtin_amdgcn_readlane((int)has_c, j) != 0, readlane_f64(uc, j),
-                        __builtin_amdgcn_readlane(ac, j), __builtin_amdgcn_readlane(rc, j), rk, ak, ck);
-            if (l == j) { bsel = rk; bact = ak; bch = ck; }
+                        __builtin_amdgcn_readlane(ac, j), __builtin_amdgcn_readlane(rc, j), rk, ak, ck, vk);
+            if (l == j) { bsel = rk; bact = ak; bch = ck; bvi = vk; }
         }
         if (in) {
-            if (bsel == V.off) bch = V.rchild;
+            if (bsel == V.off) { bch = V.rchild; bvi = vidx; }
             const int bt_ = bch >= 0 ? (int)P.nterm[bch] : 0;
-            P.nst[V.node] = NodeStat{nqs, nns, (int16_t)bsel, (int16_t)bact, bch, bt_, 0};
+            P.nst[V.node] = NodeStat{nqs, nns, (int16_t)bsel, (int16_t)bact, bch, bt_, (int16_t)bvi};
         }
         moved = min(moved, half_min_i32(in && bsel != V.off ? d : 0x7fffffff));
     }

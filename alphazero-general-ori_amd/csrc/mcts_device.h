@@ -107,7 +107,10 @@ struct __align__(16) NodeStat {
     int16_t ba;      // its action
     int32_t bchild;  // its child (global id, -1: not linked)
     int32_t bterm;   // 1: that child is terminal (its values in nrun)
-    int64_t pad;
+    int16_t bvi;     // the visit record of edge `best` (-1: none yet), so k_backup finds the
+                     // path edge's record without loading its EdgeP
+    int16_t pad1;
+    int32_t pad2;
 };
 static_assert(sizeof(NodeStat) == 32, "NodeStat layout");
 
