@@ -84,6 +84,27 @@ def test_fused_kernel_matches_reference_network(n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", (2, 3, 4))
+def test_fused_kernel_error_at_f32_resolution(n):
+    """The fused kernel's error against the reference network's recorded outputs is at float32
+    resolution: pi within 4e-9 absolute, tanh(v) within 1.2e-7 (two ulps of 1.0). Both the
+    split-bf16 per-column layers (default) and the f32-MFMA build (NN_SPLIT=0) meet it; their
+    measured maxima are equal on pi."""
+    from splendor.nnet import FusedNet, SplendorNNet
+    with np.load(os.path.join(GOLD, f"nnet_{n}p.npz")) as z:
+        g = {k: z[k] for k in z.files}
+    net = SplendorNNet(n)
+    net.load_state_dict(deterministic_weights(net.state_dict()))
+    fused = FusedNet(net.cuda().eval(), n, "cuda")
+    boards = torch.from_numpy(np.ascontiguousarray(g["boards"].astype(np.int8))).cuda()
+    mask = torch.from_numpy(_pack_mask(g["valid"])).cuda()
+    pi, v = fused(boards, mask)
+    ref = np.exp(g["log_pi"].astype(np.float64)) * g["valid"]
+    assert np.abs(pi.double().cpu().numpy() - ref).max() <= 4e-9
+    assert np.abs(v.double().cpu().numpy() - g["v"].astype(np.float64)).max() <= 1.2e-7
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", (2, 3, 4))
 def test_fused_kernel_matches_folded_net(n):
     """Random-init network, a ragged batch of real boards (golden env states, perturbed) and
     masks, incl. an all-invalid mask row: fused kernel == PyTorch FoldedNet within fp32
