@@ -390,6 +390,9 @@ def selfplay_record(cfg, r, world, steps, warmup):
             "steps": steps, "warmup": warmup, "prefill_iterations": r["prefill"], "prefill_s": r["prefill_s"],
             "phase_stagger": r["stagger"],
             "window": r["window"], "tree": r["tree"], "symmetry_expansion": r["symmetry"],
+            # every search ran on the reference's table (no prune / reset / unexpanded leaf in the
+            # window; withdrawals repeat a simulation exactly): False marks a non-conforming record
+            "reference_table": not any(r["window"].get(k, 0) for k in ("prunes", "resets", "unexpanded")),
             "network_kernel": {"kernel": f"k_nn_forward<{n}>", "avg_us": r["nn_kernel_us"],
                                "tflops": fl / (r["nn_kernel_us"] * 1e-6) / 1e12,
                                "frac_fp32_mfma_peak": fl / (r["nn_kernel_us"] * 1e-6) / 1e12 / FP32_MFMA_PEAK,
