@@ -341,25 +341,29 @@ struct RunScr {
 
 // root noise on an expanded root (MCTS.py:150-154, the stored priors): its run re-noised,
 // re-sorted, its visit records' priors and ranks updated; returns the new candidate rank.
-// Wave-collective.
+// LDS scratch: bits[7], pr[416], cp / ca / cvi [409]. Wave-collective.
 __device__ int noise_kept_root(const Pools &P, const SearchCfg &C, int t, const NodeRun &r, uint32_t stream,
-                               RunScr &S) {
+                               uint64_t *bits, float *pr, float *cp, int16_t *ca, int16_t *cvi) {
     const int l = lane_id();
-    run_bits(P, r, S.bits);
-    for (int a = l; a < 416; a += 64) S.pr[a] = 0.f;
+    run_bits(P, r, bits);
+    for (int a = l; a < 416; a += 64) pr[a] = 0.f;
     wave_lds_fence();
     for (int i = l; i < r.ec; i += 64) {
         const EdgeP e = *P.ep(r.eb + i);
-        S.pr[e.a] = e.p;
-        const int k = order_of(S.bits, e.a);
-        S.ca[k] = e.a;
-        S.cvi[k] = e.vi;
+        pr[e.a] = e.p;
+        const int k = order_of(bits, e.a);
+        ca[k] = e.a;
+        cvi[k] = e.vi;
     }
     wave_lds_fence();
-    root_noise_lds(C, t, stream, S.pr, S.bits, r.ec);
-    for (int k = l; k < r.ec; k += 64) S.cp[k] = S.pr[S.ca[k]];
+    root_noise_lds(C, t, stream, pr, bits, r.ec);
+    for (int k = l; k < r.ec; k += 64) cp[k] = pr[ca[k]];
     wave_lds_fence();
-    return write_sorted_run(P, r.eb, r.vb, r.ec, S.cp, S.ca, S.cvi);
+    return write_sorted_run(P, r.eb, r.vb, r.ec, cp, ca, cvi);
+}
+__device__ __forceinline__ int noise_kept_root(const Pools &P, const SearchCfg &C, int t, const NodeRun &r,
+                                               uint32_t stream, RunScr &S) {
+    return noise_kept_root(P, C, t, r, stream, S.bits, S.pr, S.cp, S.ca, S.cvi);
 }
 
 // ------------------------------------------------------------ page allocation
@@ -1260,6 +1264,37 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     wave_store_board<N>(P.board + (size_t)t * Lx::S, b);
     wave_roll_players<N>(s, b, nxt);                            // getCanonicalForm (:73)
     begin_search<N>(P, C, t, s, !ended, false);
+    // a kept root's Dirichlet noise at its search start: exactly what the search's first
+    // select would apply (same stored priors, same stream ST_DIR | move_no), here where every
+    // tree has a wave of its own instead of the select's one tree at a time per wave; then
+    // the root's arg-max under the noised priors (scan_run, as that select would scan) is
+    // cached. Not when a collection is queued (it may move or empty the tree first: the select
+    // or the backup of a new root then applies the noise). The move-sampling scratch is free.
+    const int nroot = uniform(H->root);
+    if (nroot >= 0 && uniform(H->noise_pending) && !uniform(H->gc_queued)) {
+        NodeRun r = P.nrun[nroot];
+        r.eb = (int64_t)uniform64((uint64_t)r.eb); r.vb = (int64_t)uniform64((uint64_t)r.vb);
+        r.ec = (int16_t)uniform(r.ec);
+        const int cand = noise_kept_root(P, C, t, r, ST_DIR | (uint32_t)uniform(H->move_no), pbits[w],
+                                         reinterpret_cast<float *>(pterm[w]), pprior[w], pact[w],
+                                         reinterpret_cast<int16_t *>(pcnt[w]));
+        wave_lds_fence();                                        // (the re-sorted run, read below)
+        const NodeStat ns = P.nst[nroot];
+        const bool forced = uniform(H->forced) != 0;
+        Pick pk{-1, 0, -1, 0};
+        if (!forced) pk = scan_run(P, r, ns.ns, ns.qs, C.cpuct, C.fpu, false, 0);
+        if (l == 0) {
+            H->noise_pending = 0;
+            P.nrun[nroot].cand = (int16_t)cand;
+            NodeStat w2 = ns;
+            w2.best = (int16_t)pk.e;                             // (-1 with forced playouts: scans)
+            w2.ba = (int16_t)pk.a;
+            w2.bchild = pk.e >= 0 ? pk.child : -1;
+            w2.bterm = pk.e >= 0 && pk.child >= 0 ? (int)P.nterm[pk.child] : 0;
+            w2.bvi = pk.e >= 0 ? P.ep(r.eb + pk.e)->vi : (int16_t)-1;
+            P.nst[nroot] = w2;
+        }
+    }
 }
 
 // flat copy of `bytes` bytes (16-byte vectors when both ends allow it), grid-stride
