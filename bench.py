@@ -339,9 +339,10 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     torch.cuda.synchronize(dev)
     sym_s = time.perf_counter() - t_s
     # the network kernel on its own: k_nn_forward over B leaves, HIP events on its stream
-    nk = 20
+    nk = 50
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev(sp.leaf_state, sp.leaf_mask)
+    for _ in range(10):
+        ev(sp.leaf_state, sp.leaf_mask)
     e0.record()
     for _ in range(nk):
         ev(sp.leaf_state, sp.leaf_mask)
@@ -396,7 +397,7 @@ def selfplay_record(cfg, r, world, steps, warmup):
             "network_kernel": {"kernel": f"k_nn_forward<{n}>", "avg_us": r["nn_kernel_us"],
                                "tflops": fl / (r["nn_kernel_us"] * 1e-6) / 1e12,
                                "frac_fp32_mfma_peak": fl / (r["nn_kernel_us"] * 1e-6) / 1e12 / FP32_MFMA_PEAK,
-                               "note": "k_nn_forward alone over B leaves (HIP events, 20 launches)"}}
+                               "note": "k_nn_forward alone over B leaves (HIP events, 10 warm-up + 50 timed launches)"}}
 
 
 def load_json_profile(pattern):
