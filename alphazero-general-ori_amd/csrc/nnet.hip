@@ -179,7 +179,10 @@ __device__ __forceinline__ void gemm_tiles(const float *__restrict__ wp, int nt,
 // in bf16: three products (the weight's parts) into one accumulator.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-constexpr int PFS = 2;                 // chunks of weight parts in flight
+#ifndef NN_PFS
+#define NN_PFS 2
+#endif
+constexpr int PFS = NN_PFS;            // chunks of weight parts in flight
 struct RingS {
     bf16x8 b[PFS][3];
 };
