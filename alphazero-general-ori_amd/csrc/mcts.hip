@@ -1,6 +1,7 @@
 // mcts.hip — device-resident batched MCTS kernels + C ABI (include/splendor_amd.h §MCTS).
-// One wave per tree; every tree advances by exactly one simulation per select/backup pair,
-// so each tree's sequence of simulations is the reference's sequential search (MCTS.py).
+// Every tree advances by exactly one simulation per select/backup pair (descent lane per
+// tree, backup two trees per wave), so each tree's sequence of simulations is the
+// reference's sequential search (MCTS.py).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -8,25 +9,7 @@
 
 #include "../../include/splendor_amd.h"
 
-#ifndef MCTS_TIMING
-#define MCTS_TIMING 0      // diagnostic builds only (tools/time_select.hip): k_select cycle probes
-#endif
-#if MCTS_TIMING
-__shared__ uint64_t spl_probe_acc[24];
-__shared__ uint64_t spl_probe_last;
-#define SPL_PROBE(k)                                                                       \
-    if (threadIdx.x == 0) {                                                                \
-        const uint64_t c_ = clock64();                                                     \
-        spl_probe_acc[k] += c_ - spl_probe_last;                                           \
-        spl_probe_last = c_;                                                               \
-    }
-__device__ unsigned long long g_select_timing[24];
-#endif
 #include "mcts_device.h"
-
-#ifndef SELECT_WAVES
-#define SELECT_WAVES 6     // k_select waves per SIMD (80 VGPRs; 7 spills)
-#endif
 
 using namespace spl;
 
@@ -1352,287 +1335,16 @@ __device__ __forceinline__ NodeRun term_run(const float v[4]) {
     return r;
 }
 
-template <int N>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SELECT_WAVES))) void k_select(Pools P, SearchCfg C, int B, int lim,
-                                                    int8_t *__restrict__ leaf_state,
-                                                    uint64_t *__restrict__ leaf_mask,
-                                                    uint8_t *__restrict__ leaf_valid,
-                                                    int32_t *__restrict__ leaf_count) {
-    using Lx = Lay<N>;
-    __shared__ __align__(16) int8_t lds[WAVES][Lx::LS];
-    __shared__ RunScr scr[WAVES];                           // root noise on a kept root
-    // trees start in P.order (deep descents first: the launch ends with its deepest descent)
-    const int w = uniform(threadIdx.x >> 6), slot = blockIdx.x * WAVES + w;
-    if (slot >= B) return;
-    const int t = uniform(P.order[slot]);
-    const int l = lane_id();
-    if (slot == 0 && l < 2) P.counters[6 + l] = 0;           // k_leaf_mask's filing counters
-    if (slot == 0 && l == 2 && leaf_count) *leaf_count = 0;
-    TreeHdr *H = P.hdr + t;
-    int8_t *s = lds[w];
-    // the root board is requested together with the header (no dependency between them)
-    wave_load_board<N>(s, P.root_state + (size_t)t * Lx::S);
-    const int sims = H->sims_done;
-    if (sims >= H->budget || H->overflow) {
-        if (l == 0) { leaf_valid[t] = 0; H->leaf_kind = LEAF_NONE; }
-        return;
-    }
-#if MCTS_TIMING
-    if (threadIdx.x == 0) {
-        for (int k = 0; k < 24; k++) spl_probe_acc[k] = 0;
-        spl_probe_last = clock64();
-    }
-#endif
-    int32_t *path_n = P.path_n + (size_t)t * (P.pcap + 1);
-    int32_t *path_x = P.path_x + (size_t)t * P.pcap;
-    // the previous simulation's path, first 64 levels (lane per level), requested with the header
-    int ppn = -1, ppx = 0;
-    if (l < P.pcap) { ppn = path_n[l]; ppx = path_x[l]; }
-    SPL_PROBE(0)
-    int node = H->root, depth = 0, kind = LEAF_NN;
-    int miss = -1;                                       // the NN leaf's empty table slot
-    int leaf_node = -1;                                  // a terminal leaf's node
-    uint64_t k0 = 0, k1 = 0;
-    float val[4] = {0, 0, 0, 0};
-    if (node < 0) {
-        wave_fingerprint<N>(s, k0, k1);                  // the root itself is the leaf
-    } else {
-        const bool noised = sims == 0 && H->noise_pending;
-        if (noised) {                                    // the stored priors re-noised (:150-154)
-            const NodeRun r = P.nrun[node];
-            const int cand = noise_kept_root(P, C, t, r, ST_DIR | (uint32_t)H->move_no, scr[w]);
-            if (l == 0) {
-                H->noise_pending = 0;                    // (a withdrawn simulation must not re-noise)
-                P.nrun[node].cand = (int16_t)cand;
-                P.nst[node].best = -1;                   // ranks moved: the root scans
-            }
-            wave_lds_fence();
-        }
-        const bool forced = H->forced;
-        // the root's cached arg-max holds unless its priors were just noised or forced
-        // playouts make its pick depend on the simulation index (MCTS.py:208-213)
-        const bool root_cache = !forced && !noised;
-        // node_boards: a linked child's board is stored, so the descent follows links without
-        // the in-tree transition and stages a board only where it needs one (the edge to
-        // expand); `bnode` is the node whose board is in LDS (the root's, from root_state)
-        const uint64_t *nbrd = reinterpret_cast<const uint64_t *>(P.nbrd);
-        int bnode = node;
-        const NodeStat *nst_t = P.nst;
-        const double cpuct = C.cpuct, fpu = C.fpu;
-        int pend = -1, pend_n = 0, pend_x = 0;               // path entry not yet stored
-        // The previous simulation's path (this search's, same root; k_gc clears H->depth when
-        // it moves nodes) is this descent's as far as its nodes' cached arg-maxes still pick
-        // its edges: k_backup rewrote exactly those nodes' records, so one round trip for the
-        // path and one for its nodes' records (lane per level) replace the first levels'
-        // dependent loads. The descent resumes at level q = the first level whose node now
-        // picks another edge (or the previous leaf's parent), with that node's record in hand.
-        bool have = false;
-        NodeStat hq{0.0, 0, -1, 0, -1, 0, 0};
-        {
-            const int pd = min(H->depth, 64);
-            const bool ok = sims > 0 && pd > 0 && __builtin_amdgcn_readfirstlane(ppn) == node;
-            if (ok) {
-                NodeStat h{0.0, 0, -1, 0, -1, 0, 0};
-                if (l < pd) h = nst_t[ppn];
-                const bool agree = l < pd && h.best == px_off(ppx) && (l > 0 || root_cache);
-                const uint64_t dis = ~__ballot(agree) & (pd < 64 ? (1ull << pd) - 1 : ~0ull);
-                const int p = dis ? __ffsll((unsigned long long)dis) - 1 : pd;
-                const int q = uniform(min(p, pd - 1));
-                node = __builtin_amdgcn_readlane(ppn, q);
-                depth = q;
-                hq.qs = readlane_f64(h.qs, q);
-                hq.ns = __builtin_amdgcn_readlane(h.ns, q);
-                hq.best = (int16_t)__builtin_amdgcn_readlane((int)h.best, q);
-                hq.ba = (int16_t)__builtin_amdgcn_readlane((int)h.ba, q);
-                hq.bchild = __builtin_amdgcn_readlane(h.bchild, q);
-                hq.bterm = __builtin_amdgcn_readlane(h.bterm, q);
-                have = true;
-                if (!nbrd) {
-                    // no node boards: the board of the resume node is the root's with the
-                    // path's moves applied (the in-tree transition, MCTS.py:227-235)
-                    for (int d = 0; d < q; d++) {
-                        const int a = px_action(__builtin_amdgcn_readlane(ppx, d));
-                        Chance ch{nullptr, 0, 0, 0, 0};
-                        int nxt;
-                        switch (move_kind_of(a)) {
-                            case MK_GEMS: nxt = make_move<N, MK_GEMS>(s, a, 0, true, ch); break;
-                            case MK_BUY: nxt = make_move<N, MK_BUY>(s, a, 0, true, ch); break;
-                            case MK_RESERVE: nxt = make_move<N, MK_RESERVE>(s, a, 0, true, ch); break;
-                            default: nxt = make_move<N, MK_BUY_RESERVED>(s, a, 0, true, ch); break;
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                        if (nxt) wave_roll_players<N>(s, s, nxt);
-                    }
-                    bnode = node;
-                }
-            }
-        }
-        for (;;) {
-            SPL_PROBE(1)
-            if (depth >= P.pcap) { kind = LEAF_NONE; if (l == 0) H->overflow = 2; break; }
-#if SPL_BOUNDS_CHECK
-            BCHK(node >= 0 && node < (long long)P.npages * NPG, 20, node, t, node = 0);
-#endif
-            // a level is ONE 32-byte load: the node's statistics with its cached arg-max and
-            // that edge's link (NodeStat)
-            NodeStat nsq = hq;
-            if (!have) nsq = nst_t[node];
-            have = false;
-            const bool use_cache = depth > 0 || root_cache;
-            // the previous level's path entry is stored behind this level's loads: vmcnt counts
-            // stores too, in issue order, so a store issued first would delay the loads' wait
-            if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_x[pend] = pend_x; }
-            pend = -1;
-            const int cbest = uniform(nsq.best);
-            Pick pk;
-            if (use_cache && cbest >= 0) {
-                pk = Pick{cbest, uniform(nsq.ba), uniform(nsq.bchild), uniform(nsq.bterm)};
-            } else {                                     // the root scans (noise, forced playouts)
-                NodeRun r = P.nrun[node];
-                r.eb = (int64_t)uniform64((uint64_t)r.eb); r.vb = (int64_t)uniform64((uint64_t)r.vb);
-                r.ec = (int16_t)uniform(r.ec);
-                pk = scan_run(P, r, nsq.ns, nsq.qs, cpuct, fpu, forced && depth == 0, sims);
-                if (pk.child < 0 && pk.e == cbest && !noised) { pk.child = uniform(nsq.bchild); pk.cterm = uniform(nsq.bterm); }
-                else pk.cterm = pk.child >= 0 ? uniform((int)P.nterm[pk.child]) : 0;
-            }
-            BCHK(pk.child >= -1 && pk.child < (long long)P.npages * NPG, 23, pk.child, t, pk.child = -1);
-            pend = depth; pend_n = node; pend_x = px_pack(pk.e, pk.a);
-            depth++;
-            int child = uniform(pk.child);
-            SPL_PROBE(2)
-            if (child >= 0 && pk.cterm) {                    // a terminal child (MCTS.py:125-132)
-                kind = LEAF_TERMINAL;
-                term_values(P, child, val);
-                leaf_node = child;
-                break;
-            }
-            if (child >= 0 && nbrd) {                        // linked: no transition needed
-                node = child;
-                continue;
-            }
-            if (bnode != node) {                             // stage this node's stored board
-                const uint64_t *src = nbrd + (size_t)node * (NodeBoard<N>::BYTES / 8);
-                for (int r = l; r < Lx::ROWS; r += 64) row(s, r) = src[r];
-                __builtin_amdgcn_wave_barrier();
-                bnode = node;
-            }
-            Chance ch{nullptr, 0, 0, 0, 0};
-            int nxt;                                         // MCTS.py:227-235, per kind
-            switch (move_kind_of(pk.a)) {                    // (uniform: a scalar branch)
-                case MK_GEMS: nxt = make_move<N, MK_GEMS>(s, pk.a, 0, true, ch); break;
-                case MK_BUY: nxt = make_move<N, MK_BUY>(s, pk.a, 0, true, ch); break;
-                case MK_RESERVE: nxt = make_move<N, MK_RESERVE>(s, pk.a, 0, true, ch); break;
-                default: nxt = make_move<N, MK_BUY_RESERVED>(s, pk.a, 0, true, ch); break;
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (nxt) wave_roll_players<N>(s, s, nxt);
-            SPL_PROBE(3)
-            // a link found here is copied into the node's cached arg-max when that is the edge
-            // (k_backup links the edge's visit record; the copy keeps a withdrawn simulation's
-            // link for the next descent)
-            const bool cached = cbest == pk.e;
-            if (child < 0) {
-                wave_fingerprint<N>(s, k0, k1);
-                k0 = uniform64(k0); k1 = uniform64(k1);
-                child = uniform(hash_lookup(P, t, k0, k1, &miss));
-                miss = uniform(miss);
-                if (child >= 0) {                            // transposition
-                    const int ct = uniform((int)P.nterm[child]);
-                    if (l == 0 && cached) { P.nst[node].bchild = child; P.nst[node].bterm = ct; }
-                    if (ct) {
-                        kind = LEAF_TERMINAL;
-                        term_values(P, child, val);
-                        leaf_node = child;
-                        break;
-                    }
-                }
-            }
-            SPL_PROBE(4)
-            if (child >= 0) {
-                node = child;
-                bnode = child;
-                continue;
-            }
-            float es[N];
-            check_end<N>(s, es);                             // MCTS.py:125
-            bool any = false;
-#pragma unroll
-            for (int i = 0; i < N; i++) any |= es[i] != 0.f;
-            if (any) {
-                kind = LEAF_TERMINAL;
-#pragma unroll
-                for (int i = 0; i < N; i++) val[i] = es[i];
-                __builtin_amdgcn_wave_barrier();
-                int g = -1;
-                if (l == 0) {
-                    const int id = H->node_count;
-                    g = node_slot(P, H, t, id);
-                    if (g < 0) {                             // no room: back up, do not store
-                        H->unexpanded += 1;
-                    } else {
-                        P.nkey0[g] = k0; P.nkey1[g] = k1;
-                        P.nrun[g] = term_run(val);
-                        P.nst[g] = NodeStat{0.0, 0, -1, 0, -1, 0, -1};
-                        P.nround[g] = (uint8_t)bt(row(s, 0), 6); P.nterm[g] = 1;
-                        hash_insert(P, t, k0, g);
-                        if (cached) { P.nst[node].bchild = g; P.nst[node].bterm = 1; }
-                        H->node_count = id + 1;
-                    }
-                }
-                leaf_node = __shfl(g, 0, 64);
-                break;
-            }
-            break;                                           // new NN leaf
-        }
-        if (pend >= 0 && l == 0) { path_n[pend] = pend_n; path_x[pend] = pend_x; }
-    }
-    __builtin_amdgcn_wave_barrier();
-    SPL_PROBE(5)
-    if (kind == LEAF_NN) {                                   // its mask: k_leaf_mask
-        wave_store_board<N>(leaf_state + (size_t)t * Lx::S, s);
-        if (P.nbrd) {                                        // the slot k_backup will insert it at
-            int g = -1;
-            if (l == 0) g = node_slot(P, H, t, H->node_count);
-            g = __shfl(g, 0, 64);
-            if (l == 0) H->leaf_slot = g;
-            if (g >= 0) {
-                uint64_t *dst = reinterpret_cast<uint64_t *>(P.nbrd + (size_t)g * NodeBoard<N>::BYTES);
-                for (int r = l; r < Lx::ROWS; r += 64) dst[r] = row(s, r);
-            }
-        }
-    }
-    SPL_PROBE(6)
-    if (l == 0) {
-        H->depth = depth;
-        H->leaf_kind = kind;
-        H->leaf_hslot = kind == LEAF_NN ? miss : -1;
-        if (!P.nbrd || kind != LEAF_NN) H->leaf_slot = -1;
-        H->leaf_k0 = k0; H->leaf_k1 = k1;
-        H->leaf_round = (uint8_t)bt(row(s, 0), 6);
-#pragma unroll
-        for (int i = 0; i < 4; i++) H->leaf_v[i] = val[i];
-        leaf_valid[t] = kind == LEAF_NN;
-        path_n[depth] = kind == LEAF_TERMINAL ? leaf_node : -1;   // the leaf's node (k_backup links it)
-    }
-#if MCTS_TIMING
-    SPL_PROBE(7)
-    if (threadIdx.x == 0) {
-        for (int k = 0; k < 24; k++) atomicAdd(&g_select_timing[k], (unsigned long long)spl_probe_acc[k]);
-        atomicAdd(&g_select_timing[21], 1ull);
-    }
-#endif
-}
-
 // ------------------------------------------------------------ select, lane per tree
-// k_select_lanes: the same descent as k_select with one LANE per tree (64 trees per wave).
-// Below the root a level is one 32-byte NodeStat load (the cached arg-max and its link), work
-// for a single lane, so a wave per tree leaves 63 lanes idle and the launch is bound by wave
-// slots x the chain latency; lane per tree keeps 64 chains in flight per wave. The steps that
+// k_select_lanes: the descent (MCTS.py:99-177 down to the leaf) with one LANE per tree (64
+// trees per wave). Below the root a level is one 32-byte NodeStat load (the cached arg-max and
+// its link), work for a single lane, so a wave per tree (round 3) left 63 lanes idle and the
+// launch was bound by wave slots x the chain latency; lane per tree keeps 64 chains in flight
+// per wave. The steps that
 // need a board — the in-tree transition at the edge to expand (MCTS.py:227-235), the
 // fingerprint lookup (:119-120), the end check (:125) and the new leaf's board — run per lane
 // on the lane's own LDS board. Root scans (a root whose priors were just noised, forced
 // playouts, a new root) and root noise stay wave-collective, one tree at a time (rare).
-// Results are identical to k_select's (same picks, paths, leaves, links).
 
 // swap_players on a lane's own LDS board, in place: every player block rotated left by its
 // stride (gems k, nobles 3k — hard-coded 3, SplendorLogicNumba.py:345 —, cards k, reserved
@@ -2027,7 +1739,7 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
         if (leaf_valid[b0 + i / 7]) leaf_mask[(size_t)b0 * 7 + i] = (&msk[0][0])[i];
 }
 
-// k_backup: expansion of the NN leaf, the path backup (MCTS.py:169-176) and every path node's
+// k_backup_h: expansion of the NN leaf, the path backup (MCTS.py:169-176) and every path node's
 // cached arg-max (NodeStat), so the next descent through the node reads its pick instead of
 // scanning. Lane per level. A level's arg-max needs only its visited edges (the visit block)
 // and its best unvisited edge (the run's candidate: MCTS.py:214 is monotone in P), plus the
@@ -2152,345 +1864,19 @@ __device__ __forceinline__ void load_levels_at(const Pools &P, int t, int d, int
         V.grow = d == 0 ? (int)V.r.ec : (V.r.vcap == 0 ? 1 : min(2 * (int)V.r.vcap, (int)V.r.ec));
     }
 }
-__device__ __forceinline__ void load_levels(const Pools &P, int t, int g0, int depth, int lid, Level &V, bool in) {
-    load_levels_at(P, t, g0 + lane_id(), depth, lid, V, in);
-}
 
 #ifndef WD_MAX
 #define WD_MAX 4           // withdrawals per search (k_backup)
 #endif
-// KINDS: the leaf kinds this launch backs up (bit 0 NN, bit 1 terminal; spl_mcts_backup_kind)
-template <int N, int KINDS>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_WAVES))) void k_backup(Pools P, SearchCfg C, int B,
-                                                    const uint64_t *__restrict__ leaf_mask,
-                                                    const float *__restrict__ pi,
-                                                    const float *__restrict__ v) {
-    __shared__ RunScr scr[WAVES];
-    const int w = uniform(threadIdx.x >> 6), t = blockIdx.x * WAVES + w;
-    if (t >= B) return;
-    const int l = lane_id();
-    TreeHdr *H = P.hdr + t;
-    const int kind = H->leaf_kind;
-    if (kind == LEAF_NONE || !((KINDS >> (kind - 1)) & 1)) return;
-    const int depth = H->depth;
-    const int h_slot = H->leaf_slot, h_hslot = H->leaf_hslot, h_round = H->leaf_round;
-    const uint64_t h_k0 = H->leaf_k0, h_k1 = H->leaf_k1;
-    const int h_sims = H->sims_done, h_noise = H->noise_pending, h_gc = H->gc_state;
-    const int32_t *path_n = P.path_n + (size_t)t * (P.pcap + 1);
-    int64_t *path_b = P.path_b + (size_t)t * P.pcap;
-    float val[4] = {0, 0, 0, 0};
-    int lid = -1;                                        // the leaf's node (terminal: stored by select)
-    RunScr &S = scr[w];
-    if (kind == LEAF_NN) {                               // the leaf's policy and mask, staged in LDS
-        const float *gp = pi + (size_t)t * SPL_ACTIONS;
-#pragma unroll
-        for (int k = 0; k < 7; k++)
-            if (64 * k + l < SPL_ACTIONS) S.pr[64 * k + l] = gp[64 * k + l];
-        if (l < 7) S.bits[l] = leaf_mask[(size_t)t * 7 + l];
-#pragma unroll
-        for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
-    } else {
-#pragma unroll
-        for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
-        lid = path_n[depth];
-    }
-    // ---- pass A: the first group's levels in registers; every visit block that must grow and
-    // the NN leaf's run allocated before anything changes, so a simulation that finds no room
-    // can still be withdrawn
-    const int cnt0 = min(depth, 64);
-    Level V;
-    load_levels(P, t, 0, depth, lid, V, l < cnt0);
-    bool fail = false;                                   // a visit block found no room
-    for (int g0 = 0; g0 < depth; g0 += 64) {
-        Level Vg;
-        if (g0 > 0) load_levels(P, t, g0, depth, lid, Vg, g0 + l < depth);
-        const int grow = g0 == 0 ? V.grow : Vg.grow;
-        uint64_t gm = __ballot(grow > 0);
-        int64_t nb = -1;
-        while (gm) {
-            const int j = __ffsll((unsigned long long)gm) - 1;
-            gm &= gm - 1;
-            const int units = REC_UNITS * __builtin_amdgcn_readlane(grow, j);
-            int64_t b = -1;
-            if (l == 0 && !fail) b = unit_alloc(P, H, t, units);
-            b = readlane64(b, 0);
-            if (b < 0) fail = true;
-            if (l == j) nb = b;
-        }
-        if (g0 == 0) V.nb = nb;
-        else if (grow > 0) path_b[g0 + l] = nb;
-    }
-    int g = -1, ec = 0;
-    int64_t eb = -1;
-    if (kind == LEAF_NN) {
-        wave_lds_fence();
-#pragma unroll
-        for (int k = 0; k < 7; k++) ec += __popcll(S.bits[k]);
-        if (!fail && l == 0) {
-            // the new node's slot (reserved by k_select with node boards) and run
-            g = h_slot >= 0 ? h_slot : node_slot(P, H, t, H->node_count);
-            if (g >= 0) eb = unit_alloc(P, H, t, ec);
-        }
-        g = __shfl(g, 0, 64);
-        eb = readlane64(eb, 0);
-    }
-    if ((fail || (kind == LEAF_NN && eb < 0)) && C.selfplay && depth > 0 &&
-        (h_gc == 0 || h_gc == 5 || (h_gc == 2 && H->wd_search < WD_MAX))) {
-        // garbage is collected lazily (begin_search), so a self-play search may run out
-        // of room with dead nodes still held: this simulation is withdrawn (no backup,
-        // not counted), k_gc (launched behind every backup of a self-play arena) collects
-        // the garbage (exact: nodes with rounds <= the root's) and the next select repeats
-        // the same descent. With the shared pools nearly empty the repeat can fail again
-        // (its own garbage is gone, other trees' collections refill the pools meanwhile):
-        // up to WD_MAX withdrawals per search, then the leaf is backed up unstored.
-        // Search-only arenas never withdraw.
-        if (l == 0) {
-            H->gc_state = 1;
-            H->leaf_kind = LEAF_NONE;
-            H->withdrawals += 1;
-            H->wd_search += 1;
-            gc_push(P, H, t);
-        }
-        return;
-    }
-    // (no withdrawal possible: a level whose visit block found no room backs up its node
-    // but leaves the edge without statistics — counted, like an unstored leaf)
-    if (fail && l == 0) H->unexpanded += 1;
-    if (kind == LEAF_NN) {
-        if (eb < 0) {                                    // no room: back up v, do not store
-            if (l == 0) H->unexpanded += 1;
-        } else {
-            // the run, sorted by (prior desc, action asc): priors normalised in NumPy's
-            // pairwise order (MCTS.py:144), or a new root's noised (:141-143)
-            float *pr = S.pr;
-            const bool noise = depth == 0 && h_sims == 0 && h_noise;
-            if (noise) {
-                root_noise_lds(C, t, ST_DIR | (uint32_t)H->move_no, pr, S.bits, ec);
-            } else {
-                const float sum = wave_np_sum409(pr);
-                wave_lds_fence();
-                for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = pr[a] / sum;
-                wave_lds_fence();
-            }
-            int run = 0;
-#pragma unroll
-            for (int k = 0; k < 7; k++) {
-                const uint64_t wd = S.bits[k];
-                if ((wd >> l) & 1) {
-                    const int r = run + __popcll(wd & lanemask_lt());
-                    S.cp[r] = pr[64 * k + l];
-                    S.ca[r] = (int16_t)(64 * k + l);
-                }
-                run += __popcll(wd);
-            }
-            wave_lds_fence();
-            (void)write_sorted_run(P, eb, 0, ec, S.cp, S.ca, nullptr);
-            // the new node's arg-max: every edge unvisited (Ns = 0, Qs = v), u = fpu_init +
-            // cpuct * P * sqrt(0 + EPS) (MCTS.py:214): the top-ranked edge unless a smaller
-            // prior rounds to the same u with a lower action (from the LDS list, action order)
-            int bsel = -1, bact = 0;
-            if (depth > 0) {
-                const double fpu_init = fpu_base(C.fpu, (double)val[0]), sq_eps = sqrt(1e-8);
-                double bu = -INFINITY;
-                int ba = 0x7fffffff;
-                for (int i = l; i < ec; i += 64) {
-                    const double u = ucb_unvisited(S.cp[i], C.cpuct, fpu_init, sq_eps);
-                    if (u > bu || (u == bu && S.ca[i] < ba)) { bu = u; ba = S.ca[i]; }
-                }
-                const double mu = wave_max_f64(bu);
-                bact = wave_min_i32(bu == mu ? ba : 0x7fffffff);
-                // its rank: edges of a larger prior, or of the same prior and a lower action
-                const float pb = S.pr[bact];
-                int r = 0;
-                for (int i = l; i < ec; i += 64) r += (S.cp[i] > pb) || (S.cp[i] == pb && S.ca[i] < bact);
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
-                bsel = uniform(r);
-            }
-            if (l == 0) {
-#if SPL_BOUNDS_CHECK
-                if (P.nbrd) {                            // the board select stored at the slot
-                    uint64_t bw[Lay<N>::ROWS];
-                    const uint64_t *src = reinterpret_cast<const uint64_t *>(P.nbrd) + (size_t)g * (NodeBoard<N>::BYTES / 8);
-                    for (int r = 0; r < Lay<N>::ROWS; r++) bw[r] = src[r];
-                    uint64_t f0, f1;
-                    lane_fingerprint<N>(reinterpret_cast<const int8_t *>(bw), f0, f1);
-                    BCHK(f0 == h_k0 && f1 == h_k1, 43, g, t, (void)0);
-                }
-#endif
-                P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
-                P.nrun[g] = NodeRun{eb, 0, (int16_t)ec, 0, 0, 0};
-                // (a new root: its priors may still be noised, and a root scans)
-                P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)bsel, (int16_t)bact, -1, 0, -1};
-                P.nround[g] = h_round; P.nterm[g] = 0;
-                if (h_hslot >= 0) P.hslot[(size_t)t * P.hcap + h_hslot] = g;   // the select's lookup ended there
-                else hash_insert(P, t, h_k0, g);
-                if (depth == 0) H->root = g;
-                H->node_count += 1;
-            }
-            lid = g;
-        }
-    }
-    if (depth > 0 && kind == LEAF_NN && l == (depth - 1 < 64 ? depth - 1 : 64)) V.child = lid;
-    // ---- pass B: levels in groups of 64, lane per level (the first group's data is in hand)
-    int moved = 0x7fffffff;                              // the first level whose cached pick moved
-    for (int g0 = 0; g0 < depth; g0 += 64) {
-        const int d = g0 + l;
-        const int cnt = min(64, depth - g0);
-        const bool in = l < cnt;
-        if (g0 > 0) {
-            load_levels(P, t, g0, depth, lid, V, in);
-            if (in && V.grow > 0) V.nb = path_b[d];
-        }
-        // visit blocks that move (a new record in a full block): every lane copies, level by
-        // level (one round trip per moving block instead of one per unit on its level's lane)
-        for (uint64_t gm = __ballot(in && V.e.vi < 0 && V.grow > 0 && V.nb >= 0 && V.r.vcnt > 0); gm; gm &= gm - 1) {
-            const int j = __ffsll((unsigned long long)gm) - 1;
-            const int64_t ob = readlane64(V.r.vb, j), nb = readlane64(V.nb, j);
-            const int nu = REC_UNITS * __builtin_amdgcn_readlane((int)V.r.vcnt, j);
-            for (int k = l; k < nu; k += 64) P.eu[nb + k] = P.eu[ob + k];
-        }
-        wave_lds_fence();                                // (copies by other lanes, read below)
-        // MCTS.py:169-176: level d sees the leaf value rolled (depth - d) times; the levels
-        // touch distinct nodes (rounds strictly increase along a path), so one lane per
-        // level applies exactly the sequential update
-        int n1 = 0, vidx = -1, nns = 0;
-        double q1 = 0.0, nqs = 0.0;
-        if (in) {
-            const int rot = (depth - d) % N, vi = (N - rot) % N;
-            float vr = val[0];
-#pragma unroll
-            for (int i = 1; i < N; i++) vr = vi == i ? val[i] : vr;   // (no dynamic index: scratch)
-            const double v0 = (double)vr;
-            nqs = ((double)(V.ns + 1) * V.qs + v0) / (double)(V.ns + 2);
-            nns = V.ns + 1;
-            q1 = ((double)V.n * V.q + v0) / (double)(V.n + 1);
-            n1 = V.n + 1;
-            if (V.e.vi >= 0) {                           // Qsa, Nsa (+ the link, if new)
-                vidx = V.e.vi;
-                VisitRec *R = P.vr(V.r.vb + REC_UNITS * vidx);
-                R->q = q1;
-                R->n = n1;
-                if (V.rchild < 0 && V.child >= 0) R->child = V.child;
-                BCHK(V.child < 0 || IN_TREE(P, t, V.child, P.nmax), 50, V.child, t, (void)0);
-                BCHK(V.child < 0 || P.nround[V.child] == P.nround[V.node] + 1, 32,
-                     ((long long)V.node << 32) | (uint32_t)V.child, t, V.child = V.child);
-                BCHK(V.rchild < 0 || V.child < 0 || V.rchild == V.child, 33,
-                     ((long long)V.rchild << 32) | (uint32_t)V.child, t, V.child = V.child);
-            } else if (V.grow > 0 && V.nb < 0) {         // no room for the record (counted)
-                vidx = -1;
-            } else {                                     // the edge's first visit: a record
-                if (V.grow > 0) {                        // (the block outgrown: moved above)
-                    V.r.vb = V.nb;
-                    V.r.vcap = (int16_t)V.grow;
-                }
-                vidx = V.r.vcnt;
-                BCHK(V.child < 0 || IN_TREE(P, t, V.child, P.nmax), 50, V.child, t, (void)0);
-                BCHK(IN_TREE(P, t, V.node, P.nmax), 55, V.node, t, (void)0);
-                BCHK(V.child < 0 || P.nround[V.child] == P.nround[V.node] + 1, 34,
-                     ((long long)V.node << 32) | (uint32_t)V.child, t, V.child = V.child);
-                *P.vr(V.r.vb + REC_UNITS * vidx) = VisitRec{q1, n1, V.child, V.e.p, (int16_t)V.off, (int16_t)V.act};
-                P.ep(V.r.eb + V.off)->vi = (int16_t)vidx;
-                V.r.vcnt = (int16_t)(vidx + 1);
-                if (V.off == V.r.cand) {                 // the next candidate: next rank without
-                    int j = V.off + 1;                   // a record (usually the next one)
-                    while (j < V.r.ec && P.ep(V.r.eb + j)->vi >= 0) j++;
-                    V.r.cand = (int16_t)j;
-                }
-                P.nrun[V.node] = V.r;
-            }
-            V.rchild = V.rchild >= 0 ? V.rchild : V.child;
-        }
-        // each level's arg-max under its new statistics
-        const bool wide = in && V.r.vcnt > BK_WIDE;
-        Screen S = screen_init(nns, nqs, C.cpuct, C.fpu);
-        bool has_c = false;
-        double uc = 0.0;
-        int ac = 0, rc = 0;
-        if (in && V.r.cand < V.r.ec) {                   // the best unvisited edge + the next
-            has_c = true;                                // unvisited one of a smaller prior
-            const EdgeP c = *P.ep(V.r.eb + V.r.cand);
-            rc = V.r.cand; ac = c.a;
-            screen_item(S, false, c.p, 0, 0.0, rc, c.a, -1);
-            if (c.p > 0.f) {
-                for (int j = V.r.cand + 1; j < V.r.ec; j++) {
-                    const EdgeP e = *P.ep(V.r.eb + j);
-                    if (e.vi >= 0 || e.p == c.p) continue;
-                    screen_item(S, false, e.p, 0, 0.0, j, e.a, -1);
-                    break;
-                }
-            }
-        }
-        int maxv = in && !wide ? V.r.vcnt : 0;
-        maxv = wave_max_i32(maxv);
-        const int myv = in && !wide ? V.r.vcnt : 0;
-        for (int base = 0; base < maxv; base += BK_BATCH) {
-            VisitRec rb[BK_BATCH];
-#pragma unroll
-            for (int k = 0; k < BK_BATCH; k++)
-                if (base + k < myv) rb[k] = *P.vr(V.r.vb + REC_UNITS * (base + k));
-#pragma unroll
-            for (int k = 0; k < BK_BATCH; k++) {
-                const int i = base + k;
-                if (i < myv) {
-                    const VisitRec &R = rb[k];
-                    const bool mine = i == vidx;
-                    screen_item(S, true, R.p, mine ? n1 : R.n, mine ? q1 : R.q, R.off, R.a,
-                                mine ? V.rchild : R.child, i);
-                }
-            }
-        }
-        bool open = in && (wide || !(S.H2 < S.L1));
-        int bsel = S.off, bact = S.a, bch = S.child, bvi = S.vi;
-        if (open && has_c) {                             // exact best unvisited edge (own lane)
-            double u;
-            rc = best_unvisited(P, V.r.eb, V.r.ec, V.r.cand, C.cpuct, fpu_base(C.fpu, nqs), sqrt((double)nns + 1e-8),
-                                u, ac);
-            uc = u;
-        }
-        wave_lds_fence();                                // records written above, read across lanes
-        uint64_t ex = __ballot(open);
-        while (ex) {
-            const int j = __ffsll((unsigned long long)ex) - 1;
-            ex &= ex - 1;
-            int rk, ak, ck, vk;
-            exact_level(P, readlane64(V.r.vb, j), __builtin_amdgcn_readlane((int)V.r.vcnt, j),
-                        __builtin_amdgcn_readlane(nns, j), C.cpuct, __builtin_amdgcn_readlane(vidx, j),
-                        __builtin_amdgcn_readlane(n1, j), readlane_f64(q1, j),
-                        __builtin_amdgcn_readlane((int)has_c, j) != 0, readlane_f64(uc, j),
-                        __builtin_amdgcn_readlane(ac, j), __builtin_amdgcn_readlane(rc, j), rk, ak, ck, vk);
-            if (l == j) { bsel = rk; bact = ak; bch = ck; bvi = vk; }
-        }
-        // the node record: statistics, arg-max and its link (the path edge's link as just set)
-        if (in) {
-            if (bsel == V.off) { bch = V.rchild; bvi = vidx; }
-            BCHK(bch < 0 || IN_TREE(P, t, bch, P.nmax), 51, bch, t, (void)0);
-            BCHK(bch < 0 || P.nround[bch] == P.nround[V.node] + 1, 35, ((long long)V.node << 32) | (uint32_t)bch, t,
-                 bch = bch);
-            const int bt_ = bch >= 0 ? (int)P.nterm[bch] : 0;
-            P.nst[V.node] = NodeStat{nqs, nns, (int16_t)bsel, (int16_t)bact, bch, bt_, (int16_t)bvi};
-        }
-        moved = min(moved, wave_min_i32(in && bsel != V.off ? d : 0x7fffffff));
-    }
-    if (l == 0) {
-        H->sims_done = h_sims + 1;
-        H->noise_pending = 0;
-        H->leaf_kind = LEAF_NONE;
-        H->depth_max = max(H->depth_max, depth);         // leaf depth statistics (diagnostic)
-        H->depth_sum += depth;
-        H->resume = min(moved, max(depth - 1, 0));
-    }
-}
-
 // ------------------------------------------------------------ backup, two trees per wave
-// k_backup_h: k_backup with each wave's halves on two trees (lanes [32h, 32h + 32) on tree
-// 2 w + h, lane per path level, levels in groups of 32). k_backup's time scales with the
-// number of trees at a fixed occupancy (latency of ~15-20 dependent round trips per tree,
-// 4 waves per SIMD by registers); two trees per wave double the trees in flight. Per-tree
+// k_backup_h: each wave's halves back up two trees (lanes [32h, 32h + 32) on tree 2 w + h,
+// lane per path level, levels in groups of 32). A wave-per-tree backup's time scales with
+// the number of trees at a fixed occupancy (latency of ~15-20 dependent round trips per
+// tree, 4 waves per SIMD by registers); two trees per wave double the trees in flight. Per-tree
 // collective steps (the policy staging and prior sums, the sorted run, the new node's
 // arg-max, allocations, the resume level) run on 32-lane halves; steps that need the whole
 // wave (root noise, the exact evaluation of a level, block copies) take the two trees' items
-// in turn. Same arithmetic, same order of every sum: bit-identical to k_backup.
+// in turn. Same arithmetic, same order of every sum as the sequential reference.
 __device__ __forceinline__ int hbase() { return lane_id() & 32; }
 __device__ __forceinline__ int half_min_i32(int x) {
 #pragma unroll
@@ -3158,18 +2544,6 @@ static bool valid_cfg(const spl_ctx *ctx, int B, const spl_mcts_config *cfg) {
            pe / UPG + 1 < (1LL << 31);
 }
 
-#if MCTS_TIMING
-// diagnostic builds only: the k_select probe accumulators (tools/select_reuse.py)
-int spl_diag_select_timing(unsigned long long *out24, int reset) {
-    if (hipMemcpyFromSymbol(out24, HIP_SYMBOL(g_select_timing), 24 * 8) != hipSuccess) return SPL_EDEVICE;
-    if (reset) {
-        unsigned long long z[24] = {0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_select_timing), z, sizeof(z)) != hipSuccess) return SPL_EDEVICE;
-    }
-    return 0;
-}
-#endif
-
 #if SPL_BOUNDS_CHECK
 // bounds-checked builds only: [0] violations, [1] first value, [2] its site, [3] its tree
 int spl_diag_bounds(unsigned long long *out4, int reset) {
@@ -3301,20 +2675,11 @@ int spl_mcts_pick_best(spl_mcts *m, const uint8_t *active, uint32_t board_base, 
     return check_launch();
 }
 
-#ifndef SELECT_LANES
-#define SELECT_LANES 1     // k_select_lanes (lane per tree); 0: k_select (wave per tree)
-#endif
 static int launch_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
                          int32_t *leaf_index, int32_t *leaf_count, void *hs) {
-    if (SELECT_LANES) {
-        SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select_lanes<N>, dim3((unsigned)((m->B + 63) / 64)), dim3(64), 0,
-                                              (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
-                                              leaf_state, leaf_valid, leaf_count));
-    } else {
-        SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select<N>, wave_grid(m->B), dim3(THREADS), 0,
-                                              (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
-                                              leaf_state, leaf_mask, leaf_valid, leaf_count));
-    }
+    SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select_lanes<N>, dim3((unsigned)((m->B + 63) / 64)), dim3(64), 0,
+                                          (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
+                                          leaf_state, leaf_valid, leaf_count));
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_leaf_mask<N>, dim3((unsigned)((m->B + 63) / 64)), dim3(256), 0,
                                           (hipStream_t)hs, m->P, m->B, m->token_limit, leaf_state, leaf_valid,
                                           leaf_mask, leaf_index, leaf_count));
@@ -3333,33 +2698,19 @@ int spl_mcts_select_compact(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask
     return launch_select(m, leaf_state, leaf_mask, leaf_valid, leaf_index, leaf_count, hs);
 }
 
-#ifndef BACKUP_HALF
-#define BACKUP_HALF 1      // k_backup_h (two trees per wave); 0: k_backup (one tree per wave)
-#endif
 int spl_mcts_backup_kind(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v, int kinds,
                          void *hs) {
     if (!m || kinds < 1 || kinds > 3 || ((kinds & SPL_LEAF_NN) && (!leaf_mask || !pi || !v))) return SPL_EINVAL;
-    if (BACKUP_HALF) {
-        const dim3 grid = wave_grid((m->B + 1) / 2);
-        if (kinds == 3) {
-            SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup_h<N, 3>), grid, dim3(THREADS), 0, (hipStream_t)hs, m->P,
-                                                  m->cfg, m->B, leaf_mask, pi, v));
-        } else if (kinds == SPL_LEAF_NN) {
-            SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup_h<N, 1>), grid, dim3(THREADS), 0, (hipStream_t)hs, m->P,
-                                                  m->cfg, m->B, leaf_mask, pi, v));
-        } else {
-            SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup_h<N, 2>), grid, dim3(THREADS), 0, (hipStream_t)hs, m->P,
-                                                  m->cfg, m->B, leaf_mask, pi, v));
-        }
-    } else if (kinds == 3) {
-        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup<N, 3>), wave_grid(m->B), dim3(THREADS), 0,
-                                              (hipStream_t)hs, m->P, m->cfg, m->B, leaf_mask, pi, v));
+    const dim3 grid = wave_grid((m->B + 1) / 2);
+    if (kinds == 3) {
+        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup_h<N, 3>), grid, dim3(THREADS), 0, (hipStream_t)hs, m->P,
+                                              m->cfg, m->B, leaf_mask, pi, v));
     } else if (kinds == SPL_LEAF_NN) {
-        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup<N, 1>), wave_grid(m->B), dim3(THREADS), 0,
-                                              (hipStream_t)hs, m->P, m->cfg, m->B, leaf_mask, pi, v));
+        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup_h<N, 1>), grid, dim3(THREADS), 0, (hipStream_t)hs, m->P,
+                                              m->cfg, m->B, leaf_mask, pi, v));
     } else {
-        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup<N, 2>), wave_grid(m->B), dim3(THREADS), 0,
-                                              (hipStream_t)hs, m->P, m->cfg, m->B, leaf_mask, pi, v));
+        SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup_h<N, 2>), grid, dim3(THREADS), 0, (hipStream_t)hs, m->P,
+                                              m->cfg, m->B, leaf_mask, pi, v));
     }
     // trees whose simulation was withdrawn (NN leaves only)
     if (m->cfg.selfplay && (kinds & SPL_LEAF_NN)) launch_gc(m, (hipStream_t)hs);

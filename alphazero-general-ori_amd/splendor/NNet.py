@@ -85,15 +85,25 @@ def _batch_generator(device):
     return g
 
 
+_CHECKSUM_CHUNK = 1 << 24     # bytes hashed per slice: transient memory independent of the set size
+
+
 def _content_checksum(ex):
     """64-bit checksum of an ExampleSet's contents (every column's bytes, position-weighted;
     integer sums wrap identically on any device), so ranks can tell whether they hold the
-    same examples — equal counts alone do not say that."""
+    same examples — equal counts alone do not say that. Hashed in slices of _CHECKSUM_CHUNK
+    bytes with a running accumulator (the position weights continue across slices), so the
+    int64 temporaries stay ~400 MB at most however many examples the set holds."""
     h = torch.zeros((), dtype=torch.int64, device=ex.board.device)
     for k, col in enumerate((ex.board, ex.pi, ex.winner, ex.scdiff, ex.valids, ex.surprise)):
-        b = col.contiguous().reshape(-1).view(torch.uint8).to(torch.int64)
-        w = torch.arange(1, b.numel() + 1, dtype=torch.int64, device=b.device) * 0x9E3779B1 + (k + 1) * 0x7F4A7C15
-        h = h * 0x100000001B3 + (b * w).sum()
+        b = col.contiguous().reshape(-1).view(torch.uint8)
+        s = torch.zeros((), dtype=torch.int64, device=b.device)
+        for off in range(0, b.numel(), _CHECKSUM_CHUNK):
+            part = b[off:off + _CHECKSUM_CHUNK].to(torch.int64)
+            w = torch.arange(off + 1, off + part.numel() + 1, dtype=torch.int64, device=b.device) * 0x9E3779B1 \
+                + (k + 1) * 0x7F4A7C15
+            s += (part * w).sum()
+        h = h * 0x100000001B3 + s
     return h
 
 
@@ -113,10 +123,14 @@ def _same_everywhere(ex, device):
 def _allreduce_grads(params, weight=None):
     """Sum (weight given: each rank's gradients scaled by its share of the global batch) or
     average (weight None) the gradients over ranks in one flat bucket (the model is ~1.25 MB
-    of fp32). Parameters without a gradient on this rank contribute zeros."""
+    of fp32). A parameter without a gradient on this rank contributes zeros to the bucket;
+    one that got no gradient on ANY rank (a per-parameter presence flag travels in the same
+    all-reduce) is left with grad None afterwards, so Adam skips it exactly as a single-rank
+    run does."""
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
         return
+    had = [p.grad is not None for p in params]
     for p in params:
         if p.grad is None:
             p.grad = torch.zeros_like(p)
@@ -124,12 +138,19 @@ def _allreduce_grads(params, weight=None):
     flat = torch.cat([g.reshape(-1) for g in grads])
     if weight is not None:
         flat *= weight
+    presence = torch.tensor(had, dtype=flat.dtype, device=flat.device)
+    flat = torch.cat([flat, presence])
     dist.all_reduce(flat)
+    present = (flat[-len(params):] > 0).tolist() if params else []
+    flat = flat[:-len(params)] if params else flat
     if weight is None:
         flat /= dist.get_world_size()
     off = 0
-    for g in grads:
-        g.copy_(flat[off:off + g.numel()].view_as(g))
+    for p, g, keep in zip(params, grads, present):
+        if keep:
+            g.copy_(flat[off:off + g.numel()].view_as(g))
+        else:
+            p.grad = None
         off += g.numel()
 
 

@@ -232,7 +232,7 @@ def stagger_marks(stagger, groups, sims, ratio):
 
 
 def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, seed, node_boards=-1,
-                 stagger=0, groups=16):
+                 stagger=0, groups=16, mem_gib=0.0):
     """Self-play at one BASELINE config: B games per GPU (shard board_base = rank * B), one
     MCTS simulation per game per iteration, leaves evaluated by the fused SplendorNNet kernel
     (fp32, random init), moves committed on device. `prefill` untimed iterations bring the
@@ -267,7 +267,8 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
         broadcast_network(net)                 # every rank searches with rank 0's network
     ev = LeafEvaluator(eng, net, B, use_graph=False)
     sp = SelfPlay(eng, B, sargs, evaluator=ev, dirichlet_noise=True, seed=seed, board_base=rank * B,
-                  node_boards=None if node_boards < 0 else bool(node_boards))
+                  node_boards=None if node_boards < 0 else bool(node_boards),
+                  mem_budget=int(mem_gib * 2**30) if mem_gib > 0 else None)
     sp.reset()
     t_fill = time.perf_counter()
     done = 0
@@ -628,6 +629,8 @@ def main():
     ap.add_argument("--c4-window", type=int, default=4000)
     ap.add_argument("--node-boards", type=int, default=-1, help="selfplay: 1/0 force node boards on/off "
                     "(default: on unless the pools do not fit)")
+    ap.add_argument("--mem-gib", type=float, default=0.0, help="selfplay: arena budget in GiB (default: "
+                    "BatchedMCTS.MEM_FRACTION of the free HBM)")
     ap.add_argument("--dry-run", action="store_true", help="multi-rank plumbing only (gloo, no GPU): "
                     "prints the line with value null")
     args = ap.parse_args()
@@ -674,7 +677,7 @@ def main():
     head = "config3" if args.workload in ("all", "selfplay") else args.workload
     n, B, sims = CONFIGS[head]
     r = run_selfplay(head, rank, world, dev, dist, args.steps, args.warmup, args.prefill, args.window, args.seed,
-                     args.node_boards, stagger=args.stagger)
+                     args.node_boards, stagger=args.stagger, mem_gib=args.mem_gib)
     rec = selfplay_record(head, r, world, args.steps, args.warmup)
     torch.cuda.empty_cache()
     extra = {}

@@ -512,10 +512,12 @@ static uint64_t splitmix64(uint64_t x) {
     return z ^ (z >> 31);
 }
 /* Hash network of the search-parity tests (device: k_hash_eval). Mode 0: priors spread over
- * (0, 1], values in [-1, 1) — shallow trees (leaf depth ~3). Mode 1 ("flat"): priors within
- * 1.6 % of each other and values within +-1/32, like the random-init SplendorNNet the bench
- * runs: with FPU reduction the search then keeps revisiting its first lines, and leaves
- * reach the depths of the bench's steady state (mean > 15, max > 64). */
+ * (0, 1], values in [-1, 1) — shallow trees (leaf depth ~3). Mode 1 ("peaked"): each legal
+ * action's hash weight w in [1, 2^24] divided by the largest legal one and raised to the
+ * 256th power, so priors are (w / max w)^256 — one or a few actions dominate and many are
+ * exactly 0 in float32 — and values are +-(1 - h 2^-30), i.e. within 2^-6 of +-1 (player 0
+ * positive). The search then commits to lines and leaves reach the depths of the bench's
+ * steady state (mean > 15, max > 64). */
 static int g_fake_mode = 0;
 void or_set_fake_mode(int mode) { g_fake_mode = mode; }
 void or_fake_predict(int n, const int8_t *st, const uint8_t *va, float *pi, float *v) {

@@ -54,7 +54,8 @@ double or_uniform(uint64_t seed, uint32_t board, uint32_t stream, uint32_t draw)
 /* deterministic stand-in network used for search parity (see make_golden.py) */
 uint64_t or_state_hash(const int8_t *state, int bytes);
 void or_fake_predict(int n, const int8_t *state, const uint8_t *valids, float *pi, float *v);
-/* hash network mode: 0 spread priors / values (default), 1 flat (deep trees, see the .c) */
+/* hash network mode: 0 spread priors / values (default), 1 peaked priors (w/max w)^256 and
+ * values near +-1 (deep trees, see the .c) */
 void or_set_fake_mode(int mode);
 /* leaf depth statistics of every search since the last reset: sum, max, simulations */
 void or_depth_stats(long long *out3, int reset);

@@ -248,3 +248,47 @@ def test_train_matches_reference_wrapper_gpu(tag):
     CPU's (still 20x below one Adam step of lr = 1e-3)."""
     g, losses, sd = _reference_training(tag, "cuda")
     _check_training(g, losses, sd, loss_rtol=1e-5, param_atol=5e-5, param_rtol=1e-5)
+
+
+def _grad_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "alphazero-general-ori_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from splendor.NNet import _allreduce_grads
+    ps = [torch.nn.Parameter(torch.zeros(3)) for _ in range(3)]
+    ps[0].grad = torch.full((3,), 2.0 + rank)                 # on every rank
+    if rank == 0:
+        ps[1].grad = torch.full((3,), 4.0)                    # on rank 0 only
+    _allreduce_grads(ps)                                      # ps[2]: on no rank
+    out = [None if p.grad is None else p.grad.tolist() for p in ps]
+    q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_grads_keeps_absent_gradients_none():
+    """a parameter without a gradient on any rank stays grad None (Adam skips it,
+    as on one rank); one with a gradient on some rank is averaged with zeros elsewhere."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for out in outs:
+        assert out[0] == [2.5] * 3 and out[1] == [2.0] * 3 and out[2] is None
+
+
+def test_content_checksum_is_chunk_independent(monkeypatch):
+    """The sliced checksum (bounded transient memory) equals the one-slice value."""
+    import splendor.NNet as NN
+    ex = synthetic(40, seed=3)
+    whole = int(NN._content_checksum(ex))
+    monkeypatch.setattr(NN, "_CHECKSUM_CHUNK", 997)
+    assert int(NN._content_checksum(ex)) == whole

@@ -1,0 +1,72 @@
+#!/bin/bash
+# The one runner for GPU-box evidence (run there from the repo root, e.g.
+#   gpurun --timeout 900 -- 'bash tools/gpu.sh tests bench'
+# ). Each step runs under its own time limit; the steps are chained and the script stops at
+# the first failure (no GPU step runs after a fault, an abort or a time limit). Outputs go
+# under gpurun_out/.
+#
+#   tests     pytest -m gpu (one process; per-test timeout)           -> gpurun_out/gpu_tests.log
+#   smoke     __graft_entry__.smoke()                                  -> gpurun_out/smoke.log
+#   bench     the default bench line (headline + secondary objects)    -> gpurun_out/bench.json
+#   selfplay  the config-3 headline alone                              -> gpurun_out/selfplay.json
+#   trace     config-3 kernel trace + stats (rocprofv3)                -> gpurun_out/prof_sp/
+#   split     per-iteration kernel split from the trace (needs trace)  -> gpurun_out/split.txt
+#   pmc       PMC passes over the self-play kernels (pmc_selfplay.sh)  -> gpurun_out/pmc_sp/
+#   nn        full-batch network trace + HBM counters (nn_fullbatch.sh) -> gpurun_out/nnfb/
+#   ab        interleaved A/B of the product library against ablib/lib<V>.so for V in $AB
+#             (config-3 bench twice each)                              -> gpurun_out/ab.txt
+#   bounds    the bounds-checked build (ablib/libchk.so: tools/bounds_check.sh on
+#             the host first) under capacity pressure                   -> gpurun_out/bounds_chk.json
+# ROUND (default r05) names the summaries; EXTRA adds bench arguments to selfplay/trace.
+set -uo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+ROUND=${ROUND:-r05}
+step() {
+    echo "$(date +%T) $1 start" >> gpurun_out/progress.log
+    case "$1" in
+    tests)
+        timeout -k 10 1000 python3 -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread \
+            > gpurun_out/gpu_tests.log 2>&1 ;;
+    smoke)
+        timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
+    bench)
+        timeout -k 10 900 python3 -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err ;;
+    selfplay)
+        timeout -k 10 300 python3 -u bench.py --workload selfplay --no-cpu-baseline ${EXTRA:-} \
+            > gpurun_out/selfplay.json 2> gpurun_out/selfplay.err ;;
+    trace)
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sp -o sp -- \
+            python3 bench.py --workload selfplay --steps 2000 --window 4000 --no-cpu-baseline ${EXTRA:-} \
+            > gpurun_out/prof_sp.log 2>&1 ;;
+    split)
+        python3 tools/trace_split.py "$(find gpurun_out/prof_sp -name '*kernel_trace.csv' | head -n 1)" 6000 \
+            > gpurun_out/split.txt ;;
+    pmc)
+        timeout -k 10 1000 bash tools/pmc_selfplay.sh gpurun_out/pmc_sp "$ROUND" > gpurun_out/pmc_sp.log 2>&1 ;;
+    nn)
+        timeout -k 10 400 bash tools/nn_fullbatch.sh "$ROUND" > gpurun_out/nnfb.log 2>&1 ;;
+    ab)
+        rm -f gpurun_out/ab.txt
+        for rep in 1 2; do
+            for v in product ${AB:-}; do
+                if [ "$v" = product ]; then lib=""; else lib="$PWD/ablib/lib$v.so"; fi
+                SPLENDOR_AMD_LIB=$lib timeout -k 10 240 python3 -u bench.py --workload selfplay --steps 2000 \
+                    --window 0 --no-cpu-baseline ${EXTRA:-} > gpurun_out/ab_$v.$rep.json 2> gpurun_out/ab_$v.$rep.err || return 1
+                echo "$v $rep $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_$v.$rep.json | head -1)" >> gpurun_out/ab.txt
+            done
+        done ;;
+    bounds)
+        SPLENDOR_AMD_LIB=$PWD/ablib/libchk.so timeout -k 10 300 python3 -u tools/bounds_check.py --tag chk \
+            --iters "${ITERS:-6000}" > gpurun_out/bounds_chk.json 2> gpurun_out/bounds_chk.err ;;
+    *)
+        echo "unknown step $1" >&2; return 2 ;;
+    esac
+    local rc=$?
+    echo "$(date +%T) $1 rc=$rc" >> gpurun_out/progress.log
+    return $rc
+}
+for s in "$@"; do
+    step "$s" || exit $?
+done

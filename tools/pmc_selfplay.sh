@@ -12,7 +12,7 @@ WARM=${3:-6000}
 STEPS=${4:-200}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
-CMD=(python3 bench.py --workload selfplay --prefill "$WARM" --warmup 20 --steps "$STEPS" --window 0 --no-cpu-baseline)
+CMD=(python3 bench.py --workload selfplay --prefill "$WARM" --warmup 20 --steps "$STEPS" --window 0 --no-cpu-baseline ${BENCH_EXTRA:-})
 # counters only for the self-play kernels, dispatches WARM+40 .. WARM+40+STEPS of each (the
 # timed steps; k_gc runs twice per iteration, so its range covers the second half of them)
 FILT=(--kernel-include-regex "k_(select|leaf_mask|nn_forward|backup|commit|gc)" --kernel-iteration-range "[$((WARM + 40))-$((WARM + 40 + STEPS))]")
