@@ -175,6 +175,41 @@ __device__ __forceinline__ int best_unvisited(const Pools &P, int64_t eb, int ec
     return bi;
 }
 
+// The candidate fields of a node record (NodeCold cand / ca / cp / np) for a run whose edges
+// before rank `from` all have visit records: cand = the first rank from `from` on without one,
+// its action and prior, and np = the prior of the first unvisited edge after it with a smaller
+// prior (-1: none; the runs are sorted by prior, so that is the largest smaller prior). One lane.
+__device__ __forceinline__ void lane_cand(const Pools &P, int64_t eb, int ec, int from, int &cand, int &ca, float &cp,
+                                          float &np) {
+    int j = from;
+    while (j < ec && P.ep(eb + j)->vi >= 0) j++;
+    cand = j; ca = 0; cp = 0.f; np = -1.f;
+    if (j >= ec) return;
+    const EdgeP c = *P.ep(eb + j);
+    ca = c.a; cp = c.p;
+    if (c.p > 0.f)
+        for (int k = j + 1; k < ec; k++) {
+            const EdgeP e = *P.ep(eb + k);
+            if (e.vi >= 0 || e.p == c.p) continue;
+            np = e.p;
+            break;
+        }
+}
+// the same with `cand` known, wave-collective (ranks lane-parallel); uniform results
+__device__ __forceinline__ void wave_cand(const Pools &P, int64_t eb, int ec, int cand, int &ca, float &cp, float &np) {
+    ca = 0; cp = 0.f; np = -1.f;
+    if (cand >= ec) return;
+    const EdgeP c = *P.ep(eb + cand);
+    ca = uniform(c.a); cp = __int_as_float(uniform(__float_as_int(c.p)));
+    float m = -1.f;
+    if (cp > 0.f)
+        for (int j = cand + 1 + lane_id(); j < ec; j += 64) {
+            const EdgeP e = *P.ep(eb + j);
+            if (e.vi < 0 && e.p < cp) m = fmaxf(m, e.p);
+        }
+    np = wave_max_f32(m);
+}
+
 // ------------------------------------------------------------ prior sums
 // numpy pairwise float32 sum of the 409 staged priors (np_sum409 order), 32 lanes:
 // lane = 8*block + j accumulates r_j of block `block`; blocks [0,96) [96,200) [200,304)
@@ -464,10 +499,10 @@ __device__ void mark_linked(const Pools &P, int t, int rootl, int32_t *mark, int
         int cnt = 0;
         if (l < nbt) {
             const int g = node_g(P, t, q[head + l]);
-            if (!P.nterm[g]) {
-                const NodeRun r = P.nrun[g];
-                vb = r.vb;
-                cnt = r.vcnt;
+            if (!P.nd[g].h.term) {
+                const NodeCold c = P.nd[g].c;
+                vb = c.vb();
+                cnt = c.vcnt();
             }
         }
         head += nbt;
@@ -546,7 +581,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     for (int base = 0; base < nc; base += GCT) {
         const int i = base + tid;
         bool keep = false;
-        if (i < nc) keep = i == rootl || (linked ? remap[i] == 1 : P.nround[node_g(P, t, i)] > root_round);
+        if (i < nc) keep = i == rootl || (linked ? remap[i] == 1 : P.nd[node_g(P, t, i)].h.round > root_round);
         int tot;
         const int ex = block_scan(keep ? 1 : 0, tot, L);
         if (i < nc) remap[i] = keep ? kept + ex : -1;
@@ -564,10 +599,8 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         if (remap[i] >= 0) {
             sz = 0;
             const int g = node_g(P, t, i);
-            if (!P.nterm[g]) {
-                const NodeRun r = P.nrun[g];
-                sz = r.ec + REC_UNITS * r.vcnt;
-            }
+            const Node nd = P.nd[g];
+            if (!nd.h.term) sz = nd.c.ec + REC_UNITS * nd.c.vcnt();
         }
         S.nvs[i] = sz;
     }
@@ -628,33 +661,31 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         const int i = base + tid;
         const int ni = i < nc ? remap[i] : -1;
         uint64_t k0 = 0, k1 = 0;
-        NodeRun nr{0, 0, 0, 0, 0, 0};
-        NodeStat nst{0.0, 0, -1, 0, -1, 0, -1};
-        int rd = 0, vs = 0;
-        int8_t term = 0;
+        Node nd{};
+        int vs = 0;
         if (ni >= 0) {
             const int g = node_g(P, t, i);
             k0 = P.nkey0[g]; k1 = P.nkey1[g];
-            nr = P.nrun[g]; nst = P.nst[g]; rd = P.nround[g];
-            term = P.nterm[g];
+            nd = P.nd[g];
             vs = S.nvs[i];
         }
         __syncthreads();
         if (ni >= 0) {
             const int ng = node_g(P, t, ni);
-            const int sz = term ? 0 : nr.ec + REC_UNITS * nr.vcnt;
-            NodeRun w = nr;                              // (a terminal node's values as they are)
+            const bool term = nd.h.term;
+            const int ec = nd.c.ec, vcnt = term ? 0 : nd.c.vcnt();
+            const int sz = term ? 0 : ec + REC_UNITS * vcnt;
+            Node w = nd;                                 // (a terminal node's values as they are)
+            S.queue[ni] = term ? -1 : nd.h.bchild;       // (the arg-max's link, remapped below)
+            S.ost[ni] = nd.c.eb(); S.ovb[ni] = nd.c.vb(); S.oec[ni] = term ? 0 : ec;
             if (!term) {
-                w.eb = nr.ec > 0 ? unit_g(P, t, vs) : 0;
-                w.vb = nr.vcnt > 0 ? unit_g(P, t, vs + nr.ec) : 0;
-                w.vcap = nr.vcnt;
+                w.c.set_eb(ec > 0 ? unit_g(P, t, vs) : 0, vcnt);
+                w.c.set_vb(vcnt > 0 ? unit_g(P, t, vs + ec) : 0, vcnt);
             }
+            w.h.h2 = -1; w.h.h3 = -1;                    // (descent hints name old ids: dropped)
             P.nkey0[ng] = k0; P.nkey1[ng] = k1;
-            P.nrun[ng] = w; P.nround[ng] = rd;
-            P.nst[ng] = nst; P.nterm[ng] = term;
-            S.queue[ni] = term ? -1 : nst.bchild;        // (the arg-max's link, remapped below)
+            P.nd[ng] = w;
             S.cs[ni] = vs; S.cnt[ni] = sz; S.inv[ni] = i;
-            S.ost[ni] = nr.eb; S.ovb[ni] = nr.vb; S.oec[ni] = term ? 0 : nr.ec;
             my_units += sz;
         }
     }
@@ -666,8 +697,8 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         if (ch >= 0) {
             BCHK(IN_TREE(P, t, ch, nc), 56, ((long long)ni << 32) | (uint32_t)ch, t, (void)0);
             const int nl = remap[node_l(P, ch)];
-            P.nst[node_g(P, t, ni)].bchild = nl >= 0 ? node_g(P, t, nl) : -1;
-            BCHK(nl < 0 || P.nround[node_g(P, t, nl)] == P.nround[node_g(P, t, ni)] + 1, 40,
+            P.nd[node_g(P, t, ni)].h.bchild = nl >= 0 ? node_g(P, t, nl) : -1;
+            BCHK(nl < 0 || P.nd[node_g(P, t, nl)].h.round == P.nd[node_g(P, t, ni)].h.round + 1, 40,
                  ((long long)ni << 32) | (uint32_t)nl, t, (void)0);
         }
     }
@@ -720,7 +751,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                 BCHK(IN_TREE(P, t, ch, nc), 57, ((long long)j[r] << 32) | (uint32_t)ch, t, (void)0);
                 const int nl = remap[node_l(P, ch)];
                 if (nl >= 0) nch = node_g(P, t, nl);
-                BCHK(nl < 0 || P.nround[nch] == P.nround[node_g(P, t, j[r])] + 1, 41,
+                BCHK(nl < 0 || P.nd[nch].h.round == P.nd[node_g(P, t, j[r])].h.round + 1, 41,
                      ((long long)j[r] << 32) | (uint32_t)nl, t, (void)0);
             }
             v[r] = (v[r] & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)nch << 32);
@@ -956,7 +987,7 @@ __global__ __launch_bounds__(GCT) void k_gc(Pools P, SearchCfg C) {
         if (st == 1 || st == 3 || st == 5) {
             // mid-search (1: the descent then repeats): rounds above the root's; search start:
             // above the root round
-            const int rr = st == 1 && root >= 0 ? P.nround[root] : H->root_round;
+            const int rr = st == 1 && root >= 0 ? P.nd[root].h.round : H->root_round;
             const int r0 = root;
             root = compact_tree<4>(P, t, r0, rr, S, L, NodeBoard<N>::UNITS);
             // capacity pressure (search start: the search would not fit; any: the compacted
@@ -1105,7 +1136,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     if (H->gc_state == 1 || H->sims_done < H->budget || H->overflow || H->root < 0) return;
     const uint32_t gb = C.board_base + (uint32_t)t;
     const int root = H->root;
-    const NodeRun rr = P.nrun[root];
+    const NodeRun rr = run_of(P.nd[root].c);
     const int ec = rr.ec;
     const bool forced = H->forced;
     const int sims = H->budget, cm = H->move_no;
@@ -1153,7 +1184,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         wave_valid_moves<N>(s, 0, lim, m);
         store_mask(P.ex_valid + x * 7, m);
         if (l == 0) {
-            const double q0 = P.nst[root].qs;
+            const double q0 = P.nd[root].h.qs;
             P.ex_player[x] = player;
             for (int i = 0; i < 4; i++)
                 P.ex_q[x * 4 + i] = i == 0 ? (float)q0 : (i < N ? (float)(-q0 / (double)(N - 1)) : 0.f);
@@ -1255,27 +1286,29 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     // or the backup of a new root then applies the noise). The move-sampling scratch is free.
     const int nroot = uniform(H->root);
     if (nroot >= 0 && uniform(H->noise_pending) && !uniform(H->gc_queued)) {
-        NodeRun r = P.nrun[nroot];
+        const Node nd0 = P.nd[nroot];
+        NodeRun r = run_of(nd0.c);
         r.eb = (int64_t)uniform64((uint64_t)r.eb); r.vb = (int64_t)uniform64((uint64_t)r.vb);
-        r.ec = (int16_t)uniform(r.ec);
+        r.ec = uniform(r.ec);
         const int cand = noise_kept_root(P, C, t, r, ST_DIR | (uint32_t)uniform(H->move_no), pbits[w],
                                          reinterpret_cast<float *>(pterm[w]), pprior[w], pact[w],
                                          reinterpret_cast<int16_t *>(pcnt[w]));
         wave_lds_fence();                                        // (the re-sorted run, read below)
-        const NodeStat ns = P.nst[nroot];
+        int ca;
+        float cp, np;
+        wave_cand(P, r.eb, r.ec, cand, ca, cp, np);
         const bool forced = uniform(H->forced) != 0;
         Pick pk{-1, 0, -1, 0};
-        if (!forced) pk = scan_run(P, r, ns.ns, ns.qs, C.cpuct, C.fpu, false, 0);
+        if (!forced) pk = scan_run(P, r, nd0.h.ns, nd0.h.qs, C.cpuct, C.fpu, false, 0);
         if (l == 0) {
             H->noise_pending = 0;
-            P.nrun[nroot].cand = (int16_t)cand;
-            NodeStat w2 = ns;
-            w2.best = (int16_t)pk.e;                             // (-1 with forced playouts: scans)
-            w2.ba = (int16_t)pk.a;
-            w2.bchild = pk.e >= 0 ? pk.child : -1;
-            w2.bterm = pk.e >= 0 && pk.child >= 0 ? (int)P.nterm[pk.child] : 0;
-            w2.bvi = pk.e >= 0 ? P.ep(r.eb + pk.e)->vi : (int16_t)-1;
-            P.nst[nroot] = w2;
+            Node w2 = nd0;
+            w2.c.cand = (int16_t)cand; w2.c.ca = (int16_t)ca; w2.c.cp = cp; w2.c.np = np;
+            w2.h.set_pick(pk.e, pk.a, pk.e >= 0 && pk.child >= 0 ? P.nd[pk.child].h.term : 0);   // (-1: scans)
+            w2.h.bchild = pk.e >= 0 ? pk.child : -1;
+            w2.h.h2 = -1; w2.h.h3 = -1;
+            w2.h.bvi = pk.e >= 0 ? P.ep(r.eb + pk.e)->vi : (int16_t)-1;
+            P.nd[nroot] = w2;
         }
     }
 }
@@ -1321,18 +1354,20 @@ __global__ void k_drain_reset(Pools P, int max, int32_t *n_out) {
 }
 
 // ------------------------------------------------------------ select
-// a terminal node's end values (NodeRun of a terminal node: es[4] in its first 16 bytes)
+// a terminal node's end values (its NodeCold's first 16 bytes hold es[4])
 __device__ __forceinline__ void term_values(const Pools &P, int g, float v[4]) {
-    const NodeRun r = P.nrun[g];
-    v[0] = __int_as_float((int)(uint32_t)(uint64_t)r.eb); v[1] = __int_as_float((int)(uint32_t)((uint64_t)r.eb >> 32));
-    v[2] = __int_as_float((int)(uint32_t)(uint64_t)r.vb); v[3] = __int_as_float((int)(uint32_t)((uint64_t)r.vb >> 32));
+    const float4 e = *reinterpret_cast<const float4 *>(&P.nd[g].c);
+    v[0] = e.x; v[1] = e.y; v[2] = e.z; v[3] = e.w;
 }
-__device__ __forceinline__ NodeRun term_run(const float v[4]) {
-    NodeRun r;
-    r.eb = (int64_t)(((uint64_t)(uint32_t)__float_as_int(v[1]) << 32) | (uint32_t)__float_as_int(v[0]));
-    r.vb = (int64_t)(((uint64_t)(uint32_t)__float_as_int(v[3]) << 32) | (uint32_t)__float_as_int(v[2]));
-    r.ec = 0; r.vcnt = 0; r.vcap = 0; r.cand = 0;
-    return r;
+// the record of a new terminal node of round rd with end values v
+__device__ __forceinline__ Node term_node(const float v[4], int rd) {
+    Node n{};
+    n.h.bchild = -1; n.h.h2 = -1; n.h.h3 = -1; n.h.set_pick(-1, 0, 0); n.h.ns = 0;
+    n.h.term = 1; n.h.round = (uint8_t)rd; n.h.qs = 0.0;
+    *reinterpret_cast<float4 *>(&n.c) = make_float4(v[0], v[1], v[2], v[3]);
+    n.h.bvi = -1;
+    n.c.ec = 0; n.c.cand = 0; n.c.ca = 0; n.c.pad = 0; n.c.cp = 0.f; n.c.np = -1.f;
+    return n;
 }
 
 // ------------------------------------------------------------ select, lane per tree
@@ -1397,6 +1432,22 @@ __device__ __forceinline__ void lane_tree_step(int8_t *s, int a) {
     if (nxt) lane_roll_players<N>(s, nxt);
 }
 
+// Per-phase cycle probes of k_select_lanes (diagnostic builds only, -DSELECT_PROBE=1; never
+// the product): per wave, s_memtime deltas summed over the waves of every launch
+#ifndef SELECT_PROBE
+#define SELECT_PROBE 0
+#endif
+#if SELECT_PROBE
+__device__ unsigned long long g_sel_probe[16];
+#define SPROBE(k)                                                  \
+    {                                                              \
+        const uint64_t c_ = __builtin_readcyclecounter();          \
+        pacc[k] += c_ - plast;                                     \
+        plast = c_;                                                \
+    }
+#else
+#define SPROBE(k)
+#endif
 #ifndef PATH_CHUNK
 #define PATH_CHUNK 8       // previous-path levels a lane checks per round trip
 #endif
@@ -1412,6 +1463,11 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
     __shared__ __align__(16) int8_t boards[64 * ST];                    // lanes on distinct banks
     __shared__ RunScr scr;                                              // root noise (one tree)
     const int l = lane_id();
+#if SELECT_PROBE
+    uint64_t pacc[6] = {0, 0, 0, 0, 0, 0}, plast = __builtin_readcyclecounter();
+    const uint64_t pstart = plast;
+    int plev = 0, pexp = 0;                              // levels descended, expansion rounds
+#endif
     const int slot = blockIdx.x * 64 + l;
     if (blockIdx.x == 0 && l < 2) P.counters[6 + l] = 0;     // k_leaf_mask's filing counters
     if (blockIdx.x == 0 && l == 2 && leaf_count) *leaf_count = 0;
@@ -1441,14 +1497,19 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
     for (uint64_t m = __ballot(noised); m; m &= m - 1) {
         const int j = __ffsll((unsigned long long)m) - 1;
         const int tj = __builtin_amdgcn_readlane(t, j), rj = __builtin_amdgcn_readlane(root, j);
-        NodeRun r = P.nrun[rj];
+        NodeRun r = run_of(P.nd[rj].c);
         r.eb = (int64_t)uniform64((uint64_t)r.eb); r.vb = (int64_t)uniform64((uint64_t)r.vb);
-        r.ec = (int16_t)uniform(r.ec);
+        r.ec = uniform(r.ec);
         const int cand = noise_kept_root(P, C, tj, r, ST_DIR | (uint32_t)__builtin_amdgcn_readlane(mv, j), scr);
+        wave_lds_fence();
+        int ca;
+        float cp, np;
+        wave_cand(P, r.eb, r.ec, cand, ca, cp, np);
         if (l == 0) {
             P.hdr[tj].noise_pending = 0;                 // (a withdrawn simulation must not re-noise)
-            P.nrun[rj].cand = (int16_t)cand;
-            P.nst[rj].best = -1;                         // ranks moved: the root scans
+            NodeCold &c = P.nd[rj].c;
+            c.cand = (int16_t)cand; c.ca = (int16_t)ca; c.cp = cp; c.np = np;
+            P.nd[rj].h.best = -1;                        // ranks moved: the root scans
         }
         wave_lds_fence();
     }
@@ -1471,24 +1532,33 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
     // root): wave-collective, one tree at a time, before the lanes descend
     Pick pk{0, 0, -1, 0};
     bool have_pk = false;
-    NodeStat nsq{0.0, 0, -1, 0, -1, 0, -1};
-    if (state == LS_DESCEND) nsq = P.nst[node];
+    NodeHot nsq{-1, -1, -1, -1, 0, 0, 0, 0, -1, 0.0};   // (the first node's whole hot half)
+    if (state == LS_DESCEND) nsq = P.nd[node].h;
     const bool scan = state == LS_DESCEND && depth == 0 && (!root_cache || nsq.best < 0);
     for (uint64_t m = __ballot(scan); m; m &= m - 1) {
         const int j = __ffsll((unsigned long long)m) - 1;
         const int nj = __builtin_amdgcn_readlane(node, j);
-        NodeRun r = P.nrun[nj];
+        NodeRun r = run_of(P.nd[nj].c);
         r.eb = (int64_t)uniform64((uint64_t)r.eb); r.vb = (int64_t)uniform64((uint64_t)r.vb);
-        r.ec = (int16_t)uniform(r.ec);
+        r.ec = uniform(r.ec);
         const Pick p = scan_run(P, r, __builtin_amdgcn_readlane(nsq.ns, j), readlane_f64(nsq.qs, j), C.cpuct, C.fpu,
                                 __builtin_amdgcn_readlane((int)forced, j) != 0, __builtin_amdgcn_readlane(sims, j));
         if (l == j) { pk = p; have_pk = true; }
     }
     if (have_pk) {                                       // the scanned edge's link and whether terminal
-        if (pk.child < 0 && pk.e == nsq.best && !noised) { pk.child = nsq.bchild; pk.cterm = nsq.bterm; }
-        else pk.cterm = pk.child >= 0 ? (int)P.nterm[pk.child] : 0;
+        if (pk.child < 0 && pk.e == nsq.best && !noised) { pk.child = nsq.bchild; pk.cterm = nsq.bterm(); }
+        else pk.cterm = pk.child >= 0 ? (int)P.nd[pk.child].h.term : 0;
     }
-    bool have_nsq = state == LS_DESCEND;
+    // The descent's record queue (descent hints, mcts_device.h Node): the link records of the
+    // next levels' nodes q1 .. q3, loaded ahead. Leaving a level whose pick is the cached one
+    // asks for its child (the authoritative link) and the child's and grandchild's cached picks
+    // as the record's hints name them; a level takes its record from the queue when q1 is its
+    // node (always, once the queue is primed), so a correct chain of hints keeps three loads of
+    // the dependent chain in flight.
+    NodeLink cur = *reinterpret_cast<const NodeLink *>(&nsq);
+    NodeLink l1{-1, -1, -1, -1, 0}, l2{-1, -1, -1, -1, 0}, l3{-1, -1, -1, -1, 0};
+    int q1 = -1, q2 = -1, q3 = -1;
+    bool have_cur = state == LS_DESCEND;
     int bnode = nbrd ? -1 : node;                        // the node whose board the lane holds
     int miss = -1, leaf_node = -1, cbest = -1;
     uint64_t k0 = 0, k1 = 0;
@@ -1499,18 +1569,27 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
     // the expansion (board staging, transition, fingerprint, lookup) is long, and lanes
     // reaching it at different levels would otherwise run it once per level in turn
     // (measured: 342 us per select at config 3 with the two phases interleaved)
+    SPROBE(0)
     while (__ballot(state != LS_DONE)) {
       while (__ballot(state == LS_DESCEND)) {
         if (state == LS_DESCEND) {
             if (depth >= P.pcap) {
                 state = LS_DONE; kind = LEAF_NONE; H->overflow = 2;
             } else {
-                if (!have_pk) {                          // ONE 32-byte load per level
-                    if (!have_nsq) nsq = P.nst[node];
-                    pk = Pick{nsq.best, nsq.ba, nsq.bchild, nsq.bterm};
+                if (!have_pk) {                          // ONE 16-byte record per level
+                    if (!have_cur) {
+                        if (q1 != node) { l1 = link_of(P.nd, node); q2 = -1; q3 = -1; }
+                        cur = l1;
+                        q1 = q2; l1 = l2; q2 = q3; l2 = l3; q3 = -1;
+                    }
+                    pk = Pick{cur.best, cur.ba(), cur.bchild, cur.bterm()};
                 }
-                have_pk = false; have_nsq = false;
-                cbest = nsq.best;
+                const bool hinted = pk.e == cur.best;    // (the cached pick: its hints apply)
+                have_pk = false; have_cur = false;
+                cbest = cur.best;
+#if SELECT_PROBE
+                plev++;
+#endif
                 if (pend >= 0) { path_n[pend] = pend_n; path_x[pend] = pend_x; }
                 pend = depth; pend_n = node; pend_x = px_pack(pk.e, pk.a);
                 depth++;
@@ -1521,25 +1600,34 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                     state = LS_DONE;
                 } else if (pk.child >= 0 && nbrd) {      // linked: no transition needed
                     BCHK(IN_TREE(P, t, pk.child, H->node_count), 52, pk.child, t, (void)0);
-                    BCHK(P.nround[pk.child] == P.nround[node] + 1, 30, ((long long)node << 32) | (uint32_t)pk.child, t,
+                    BCHK(P.nd[pk.child].h.round == P.nd[node].h.round + 1, 30, ((long long)node << 32) | (uint32_t)pk.child, t,
                          pk.child = pk.child);
                     node = pk.child;
+                    const int w2 = hinted ? cur.h2 : -1, w3 = hinted ? cur.h3 : -1;
+                    if (q1 != node) { q1 = node; l1 = link_of(P.nd, node); q2 = -1; q3 = -1; }
+                    if (w2 >= 0 && q2 != w2) { q2 = w2; l2 = link_of(P.nd, w2); q3 = -1; }
+                    if (w3 >= 0 && q2 == w2 && q3 != w3) { q3 = w3; l3 = link_of(P.nd, w3); }
                 } else {
                     state = LS_EXPAND;
                 }
             }
         }
       }
-        if (state == LS_EXPAND) {
-            if (nbrd && bnode != node) {                 // stage this node's stored board
-                const uint64_t *src = nbrd + (size_t)node * (NodeBoard<N>::BYTES / 8);
-                for (int r = 0; r < Lx::ROWS; r++) row(s, r) = src[r];
+        SPROBE(1)
+        if (state == LS_EXPAND && nbrd && bnode != node) {   // stage this node's stored board
+            const uint64_t *src = nbrd + (size_t)node * (NodeBoard<N>::BYTES / 8);
+            for (int r = 0; r < Lx::ROWS; r++) row(s, r) = src[r];
 #if SPL_BOUNDS_CHECK
-                uint64_t f0, f1;
-                lane_fingerprint<N>(s, f0, f1);
-                BCHK(f0 == P.nkey0[node] && f1 == P.nkey1[node], 36, node, t, (void)0);
+            uint64_t f0, f1;
+            lane_fingerprint<N>(s, f0, f1);
+            BCHK(f0 == P.nkey0[node] && f1 == P.nkey1[node], 36, node, t, (void)0);
 #endif
-            }
+        }
+        SPROBE(2)
+#if SELECT_PROBE
+        pexp += __ballot(state == LS_EXPAND) != 0;
+#endif
+        if (state == LS_EXPAND) {
             lane_tree_step<N>(s, pk.a);
             int child = pk.child;
             const bool cached = cbest == pk.e;
@@ -1547,10 +1635,10 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                 lane_fingerprint<N>(s, k0, k1);
                 child = hash_lookup(P, t, k0, k1, &miss);
                 if (child >= 0) {                        // transposition: link the cached pick
-                    const int ct = P.nterm[child];
+                    const int ct = P.nd[child].h.term;
                     BCHK(IN_TREE(P, t, child, H->node_count), 53, child, t, (void)0);
-                    BCHK(P.nround[child] == P.nround[node] + 1, 37, ((long long)node << 32) | (uint32_t)child, t, (void)0);
-                    if (cached) { P.nst[node].bchild = child; P.nst[node].bterm = ct; }
+                    BCHK(P.nd[child].h.round == P.nd[node].h.round + 1, 37, ((long long)node << 32) | (uint32_t)child, t, (void)0);
+                    if (cached) { P.nd[node].h.bchild = child; P.nd[node].h.babt = (uint16_t)(pk.a | (ct << 15)); }
                     if (ct) {
                         kind = LEAF_TERMINAL;
                         term_values(P, child, val);
@@ -1560,7 +1648,7 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                 }
             }
             if (state == LS_EXPAND) {
-                BCHK(child < 0 || P.nround[child] == (uint8_t)bt(row(s, 0), 6), 31,
+                BCHK(child < 0 || P.nd[child].h.round == (uint8_t)bt(row(s, 0), 6), 31,
                      ((long long)node << 32) | (uint32_t)child, t, child = child);
                 if (child >= 0) {                        // continue below the linked node
                     node = child;
@@ -1582,11 +1670,9 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                             H->unexpanded += 1;
                         } else {
                             P.nkey0[g] = k0; P.nkey1[g] = k1;
-                            P.nrun[g] = term_run(val);
-                            P.nst[g] = NodeStat{0.0, 0, -1, 0, -1, 0, -1};
-                            P.nround[g] = (uint8_t)bt(row(s, 0), 6); P.nterm[g] = 1;
+                            P.nd[g] = term_node(val, (uint8_t)bt(row(s, 0), 6));
                             hash_insert(P, t, k0, g);
-                            if (cached) { P.nst[node].bchild = g; P.nst[node].bterm = 1; }
+                            if (cached) { P.nd[node].h.bchild = g; P.nd[node].h.babt = (uint16_t)(pk.a | (1 << 15)); }
                             H->node_count = id + 1;
                         }
                         leaf_node = g;
@@ -1595,6 +1681,7 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                 }
             }
         }
+        SPROBE(3)
     }
     if (pend >= 0) { path_n[pend] = pend_n; path_x[pend] = pend_x; }
     if (act && root < 0) lane_fingerprint<N>(s, k0, k1);   // the root itself is the leaf
@@ -1622,6 +1709,27 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
         leaf_valid[t] = kind == LEAF_NN;
         path_n[depth] = kind == LEAF_TERMINAL ? leaf_node : -1;
     }
+#if SELECT_PROBE
+    SPROBE(4)
+    if (l == 0) {
+        for (int k = 0; k < 5; k++) atomicAdd(&g_sel_probe[k], (unsigned long long)pacc[k]);
+        atomicAdd(&g_sel_probe[5], 1ull);
+        atomicMax(&g_sel_probe[6], (unsigned long long)(plast - pstart));
+        atomicAdd(&g_sel_probe[7], (unsigned long long)(plast - pstart));
+    }
+    {
+        const int lmax = wave_max_i32(plev);
+        int lsum = plev;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
+        if (l == 0) {
+            atomicAdd(&g_sel_probe[8], (unsigned long long)lmax);
+            atomicAdd(&g_sel_probe[9], (unsigned long long)lsum);
+            atomicMax(&g_sel_probe[10], (unsigned long long)lmax);
+            atomicAdd(&g_sel_probe[11], (unsigned long long)pexp);
+        }
+    }
+#endif
 }
 
 // ------------------------------------------------------------ leaf masks
@@ -1826,6 +1934,9 @@ struct Level {
     int ns;                     // Ns before the update
     double qs;
     NodeRun r;                  // the node's run / visit block
+    int16_t ca;                 // its candidate's action (prior cp, screen bound np), its round
+    uint8_t round;
+    float cp, np;
     EdgeP e;                    // the edge taken
     int n;                      // its Nsa (0 without a visit record)
     double q;                   // its Qsa
@@ -1841,19 +1952,20 @@ __device__ __forceinline__ void load_levels_at(const Pools &P, int t, int d, int
     const int32_t *path_x = P.path_x + (size_t)t * P.pcap;
     V.node = 0; V.off = 0; V.act = 0; V.child = -1; V.ns = 0; V.qs = 0.0;
     V.r = NodeRun{0, 0, 0, 0, 0, 0}; V.e = EdgeP{0.f, 0, -1}; V.n = 0; V.q = Q_UNSET; V.rchild = -1;
-    V.grow = 0; V.nb = -1;
+    V.grow = 0; V.nb = -1; V.ca = 0; V.round = 0; V.cp = 0.f; V.np = -1.f;
     if (!in) return;
     V.node = path_n[d];
     const int px = path_x[d];
     V.child = d + 1 < depth ? path_n[d + 1] : lid;
     V.off = px_off(px); V.act = px_action(px);
-    const NodeStat st = P.nst[V.node];
-    V.ns = st.ns; V.qs = st.qs;
-    V.r = P.nrun[V.node];
+    const Node nd = P.nd[V.node];                        // the level's one record (64 bytes)
+    V.ns = nd.h.ns; V.qs = nd.h.qs; V.round = nd.h.round;
+    V.r = run_of(nd.c);
+    V.ca = nd.c.ca; V.cp = nd.c.cp; V.np = nd.c.np;
     // the path edge is the node's cached pick (the descent followed it) unless the root
     // level scanned: its visit record is then known without the EdgeP (whose prior only a
     // new record needs)
-    if (st.best == V.off && st.bvi >= 0) V.e = EdgeP{0.f, (int16_t)V.act, st.bvi};
+    if (nd.h.best == V.off && nd.h.bvi >= 0) V.e = EdgeP{0.f, (int16_t)V.act, nd.h.bvi};
     else V.e = *P.ep(V.r.eb + V.off);
     if (V.e.vi >= 0) {
         const VisitRec v = *P.vr(V.r.vb + REC_UNITS * V.e.vi);
@@ -1863,6 +1975,21 @@ __device__ __forceinline__ void load_levels_at(const Pools &P, int t, int d, int
         // edges fastest, and its block then never moves again during the search)
         V.grow = d == 0 ? (int)V.r.ec : (V.r.vcap == 0 ? 1 : min(2 * (int)V.r.vcap, (int)V.r.ec));
     }
+}
+
+// pass A's view of a deeper group's level d: the new visit-block capacity its backup needs
+// (load_levels_at's V.grow) from the fields that decide it only
+__device__ __forceinline__ int grow_at(const Pools &P, int t, int d, bool in) {
+    if (!in) return 0;
+    const int node = P.path_n[(size_t)t * (P.pcap + 1) + d];
+    const int off = px_off(P.path_x[(size_t)t * P.pcap + d]);
+    const Node *nd = P.nd + node;
+    const int best = nd->h.best, bvi = nd->h.bvi;
+    const uint64_t ebq = nd->c.ebq, vbq = nd->c.vbq;
+    const int ec = nd->c.ec, vcap = (int)(ebq >> 48), vcnt = (int)(vbq >> 48);
+    const int vi = best == off && bvi >= 0 ? bvi : P.ep((int64_t)(ebq & LOW48) + off)->vi;
+    if (vi >= 0 || vcnt != vcap) return 0;
+    return d == 0 ? ec : (vcap == 0 ? 1 : min(2 * vcap, ec));
 }
 
 #ifndef WD_MAX
@@ -1894,6 +2021,11 @@ __device__ __forceinline__ double half_max_f64(double x) {
         const int lo = __shfl_xor(__double2loint(x), o, 64), hi = __shfl_xor(__double2hiint(x), o, 64);
         x = fmax(x, __hiloint2double(hi, lo));
     }
+    return x;
+}
+__device__ __forceinline__ float half_max_f32(float x) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
     return x;
 }
 __device__ __forceinline__ int64_t shfl64(int64_t x, int src) {
@@ -1959,7 +2091,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     const uint64_t h_k0 = H->leaf_k0, h_k1 = H->leaf_k1;
     const int h_sims = H->sims_done, h_noise = H->noise_pending, h_gc = H->gc_state;
     const int32_t *path_n = P.path_n + (size_t)(tv ? t : 0) * (P.pcap + 1);
-    int64_t *path_b = P.path_b + (size_t)(tv ? t : 0) * P.pcap;
+    const size_t pb0 = (size_t)(tv ? t : 0) * P.pcap;   // this tree's k_backup scratch in P.path_b
     float val[4] = {0, 0, 0, 0};
     int lid = -1;
     BkScr &S = scr[2 * w + half];
@@ -1982,9 +2114,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     load_levels_at(P, t, hl, depth, lid, V, act && hl < min(depth, 32));
     bool fail = false;
     for (int g0 = 0; g0 < dmax; g0 += 32) {
-        Level Vg;
-        if (g0 > 0) load_levels_at(P, t, g0 + hl, depth, lid, Vg, act && g0 + hl < depth);
-        const int grow = g0 == 0 ? V.grow : Vg.grow;
+        const int grow = g0 == 0 ? V.grow : grow_at(P, t, g0 + hl, act && g0 + hl < depth);
         uint64_t gm = __ballot(grow > 0);
         int64_t nb = -1;
         while (gm) {                                     // (both halves' blocks in turn)
@@ -1999,7 +2129,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             if (l == j) nb = b;
         }
         if (g0 == 0) V.nb = nb;
-        else if (grow > 0) path_b[g0 + hl] = nb;
+        else if (grow > 0) P.path_b[pb0 + g0 + hl] = nb;
     }
     int g = -1, ec = 0;
     int64_t eb = -1;
@@ -2066,29 +2196,52 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         int bsel = -1, bact = 0;
         double bu = -INFINITY;
         int ba = 0x7fffffff;
+        float pm = -1.f;                                 // its candidate's prior (rank 0)
         const bool narg = expand && depth > 0;
-        if (narg) {
+        if (expand) {
             const double fpu_init = fpu_base(C.fpu, (double)val[0]), sq_eps = sqrt(1e-8);
             for (int i = hl; i < ec; i += 32) {
-                const double u = ucb_unvisited(S.cp[i], C.cpuct, fpu_init, sq_eps);
-                if (u > bu || (u == bu && S.ca[i] < ba)) { bu = u; ba = S.ca[i]; }
+                const float p = S.cp[i];
+                pm = fmaxf(pm, p);
+                if (narg) {
+                    const double u = ucb_unvisited(p, C.cpuct, fpu_init, sq_eps);
+                    if (u > bu || (u == bu && S.ca[i] < ba)) { bu = u; ba = S.ca[i]; }
+                }
             }
         }
         const double mu = half_max_f64(bu);
         bact = half_min_i32(bu == mu ? ba : 0x7fffffff);
-        int r = 0;
-        if (narg) {
-            const float pb = S.pr[bact];
-            for (int i = hl; i < ec; i += 32) r += (S.cp[i] > pb) || (S.cp[i] == pb && S.ca[i] < bact);
+        pm = half_max_f32(pm);
+        // its rank; the candidate (rank 0: the largest prior, lowest action among equals) and
+        // the screen bound np (the largest smaller prior)
+        int r = 0, cam = 0x7fffffff;
+        float npm = -1.f;
+        if (expand) {
+            const float pb = narg ? S.pr[bact] : 0.f;
+            for (int i = hl; i < ec; i += 32) {
+                const float p = S.cp[i];
+                const int a = S.ca[i];
+                r += (p > pb) || (p == pb && a < bact);
+                if (p == pm) cam = min(cam, a);
+                else npm = fmaxf(npm, p);
+            }
         }
         r = half_sum_i32(r);
+        cam = half_min_i32(cam);
+        npm = half_max_f32(npm);
         if (narg) bsel = r;
         else bact = 0;
         if (expand && hl == 0) {
             P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
-            P.nrun[g] = NodeRun{eb, 0, (int16_t)ec, 0, 0, 0};
-            P.nst[g] = NodeStat{(double)val[0], 0, (int16_t)bsel, (int16_t)bact, -1, 0, -1};
-            P.nround[g] = h_round; P.nterm[g] = 0;
+            Node nn;
+            nn.h.bchild = -1; nn.h.h2 = -1; nn.h.h3 = -1;
+            nn.h.set_pick(bsel, bact, 0); nn.h.ns = 0;
+            nn.h.term = 0; nn.h.round = (uint8_t)h_round; nn.h.bvi = -1;
+            nn.h.qs = (double)val[0];
+            nn.c.set_eb(eb, 0); nn.c.set_vb(0, 0);
+            nn.c.ec = (int16_t)ec; nn.c.cand = 0; nn.c.ca = (int16_t)cam; nn.c.pad = 0;
+            nn.c.cp = pm; nn.c.np = pm > 0.f ? npm : -1.f;
+            P.nd[g] = nn;
             if (h_hslot >= 0) P.hslot[(size_t)t * P.hcap + h_hslot] = g;
             else hash_insert(P, t, h_k0, g);
             if (depth == 0) H->root = g;
@@ -2098,15 +2251,20 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     }
     if (!done && depth > 0 && kind == LEAF_NN && hl == (depth - 1 < 32 ? depth - 1 : 32)) V.child = lid;
     // ---- pass B (as k_backup), levels in groups of 32 per half
-    int moved = 0x7fffffff;
+    int moved = 0x7fffffff, n_wide_lo = 0, n_wide_hi = 0, n_big_lo = 0, n_big_hi = 0;
     for (int g0 = 0; g0 < dmax; g0 += 32) {
         const int d = g0 + hl;
         const bool in = !done && d < depth;
         if (g0 > 0) {
             load_levels_at(P, t, d, depth, lid, V, in);
-            if (in && V.grow > 0) V.nb = path_b[d];
+            if (in && V.grow > 0) V.nb = P.path_b[pb0 + d];
         }
-        for (uint64_t gm = __ballot(in && V.e.vi < 0 && V.grow > 0 && V.nb >= 0 && V.r.vcnt > 0); gm; gm &= gm - 1) {
+        const bool reloc = in && V.e.vi < 0 && V.grow > 0 && V.nb >= 0 && V.r.vcnt > 0;
+        {                                                // (per-half counts, in SGPRs)
+            const uint64_t bm = __ballot(reloc && V.grow >= 128);
+            n_big_lo += __popcll(bm & 0xFFFFFFFFull); n_big_hi += __popcll(bm >> 32);
+        }
+        for (uint64_t gm = __ballot(reloc); gm; gm &= gm - 1) {
             const int j = __ffsll((unsigned long long)gm) - 1;
             const int64_t ob = readlane64(V.r.vb, j), nb = readlane64(V.nb, j);
             const int nu = REC_UNITS * __builtin_amdgcn_readlane((int)V.r.vcnt, j);
@@ -2142,33 +2300,34 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 *P.vr(V.r.vb + REC_UNITS * vidx) = VisitRec{q1, n1, V.child, V.e.p, (int16_t)V.off, (int16_t)V.act};
                 P.ep(V.r.eb + V.off)->vi = (int16_t)vidx;
                 V.r.vcnt = (int16_t)(vidx + 1);
+                // (a record elsewhere leaves np an upper bound: the screen stays exact)
                 if (V.off == V.r.cand) {
-                    int j = V.off + 1;
-                    while (j < V.r.ec && P.ep(V.r.eb + j)->vi >= 0) j++;
-                    V.r.cand = (int16_t)j;
+                    int cd, ca;
+                    lane_cand(P, V.r.eb, V.r.ec, V.off + 1, cd, ca, V.cp, V.np);
+                    V.r.cand = (int16_t)cd; V.ca = (int16_t)ca;
                 }
-                P.nrun[V.node] = V.r;
+                NodeCold c;                              // the record's second half (run / block)
+                c.set_eb(V.r.eb, V.r.vcap); c.set_vb(V.r.vb, V.r.vcnt);
+                c.ec = (int16_t)V.r.ec; c.cand = (int16_t)V.r.cand; c.ca = (int16_t)V.ca; c.pad = 0;
+                c.cp = V.cp; c.np = V.np;
+                P.nd[V.node].c = c;
             }
             V.rchild = V.rchild >= 0 ? V.rchild : V.child;
         }
         const bool wide = in && V.r.vcnt > BK_WIDE;
+        {
+            const uint64_t wm = __ballot(wide && d > 0);
+            n_wide_lo += __popcll(wm & 0xFFFFFFFFull); n_wide_hi += __popcll(wm >> 32);
+        }
         Screen Sc = screen_init(nns, nqs, C.cpuct, C.fpu);
         bool has_c = false;
         double uc = 0.0;
         int ac = 0, rc = 0;
-        if (in && V.r.cand < V.r.ec) {
-            has_c = true;
-            const EdgeP c = *P.ep(V.r.eb + V.r.cand);
-            rc = V.r.cand; ac = c.a;
-            screen_item(Sc, false, c.p, 0, 0.0, rc, c.a, -1);
-            if (c.p > 0.f) {
-                for (int j = V.r.cand + 1; j < V.r.ec; j++) {
-                    const EdgeP e = *P.ep(V.r.eb + j);
-                    if (e.vi >= 0 || e.p == c.p) continue;
-                    screen_item(Sc, false, e.p, 0, 0.0, j, e.a, -1);
-                    break;
-                }
-            }
+        if (in && V.r.cand < V.r.ec) {                  // the best unvisited edge, and the bound
+            has_c = true;                                // on every other one (cached in the record)
+            rc = V.r.cand; ac = V.ca;
+            screen_item(Sc, false, V.cp, 0, 0.0, rc, V.ca, -1);
+            if (V.np >= 0.f) screen_item(Sc, false, V.np, 0, 0.0, 0, 0, -1);   // (never leads: np < cp)
         }
         const int myv = in && !wide ? V.r.vcnt : 0;
         const int maxv = wave_max_i32(myv);
@@ -2206,13 +2365,29 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                         __builtin_amdgcn_readlane(ac, j), __builtin_amdgcn_readlane(rc, j), rk, ak, ck, vk);
             if (l == j) { bsel = rk; bact = ak; bch = ck; bvi = vk; }
         }
-        if (in) {
-            if (bsel == V.off) { bch = V.rchild; bvi = vidx; }
-            const int bt_ = bch >= 0 ? (int)P.nterm[bch] : 0;
-            P.nst[V.node] = NodeStat{nqs, nns, (int16_t)bsel, (int16_t)bact, bch, bt_, (int16_t)bvi};
+        // descent hints: a level whose pick stays on the path edge names the new picks of the
+        // next two path levels (lanes hl + 1, hl + 2 of this half; none across a group boundary)
+        const bool stay = in && bsel == V.off;
+        if (stay) { bch = V.rchild; bvi = vidx; }
+        const int src1 = min(l + 1, 63), src2 = min(l + 2, 63);
+        const int nb1 = __shfl(bch, src1, 64), nb2 = __shfl(bch, src2, 64);
+        const int ns1 = __shfl((int)stay, src1, 64);
+        const int hh2 = stay && hl < 31 && d + 1 < depth ? nb1 : -1;
+        const int hh3 = hh2 >= 0 && ns1 && hl < 30 && d + 2 < depth ? nb2 : -1;
+        if (in) {                                        // the level's record, written once
+            int bt_;
+            if (stay) bt_ = kind == LEAF_TERMINAL && bch >= 0 && bch == lid;   // (the path's child:
+            else bt_ = bch >= 0 ? (int)P.nd[bch].h.term : 0;                   //  terminal only as the leaf)
+            NodeHot w;                                   // (the second half: written with a new record)
+            w.bchild = bch; w.h2 = hh2; w.h3 = hh3;
+            w.set_pick(bsel, bact, bt_); w.ns = nns;
+            w.term = 0; w.round = (uint8_t)V.round; w.bvi = (int16_t)bvi;
+            w.qs = nqs;
+            P.nd[V.node].h = w;
         }
         moved = min(moved, half_min_i32(in && bsel != V.off ? d : 0x7fffffff));
     }
+    const int n_wide = hb ? n_wide_hi : n_wide_lo, n_big = hb ? n_big_hi : n_big_lo;
     if (!done && hl == 0) {
         H->sims_done = h_sims + 1;
         H->noise_pending = 0;
@@ -2220,6 +2395,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         H->depth_max = max(H->depth_max, depth);
         H->depth_sum += depth;
         H->resume = min(moved, max(depth - 1, 0));
+        H->sims_backed += 1;
+        if (n_wide) H->exact_wide += n_wide;
+        if (n_big) H->big_moves += n_big;
     }
 }
 
@@ -2245,7 +2423,7 @@ __global__ __launch_bounds__(THREADS) void k_pick_best(Pools P, SearchCfg C, int
         if (l == 0) action[t] = (int16_t)(int)(u * (double)SPL_ACTIONS);
         return;
     }
-    const NodeRun r = P.nrun[root];
+    const NodeRun r = run_of(P.nd[root].c);
     const int sims = H->budget;
     const bool forced = H->forced;
     auto count = [&](int i, float &p, int &a) {
@@ -2303,7 +2481,7 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
     if (root < 0) return;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const NodeRun r = P.nrun[root];
+    const NodeRun r = run_of(P.nd[root].c);
     int best = 0;
     for (int i = l; i < r.ec; i += 64) {
         const EdgeP e = *P.ep(r.eb + i);
@@ -2335,7 +2513,7 @@ __global__ __launch_bounds__(THREADS) void k_root_stats(Pools P, SearchCfg C, in
         if (probs) probs[(size_t)t * SPL_ACTIONS + e.a] = (double)c / (double)tot;
     }
     if (q && l == 0) {
-        const double q0 = P.nst[root].qs;
+        const double q0 = P.nd[root].h.qs;
         q[(size_t)t * n] = q0;
         for (int i = 1; i < n; i++) q[(size_t)t * n + i] = -q0 / (double)(n - 1);
     }
@@ -2352,7 +2530,7 @@ __global__ __launch_bounds__(THREADS) void k_root_priors(Pools P, int B, float *
     if (root < 0) return;
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    const NodeRun r = P.nrun[root];
+    const NodeRun r = run_of(P.nd[root].c);
     for (int i = l; i < r.ec; i += 64) {
         const EdgeP e = *P.ep(r.eb + i);
         o[e.a] = e.p;
@@ -2386,18 +2564,15 @@ __global__ __launch_bounds__(64) void k_tree_sizes(Pools P, int B, int32_t *out)
     const int l = lane_id();
     const TreeHdr *H = P.hdr + t;
     const int nc = H->node_count, root = H->root;
-    const int rr = root >= 0 ? P.nround[root] : 1 << 30;
+    const int rr = root >= 0 ? P.nd[root].h.round : 1 << 30;
     int ln = 0, le = 0;
     for (int i = l; i < nc; i += 64) {
         const int g = node_g(P, t, i);
-        if (g == root || P.nround[g] > rr) {
+        const Node nd = P.nd[g];
+        if (g == root || nd.h.round > rr) {
             ln++;
-            if (!P.nterm[g]) {
-                const NodeRun r = P.nrun[g];
-                le += r.ec + REC_UNITS * r.vcnt;         // (content: block slack depends on the
-                                                         //  collection history)
-            }
-        }
+            if (!nd.h.term) le += nd.c.ec + REC_UNITS * nd.c.vcnt();   // (content: block slack depends
+        }                                                           //  on the collection history)
     }
     for (int o = 32; o > 0; o >>= 1) { ln += __shfl_xor(ln, o, 64); le += __shfl_xor(le, o, 64); }
     if (l == 0) {
@@ -2517,8 +2692,8 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     const int gcw = B < GC_WG ? B : GC_WG;
     size_t bytes = 0;
     auto acc = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
-    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn); acc(4 * nn);
-    acc(sizeof(NodeStat) * nn); acc(sizeof(NodeRun) * nn); acc(nn); acc(8 * ne);
+    acc(sizeof(TreeHdr) * B); acc(8 * nn); acc(8 * nn);
+    acc(sizeof(Node) * nn); acc(8 * ne);
     acc(4 * (size_t)B * L.nptab); acc(4 * (size_t)B * L.eptab); acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages);
     acc(4 * (size_t)L.npages); acc(4 * (size_t)L.epages); acc(64);
     acc(4 * (size_t)B * L.hcap); acc(4 * (size_t)B * (L.pcap + 1)); acc(4 * (size_t)B * L.pcap); acc(8 * (size_t)B * L.pcap);
@@ -2543,6 +2718,21 @@ static bool valid_cfg(const spl_ctx *ctx, int B, const spl_mcts_config *cfg) {
     return cfg->node_cap <= (1 << 24) && cfg->edge_cap <= (1 << 28) && pn + NPG < (1LL << 31) &&
            pe / UPG + 1 < (1LL << 31);
 }
+
+#if SELECT_PROBE
+// k_select_lanes phase probes: [0] prologue [1] descents [2] board staging [3] expansions
+// [4] leaf outputs (cycles summed over waves), [5] waves, [6] max wave cycles, [7] total,
+// [8] the deepest lane's levels summed over waves, [9] levels of all lanes, [10] most levels of
+// one lane, [11] expansion rounds summed over waves
+int spl_diag_select_probe(unsigned long long *out16, int reset) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_sel_probe), 16 * 8) != hipSuccess) return SPL_EDEVICE;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sel_probe), z, sizeof(z)) != hipSuccess) return SPL_EDEVICE;
+    }
+    return 0;
+}
+#endif
 
 #if SPL_BOUNDS_CHECK
 // bounds-checked builds only: [0] violations, [1] first value, [2] its site, [3] its tree
@@ -2592,8 +2782,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     char *p = (char *)arena;
     P.hdr = carve<TreeHdr>(p, B);
     P.nkey0 = carve<uint64_t>(p, nn); P.nkey1 = carve<uint64_t>(p, nn);
-    P.nround = carve<int32_t>(p, nn);
-    P.nst = carve<NodeStat>(p, nn); P.nrun = carve<NodeRun>(p, nn); P.nterm = carve<int8_t>(p, nn);
+    P.nd = carve<Node>(p, nn);
     P.eu = carve<uint64_t>(p, ne);                                   // EdgeP runs, VisitRec blocks
     P.ntab = carve<int32_t>(p, (size_t)B * P.nptab); P.etab = carve<int32_t>(p, (size_t)B * P.eptab);
     P.npidx = carve<int32_t>(p, (size_t)P.npages); P.epidx = carve<int32_t>(p, (size_t)P.epages);

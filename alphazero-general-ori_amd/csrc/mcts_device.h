@@ -42,7 +42,10 @@ struct TreeHdr {
     int32_t depth_max, depth_sum;        // leaf depths of the simulations backed up: maximum, sum
     int32_t resume;                      // the next descent's first new level (k_backup: the first
                                          // path level whose cached pick moved, else the leaf's parent)
-    int32_t pad1, pad2, pad3;
+    // search-path coverage counters (cumulative; tests assert the large-budget paths ran):
+    // simulations backed up, non-root levels with more than BK_WIDE visit records evaluated
+    // exactly, visit blocks relocated to a capacity of at least 128 records
+    int32_t sims_backed, exact_wide, big_moves;
 };
 static_assert(sizeof(TreeHdr) == 208, "TreeHdr layout (splendor/mcts.py HDR_DTYPE)");
 // gc_state: 0 none; 1 a leaf did not fit mid-search (withdrawn, k_gc collects, the descent
@@ -79,40 +82,84 @@ struct VisitRec {
 static_assert(sizeof(VisitRec) == 24, "VisitRec layout");
 constexpr int REC_UNITS = 3;
 
-// a node's allocation: its run and visit block (global unit indices), or, for a terminal
-// node, its end values (the first 16 bytes hold es[4])
-struct NodeRun {
-    int64_t eb;      // run base
-    int64_t vb;      // visit block base
-    int16_t ec;      // edges (legal actions; 0: terminal)
-    int16_t vcnt;    // visit records in use
-    int16_t vcap;    // visit block capacity (records)
-    int16_t cand;    // lowest rank without a visit record (ec: none) = the best unvisited edge
-};
-static_assert(sizeof(NodeRun) == 24, "NodeRun layout");
-
-// a node's visit statistics (Ns, Qs) and its cached arg-max, one 32-byte record.
+// A node is one 64-byte record (round 5; round 4 kept a 32-byte NodeStat, a 24-byte NodeRun, a
+// round and a terminal flag in four arrays: three to four lines per path level for k_backup).
 // pick_highest_UCB (MCTS.py:199-219) at a non-root node reads only that node's Ns, Qs and its
 // edges' P, N, Q; all of them change only when a simulation backs up through the node (priors
 // change only at a root: Dirichlet noise, :150-154; forced playouts are root-only, :157). So the
 // arg-max k_backup computes right after a node's update is exactly the edge the next descent
-// through the node picks: the descent follows `best` and its link (one 32-byte load per level,
-// no edge scan). The root level scans when its priors were just noised or forced playouts are
-// on. Invariant (k_backup, k_select's links, k_gc's remap): bchild is the child of edge `best`
-// (-1: not linked), bterm whether that child is terminal.
-struct __align__(16) NodeStat {
-    double qs;       // Qs
-    int32_t ns;      // Ns
-    int16_t best;    // cached arg-max: rank of the edge in the run (-1: unknown, scan)
-    int16_t ba;      // its action
-    int32_t bchild;  // its child (global id, -1: not linked)
-    int32_t bterm;   // 1: that child is terminal (its values in nrun)
-    int16_t bvi;     // the visit record of edge `best` (-1: none yet), so k_backup finds the
-                     // path edge's record without loading its EdgeP
-    int16_t pad1;
-    int32_t pad2;
+// through the node picks: the descent follows `best` and its link (one load of the record's first
+// half per level, no edge scan). The root level scans when its priors were just noised or forced
+// playouts are on. Invariant (k_backup, k_select's links, k_gc's remap): bchild is the child of
+// edge `best` (-1: not linked), bterm whether that child is terminal.
+// Descent hints: h2 / h3 name the cached pick's child of bchild and of h2 as the last backup
+// through the node saw them; they may be stale (a transposition's other parent changed them, a
+// collection moved nodes), so the descent loads bchild, h2 and h3 together and uses a hinted
+// record only when the authoritative link of the level above names it: up to three levels per
+// round trip on the dependent chain.
+struct NodeHot {             // first half: the descent reads its first 16 bytes per level
+    int32_t bchild;          // cached arg-max's child (global id, -1: not linked)
+    int32_t h2, h3;          // hints (-1: none)
+    int16_t best;            // cached arg-max: rank of the edge in the run (-1: unknown, scan)
+    uint16_t babt;           // its action | (1: that child is terminal) << 15
+    int32_t ns;              // Ns
+    uint8_t term;            // 1: this node is terminal (end values in NodeCold's first 16 bytes)
+    uint8_t round;           // the node's round counter (GC: rounds <= the root's are garbage)
+    int16_t bvi;             // the visit record of edge `best` (-1: none yet), so k_backup finds the
+                             // path edge's record without loading its EdgeP
+    double qs;               // Qs
+    __device__ __forceinline__ int ba() const { return babt & 0x7FFF; }
+    __device__ __forceinline__ int bterm() const { return babt >> 15; }
+    __device__ __forceinline__ void set_pick(int rank, int a, int term_child) {
+        best = (int16_t)rank;
+        babt = (uint16_t)(a | (term_child << 15));
+    }
 };
-static_assert(sizeof(NodeStat) == 32, "NodeStat layout");
+// the descent's view of a record (NodeHot's first 16 bytes: one dwordx4 load)
+struct __align__(16) NodeLink {
+    int32_t bchild, h2, h3;
+    int16_t best;
+    uint16_t babt;
+    __device__ __forceinline__ int ba() const { return babt & 0x7FFF; }
+    __device__ __forceinline__ int bterm() const { return babt >> 15; }
+};
+constexpr uint64_t LOW48 = (1ull << 48) - 1;
+struct NodeCold {            // second half: the run / visit block, the best unvisited edge
+    uint64_t ebq;            // run base (global unit, 48 bits) | visit-block capacity << 48
+    uint64_t vbq;            // visit-block base | visit records in use << 48
+    int16_t ec;              // edges (legal actions; 0: terminal)
+    int16_t cand;            // lowest rank without a visit record (ec: none) = the best unvisited edge
+    int16_t ca;              // its action
+    int16_t pad;
+    float cp;                // its prior
+    float np;                // an upper bound on the priors below cp of the unvisited edges after
+                             // cand (-1: none; 0 when cp is 0): the float32 screen's bound on every
+                             // other unvisited edge (equal priors tie cand and lose on the action)
+    __device__ __forceinline__ int64_t eb() const { return (int64_t)(ebq & LOW48); }
+    __device__ __forceinline__ int64_t vb() const { return (int64_t)(vbq & LOW48); }
+    __device__ __forceinline__ int vcap() const { return (int)(ebq >> 48); }
+    __device__ __forceinline__ int vcnt() const { return (int)(vbq >> 48); }
+    __device__ __forceinline__ void set_eb(int64_t eb, int vcap) { ebq = (uint64_t)eb | ((uint64_t)vcap << 48); }
+    __device__ __forceinline__ void set_vb(int64_t vb, int vcnt) { vbq = (uint64_t)vb | ((uint64_t)vcnt << 48); }
+};
+struct __align__(64) Node {
+    NodeHot h;
+    NodeCold c;
+};
+static_assert(sizeof(NodeHot) == 32 && sizeof(NodeCold) == 32 && sizeof(Node) == 64 && sizeof(NodeLink) == 16,
+              "Node layout");
+__device__ __forceinline__ NodeLink link_of(const Node *nd, int g) {
+    return *reinterpret_cast<const NodeLink *>(&nd[g].h);
+}
+
+// a node's run / visit block in registers (the packed NodeCold unpacked)
+struct NodeRun {
+    int64_t eb, vb;
+    int16_t ec, vcnt, vcap, cand;
+};
+__device__ __forceinline__ NodeRun run_of(const NodeCold &c) {
+    return NodeRun{c.eb(), c.vb(), c.ec, (int16_t)c.vcnt(), (int16_t)c.vcap(), c.cand};
+}
 
 // Per-GPU shared arena. Nodes and edge units live in pools shared by all trees
 // and are handed out in pages: node page = NPG consecutive global node ids, edge page = UPG
@@ -135,11 +182,8 @@ struct Pools {
     int nptab, eptab;                    // page-table entries per tree (nmax / NPG, emax / UPG)
     int npages, epages;                  // pages in the pools
     TreeHdr *hdr;
-    uint64_t *nkey0, *nkey1;             // node pool, indexed by global node id
-    int32_t *nround;
-    NodeStat *nst;                       // statistics + cached arg-max of every node
-    NodeRun *nrun;                       // its run / visit block (terminal: end values)
-    int8_t *nterm;
+    uint64_t *nkey0, *nkey1;             // node pool, indexed by global node id: fingerprints
+    Node *nd;                            // the nodes' records
     uint64_t *eu;                        // edge unit pool (EdgeP runs, VisitRec blocks)
     int32_t *ntab, *etab;                // B x nptab / B x eptab page tables
     int32_t *npidx, *epidx;              // per page: its index in the owning tree's page table

@@ -4,67 +4,62 @@
 //
 // One 512-thread workgroup (8 waves, two per SIMD so one wave's LDS / L2 latency hides
 // behind the other's MFMAs) evaluates ML = 32 leaves through all 13 dense layers with every
-// activation on chip:
-//   * GEMMs on f32 MFMA (exact f32 products, f32 accumulation: the reference network's
-//     precision). Per-column layers: v_mfma_f32_32x32x2_f32, wave w owns output columns
-//     [32(w&3), 32(w&3)+32) for half of the token tiles (w>>2). Per-leaf layers:
-//     v_mfma_f32_16x16x4_f32, wave w owns 16-column tile w for both 16-leaf row tiles.
-//   * The per-board-column layers (dense2d_1, dense2d_3, partialgpool_1) treat the 7 board
-//     columns of the 32 leaves as 7 token tiles of 32 (channel-major), so the per-column
-//     BatchNorm affine is uniform across an MFMA tile.
-//   * K is split across the MFMA's lane groups (32x32x2: lane half h feeds k = s + h*S;
-//     16x16x4: lane quarter g feeds k = s + g*S), so a lane's A operand for 4 steps is one
-//     ds_read_b128 and its B operand one coalesced global float4 from the pre-packed
-//     weights (pack order in splendor_amd.h, spl_nn_forward).
-//   * Activations live in LDS with a 132-float row stride (= 4 mod 64 dwords: the 16 lanes
-//     of a ds_read_b128 group hit distinct 16-byte bank slots).
+// activation on chip. f32 arithmetic, the reference network's precision, on bf16 MFMAs: every
+// f32 operand is split exactly into three bf16 parts (x = hi + mid + lo by truncation) and
+// x y is the sum of six part products (all but the three smallest, < 2^-22 |x y| together),
+// the largest in an f32 accumulator of its own. gfx950 has no xf32 and its f32 MFMA runs at
+// 1/16 of the bf16 rate, so six bf16 products cost 3/8 of one f32 product's MFMA time.
+//   * Per-column layers (dense2d_1, its second linear, partialgpool_1, dense2d_3; round 4)
+//     on v_mfma_f32_32x32x16_bf16: the 7 board columns of the 32 leaves as 7 token tiles of
+//     32 (channel-major, so the per-column BatchNorm affine is uniform across a tile); wave w
+//     owns output columns [32(w&3), 32(w&3)+32) for half of the token tiles (w>>2); the
+//     activations (f32 LDS rows, 132-float stride) are split in registers.
+//   * Per-leaf layers (round 5) on v_mfma_f32_16x16x32_bf16 over 16-leaf row tiles. Their
+//     activations live in LDS ALREADY SPLIT: each producing epilogue writes its outputs as
+//     three bf16 planes (SplitAct), split once instead of once per consuming wave (8 waves
+//     read every input). dense1d_4's input, the 704-feature flattened image, is too large
+//     for three planes: it stays f32 and each wave splits the one row tile it needs (two
+//     column tiles per wave, half the splitting of one column tile over both row tiles).
+//   * Weights: every layer's parts split and packed once on the host in MFMA B-fragment order
+//     (spl_nn_forward in splendor_amd.h), each lane's B operand one coalesced 16-byte load,
+//     prefetched a chunk ahead in a register ring; the next layer's ring is issued behind the
+//     last MFMA of the current one; barriers wait for LDS only.
 #include <hip/hip_runtime.h>
 
 #include "../../include/splendor_amd.h"
 
-#ifndef NN_TIMING
-#define NN_TIMING 0        // diagnostic builds only (tools/time_nn.hip): per-layer cycle probes
-#endif
-#if NN_TIMING
-__shared__ uint64_t nn_probe_acc[16];
-__shared__ uint64_t nn_probe_last;
-__device__ unsigned long long g_nn_timing[16];
-#define NN_PROBE(k)                                                                        \
-    if (threadIdx.x == 0) {                                                                \
-        const uint64_t c_ = clock64();                                                     \
-        nn_probe_acc[k] += c_ - nn_probe_last;                                             \
-        nn_probe_last = c_;                                                                \
-    }
-#else
-#define NN_PROBE(k)
-#endif
-
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef NN_PF1
-#define NN_PF1 4               // weight-prefetch depth (k steps) of the per-leaf GEMMs
-#endif
 constexpr int NNT = 512;      // threads per workgroup (8 waves)
 constexpr int ML = 32;         // leaves per workgroup
-constexpr int XS = 132;        // activation row stride (floats)
+constexpr int XS = 132;        // per-column activation row stride (floats)
 constexpr int LS = 420;        // logits row stride (floats)
-// per-leaf operands are read by ds_read_b128 with lane l on row l & 15 and k group l >> 4
-// 4 floats apart: with rows 8 banks apart, the groups {0-3,12-15,20-27}, ... that share an
-// LDS cycle land on disjoint banks (MI355X_MICROARCH.md §LDS)
-constexpr int PS = 136;        // per-leaf activation row stride (floats)
-constexpr int ZS = 712;        // flattened trunk row stride (704 features)
-static_assert(ML * ZS <= 7 * ML * XS && ML * (PS + LS) <= 7 * ML * XS, "bufA overlays");
-static_assert(2 * 64 * ML <= ML * PS, "dense2d_3 pool partials fit bufP");
+constexpr int ZS = 712;        // flattened trunk row stride (704 features; 8 mod 64 dwords)
 constexpr int ACT = 409;
+// split per-leaf activations: three bf16 planes of ML rows, row stride SS bf16 (72 dwords = 8
+// mod 64: the 16 rows x 4 k groups of a 16x16x32 operand read, ds_read_b128, spread over the
+// banks); columns [128, 144) hold zeros (the pool layers read k = 16 .. 143 against 0 weights)
+constexpr int SS = 144;
+struct SplitAct {
+    uint16_t p[3][ML][SS];
+};
+constexpr int SAB = (int)sizeof(SplitAct);                 // 27,648 bytes
+// bufA (bytes) holds the per-column activations (7 x ML x XS floats), then the flattened trunk
+// Z, then — once dense1d_4 has read Z — split buffers SB1 [0, SAB), SB2 [SAB, 2 SAB) and the
+// logits from 2 SAB on; SB0 has its own array (dense2d_3's pool partials before dense1d_4)
+constexpr int BUFA = 7 * ML * XS * 4;
+static_assert(ML * ZS * 4 <= BUFA && 2 * SAB + ML * LS * 4 <= BUFA, "bufA overlays");
+static_assert(2 * 64 * ML * 4 <= SAB, "dense2d_3 pool partials fit SB0");
 
 __host__ __device__ constexpr int kpad(int K) { return (K + 7) / 8 * 8; }
 __host__ __device__ constexpr int ntiles(int N) { return (N + 31) / 32; }
 __host__ __device__ constexpr int ntiles16(int N) { return (N + 15) / 16; }
-// packed floats of a layer: the 4 per-column layers use 32x32x2 B fragments (32-column
-// tiles, K in 2 halves), the 9 per-leaf layers 16x16x4 B fragments (16-column tiles, K in
-// 4 quarters); see splendor_amd.h spl_nn_forward
+// f32 copy of every layer (kept in the packed layout: the biases are read from it, the host
+// reference and older builds read the rest): the 4 per-column layers in 32x32x2 B fragments,
+// the 9 per-leaf layers in 16x16x4 B fragments
 __host__ __device__ constexpr bool f16(int l) { return l >= 4; }
 __host__ __device__ constexpr int colpad(int l, int N) { return f16(l) ? ntiles16(N) * 16 : ntiles(N) * 32; }
 __host__ __device__ constexpr int wfloats(int l, int N, int K) { return colpad(l, N) * kpad(K); }
@@ -72,10 +67,15 @@ __host__ __device__ constexpr int wfloats(int l, int N, int K) { return colpad(l
 // W[32 nt + l % 32][16 c + 8 (l / 32) + j]), as floats
 __host__ __device__ constexpr int kp16(int K) { return (K + 15) / 16 * 16; }
 __host__ __device__ constexpr int sfloats(int K) { return 4 * (kp16(K) / 16) * 3 * 64 * 8 / 2; }
+// the split copy of a per-leaf layer: [NT16][Kp32/32][3][64][8] bf16 (parts of
+// W[16 nt + l % 16][32 c + 8 (l / 16) + j]), as floats
+__host__ __device__ constexpr int kp32(int K) { return (K + 31) / 32 * 32; }
+__host__ __device__ constexpr int lfloats(int N, int K) { return ntiles16(N) * (kp32(K) / 32) * 3 * 64 * 8 / 2; }
 
 // layer order of the packed weights: dense2d_1, dense2d_1[3], partialgpool_1 dense,
 // dense2d_3, dense1d_4, partialgpool_4 dense, dense1d_5[0], dense1d_5[3], partialgpool_5
-// dense, PI[0], PI[1], V[0], V[1]; then the per-column BN affines s1, t1, sp1, tp1 (7 each)
+// dense, PI[0], PI[1], V[0], V[1]; then the per-column BN affines s1, t1, sp1, tp1 (7 each);
+// then (16-byte aligned) the split copies of all 13 layers
 template <int NP>
 struct Net {
     static constexpr int R = 32 + 10 * NP + NP * NP;
@@ -89,14 +89,13 @@ struct Net {
     }
     static constexpr int boff(int l) { return woff(l) + wfloats(l, Ns[l], Ks[l]); }
     static constexpr int AFF = woff(NL);
-    // bf16 x 3 copies of the 4 per-column layers (NN_SPLIT), 16-byte aligned after the affines
     static constexpr int SBASE = (AFF + 28 + 3) / 4 * 4;
     static constexpr int soff(int l) {
         int o = SBASE;
-        for (int j = 0; j < l; j++) o += sfloats(Ks[j]);
+        for (int j = 0; j < l; j++) o += j < 4 ? sfloats(Ks[j]) : lfloats(Ns[j], Ks[j]);
         return o;
     }
-    static constexpr int TOTAL = soff(4);
+    static constexpr int TOTAL = soff(NL);
     static constexpr int X0S = (kpad(R) / 4) % 2 ? kpad(R) : kpad(R) + 4;   // int8 input stride (odd dwords)
 };
 
@@ -107,76 +106,22 @@ __device__ __forceinline__ f32x16 zero16() {
     return z;
 }
 
-[[maybe_unused]] __device__ __forceinline__ void mfma4(const float4 &a, const float4 &b, f32x16 &acc) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
-}
-
 template <int V> struct IntC {
     static constexpr int value = V;
 };
 
-// weight-fragment ring of the per-column GEMMs (a k-step is 4 T MFMAs of 64 cycles)
-constexpr int PFC = 2;
-typedef float4 RingC[PFC];
-
-// first PFC k-steps of column block nt of a per-column layer (K = 2S) into the ring
-template <int S>
-__device__ __forceinline__ void ringc_load(const float *__restrict__ wp, int nt, RingC &bq) {
-    const float4 *w4 = reinterpret_cast<const float4 *>(wp) + (size_t)nt * (S / 4) * 64 + (threadIdx.x & 63);
-#pragma unroll
-    for (int p = 0; p < PFC; p++) bq[p] = w4[(p < S / 4 ? p : S / 4 - 1) * 64];
-}
-
-// token tiles t0 .. t0+T-1 x one N tile (column block nt) over K = 2S; bq holds the first
-// PFC steps (ringc_load); afetch(t, col) -> float4 of A[token tile t][lane row][col..col+3];
-// next() runs after the last MFMA is issued. Unrolled and branch-free like gemm16.
-template <int T, int S, class AF, class NX>
-__device__ __forceinline__ void gemm_tiles(const float *__restrict__ wp, int nt, int t0, RingC &bq, AF afetch,
-                                           f32x16 *acc, NX next) {
-    constexpr int Q = S / 4;
-    const int lane = threadIdx.x & 63, h = lane >> 5;
-    const float4 *w4 = reinterpret_cast<const float4 *>(wp) + (size_t)nt * Q * 64 + lane;
-#pragma unroll
-    for (int t = 0; t < T; t++) acc[t] = zero16();
-    float4 a[T];
-#pragma unroll
-    for (int t = 0; t < T; t++) a[t] = afetch(t0 + t, h * S);
-#pragma unroll
-    for (int q = 0; q < Q; q++) {
-        float4 x[T];
-#pragma unroll
-        for (int t = 0; t < T; t++) x[t] = a[t];
-        if (q + 1 < Q)
-#pragma unroll
-            for (int t = 0; t < T; t++) a[t] = afetch(t0 + t, h * S + 4 * (q + 1));
-        const float4 b = bq[q % PFC];
-        if (q + PFC < Q) bq[q % PFC] = w4[(q + PFC) * 64];
-#pragma unroll
-        for (int t = 0; t < T; t++) mfma4(x[t], b, acc[t]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    next();
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-
-#ifndef NN_SPLIT
-#define NN_SPLIT 1      // per-column layers on bf16 MFMAs with operands split in three parts (0: f32 MFMA)
-#endif
-// Split per-column GEMMs (NN_SPLIT): an f32 x is exactly hi + mid + lo, three bf16 parts
-// taken by truncation (hi: the top 8 significant bits, mid: the top 8 of the residual, lo: the
-// rest, at most 8 significant bits), and x y = Σ over the parts' products minus the three
-// smallest (mid lo, lo mid, lo lo: < 2^-22 |x y| together, ~2^-24 typically). v_mfma_f32_32x32x16_bf16 takes 16 k per instruction at 16 times the f32
-// MFMA's rate, so the six products of a 16-k chunk cost 6 x 32 cycles against 8 x 64 for
-// v_mfma_f32_32x32x2_f32. Each bf16 product is exact in f32; hi hi goes into the layer's
-// accumulator and the five smaller products into a second one (added in the epilogue), so
-// the large accumulator rounds once per MFMA (16 k) instead of once per k, and the small one's
-// roundings are ~2^-8 smaller: measured against float64 the split layer's error is below the
-// f32 MFMA's (tools/nn_split_probe.hip). The int8 boards of dense2d_1 are exact
-// in bf16: three products (the weight's parts) into one accumulator.
+// Split per-column GEMMs: an f32 x is exactly hi + mid + lo, three bf16 parts taken by
+// truncation (hi: the top 8 significant bits, mid: the top 8 of the residual, lo: the rest, at
+// most 8 significant bits), and x y = the sum over the parts' products minus the three smallest
+// (mid lo, lo mid, lo lo: < 2^-22 |x y| together, ~2^-24 typically). v_mfma_f32_32x32x16_bf16
+// takes 16 k per instruction at 16 times the f32 MFMA's rate, so the six products of a 16-k chunk
+// cost 6 x 32 cycles against 8 x 64 for v_mfma_f32_32x32x2_f32. Each bf16 product is exact in
+// f32; hi hi goes into the layer's accumulator and the five smaller products into a second one
+// (added in the epilogue), so the large accumulator rounds once per MFMA (16 k) instead of once
+// per k, and the small one's roundings are ~2^-8 smaller: measured against float64 the split
+// layer's error is below the f32 MFMA's (tools/nn_split_probe.hip). The int8
+// boards of dense2d_1 are exact in bf16: three products (the weight's parts) into one
+// accumulator.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef NN_PFS
@@ -190,7 +135,7 @@ struct F8 {
     float4 lo, hi;                     // 8 consecutive k of one lane's A row
 };
 
-[[maybe_unused]] __device__ __forceinline__ void split8(const F8 &x, bf16x8 &hi, bf16x8 &mid, bf16x8 &lo) {
+__device__ __forceinline__ void split8(const F8 &x, bf16x8 &hi, bf16x8 &mid, bf16x8 &lo) {
     const float xs[8] = {x.lo.x, x.lo.y, x.lo.z, x.lo.w, x.hi.x, x.hi.y, x.hi.z, x.hi.w};
     uint32_t h[8], m[8], l[8];
 #pragma unroll
@@ -212,7 +157,7 @@ struct F8 {
     lo = __builtin_bit_cast(bf16x8, L);
 }
 // 8 int8 (two dwords) -> 8 bf16, exact
-[[maybe_unused]] __device__ __forceinline__ bf16x8 i8_to_bf16x8(int v0, int v1) {
+__device__ __forceinline__ bf16x8 i8_to_bf16x8(int v0, int v1) {
     u32x4 r;
 #pragma unroll
     for (int p = 0; p < 4; p++) {
@@ -287,95 +232,112 @@ __device__ __forceinline__ void gemm_split(const float *__restrict__ ws, int nt,
 }
 
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// both row tiles against one B fragment, alternating accumulators: a 16x16x4 f32 MFMA
-// issues every 32 cycles but its result is ready for a dependent one only after 40
-// (MI355X_MICROARCH.md, cycle constants)
-__device__ __forceinline__ void mfma4_16x2(const float4 &a0, const float4 &a1, const float4 &b, f32x4 &c0,
-                                          f32x4 &c1) {
-    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b.x, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b.x, c1, 0, 0, 0);
-    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b.y, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b.y, c1, 0, 0, 0);
-    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b.z, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b.z, c1, 0, 0, 0);
-    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b.w, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b.w, c1, 0, 0, 0);
-}
-
 // workgroup barrier for LDS traffic only: waits for this wave's LDS operations, not for its
 // global loads, so weight fragments prefetched for the next layer stay in flight across it
 // (__syncthreads() waits vmcnt(0) first); the memory clobber keeps the compiler from moving
 // LDS accesses across it
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// weight-fragment ring of the per-leaf GEMMs: PF16 k-steps x up to 4 column tiles
-constexpr int PF16 = NN_PF1;
-typedef float4 Ring16[PF16][4];
 
+// ------------------------------------------------------------ per-leaf layers
+// one f32 into the three planes of a SplitAct (the truncation of split8 and of the host's
+// _bf16_parts: hi + mid + lo == x exactly)
+__device__ __forceinline__ void put_split(SplitAct *d, int row, int col, float x) {
+    const uint32_t h = __float_as_uint(x) & 0xFFFF0000u;
+    const float r1 = x - __uint_as_float(h);
+    const uint32_t m = __float_as_uint(r1) & 0xFFFF0000u;
+    const float r2 = r1 - __uint_as_float(m);
+    d->p[0][row][col] = (uint16_t)(h >> 16);
+    d->p[1][row][col] = (uint16_t)(m >> 16);
+    d->p[2][row][col] = (uint16_t)(__float_as_uint(r2) >> 16);
+}
+// ... and back, exactly (mid + lo, then + hi, as the split took them apart)
+__device__ __forceinline__ float get_split(const SplitAct *s, int row, int col) {
+    const float h = __uint_as_float((uint32_t)s->p[0][row][col] << 16);
+    const float m = __uint_as_float((uint32_t)s->p[1][row][col] << 16);
+    const float l = __uint_as_float((uint32_t)s->p[2][row][col] << 16);
+    return h + (m + l);
+}
+
+// weight-part ring of a per-leaf GEMM: PF chunks (32 k) x NC column tiles x 3 parts
+template <int NC, int PF>
+struct RingL {
+    static constexpr int P = PF;
+    bf16x8 b[PF][NC][3];
+};
 // column tile j of a per-leaf layer: tile min(c0 + j cstep, ctot - 1) (a clamped tile is
 // loaded but never multiplied)
-template <int Q4>
-__device__ __forceinline__ const float4 *tile16(const float *__restrict__ wp, int c0, int cstep, int ctot, int j) {
-    return reinterpret_cast<const float4 *>(wp) + (size_t)min(c0 + j * cstep, ctot - 1) * Q4 * 64 + (threadIdx.x & 63);
+template <int C>
+__device__ __forceinline__ const bf16x8 *tilel(const float *__restrict__ ws, int c0, int cstep, int ctot, int j) {
+    return reinterpret_cast<const bf16x8 *>(ws) + (size_t)min(c0 + j * cstep, ctot - 1) * C * 3 * 64 + (threadIdx.x & 63);
 }
-
-// issue the first PF16 k-steps of a per-leaf layer's weight fragments into the ring; a
-// caller does this right after the previous layer's last MFMA, ahead of its epilogue and
-// barrier, so no layer starts on an L2 round trip
-template <int NC, int Q4>
-__device__ __forceinline__ void ring_load(const float *__restrict__ wp, int c0, int cstep, int ctot, Ring16 &bq) {
+// the first chunks of a per-leaf layer's weight parts into the ring; callers issue this behind
+// the previous layer's last MFMA, ahead of its epilogue and barrier, so no layer starts on an
+// L2 round trip
+template <int C, class RG>
+__device__ __forceinline__ void ringl_load(const float *__restrict__ ws, int c0, int cstep, int ctot, RG &r) {
+    constexpr int NC = sizeof(r.b[0]) / sizeof(r.b[0][0]);
 #pragma unroll
     for (int j = 0; j < NC; j++) {
-        const float4 *w4 = tile16<Q4>(wp, c0, cstep, ctot, j);
+        const bf16x8 *w = tilel<C>(ws, c0, cstep, ctot, j);
 #pragma unroll
-        for (int p = 0; p < PF16; p++) bq[p][j] = w4[(p < Q4 ? p : Q4 - 1) * 64];
+        for (int p = 0; p < RG::P; p++)
+#pragma unroll
+            for (int q = 0; q < 3; q++) r.b[p][j][q] = w[((p < C ? p : C - 1) * 3 + q) * 64];
     }
 }
-
-// per-leaf GEMM on v_mfma_f32_16x16x4_f32: the 32 leaves as 2 row tiles of 16 x NC
-// 16-column tiles {c0, c0 + cstep, ...} (all valid: the caller picks NC for its wave),
-// K = 16 * Q4 (lane group g = lane >> 4 feeds k = 16 q + 4 g + j at step q, MFMA j).
-// bq holds the first PF16 steps (ring_load); afetch(rt, col) -> float4 of
-// A[row tile rt][lane row][col..+3]; next() runs after the last MFMA is issued.
-// The k loop is fully unrolled with no branch in it: a conditional weight load makes the
-// compiler copy the loaded fragment into the ring register under an s_waitcnt vmcnt(0)
-// at once, and every step then pays the whole L2 round trip.
-template <int NC, int Q4, class AF, class NX>
-__device__ __forceinline__ void gemm16(const float *__restrict__ wp, int c0, int cstep, Ring16 &bq, AF afetch,
-                                       f32x4 (*acc)[2], NX next) {
-    // a k-step is only 8 NC MFMAs (~256 NC cycles), shorter than an L2 round trip: the
-    // weight fragments are prefetched PF16 steps ahead, the activations one step ahead
-    constexpr int PF = PF16;
-    const int lane = threadIdx.x & 63, g = lane >> 4;
+// per-leaf GEMM on v_mfma_f32_16x16x32_bf16: RT row tiles of 16 leaves x NC column tiles
+// {c0, c0 + cstep, ...} (NC <= the ring's) over C chunks of 32 k. afetch(t, c, a0, a1, a2):
+// the three parts of this lane's A operand for row tile t (row l % 16 of it, k = 32 c +
+// 8 (l / 16) .. + 7); the ring holds the first chunks (ringl_load); next() runs after the last
+// MFMA is issued. Each (column, row) tile keeps two accumulators, the hi x hi products and
+// the five smaller ones, added at the end. Unrolled and branch-free like gemm_split.
+template <int NC, int RT, int C, class RG, class AF, class NX>
+__device__ __forceinline__ void gemm_leaf(const float *__restrict__ ws, int c0, int cstep, RG &r, AF afetch,
+                                          f32x4 (*acc)[2], NX next) {
+    constexpr int PF = RG::P;
+    const bf16x8 *w[NC];
+#pragma unroll
+    for (int j = 0; j < NC; j++) w[j] = tilel<C>(ws, c0, cstep, 1 << 30, j);
+    f32x4 acl[NC][RT];
 #pragma unroll
     for (int j = 0; j < NC; j++)
 #pragma unroll
-        for (int r = 0; r < 2; r++) acc[j][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const float4 *w4[NC];
-#pragma unroll
-    for (int j = 0; j < NC; j++) w4[j] = tile16<Q4>(wp, c0, cstep, 1 << 30, j);
-    float4 a0 = afetch(0, 4 * g), a1 = afetch(1, 4 * g);
-#pragma unroll
-    for (int q = 0; q < Q4; q++) {
-        const float4 x0 = a0, x1 = a1;
-        if (q + 1 < Q4) {
-            a0 = afetch(0, 4 * g + 16 * (q + 1));
-            a1 = afetch(1, 4 * g + 16 * (q + 1));
+        for (int t = 0; t < RT; t++) {
+            acc[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            acl[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+        bf16x8 a[RT][3];
+#pragma unroll
+        for (int t = 0; t < RT; t++) afetch(t, c, a[t][0], a[t][1], a[t][2]);
 #pragma unroll
         for (int j = 0; j < NC; j++) {
-            const float4 b = bq[q % PF][j];
-            if (q + PF < Q4) bq[q % PF][j] = w4[j][(q + PF) * 64];
-            mfma4_16x2(x0, x1, b, acc[j][0], acc[j][1]);
+            const bf16x8 b0 = r.b[c % PF][j][0], b1 = r.b[c % PF][j][1], b2 = r.b[c % PF][j][2];
+            if (c + PF < C)
+#pragma unroll
+                for (int q = 0; q < 3; q++) r.b[c % PF][j][q] = w[j][((c + PF) * 3 + q) * 64];
+#pragma unroll
+            for (int t = 0; t < RT; t++) {
+                acl[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t][2], b0, acl[j][t], 0, 0, 0);
+                acl[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t][1], b1, acl[j][t], 0, 0, 0);
+                acl[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t][0], b2, acl[j][t], 0, 0, 0);
+                acl[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t][1], b0, acl[j][t], 0, 0, 0);
+                acl[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t][0], b1, acl[j][t], 0, 0, 0);
+                acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t][0], b0, acc[j][t], 0, 0, 0);
+            }
         }
-        // keep each step's loads in its step: left alone, the scheduler sinks them next to
-        // their MFMAs PF steps later (vmcnt(1) waits, the ring gone)
+        // keep each chunk's loads in its chunk: left alone, the scheduler sinks them next to
+        // their MFMAs PF chunks later (vmcnt waits, the ring gone)
         __builtin_amdgcn_sched_barrier(0);
     }
     next();
     __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NC; j++)
+#pragma unroll
+        for (int t = 0; t < RT; t++) acc[j][t] += acl[j][t];
 }
 struct NoNext {
     __device__ void operator()() const {}
@@ -429,17 +391,12 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                                                     const int32_t *__restrict__ count) {
     using Nt = Net<NP>;
     constexpr int R = Nt::R, X0S = Nt::X0S;
-    __shared__ __align__(16) float bufA[7 * ML * XS];      // per-column activations / logits
-    __shared__ __align__(16) float bufP[ML * PS];          // per-leaf ping
-    __shared__ __align__(16) float bufQ[ML * PS];          // per-leaf pong
+    __shared__ __align__(16) float bufA[BUFA / 4];         // per-column activations, Z, SB1, SB2, logits
+    __shared__ __align__(16) SplitAct sb0;                 // per-leaf split activations
     __shared__ uint64_t mskl[ML * 7];                      // legality masks (read at the softmax)
     // wave index in an SGPR: every per-wave choice below is a scalar branch
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, li = lane & 31;
     const int wc = w & 3, wg = w >> 2;                     // column block, wave group
-#if NN_TIMING
-    if (tid < 16) nn_probe_acc[tid] = 0;
-    if (tid == 0) nn_probe_last = clock64();
-#endif
     const int b0 = blockIdx.x * ML;
     const int cnt = count ? __builtin_amdgcn_readfirstlane(*count) : B;
     if (b0 >= cnt) return;
@@ -448,15 +405,9 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const auto rowof = [&](int i) -> size_t { return idx ? (size_t)idx[b0 + i] : (size_t)(b0 + i); };
     const float *aff = W + Nt::AFF;                        // s1, t1, sp1, tp1
     const int t0 = 4 * wg, ntok = wg ? 3 : 4;              // this wave's token tiles (per-column layers)
-#if NN_SPLIT
     constexpr int C1 = kp16(R) / 16;
     RingS rings;                                           // per-column weight parts, one layer ahead
     rings_load<C1>(W + Nt::soff(0), wc, rings);
-#else
-    constexpr int S1 = kpad(R) / 2;
-    RingC ringc;                                           // per-column weight fragments, one layer ahead
-    ringc_load<S1>(W + Nt::woff(0), wc, ringc);
-#endif
 
     // ---- input: x[column c][leaf i][row r] = state[leaf][r][c] as int8 (token c*32+i)
     int8_t *x0 = reinterpret_cast<int8_t *>(bufA);
@@ -498,8 +449,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     f32x16 acc[4];
     const int col = 32 * wc + acc_col();
     // this wave's 4 (group 0) or 3 (group 1) token tiles of column block wc
-#if NN_SPLIT
-    // (s_const: chunks of 16 k; i8_const: A is the int8 input)
+    // (c_const: chunks of 16 k; i8_const: A is the int8 input)
     auto gemm_cols = [&](auto c_const, auto i8_const, const float *ws, auto afetch, auto next) {
         constexpr int C = decltype(c_const)::value;
         constexpr bool I8 = decltype(i8_const)::value != 0;
@@ -514,15 +464,6 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             return F8{ld4(p), ld4(p + 4)};
         };
     };
-#else
-    auto gemm_col = [&](auto s_const, const float *wp, auto afetch, auto next) {
-        constexpr int S = decltype(s_const)::value;
-        if (wg == 0)
-            gemm_tiles<4, S>(wp, wc, 0, ringc, afetch, acc, next);
-        else
-            gemm_tiles<3, S>(wp, wc, 4, ringc, afetch, acc, next);
-    };
-#endif
     // per-column epilogue over this wave's token tiles: dst = f(acc, t, n)
     auto store_tiles = [&](int coloff, auto f) {
 #pragma unroll
@@ -532,55 +473,32 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 for (int r = 0; r < 16; r++)
                     bufA[((t0 + t) * ML + acc_row(r)) * XS + coloff] = f(acc[t][r], t0 + t);
     };
-#if !NN_SPLIT
-    auto fetchA = [&](int col0) {
-        return [&, col0](int t, int c) { return ld4(bufA + (t * ML + li) * XS + col0 + c); };
-    };
-#endif
-    NN_PROBE(0)
     // ---- dense2d_1: relu(s1[c] * (W1 x + b1) + t1[c])
     // (each layer's bias is read before its GEMM, ahead of the next layer's ring: vmcnt
     // retires loads in order)
     {
         const float bias = W[Nt::boff(0) + col];
-#if NN_SPLIT
         // (k past R reads zero padding or the next row's bytes: their weights are 0)
         gemm_cols(IntC<C1>(), IntC<1>(), W + Nt::soff(0), [&](int t, int c) {
             const int32_t *p = reinterpret_cast<const int32_t *>(x0 + (t * ML + li) * X0S + c);
             return i8_to_bf16x8(p[0], p[1]);
         }, [&] { rings_load<8>(W + Nt::soff(1), wc, rings); });
-#else
-        gemm_col(IntC<S1>(), W + Nt::woff(0), [&](int t, int c) {
-            const int v = *reinterpret_cast<const int32_t *>(x0 + (t * ML + li) * X0S + c);
-            return make_float4((float)(int8_t)v, (float)(int8_t)(v >> 8), (float)(int8_t)(v >> 16), (float)(v >> 24));
-        }, [&] { ringc_load<64>(W + Nt::woff(1), wc, ringc); });
-#endif
         lds_barrier();
         store_tiles(col, [&](float x, int t) { return fmaxf((x + bias) * aff[t] + aff[7 + t], 0.f); });
         lds_barrier();
     }
-    NN_PROBE(1)
     // ---- dense2d_1[3]: relu(W2 x + b2)
     {
         const float bias = W[Nt::boff(1) + col];
-#if NN_SPLIT
         gemm_cols(IntC<8>(), IntC<0>(), W + Nt::soff(1), fetchA8(0), [&] { rings_load<6>(W + Nt::soff(2), wc, rings); });
-#else
-        gemm_col(IntC<64>(), W + Nt::woff(1), fetchA(0), [&] { ringc_load<48>(W + Nt::woff(2), wc, ringc); });
-#endif
         lds_barrier();
         store_tiles(col, [&](float x, int) { return fmaxf(x + bias, 0.f); });
         lds_barrier();
     }
-    NN_PROBE(2)
     // ---- partialgpool_1: [max, mean over 4 groups of 8 of x[0:32]] ++ relu(BN(Wp1 x[32:] + bp1))
     {
         const float bias = W[Nt::boff(2) + col];  // 0-padded to 128 columns
-#if NN_SPLIT
         gemm_cols(IntC<6>(), IntC<0>(), W + Nt::soff(2), fetchA8(32), [&] { rings_load<8>(W + Nt::soff(3), wc, rings); });
-#else
-        gemm_col(IntC<48>(), W + Nt::woff(2), fetchA(32), [&] { ringc_load<64>(W + Nt::woff(3), wc, ringc); });
-#endif
         constexpr int NQ = (7 * ML * 8 + NNT - 1) / NNT;
         float pv[NQ];
 #pragma unroll
@@ -605,19 +523,22 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             store_tiles(8 + col, [&](float x, int t) { return fmaxf((x + bias) * aff[14 + t] + aff[21 + t], 0.f); });
         lds_barrier();
     }
-    NN_PROBE(3)
     // ---- dense2d_3: relu(W3 x + b3), written straight into the flattened per-leaf image
     // Z[leaf][704] = [max_c<5 x[c][:64]][mean_c<5 x[c][:64]][x[5][:64]][x[6][:64]][x[c][64:], c<7]
     // (FlattenAndPartialGPool(64, 5)), so dense1d_4 reads plain rows
     float *Z = bufA;
-    Ring16 ring;                           // per-leaf weight fragments, one layer ahead
+    SplitAct *SB0 = &sb0;
+    SplitAct *SB1 = reinterpret_cast<SplitAct *>(bufA);
+    SplitAct *SB2 = reinterpret_cast<SplitAct *>(reinterpret_cast<char *>(bufA) + SAB);
+    float *logits = reinterpret_cast<float *>(reinterpret_cast<char *>(bufA) + 2 * SAB);
+    float *part = reinterpret_cast<float *>(&sb0);         // (channels 0-3: pool partials)
+    // dense1d_4: wave w takes row tile w & 1 and column tiles 2 (w >> 1), 2 (w >> 1) + 1
+    const int rt4 = w & 1, ct4 = 2 * (w >> 1);
+    RingL<2, 2> ring2;
     {
         const float bias = W[Nt::boff(3) + col];
-#if NN_SPLIT
-        gemm_cols(IntC<8>(), IntC<0>(), W + Nt::soff(3), fetchA8(0), [&] { ring_load<1, 44>(W + Nt::woff(4), w, 8, 8, ring); });
-#else
-        gemm_col(IntC<64>(), W + Nt::woff(3), fetchA(0), [&] { ring_load<1, 44>(W + Nt::woff(4), w, 8, 8, ring); });
-#endif
+        gemm_cols(IntC<8>(), IntC<0>(), W + Nt::soff(3), fetchA8(0),
+                  [&] { ringl_load<22>(W + Nt::soff(4), ct4, 1, 8, ring2); });
         lds_barrier();
 #pragma unroll
         for (int t = 0; t < 4; t++)
@@ -629,11 +550,11 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 if (t < ntok)
 #pragma unroll
                     for (int r = 0; r < 16; r++) Z[acc_row(r) * ZS + 256 + 64 * (t0 + t) + col - 64] = acc[t][r];
-        } else if (wg == 0) {              // channels 0-3: partial max / sum -> bufP
+        } else if (wg == 0) {              // channels 0-3: partial max / sum -> part
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                bufP[acc_row(r) * 128 + col] = fmaxf(fmaxf(acc[0][r], acc[1][r]), fmaxf(acc[2][r], acc[3][r]));
-                bufP[acc_row(r) * 128 + 64 + col] = acc[0][r] + acc[1][r] + acc[2][r] + acc[3][r];
+                part[acc_row(r) * 128 + col] = fmaxf(fmaxf(acc[0][r], acc[1][r]), fmaxf(acc[2][r], acc[3][r]));
+                part[acc_row(r) * 128 + 64 + col] = acc[0][r] + acc[1][r] + acc[2][r] + acc[3][r];
             }
         } else {                           // channels 5, 6 pass through
 #pragma unroll
@@ -647,82 +568,99 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const int i = acc_row(r);
-                Z[i * ZS + col] = fmaxf(bufP[i * 128 + col], acc[0][r]);
-                Z[i * ZS + 64 + col] = (bufP[i * 128 + 64 + col] + acc[0][r]) / 5.f;
+                Z[i * ZS + col] = fmaxf(part[i * 128 + col], acc[0][r]);
+                Z[i * ZS + 64 + col] = (part[i * 128 + 64 + col] + acc[0][r]) / 5.f;
             }
         }
         lds_barrier();
     }
-    NN_PROBE(4)
-    // ---- per-leaf layers on 16x16x4 tiles: wave w owns 16-column tile w (both 16-leaf row
-    // tiles) of a 128-wide layer; dst[row][dst_off + col] = f(acc, col) for col < nmax
+    // ---- per-leaf layers: split activations in SB0 / SB1 / SB2 (SplitAct), 16x16x32 tiles
     f32x4 a16[4][2];
-    auto store16 = [&](int j, int ct, float *dst, int stride, int dst_off, int nmax, auto f) {
-        const int col = 16 * ct + acc16_col();
-        if (col < nmax) {
+    // bias of this lane's column in tile ct of a per-leaf layer (0-padded to whole tiles), read
+    // before the layer's GEMM (vmcnt retires loads in order)
+    auto bias16 = [&](int layer, int ct) { return W[Nt::boff(layer) + 16 * ct + acc16_col()]; };
+    // A operand of a split source: the three planes' 8 bf16 at (row, k) of this lane
+    auto split_fetch = [&](const SplitAct *src, int koff) {
+        return [=](int t, int c, bf16x8 &a0, bf16x8 &a1, bf16x8 &a2) {
+            const int row = 16 * t + (lane & 15), k = koff + 32 * c + 8 * (lane >> 4);
+            a0 = *reinterpret_cast<const bf16x8 *>(&src->p[0][row][k]);
+            a1 = *reinterpret_cast<const bf16x8 *>(&src->p[1][row][k]);
+            a2 = *reinterpret_cast<const bf16x8 *>(&src->p[2][row][k]);
+        };
+    };
+    // epilogue: tile j (column tile ct) of both row tiles into dst, columns < nmax
+    auto store_split = [&](int j, int ct, SplitAct *dst, int dst_off, int nmax, auto f) {
+        const int c = 16 * ct + acc16_col();
+        if (c < nmax) {
 #pragma unroll
-            for (int rt = 0; rt < 2; rt++)
+            for (int t = 0; t < 2; t++)
 #pragma unroll
-                for (int r = 0; r < 4; r++) dst[(16 * rt + acc16_row(r)) * stride + dst_off + col] = f(a16[j][rt][r], col);
+                for (int r = 0; r < 4; r++) put_split(dst, 16 * t + acc16_row(r), dst_off + c, f(a16[j][t][r]));
         }
     };
-    auto leaf_fetch = [&](const float *src, int col0, int stride = PS) {
-        return [=](int rt, int c) { return ld4(src + (16 * rt + (lane & 15)) * stride + col0 + c); };
-    };
-    // bias of this lane's column in tile ct of a per-leaf layer (biases are 0-padded to whole
-    // tiles). Read before the layer's GEMM: vmcnt retires loads in order, so a bias load
-    // issued behind the next layer's ring prefetch would wait for the whole ring.
-    auto bias16 = [&](int layer, int ct) { return W[Nt::boff(layer) + 16 * ct + acc16_col()]; };
-    auto ring7 = [&](int layer) { return [&, layer] { ring_load<1, 7>(W + Nt::woff(layer), w, 8, 8, ring); }; };
-    auto ring8 = [&](int layer) { return [&, layer] { ring_load<1, 8>(W + Nt::woff(layer), w, 8, 8, ring); }; };
-    constexpr int CT = ntiles16(ACT);      // PI[1] column tiles
-    static_assert(CT > 24 && CT <= 32, "PI[1] tiles: 3 or 4 per wave");
-    NN_PROBE(5)
-    // ---- dense1d_4 over the 704 flattened features Z
+    RingL<1, 2> ring1;
+    // ---- dense1d_4 over the 704 flattened features Z (f32, split here: this wave's row tile)
     {
-        const float bl = bias16(4, w);
-        gemm16<1, 44>(W + Nt::woff(4), w, 8, ring, leaf_fetch(Z, 0, ZS), a16, ring7(5));
-        store16(0, w, bufQ, PS, 0, 128, [&](float x, int) { return fmaxf(x + bl, 0.f); });
+        const float b4a = bias16(4, ct4), b4b = bias16(4, ct4 + 1);
+        gemm_leaf<2, 1, 22>(W + Nt::soff(4), ct4, 1, ring2, [&](int, int c, bf16x8 &a0, bf16x8 &a1, bf16x8 &a2) {
+            const float *p = Z + (16 * rt4 + (lane & 15)) * ZS + 32 * c + 8 * (lane >> 4);
+            split8(F8{ld4(p), ld4(p + 4)}, a0, a1, a2);
+        }, a16, [&] { ringl_load<4>(W + Nt::soff(5), w, 8, 8, ring1); });
+        lds_barrier();                     // (Z read by every wave: SB1 / SB2 may overwrite it)
+        // the split buffers' padding columns [128, 144) to zero (SB1 / SB2 overlay Z, SB0 held
+        // dense2d_3's pool partials)
+        for (int i = tid; i < 3 * 3 * ML * 8; i += NNT) {
+            const int b = i / (3 * ML * 8), rem = i - b * 3 * ML * 8, pl = rem / (ML * 8), rr = (rem >> 3) % ML;
+            SplitAct *d = b == 0 ? SB0 : (b == 1 ? SB1 : SB2);
+            reinterpret_cast<uint32_t *>(&d->p[pl][rr][128])[i & 7] = 0u;
+        }
+        const int c = acc16_col();
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                put_split(SB0, 16 * rt4 + acc16_row(r), 16 * (ct4 + j) + c, fmaxf(a16[j][0][r] + (j ? b4b : b4a), 0.f));
         lds_barrier();
     }
     // partial pool over 4 groups of 4 of x[0:16] ++ relu(Wp x[16:] + bp) (BN folded): src -> dst
-    auto pool44 = [&](const float *src, float *dst, int layer, auto next) {
+    auto pool44 = [&](const SplitAct *src, SplitAct *dst, int layer, auto next) {
         const float bl = bias16(layer, w);
         float pv = 0.f;
         if (tid < ML * 8) {
             const int i = tid >> 3, j = tid & 7, g = j & 3;
-            const float *p = src + i * PS + 4 * g;
-            pv = j < 4 ? fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3])) : (p[0] + p[1] + p[2] + p[3]) / 4.f;
+            const float p0 = get_split(src, i, 4 * g), p1 = get_split(src, i, 4 * g + 1);
+            const float p2 = get_split(src, i, 4 * g + 2), p3 = get_split(src, i, 4 * g + 3);
+            pv = j < 4 ? fmaxf(fmaxf(p0, p1), fmaxf(p2, p3)) : (p0 + p1 + p2 + p3) / 4.f;
         }
-        gemm16<1, 7>(W + Nt::woff(layer), w, 8, ring, leaf_fetch(src, 16), a16, next);
-        if (tid < ML * 8) dst[(tid >> 3) * PS + (tid & 7)] = pv;
-        store16(0, w, dst, PS, 8, 120, [&](float x, int) { return fmaxf(x + bl, 0.f); });
+        gemm_leaf<1, 2, 4>(W + Nt::soff(layer), w, 8, ring1, split_fetch(src, 16), a16, next);
+        if (tid < ML * 8) put_split(dst, tid >> 3, tid & 7, pv);
+        store_split(0, w, dst, 8, 120, [&](float x) { return fmaxf(x + bl, 0.f); });
         lds_barrier();
     };
-    auto dense128 = [&](const float *src, float *dst, int layer, auto next) {
+    auto dense128 = [&](const SplitAct *src, SplitAct *dst, int layer, auto next) {
         const float bl = bias16(layer, w);
-        gemm16<1, 8>(W + Nt::woff(layer), w, 8, ring, leaf_fetch(src, 0), a16, next);
-        store16(0, w, dst, PS, 0, 128, [&](float x, int) { return fmaxf(x + bl, 0.f); });
+        gemm_leaf<1, 2, 4>(W + Nt::soff(layer), w, 8, ring1, split_fetch(src, 0), a16, next);
+        store_split(0, w, dst, 0, 128, [&](float x) { return fmaxf(x + bl, 0.f); });
         lds_barrier();
     };
-    NN_PROBE(6)
-    pool44(bufQ, bufP, 5, ring8(6));        // partialgpool_4
-    dense128(bufP, bufQ, 6, ring8(7));      // dense1d_5[0] (+BN folded)
-    dense128(bufQ, bufP, 7, ring7(8));      // dense1d_5[3]
-    pool44(bufP, bufQ, 8, ring8(9));        // partialgpool_5 -> trunk output in bufQ
-    NN_PROBE(7)
-    // ---- heads: PI[0] -> bufP, V[0] -> bufA (no activation); wave w: column tile w of both
+    auto ringn = [&](int layer) { return [&, layer] { ringl_load<4>(W + Nt::soff(layer), w, 8, 8, ring1); }; };
+    pool44(SB0, SB1, 5, ringn(6));          // partialgpool_4
+    dense128(SB1, SB2, 6, ringn(7));        // dense1d_5[0] (+BN folded)
+    dense128(SB2, SB1, 7, ringn(8));        // dense1d_5[3]
+    pool44(SB1, SB0, 8, ringn(9));          // partialgpool_5 -> trunk output in SB0
+    // ---- heads: PI[0] -> SB1, V[0] -> SB2 (no activation); wave w: column tile w of both
+    constexpr int CT = ntiles16(ACT);      // PI[1] column tiles
+    static_assert(CT > 24 && CT <= 32, "PI[1] tiles: 3 or 4 per wave");
+    RingL<4, 1> ring4;
     {
         const float bp = bias16(9, w), bv = bias16(11, w);
-        gemm16<1, 8>(W + Nt::woff(9), w, 8, ring, leaf_fetch(bufQ, 0), a16, ring8(11));
-        gemm16<1, 8>(W + Nt::woff(11), w, 8, ring, leaf_fetch(bufQ, 0), a16 + 1,
-                     [&] { ring_load<4, 8>(W + Nt::woff(10), w, 8, CT, ring); });
-        store16(0, w, bufP, PS, 0, 128, [&](float x, int) { return x + bp; });
-        store16(1, w, bufA, PS, 0, 128, [&](float x, int) { return x + bv; });
+        gemm_leaf<1, 2, 4>(W + Nt::soff(9), w, 8, ring1, split_fetch(SB0, 0), a16, ringn(11));
+        gemm_leaf<1, 2, 4>(W + Nt::soff(11), w, 8, ring1, split_fetch(SB0, 0), a16 + 1,
+                           [&] { ringl_load<4>(W + Nt::soff(10), w, 8, CT, ring4); });
+        store_split(0, w, SB1, 0, 128, [&](float x) { return x + bp; });
+        store_split(1, w, SB2, 0, 128, [&](float x) { return x + bv; });
         lds_barrier();
     }
-    NN_PROBE(8)
-    float *logits = bufA + ML * PS;
     // ---- PI[1] (409 outputs, 26 column tiles: waves 0-1 take 4, the others 3) and V[1]
     // (NP outputs, wave 7, whose ring is loaded behind its last PI[1] MFMA)
     {
@@ -733,33 +671,38 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         auto store_logits = [&](int nc) {
 #pragma unroll
             for (int j = 0; j < 4; j++)
-                if (j < nc) store16(j, w + 8 * j, logits, LS, 0, 16 * CT, [&](float x, int) { return x + bp[j]; });
+                if (j < nc) {
+                    const int c = 16 * (w + 8 * j) + acc16_col();
+#pragma unroll
+                    for (int t = 0; t < 2; t++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) logits[(16 * t + acc16_row(r)) * LS + c] = a16[j][t][r] + bp[j];
+                }
         };
         if (w + 24 < CT) {
-            gemm16<4, 8>(W + Nt::woff(10), w, 8, ring, leaf_fetch(bufP, 0), a16, NoNext());
+            gemm_leaf<4, 2, 4>(W + Nt::soff(10), w, 8, ring4, split_fetch(SB1, 0), a16, NoNext());
             store_logits(4);
         } else if (w != 7) {
-            gemm16<3, 8>(W + Nt::woff(10), w, 8, ring, leaf_fetch(bufP, 0), a16, NoNext());
+            gemm_leaf<3, 2, 4>(W + Nt::soff(10), w, 8, ring4, split_fetch(SB1, 0), a16, NoNext());
             store_logits(3);
         } else {
-            gemm16<3, 8>(W + Nt::woff(10), w, 8, ring, leaf_fetch(bufP, 0), a16,
-                         [&] { ring_load<1, 8>(W + Nt::woff(12), 0, 1, 1, ring); });
+            gemm_leaf<3, 2, 4>(W + Nt::soff(10), w, 8, ring4, split_fetch(SB1, 0), a16,
+                               [&] { ringl_load<4>(W + Nt::soff(12), 0, 1, 1, ring1); });
             store_logits(3);
-            gemm16<1, 8>(W + Nt::woff(12), 0, 1, ring, leaf_fetch(bufA, 0), a16, NoNext());
+            gemm_leaf<1, 2, 4>(W + Nt::soff(12), 0, 1, ring1, split_fetch(SB2, 0), a16, NoNext());
             const int n = acc16_col();
             if (n < NP) {
 #pragma unroll
-                for (int rt = 0; rt < 2; rt++)
+                for (int t = 0; t < 2; t++)
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
-                        const int i = 16 * rt + acc16_row(r);
-                        if (i < nb) v_out[rowof(i) * NP + n] = tanhf(a16[0][rt][r] + bv);
+                        const int i = 16 * t + acc16_row(r);
+                        if (i < nb) v_out[rowof(i) * NP + n] = tanhf(a16[0][t][r] + bv);
                     }
             }
         }
         lds_barrier();
     }
-    NN_PROBE(9)
     // ---- masked softmax (invalid -> -1e8, as the reference's masked_fill + log_softmax);
     // the wave's leaves are processed together so their reductions overlap
     {
@@ -804,11 +747,6 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             }
         }
     }
-#if NN_TIMING
-    NN_PROBE(10)
-    if (tid == 0)
-        for (int k = 0; k < 16; k++) atomicAdd(&g_nn_timing[k], (unsigned long long)nn_probe_acc[k]);
-#endif
 }
 
 inline int check_launch() { return hipGetLastError() == hipSuccess ? 0 : SPL_EDEVICE; }

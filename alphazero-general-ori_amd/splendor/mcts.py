@@ -35,7 +35,7 @@ HDR_DTYPE = np.dtype([
     ("npg", "<i4"), ("epg", "<i4"), ("eleft", "<i4"), ("live_gc", "<i4"),
     ("root_round", "<i4"), ("gc_queued", "<i4"), ("withdrawals", "<i4"), ("gcs", "<i4"),
     ("leaf_hslot", "<i4"), ("leaf_slot", "<i4"), ("depth_max", "<i4"), ("depth_sum", "<i4"),
-    ("resume", "<i4"), ("pad1", "<i4"), ("pad2", "<i4"), ("pad3", "<i4")])
+    ("resume", "<i4"), ("sims_backed", "<i4"), ("exact_wide", "<i4"), ("big_moves", "<i4")])
 assert HDR_DTYPE.itemsize == 208
 
 DEFAULT_ARGS = dict(numMCTSSims=100, cpuct=1.0, fpu=0.0, prob_fullMCTS=1.0, ratio_fullMCTS=5,

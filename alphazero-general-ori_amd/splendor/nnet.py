@@ -215,14 +215,31 @@ def _split_layer(w):
     return packed.view(torch.float32)
 
 
+def _split_leaf_layer(w):
+    """The bf16 x 3 copy of a per-leaf layer (16x16x32 bf16 MFMA B fragments):
+    [NT16][Kp32/32][3][64][8] bf16, element (nt, c, p, l, j) = part p of
+    W[16 nt + l % 16][32 c + 8 (l / 16) + j], as float32 storage (two bf16 per float)."""
+    N, K = w.shape
+    nt = (N + 15) // 16
+    k32 = (K + 31) // 32 * 32
+    wp = torch.zeros((nt * 16, k32), dtype=torch.float32, device=w.device)
+    wp[:N, :K] = w
+    parts = torch.stack(_bf16_parts(wp))                           # [3][16 nt][k32]
+    # [p][nt][col][c][g][j] -> [nt][c][p][g][col][j]; lane = 16 g + col
+    t = parts.view(3, nt, 16, k32 // 32, 4, 8).permute(1, 3, 0, 4, 2, 5).reshape(-1, 2)
+    packed = (t[:, 0] | (t[:, 1] << 16)).to(torch.int32)
+    return packed.view(torch.float32)
+
+
 def pack_weights(folded, n_players):
     """Pack a FoldedNet into the layout k_nn_forward reads (include/splendor_amd.h,
     spl_nn_forward): per layer the MFMA B-fragment order — layers 0-3 (32x32x2):
     [NT][S/4][64][4], element (nt, q, l, j) = W[32 nt + (l & 31)][4 q + j + (l >> 5) S],
     S = Kp/2; layers 4-12 (16x16x4, Kp % 16 == 0): [NT][Kp/16][64][4], element (nt, q, l, j)
     = W[16 nt + (l & 15)][16 q + 4 (l >> 4) + j] — then the 0-padded bias; then the
-    per-column BN affines; then (16-byte aligned) the bf16 x 3 copies of layers 0-3 that
-    NN_SPLIT kernels read (_split_layer)."""
+    per-column BN affines; then (16-byte aligned) the bf16 x 3 copies the kernel multiplies:
+    layers 0-3 in 32x32x16 fragments (_split_layer), layers 4-12 in 16x16x32 fragments
+    (_split_leaf_layer)."""
     f = folded
     layers = [(f.w1, f.b1), (f.w2, f.b2), (f.wp1, f.bp1), (f.w3, f.b3), (f.w4, f.b4), (f.wp4, f.bp4),
               (f.w5a, f.b5a), (f.w5b, f.b5b), (f.wp5, f.bp5), (f.wpi1, f.bpi1), (f.wpi2, f.bpi2),
@@ -252,6 +269,7 @@ def pack_weights(folded, n_players):
         pad = -sum(p.numel() for p in parts) % 4                    # 16-byte aligned split copies
         parts.append(torch.zeros(pad, dtype=torch.float32, device=f.w1.device))
         parts += [_split_layer(w) for w, _ in layers[:4]]
+        parts += [_split_leaf_layer(w) for w, _ in layers[4:]]
         out = torch.cat([p.float() for p in parts]).contiguous()
     want = _lib.lib().spl_nn_packed_floats(n_players)
     if out.numel() != want:

@@ -144,8 +144,11 @@ class SelfPlay(BatchedMCTS):
                 "withdrawals": int(h["withdrawals"].sum()), "collections": int(h["gcs"].sum()),
                 "overflow": int((h["overflow"] != 0).sum()),
                 "nodes_max": int(h["node_count"].max()), "edges_max": int(h["edge_count"].max()),
-                "leaf_depth_mean": float(h["depth"].mean()), "leaf_depth_max": int(h["depth"].max()),
+                "leaf_depth_now": float(h["depth"].mean()), "leaf_depth_max": int(h["depth"].max()),
                 "depth_sum": int(h["depth_sum"].astype("int64").sum()), "depth_max_all": int(h["depth_max"].max()),
+                "sims_backed": int(h["sims_backed"].astype("int64").sum()),
+                "exact_wide": int(h["exact_wide"].astype("int64").sum()),
+                "big_moves": int(h["big_moves"].astype("int64").sum()),
                 **self.capacity_events(h), "examples_dropped": self.dropped_examples()}
 
 

@@ -40,6 +40,7 @@ import torch  # noqa: E402
 METRIC = "self-play rollouts/sec (32k boards, 2p Splendor) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP32_MFMA_PEAK = 157.3    # TFLOP/s, dense fp32 MFMA (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK = 2500.0   # TFLOP/s, dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 RAMP_S = 0.05             # untimed launches before the env window (GPU clock ramp)
 _T0 = time.perf_counter()
 
@@ -205,6 +206,30 @@ def nn_flops_per_eval(n):
     return 2 * macs
 
 
+def nn_mfma_per_tile(n):
+    """MFMA instructions k_nn_forward issues per 32-leaf tile (csrc/nnet.hip): the 4 per-column
+    layers on v_mfma_f32_32x32x16_bf16 (7 token tiles x 4 column tiles; three part products
+    per 16-k chunk for dense2d_1's exact int8 input, six for the others) and the 9 per-leaf
+    layers on v_mfma_f32_16x16x32_bf16 (2 row tiles x the column tiles; six per 32-k chunk),
+    K rounded up to the chunk and N to the tile as the kernel runs them."""
+    R = 32 + 10 * n + n * n
+    c16 = lambda K: (K + 15) // 16
+    c32 = lambda K: (K + 31) // 32
+    t16 = lambda N: (N + 15) // 16
+    m32 = 28 * (3 * c16(R) + 6 * (c16(128) + c16(96) + c16(128)))
+    leaf = [(128, 704), (120, 112), (128, 128), (128, 128), (120, 112), (128, 128), (409, 128), (128, 128), (n, 128)]
+    m16 = sum(2 * t16(N) * c32(K) * 6 for N, K in leaf)
+    return m32, m16
+
+
+def nn_mix_ceiling_us(n, leaves):
+    """The MFMA floor of the shipping instruction mix: the bf16 MFMA FLOPs k_nn_forward
+    executes over `leaves` leaves (whole 32-leaf tiles) at the dense bf16 peak."""
+    m32, m16 = nn_mfma_per_tile(n)
+    flops = ((leaves + 31) // 32) * (m32 * 32 * 32 * 16 * 2 + m16 * 16 * 16 * 32 * 2)
+    return flops / (BF16_MFMA_PEAK * 1e12) * 1e6, flops
+
+
 def bytes_per_rollout(n, depth):
     """SURVEY.md §8(d) algorithmic HBM bytes of one MCTS simulation: leaf state as the f32
     network input (4S), bool mask (409), f32 policy out (4 x 409), f32 values (4n), and the
@@ -219,6 +244,13 @@ CONFIGS = {  # BASELINE.json configs: (players, games per GPU, numMCTSSims)
     "config4": (2, 32768, 1600),
     "config5": (4, 16384, 400),
 }
+# per workload: untimed prefill iterations to the steady state, the phase stagger inside it
+# (~ one game length), and the statistics window after the timed steps
+PHASES = {
+    "config3": dict(prefill=6000, stagger=4800, window=10000),
+    "config4": dict(prefill=45000, stagger=40000, window=4000),
+    "config5": dict(prefill=40000, stagger=32000, window=6000),
+}
 
 
 def stagger_marks(stagger, groups, sims, ratio):
@@ -232,7 +264,7 @@ def stagger_marks(stagger, groups, sims, ratio):
 
 
 def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, seed, node_boards=-1,
-                 stagger=0, groups=16, mem_gib=0.0):
+                 stagger=0, groups=16, mem_gib=0.0, on_steady=None):
     """Self-play at one BASELINE config: B games per GPU (shard board_base = rank * B), one
     MCTS simulation per game per iteration, leaves evaluated by the fused SplendorNNet kernel
     (fp32, random init), moves committed on device. `prefill` untimed iterations bring the
@@ -296,6 +328,8 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    if on_steady:
+        on_steady(sp)                          # (diagnostic tools: counters reset here)
     t0 = time.perf_counter()
     ev0.record()
     sp.run(steps, use_graph=True)
@@ -350,8 +384,12 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     e1.record()
     torch.cuda.synchronize(dev)
     nn_us = e0.elapsed_time(e1) / nk * 1e3
-    keys = ("games_done", "moves", "prunes", "resets", "unexpanded", "withdrawals", "collections")
+    keys = ("games_done", "moves", "prunes", "resets", "unexpanded", "withdrawals", "collections", "depth_sum",
+            "sims_backed", "exact_wide", "big_moves")
     delta = {k: st[k] - st0[k] for k in keys}
+    # leaf depth over every simulation backed up in the window (a snapshot of the trees'
+    # current path depths swings with the 20-iteration search cycle)
+    depth_mean = delta["depth_sum"] / delta["sims_backed"] if delta["sims_backed"] else st["leaf_depth_now"]
     delta["iterations"] = window
     delta["seconds"] = window_s
     delta["rollouts_per_s"] = world * B * window / window_s
@@ -361,12 +399,17 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
                                       for k in ("prunes", "resets", "unexpanded")}
     delta["examples_drained"] = ex_local
     delta["examples_gathered"] = int(ex["board"].shape[0])
+    if dist:
+        t = torch.tensor([ex_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        delta["examples_drained_all_ranks"] = int(t.item())
     delta["drain_allgather_s"] = gather_s
     live_n, live_e = ts[:, 2].astype("int64"), ts[:, 3].astype("int64")
     tree = {"nodes_max": st["nodes_max"], "edges_max": st["edges_max"],
             "live_nodes_mean": float(live_n.mean()), "live_nodes_max": int(live_n.max()),
             "live_edges_mean": float(live_e.mean()), "live_edges_max": int(live_e.max()),
-            "leaf_depth_mean": st["leaf_depth_mean"], "leaf_depth_max": st["leaf_depth_max"],
+            "leaf_depth_mean": depth_mean, "leaf_depth_max": st["depth_max_all"],
+            "leaf_depth_mean_note": "window depth_sum / simulations backed up (every simulation's leaf depth)",
             "overflow": st["overflow"], "examples_dropped": st["examples_dropped"],
             "node_cap_per_tree": int(sp.cfg.node_cap), "pool_nodes": int(sp.cfg.pool_nodes),
             "pool_edges": int(sp.cfg.pool_edges), "node_boards": int(sp.cfg.node_boards),
@@ -388,6 +431,7 @@ def selfplay_record(cfg, r, world, steps, warmup):
     return {"workload": f"{cfg}: {n}-player batched self-play, {B} games per GPU, numMCTSSims={sims}, genbu "
                         "search args, SplendorNNet fp32 leaf eval (random init), device move commit",
             "value": world * B * steps / r["elapsed"], "unit": "rollouts/s (MCTS simulations)",
+            "n_gpus": world, "global_games": world * B,
             "ms_per_iteration": r["elapsed"] / steps * 1e3, "ms_per_iteration_events": r["iter_ms_events"],
             "steps": steps, "warmup": warmup, "prefill_iterations": r["prefill"], "prefill_s": r["prefill_s"],
             "phase_stagger": r["stagger"],
@@ -395,10 +439,24 @@ def selfplay_record(cfg, r, world, steps, warmup):
             # every search ran on the reference's table (no prune / reset / unexpanded leaf in the
             # window; withdrawals repeat a simulation exactly): False marks a non-conforming record
             "reference_table": not any(r["window"].get(k, 0) for k in ("prunes", "resets", "unexpanded")),
-            "network_kernel": {"kernel": f"k_nn_forward<{n}>", "avg_us": r["nn_kernel_us"],
-                               "tflops": fl / (r["nn_kernel_us"] * 1e-6) / 1e12,
-                               "frac_fp32_mfma_peak": fl / (r["nn_kernel_us"] * 1e-6) / 1e12 / FP32_MFMA_PEAK,
-                               "note": "k_nn_forward alone over B leaves (HIP events, 10 warm-up + 50 timed launches)"}}
+            "network_kernel": _network_kernel(n, B, r["nn_kernel_us"])}
+
+
+def _network_kernel(n, B, us):
+    """k_nn_forward alone over B leaves: f32-equivalent throughput (the network's FLOPs) and
+    the bf16 MFMA throughput it executes (six part products per f32 product), the latter
+    against the dense bf16 peak and the instruction mix's MFMA floor."""
+    fl = nn_flops_per_eval(n) * B
+    ceil_us, xfl = nn_mix_ceiling_us(n, B)
+    return {"kernel": f"k_nn_forward<{n}>", "avg_us": us,
+            "tflops_f32_equivalent": fl / (us * 1e-6) / 1e12,
+            "frac_fp32_mfma_peak": fl / (us * 1e-6) / 1e12 / FP32_MFMA_PEAK,
+            "executed_bf16_tflops": xfl / (us * 1e-6) / 1e12,
+            "frac_bf16_mfma_peak": xfl / (us * 1e-6) / 1e12 / BF16_MFMA_PEAK,
+            "executed_bf16_flop_per_launch": xfl, "mix_ceiling_us": ceil_us, "frac_of_mix_ceiling": ceil_us / us,
+            "note": "k_nn_forward alone over B leaves (HIP events, 10 warm-up + 50 timed launches); f32 "
+                    "arithmetic as bf16 part products: 'f32-equivalent' counts the network's own FLOPs "
+                    "(1.19 MFLOP per leaf), 'executed' the bf16 MFMA FLOPs issued"}
 
 
 def load_json_profile(pattern):
@@ -450,13 +508,18 @@ def selfplay_roofline(rec, n, depth):
     tree = {k: {"hbm_bytes_per_sim": per_sim(k), "avg_us_rocprof": kern.get(k, {}).get("avg_us")}
             for k in ("k_select", "k_backup", "k_leaf_mask", "k_commit", "k_gc")}
     tot = sum(v["hbm_bytes_per_sim"] or 0.0 for v in tree.values())
-    return {"bound": "mfma", "achieved": nk["tflops"], "peak": FP32_MFMA_PEAK, "unit": "TFLOP/s",
-            "frac": nk["frac_fp32_mfma_peak"],
-            "mfma_mix": "f32 arithmetic (the reference's precision): the 4 per-column layers (61 % of the "
-                        "FLOPs) on v_mfma_f32_32x32x16_bf16 with each f32 operand split exactly into three "
-                        "bf16 parts (six products per 16-k chunk, DESIGN.md §4), the 9 per-leaf layers on "
-                        "v_mfma_f32_16x16x4_f32; achieved counts the network's f32 FLOPs only, against "
-                        "the dense f32 MFMA peak",
+    return {"bound": "mfma", "achieved": nk["executed_bf16_tflops"], "peak": BF16_MFMA_PEAK, "unit": "TFLOP/s",
+            "frac": nk["frac_bf16_mfma_peak"],
+            "mfma_mix": "f32 arithmetic (the reference's precision) with every f32 operand split exactly into "
+                        "three bf16 parts: the 4 per-column layers on v_mfma_f32_32x32x16_bf16, the 9 per-leaf "
+                        "layers on v_mfma_f32_16x16x32_bf16 (six part products per chunk, DESIGN.md §4); "
+                        "achieved = the bf16 MFMA FLOPs executed, against the dense bf16 peak",
+            "mix_ceiling_us": nk["mix_ceiling_us"], "frac_of_mix_ceiling": nk["frac_of_mix_ceiling"],
+            "f32_equivalent": {"achieved": nk["tflops_f32_equivalent"], "peak": FP32_MFMA_PEAK,
+                               "frac": nk["frac_fp32_mfma_peak"],
+                               "note": "the network's own f32 FLOPs per second against the f32 MFMA peak: an "
+                                       "f32-equivalent throughput, not the utilisation of the pipe that runs "
+                                       "them (may exceed 1)"},
             "traffic": nnfb.get("hbm_bytes_per_launch"),
             "kernel": nk["kernel"], "kernel_avg_us": nk["avg_us"],
             "kernel_avg_us_rocprof": nnfb.get("avg_us"), "rocprof_file": nnfb.get("file"),
@@ -578,9 +641,13 @@ def launch_ranks(nproc, argv):
 
 
 def dry_run(args, rank, world):
-    """--dry-run: the multi-rank plumbing of the bench line without a GPU (gloo): barrier,
-    a timed no-op interval, max over ranks, rank 0 prints the line (value null)."""
+    """--dry-run: the multi-rank plumbing of the bench line without a GPU (gloo): barrier, a
+    timed no-op interval, max over ranks, the episode-end example all-gather (splendor.
+    selfplay.gather_examples over a few synthetic examples per rank, as config 4's window
+    gathers), rank 0 prints the line (values null) with the record of each workload the run
+    would measure at this N."""
     import torch.distributed as dist
+    from splendor.selfplay import gather_examples
     if world > 1:
         dist.init_process_group("gloo")
         dist.barrier()
@@ -591,13 +658,28 @@ def dry_run(args, rank, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
+    k = 3 + rank                                         # synthetic examples of this rank
+    R = 32 + 10 * 2 + 4
+    ex = {"board": torch.zeros((k, R, 7), dtype=torch.int8), "pi": torch.zeros((k, 409)),
+          "meta": torch.full((k, 4), rank, dtype=torch.int32)}
+    gathered = int(gather_examples(ex)["board"].shape[0])
+
+    def record(cfg):
+        n, B, sims = CONFIGS[cfg]
+        return {"workload": cfg, "value": None, "n_gpus": world, "global_games": world * B, "numMCTSSims": sims,
+                "window": {"examples_drained": k, "examples_gathered": gathered, **PHASES[cfg]}}
+    head = "config3" if args.workload in ("all", "selfplay") else args.workload
+    extra = {}
+    if args.workload == "all" and world > 1 and not args.no_secondary:
+        extra["config4_shard"] = record("config4")
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "rollouts/s (MCTS simulations)",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
                           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dry_run": True,
                           "ranks_reporting": world, "max_elapsed_s": elapsed,
-                          "config": {"parallelism": f"dp{world} (game shards; RCCL all-gather of examples)"}}),
-              flush=True)
+                          "config": {"workload": head, "global_games": world * CONFIGS[head][1],
+                                     "parallelism": f"dp{world} (game shards; RCCL all-gather of examples)"},
+                          "selfplay": record(head), **extra}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -607,10 +689,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000, help="timed self-play iterations (headline)")
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--prefill", type=int, default=6000, help="untimed iterations to the steady state first")
-    ap.add_argument("--stagger", type=int, default=4800, help="prefill iterations over which the games' phases "
+    ap.add_argument("--prefill", type=int, default=None, help="untimed iterations to the steady state first "
+                    "(default: the workload's, PHASES)")
+    ap.add_argument("--stagger", type=int, default=None, help="prefill iterations over which the games' phases "
                     "are spread (run_selfplay; ~ the mean game length: config 3 ~4,800 iterations)")
-    ap.add_argument("--window", type=int, default=10000, help="statistics window after the timed steps")
+    ap.add_argument("--window", type=int, default=None, help="statistics window after the timed steps")
     ap.add_argument("--boards", type=int, default=32768, help="env workload: boards per GPU")
     ap.add_argument("--players", type=int, default=2, help="env workload: players")
     ap.add_argument("--seed", type=int, default=0x5EED)
@@ -621,12 +704,12 @@ def main():
     ap.add_argument("--no-secondary", action="store_true", help="all: the headline only")
     ap.add_argument("--chunk", type=int, default=100, help="env: moves per rollout launch")
     ap.add_argument("--env-steps", type=int, default=1000, help="config-2 object: timed moves")
-    ap.add_argument("--c5-prefill", type=int, default=40000)
-    ap.add_argument("--c5-stagger", type=int, default=32000)
-    ap.add_argument("--c5-window", type=int, default=6000)
-    ap.add_argument("--c4-prefill", type=int, default=45000)
-    ap.add_argument("--c4-stagger", type=int, default=40000)
-    ap.add_argument("--c4-window", type=int, default=4000)
+    ap.add_argument("--c5-prefill", type=int, default=PHASES["config5"]["prefill"])
+    ap.add_argument("--c5-stagger", type=int, default=PHASES["config5"]["stagger"])
+    ap.add_argument("--c5-window", type=int, default=PHASES["config5"]["window"])
+    ap.add_argument("--c4-prefill", type=int, default=PHASES["config4"]["prefill"])
+    ap.add_argument("--c4-stagger", type=int, default=PHASES["config4"]["stagger"])
+    ap.add_argument("--c4-window", type=int, default=PHASES["config4"]["window"])
     ap.add_argument("--node-boards", type=int, default=-1, help="selfplay: 1/0 force node boards on/off "
                     "(default: on unless the pools do not fit)")
     ap.add_argument("--mem-gib", type=float, default=0.0, help="selfplay: arena budget in GiB (default: "
@@ -676,16 +759,24 @@ def main():
 
     head = "config3" if args.workload in ("all", "selfplay") else args.workload
     n, B, sims = CONFIGS[head]
-    r = run_selfplay(head, rank, world, dev, dist, args.steps, args.warmup, args.prefill, args.window, args.seed,
-                     args.node_boards, stagger=args.stagger, mem_gib=args.mem_gib)
+    ph = {k: (getattr(args, k) if getattr(args, k) is not None else v) for k, v in PHASES[head].items()}
+    r = run_selfplay(head, rank, world, dev, dist, args.steps, args.warmup, ph["prefill"], ph["window"], args.seed,
+                     args.node_boards, stagger=ph["stagger"], mem_gib=args.mem_gib)
     rec = selfplay_record(head, r, world, args.steps, args.warmup)
     torch.cuda.empty_cache()
     extra = {}
-    secondary = args.workload == "all" and world == 1 and not args.no_secondary
+    secondary = args.workload == "all" and not args.no_secondary
     cpu_ok = rank == 0 and world == 1 and not args.no_cpu_baseline
     if cpu_ok:
         rec["cpu_baseline"] = cpu_baseline_selfplay(n, args.seed, sims)
-    if secondary:
+    if secondary and world > 1:
+        # BASELINE config 4 proper: 32,768 games per GPU (262,144 on 8), 1,600 simulations,
+        # the examples all-gathered over RCCL at the end of its window (Coach.py:117-124)
+        rr = run_selfplay("config4", rank, world, dev, dist, 1000, 100, args.c4_prefill, args.c4_window, args.seed,
+                          args.node_boards, stagger=args.c4_stagger)
+        extra["config4_shard"] = selfplay_record("config4", rr, world, 1000, 100)
+        torch.cuda.empty_cache()
+    elif secondary:
         extra["config2_env"] = run_env(args, rank, world, dev, dist, args.env_steps, 100, cpu=cpu_ok)
         for cfg, pf, sg, win in (("config5", args.c5_prefill, args.c5_stagger, args.c5_window),
                                  ("config4", args.c4_prefill, args.c4_stagger, args.c4_window)):
@@ -706,8 +797,8 @@ def main():
             "data": "synthetic (Philox-seeded deals), random-init SplendorNNet (genbu.pt is refused by the "
                     "weights-only loader)",
             "config": {"workload": rec["workload"], "players": n, "games_per_gpu": B, "global_games": world * B,
-                       "numMCTSSims": sims, "prefill_iterations": args.prefill,
-                       "phase_stagger_iterations": args.stagger,
+                       "numMCTSSims": sims, "prefill_iterations": ph["prefill"],
+                       "phase_stagger_iterations": ph["stagger"],
                        "parallelism": f"dp{world} (game shards; RCCL all-gather of examples)"},
             "roofline": selfplay_roofline(rec, n, rec["tree"]["leaf_depth_mean"]),
             "cpu_baseline": cpu,

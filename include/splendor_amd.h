@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 7
+#define SPL_ABI_VERSION 8
 #define SPL_ACTIONS 409
 #define SPL_MASK_WORDS 7
 #define SPL_EINVAL (-1)
@@ -283,9 +283,10 @@ int spl_hash_eval_mode(const spl_ctx *ctx, int B, const int8_t *state, const uin
  * SplendorNNet inference (SplendorNNet.py:56-159 in eval mode; GenericNNetWrapper.predict
  * :141-168 minus the host round trip) as one fused kernel: int8 boards [B][R][7] + packed
  * masks [B][7] -> pi [B][409] = softmax(masked logits, invalid -> -1e8) and v [B][n] =
- * tanh(value head). f32 arithmetic: the per-column layers on bf16 MFMAs with every f32
- * operand split exactly into three bf16 parts (six products per 16-k chunk, the largest in its
- * own f32 accumulator), the per-leaf layers on f32 MFMA.
+ * tanh(value head). f32 arithmetic on bf16 MFMAs, every f32 operand split exactly into three
+ * bf16 parts (six products per chunk, the largest in its own f32 accumulator): the per-column
+ * layers on v_mfma_f32_32x32x16_bf16, the per-leaf layers on v_mfma_f32_16x16x32_bf16
+ * (DESIGN.md §4).
  *
  * packed_weights: spl_nn_packed_floats(n) floats, 16-byte aligned, the eval-mode network
  * with BatchNorms folded (splendor/nnet.py pack_weights). For each of the 13 linear layers
@@ -304,7 +305,11 @@ int spl_hash_eval_mode(const spl_ctx *ctx, int B, const int8_t *state, const uin
  * first 4 layers again as exact three-part bf16 splits (w = hi + mid + lo by truncation) for
  * the bf16-MFMA form of those layers: per layer [4][Kp16/16][3][64][8] bf16 (Kp16 = K rounded
  * up to 16), element (nt, c, p, l, j) = part p of W[32 nt + l % 32][16 c + 8 (l / 32) + j],
- * two bf16 per float slot. Returns the float count or SPL_EINVAL. */
+ * two bf16 per float slot; then the other 9 layers the same way for 16x16x32: per layer
+ * [NT16][Kp32/32][3][64][8] bf16 (NT16 = ceil(N / 16), Kp32 = K rounded up to 32), element
+ * (nt, c, p, l, j) = part p of W[16 nt + l % 16][32 c + 8 (l / 16) + j]. The f32 copies of the
+ * 13 layers stay in the layout (the biases are read from them). Returns the float count or
+ * SPL_EINVAL. */
 int spl_nn_packed_floats(int n_players);
 int spl_nn_forward(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
                    const float *packed_weights, float *pi, float *v, void *hip_stream);

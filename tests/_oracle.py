@@ -310,3 +310,42 @@ def arena_play(n, G, sims, cpuct, fpu, seed, neg2=False):
                 break
         out.append((result, plies, [score(n, st, p) for p in range(n)], actions))
     return out
+
+
+def _selfplay_part(a):
+    args, kw = a
+    return selfplay_run(*args, **kw)
+
+
+def selfplay_run_parallel(n, B, iters, seed, num_sims, ratio_full, prob_full, cpuct, fpu, forced, temp_threshold,
+                          lag=None, workers=None, **kw):
+    """selfplay_run over board ids 0 .. B-1 split into contiguous parts run in worker
+    processes (every draw is keyed by the global board id, so parts are independent; the
+    oracle's depth statistics are per process). Board t runs iters - lag[t] iterations (a
+    device tree that withdrew w simulations is exactly w simulations behind). Returns the
+    concatenated result; "depth" = (sum, max, count) over all parts."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    import os
+    lag = np.zeros(B, np.int64) if lag is None else np.asarray(lag, np.int64)
+    if workers is None:
+        try:
+            workers = len(os.sched_getaffinity(0))
+        except AttributeError:
+            workers = os.cpu_count() or 1
+        workers = max(1, min(16, workers))
+    size = max(1, -(-B // workers))
+    parts, t0 = [], 0
+    while t0 < B:
+        t1 = t0 + 1
+        while t1 < B and t1 - t0 < size and lag[t1] == lag[t0]:
+            t1 += 1
+        parts.append(((n, t1 - t0, iters - int(lag[t0]), seed, num_sims, ratio_full, prob_full, cpuct, fpu, forced,
+                       temp_threshold), dict(kw, board_base=kw.get("board_base", 0) + t0)))
+        t0 = t1
+    with cf.ProcessPoolExecutor(max_workers=min(workers, len(parts)), mp_context=mp.get_context("spawn")) as ex:
+        res = list(ex.map(_selfplay_part, parts))
+    out = {k: np.concatenate([r[k] for r in res]) for k in res[0] if k != "depth"}
+    d = [r["depth"] for r in res]
+    out["depth"] = (sum(x[0] for x in d), max(x[1] for x in d), sum(x[2] for x in d))
+    return out

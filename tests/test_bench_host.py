@@ -63,3 +63,25 @@ def test_gpus_flag_launches_that_many_ranks():
 def test_gpus_flag_must_match_world_size():
     r = _run_bench(["--gpus", "2", "--dry-run"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE 1" in r.stderr
+
+
+@pytest.mark.parametrize("workload", ["config4", "all"])
+def test_config4_multi_rank_dry_run(workload):
+    """BASELINE config 4 at N = 2: the run measures config 4's per-GPU shard
+    on every rank (65,536 games in all) with its own prefill / stagger / window, and its
+    window's example all-gather runs over the ranks (gloo here, RCCL on the GPUs)."""
+    import json
+    r = _run_bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--workload", workload, "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    c4 = out["selfplay"] if workload == "config4" else out["config4_shard"]
+    assert out["n_gpus"] == 2 and c4["n_gpus"] == 2 and c4["global_games"] == 65536
+    assert c4["window"]["examples_gathered"] == 3 + 4          # rank 0: 3 examples, rank 1: 4
+    assert (c4["window"]["prefill"], c4["window"]["stagger"], c4["window"]["window"]) == (45000, 40000, 4000)
+    if workload == "all":
+        assert out["selfplay"]["global_games"] == 65536 and out["selfplay"]["numMCTSSims"] == 100
+
+
+def test_phase_defaults_per_workload(bench):
+    assert bench.PHASES["config3"] == dict(prefill=6000, stagger=4800, window=10000)
+    assert bench.PHASES["config4"]["prefill"] == 45000 and bench.PHASES["config5"]["prefill"] == 40000

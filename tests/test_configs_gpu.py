@@ -98,11 +98,16 @@ def test_config5_shard_equals_slice_and_oracle():
     assert st["prunes"] == st["resets"] == 0
     del full
     free_all()
-    ref = O.selfplay_run(n, Bs, iters, 0x5EED, sims, GENBU["ratio_fullMCTS"], GENBU["prob_fullMCTS"], GENBU["cpuct"],
-                         GENBU["fpu"], False, GENBU["tempThreshold"], board_base=b0, dir_alpha=0.3, dir_temp=1.25)
+    ref = O.selfplay_run_parallel(n, Bs, iters, 0x5EED, sims, GENBU["ratio_fullMCTS"], GENBU["prob_fullMCTS"],
+                                  GENBU["cpuct"], GENBU["fpu"], False, GENBU["tempThreshold"], board_base=b0,
+                                  dir_alpha=0.3, dir_temp=1.25)
     h = shard.headers()
     for j, k in enumerate(("player", "episode_step", "move_no", "game_no", "games_done", "moves", "sims_done", "budget")):
         np.testing.assert_array_equal(h[k], ref["hdr"][:, j], err_msg=k)
+    ss = shard.stats()                          # every simulation's leaf depth (sum, maximum)
+    assert (ss["depth_sum"], ss["depth_max_all"]) == ref["depth"][:2]
+    # (the full example / pi comparison at this budget: test_selfplay_gpu.py::
+    # test_large_budget_selfplay_matches_oracle[4-400-45000])
 
 
 @pytest.mark.parametrize("n,B,sims,iters", [(4, 16384, 400, 1000), (2, 32768, 1600, 2400)])

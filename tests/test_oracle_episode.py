@@ -152,3 +152,20 @@ def test_arena_matches_reference(n):
         one += res[0] == (1.0 if ovt else -1.0)
         two += res[0] == (-1.0 if ovt else 1.0)
     assert (one, two, G - one - two) == (int(d["one"]), int(d["two"]), int(d["draws"]))
+
+
+def test_parallel_oracle_selfplay_equals_serial():
+    """The parallel oracle driver (board-id parts in worker processes, used by the GPU
+    large-budget parity tests) equals one sequential run, lags included."""
+    args = (2, 12, 700, 11, 30, 5, 0.25, 2.5, 0.3, False, 10)
+    kw = dict(max_ex=4000, dir_alpha=0.3, dir_temp=1.25, fake_mode=1)
+    ref = O.selfplay_run(*args, **kw)
+    par = O.selfplay_run_parallel(*args, workers=3, **kw)
+    for k in ("hdr", "board", "ex_board", "pi", "valids", "winner", "scdiff", "surprise", "meta"):
+        np.testing.assert_array_equal(par[k], ref[k], err_msg=k)
+    assert par["depth"] == ref["depth"]
+    lag = np.array([0] * 6 + [3] * 6)
+    par = O.selfplay_run_parallel(*args, lag=lag, workers=4, **kw)
+    a = O.selfplay_run(2, 6, 700, 11, *args[4:], **kw)
+    b = O.selfplay_run(2, 6, 697, 11, *args[4:], board_base=6, **kw)
+    np.testing.assert_array_equal(par["hdr"], np.concatenate([a["hdr"], b["hdr"]]))

@@ -5,6 +5,8 @@ network) and against whole reference episodes recorded with the same draws injec
 training example."""
 import os
 
+import time
+
 import numpy as np
 import pytest
 
@@ -334,7 +336,7 @@ HDR_KEYS = ("node_count", "edge_count", "root", "sims_done", "budget", "full", "
 GENBU = dict(cpuct=2.5, fpu=0.3, prob_full=0.25, ratio=5, noise=True)
 
 
-def _deep_device(n, B, iters, sims=100, seed=11, **kw):
+def _deep_device(n, B, iters, sims=100, seed=11, mode=1, **kw):
     from splendor.env import SplendorEngine
     from splendor.mcts import HashEvaluator
     from splendor.selfplay import SelfPlay
@@ -342,7 +344,7 @@ def _deep_device(n, B, iters, sims=100, seed=11, **kw):
                 ratio_fullMCTS=GENBU["ratio"], forced_playouts=False, dirichletAlpha=0.3, temperature=[1.25, 0.8],
                 tempThreshold=10)
     e = SplendorEngine(n)
-    sp = SelfPlay(e, B, args, evaluator=HashEvaluator(e, mode=1), dirichlet_noise=True, seed=seed,
+    sp = SelfPlay(e, B, args, evaluator=HashEvaluator(e, mode=mode), dirichlet_noise=True, seed=seed,
                   out_cap=60000, **kw)
     sp.reset()
     sp.run(iters, use_graph=True)
@@ -355,32 +357,23 @@ def _deep_device(n, B, iters, sims=100, seed=11, **kw):
     return hdr, st, ex
 
 
-def _oracle_lagged(n, B, iters, seed, sims, lag):
+def _oracle_lagged(n, B, iters, seed, sims, lag, mode=1):
     """The oracle's self-play loop (peaked hash network, genbu arguments) where tree t runs
     iters - lag[t] iterations: a withdrawn simulation repeats in the next iteration, so a tree
-    that withdrew w times is exactly w simulations behind. Runs of trees with equal lag go
-    together (every draw is keyed by the global board id)."""
+    that withdrew w times is exactly w simulations behind. Board-id parts run in worker
+    processes (every draw is keyed by the global board id)."""
     args = (sims, GENBU["ratio"], GENBU["prob_full"], GENBU["cpuct"], GENBU["fpu"], False, 10)
-    kw = dict(max_ex=60000, dir_alpha=0.3, dir_temp=1.25, fake_mode=1)
-    lag = np.asarray(lag, np.int64)
-    parts, t0 = [], 0
-    while t0 < B:
-        t1 = t0 + 1
-        while t1 < B and lag[t1] == lag[t0]:
-            t1 += 1
-        parts.append(O.selfplay_run(n, t1 - t0, iters - int(lag[t0]), seed, *args, board_base=t0, **kw))
-        t0 = t1
-    ref = {k: np.concatenate([p[k] for p in parts]) for k in parts[0] if k != "depth"}
-    d = [p["depth"] for p in parts]
-    ref["depth"] = (sum(x[0] for x in d), max(x[1] for x in d), sum(x[2] for x in d))
-    return ref
+    return O.selfplay_run_parallel(n, B, iters, seed, *args, lag=lag, max_ex=60000, dir_alpha=0.3, dir_temp=1.25,
+                                   fake_mode=mode)
 
 
-def _deep_selfplay(n, B, iters, sims=100, seed=11, device_run=None, **kw):
+def _deep_selfplay(n, B, iters, sims=100, seed=11, device_run=None, mode=1, **kw):
     """Self-play with the peaked hash network (mode 1: the random-init SplendorNNet's regime:
     deep trees, long terminal lines) against the oracle's sequential loop, bit for bit."""
-    hdr, st, ex = device_run or _deep_device(n, B, iters, sims, seed, **kw)
-    ref = _oracle_lagged(n, B, iters, seed, sims, hdr["withdrawals"])
+    hdr, st, ex = device_run or _deep_device(n, B, iters, sims, seed, mode=mode, **kw)
+    t0 = time.perf_counter()
+    ref = _oracle_lagged(n, B, iters, seed, sims, hdr["withdrawals"], mode=mode)
+    print(f"oracle: {time.perf_counter() - t0:.1f} s", flush=True)
     rh = ref["hdr"]
     for k, j in (("player", 0), ("episode_step", 1), ("move_no", 2), ("game_no", 3), ("games_done", 4),
                  ("moves", 5), ("sims_done", 6)):
@@ -408,6 +401,34 @@ def test_deep_selfplay_matches_oracle(n, B, iters):
     st, mean, mx = _deep_selfplay(n, B, iters)
     assert mean > 15 and mx > 64, (mean, mx)
     assert st["prunes"] == st["resets"] == st["unexpanded"] == 0
+
+
+@pytest.mark.parametrize("n,sims,iters,mode", [(2, 1600, 90000, 1), (2, 1600, 90000, 0), (4, 400, 45000, 1),
+                                               (4, 400, 45000, 0)])
+def test_large_budget_selfplay_matches_oracle(n, sims, iters, mode):
+    """BASELINE configs 4 (2p, numMCTSSims 1,600) and 5 (4p, 400) at their search budgets
+    (MCTS.py:45-60 full / fast searches, :99-177, :199-219): 32 games of self-play with genbu's
+    arguments and Dirichlet noise, long enough for the games to finish (2p: up to 124 moves of
+    ~640 simulations; 4p: 248 of ~160), bit for bit against the oracle — headers, every
+    simulation's leaf depth, every finished example (board, pi, winner, scdiff, surprise,
+    valids). Two hash networks: the peaked one (mode 1: deep trees, leaves past 64 levels) and
+    the spread one (mode 0: wide nodes — the peaked network never gives a non-root node more
+    than 12 visited edges). Asserted to have run, from the device's counters: visit blocks
+    relocated to 128 or more records (both), and (mode 0) non-root levels with more than 12
+    visit records evaluated exactly."""
+    B = 32
+    t0 = time.perf_counter()
+    run = _deep_device(n, B, iters, sims=sims, mode=mode, mem_budget=16 << 30)
+    print(f"device: {time.perf_counter() - t0:.1f} s", flush=True)
+    st, mean, mx = _deep_selfplay(n, B, iters, sims=sims, device_run=run, mode=mode)
+    print(f"large budget n={n} sims={sims} mode={mode}: mean leaf depth {mean:.1f}, max {mx}, {st}", flush=True)
+    assert st["games_done"] >= B // 2
+    assert st["prunes"] == st["resets"] == st["unexpanded"] == 0
+    assert st["big_moves"] > 0, "no visit block was relocated to 128 or more records"
+    if mode == 1:
+        assert mean > 15 and mx > 64, (mean, mx)
+    else:
+        assert st["exact_wide"] > 0, "no non-root level with more than 12 visit records was evaluated exactly"
 
 
 def test_withdrawals_repeat_the_same_simulation():

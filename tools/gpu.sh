@@ -13,8 +13,9 @@
 #   split     per-iteration kernel split from the trace (needs trace)  -> gpurun_out/split.txt
 #   pmc       PMC passes over the self-play kernels (pmc_selfplay.sh)  -> gpurun_out/pmc_sp/
 #   nn        full-batch network trace + HBM counters (nn_fullbatch.sh) -> gpurun_out/nnfb/
-#   ab        interleaved A/B of the product library against ablib/lib<V>.so for V in $AB
-#             (config-3 bench twice each)                              -> gpurun_out/ab.txt
+#   ab        interleaved A/B of the product against each V in $AB: ablib/lib<V>.so, or a whole
+#             older tree ablib/<V>/ (bench.py + package) (config-3 bench twice each) -> gpurun_out/ab.txt
+#   probe     k_select_lanes phase probes (ablib/libprobe.so, -DSELECT_PROBE=1) -> gpurun_out/probe.json
 #   bounds    the bounds-checked build (ablib/libchk.so: tools/bounds_check.sh on
 #             the host first) under capacity pressure                   -> gpurun_out/bounds_chk.json
 # ROUND (default r05) names the summaries; EXTRA adds bench arguments to selfplay/trace.
@@ -51,12 +52,18 @@ step() {
         rm -f gpurun_out/ab.txt
         for rep in 1 2; do
             for v in product ${AB:-}; do
-                if [ "$v" = product ]; then lib=""; else lib="$PWD/ablib/lib$v.so"; fi
-                SPLENDOR_AMD_LIB=$lib timeout -k 10 240 python3 -u bench.py --workload selfplay --steps 2000 \
+                # a variant is a library (ablib/lib<V>.so under this tree's Python) or a whole
+                # tree (ablib/<V>/bench.py with its own package: builds whose ABI differs)
+                b=bench.py; lib=""
+                if [ -f "ablib/$v/bench.py" ]; then b="ablib/$v/bench.py"; elif [ "$v" != product ]; then lib="$PWD/ablib/lib$v.so"; fi
+                SPLENDOR_AMD_LIB=$lib timeout -k 10 240 python3 -u "$b" --workload selfplay --steps 2000 \
                     --window 0 --no-cpu-baseline ${EXTRA:-} > gpurun_out/ab_$v.$rep.json 2> gpurun_out/ab_$v.$rep.err || return 1
                 echo "$v $rep $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_$v.$rep.json | head -1)" >> gpurun_out/ab.txt
             done
         done ;;
+    probe)
+        SPLENDOR_AMD_LIB=$PWD/ablib/libprobe.so timeout -k 10 200 python3 -u tools/select_probe.py \
+            > gpurun_out/probe.json 2> gpurun_out/probe.err ;;
     bounds)
         SPLENDOR_AMD_LIB=$PWD/ablib/libchk.so timeout -k 10 300 python3 -u tools/bounds_check.py --tag chk \
             --iters "${ITERS:-6000}" > gpurun_out/bounds_chk.json 2> gpurun_out/bounds_chk.err ;;
