@@ -682,7 +682,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                 w.c.set_eb(ec > 0 ? unit_g(P, t, vs) : 0, vcnt);
                 w.c.set_vb(vcnt > 0 ? unit_g(P, t, vs + ec) : 0, vcnt);
             }
-            w.h.h2 = -1; w.h.h3 = -1;                    // (descent hints name old ids: dropped)
+            w.h.rsv0 = -1; w.h.rsv1 = -1;
             P.nkey0[ng] = k0; P.nkey1[ng] = k1;
             P.nd[ng] = w;
             S.cs[ni] = vs; S.cnt[ni] = sz; S.inv[ni] = i;
@@ -1306,7 +1306,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
             w2.c.cand = (int16_t)cand; w2.c.ca = (int16_t)ca; w2.c.cp = cp; w2.c.np = np;
             w2.h.set_pick(pk.e, pk.a, pk.e >= 0 && pk.child >= 0 ? P.nd[pk.child].h.term : 0);   // (-1: scans)
             w2.h.bchild = pk.e >= 0 ? pk.child : -1;
-            w2.h.h2 = -1; w2.h.h3 = -1;
+            w2.h.rsv0 = -1; w2.h.rsv1 = -1;
             w2.h.bvi = pk.e >= 0 ? P.ep(r.eb + pk.e)->vi : (int16_t)-1;
             P.nd[nroot] = w2;
         }
@@ -1362,7 +1362,7 @@ __device__ __forceinline__ void term_values(const Pools &P, int g, float v[4]) {
 // the record of a new terminal node of round rd with end values v
 __device__ __forceinline__ Node term_node(const float v[4], int rd) {
     Node n{};
-    n.h.bchild = -1; n.h.h2 = -1; n.h.h3 = -1; n.h.set_pick(-1, 0, 0); n.h.ns = 0;
+    n.h.bchild = -1; n.h.rsv0 = -1; n.h.rsv1 = -1; n.h.set_pick(-1, 0, 0); n.h.ns = 0;
     n.h.term = 1; n.h.round = (uint8_t)rd; n.h.qs = 0.0;
     *reinterpret_cast<float4 *>(&n.c) = make_float4(v[0], v[1], v[2], v[3]);
     n.h.bvi = -1;
@@ -1549,64 +1549,66 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
         if (pk.child < 0 && pk.e == nsq.best && !noised) { pk.child = nsq.bchild; pk.cterm = nsq.bterm(); }
         else pk.cterm = pk.child >= 0 ? (int)P.nd[pk.child].h.term : 0;
     }
-    // The descent's record queue (descent hints, mcts_device.h Node): the link records of the
-    // next levels' nodes q1 .. q3, loaded ahead. Leaving a level whose pick is the cached one
-    // asks for its child (the authoritative link) and the child's and grandchild's cached picks
-    // as the record's hints name them; a level takes its record from the queue when q1 is its
-    // node (always, once the queue is primed), so a correct chain of hints keeps three loads of
-    // the dependent chain in flight.
-    NodeLink cur = *reinterpret_cast<const NodeLink *>(&nsq);
-    NodeLink l1{-1, -1, -1, -1, 0}, l2{-1, -1, -1, -1, 0}, l3{-1, -1, -1, -1, 0};
-    int q1 = -1, q2 = -1, q3 = -1;
-    bool have_cur = state == LS_DESCEND;
     int bnode = nbrd ? -1 : node;                        // the node whose board the lane holds
     int miss = -1, leaf_node = -1, cbest = -1;
     uint64_t k0 = 0, k1 = 0;
     float val[4] = {0, 0, 0, 0};
-    int pend = -1, pend_n = 0, pend_x = 0;
+    // the descent reads ONE 16-byte link record per level: rec is `node`'s (nsq's at the start)
+    NodeLink rec = *reinterpret_cast<const NodeLink *>(&nsq);
+    int tv_node = -1;                                    // a stored terminal leaf: its end values
     // descend phase: every lane in DESCEND takes one level per round trip until it reaches the
     // edge it expands (or a terminal child); then the expansions of all lanes run together —
     // the expansion (board staging, transition, fingerprint, lookup) is long, and lanes
     // reaching it at different levels would otherwise run it once per level in turn
-    // (measured: 342 us per select at config 3 with the two phases interleaved)
+    // (measured: 342 us per select at config 3 with the two phases interleaved).
+    // The common level — the cached pick is linked and its child is not terminal — runs in a
+    // tight loop that carries only (node, depth, rec): a lane issues the child's record load,
+    // then its two path stores, and the next level waits for that load alone (gfx950 counts
+    // stores in vmcnt: vmcnt(2)); other levels (a scanned root pick, a terminal child, an
+    // edge to expand, the path limit) take the general step below it once.
     SPROBE(0)
     while (__ballot(state != LS_DONE)) {
       while (__ballot(state == LS_DESCEND)) {
-        if (state == LS_DESCEND) {
+        bool run = state == LS_DESCEND && !have_pk && nbrd;
+        while (__ballot(run)) {
+            if (run) {
+                const int c = rec.bchild;
+                run = c >= 0 && !rec.bterm() && depth < P.pcap;
+                if (run) {
+                    BCHK(IN_TREE(P, t, c, H->node_count), 52, c, t, (void)0);
+                    BCHK(P.nd[c].h.round == P.nd[node].h.round + 1, 30, ((long long)node << 32) | (uint32_t)c, t, (void)0);
+                    const NodeLink nx = link_of(P.nd, c);
+                    path_n[depth] = node; path_x[depth] = px_pack(rec.best, rec.ba());
+                    depth++;
+                    node = c;
+                    rec = nx;
+#if SELECT_PROBE
+                    plev++;
+#endif
+                }
+            }
+        }
+        if (state == LS_DESCEND) {                       // the general step
             if (depth >= P.pcap) {
                 state = LS_DONE; kind = LEAF_NONE; H->overflow = 2;
             } else {
-                if (!have_pk) {                          // ONE 16-byte record per level
-                    if (!have_cur) {
-                        if (q1 != node) { l1 = link_of(P.nd, node); q2 = -1; q3 = -1; }
-                        cur = l1;
-                        q1 = q2; l1 = l2; q2 = q3; l2 = l3; q3 = -1;
-                    }
-                    pk = Pick{cur.best, cur.ba(), cur.bchild, cur.bterm()};
-                }
-                const bool hinted = pk.e == cur.best;    // (the cached pick: its hints apply)
-                have_pk = false; have_cur = false;
-                cbest = cur.best;
+                if (!have_pk) pk = Pick{rec.best, rec.ba(), rec.bchild, rec.bterm()};
+                have_pk = false;
+                cbest = rec.best;
 #if SELECT_PROBE
                 plev++;
 #endif
-                if (pend >= 0) { path_n[pend] = pend_n; path_x[pend] = pend_x; }
-                pend = depth; pend_n = node; pend_x = px_pack(pk.e, pk.a);
+                path_n[depth] = node; path_x[depth] = px_pack(pk.e, pk.a);
                 depth++;
                 if (pk.child >= 0 && pk.cterm) {         // a terminal child (MCTS.py:125-132)
-                    kind = LEAF_TERMINAL;
-                    term_values(P, pk.child, val);
+                    kind = LEAF_TERMINAL;                // (its end values after the loop)
                     leaf_node = pk.child;
+                    tv_node = pk.child;
                     state = LS_DONE;
-                } else if (pk.child >= 0 && nbrd) {      // linked: no transition needed
+                } else if (pk.child >= 0 && nbrd) {      // linked (a scanned root pick)
                     BCHK(IN_TREE(P, t, pk.child, H->node_count), 52, pk.child, t, (void)0);
-                    BCHK(P.nd[pk.child].h.round == P.nd[node].h.round + 1, 30, ((long long)node << 32) | (uint32_t)pk.child, t,
-                         pk.child = pk.child);
+                    rec = link_of(P.nd, pk.child);
                     node = pk.child;
-                    const int w2 = hinted ? cur.h2 : -1, w3 = hinted ? cur.h3 : -1;
-                    if (q1 != node) { q1 = node; l1 = link_of(P.nd, node); q2 = -1; q3 = -1; }
-                    if (w2 >= 0 && q2 != w2) { q2 = w2; l2 = link_of(P.nd, w2); q3 = -1; }
-                    if (w3 >= 0 && q2 == w2 && q3 != w3) { q3 = w3; l3 = link_of(P.nd, w3); }
                 } else {
                     state = LS_EXPAND;
                 }
@@ -1641,7 +1643,7 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                     if (cached) { P.nd[node].h.bchild = child; P.nd[node].h.babt = (uint16_t)(pk.a | (ct << 15)); }
                     if (ct) {
                         kind = LEAF_TERMINAL;
-                        term_values(P, child, val);
+                        tv_node = child;
                         leaf_node = child;
                         state = LS_DONE;
                     }
@@ -1651,6 +1653,7 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                 BCHK(child < 0 || P.nd[child].h.round == (uint8_t)bt(row(s, 0), 6), 31,
                      ((long long)node << 32) | (uint32_t)child, t, child = child);
                 if (child >= 0) {                        // continue below the linked node
+                    rec = link_of(P.nd, child);
                     node = child;
                     bnode = child;
                     state = LS_DESCEND;
@@ -1683,7 +1686,7 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
         }
         SPROBE(3)
     }
-    if (pend >= 0) { path_n[pend] = pend_n; path_x[pend] = pend_x; }
+    if (tv_node >= 0) term_values(P, tv_node, val);
     if (act && root < 0) lane_fingerprint<N>(s, k0, k1);   // the root itself is the leaf
     if (act && kind == LEAF_NN) {                        // its board for k_leaf_mask / the network
         for (int u = 0; u < Conv<N>::UNITS; u++) Conv<N>::store(leaf_state + (size_t)t * Lx::S, s, u);
@@ -1992,6 +1995,23 @@ __device__ __forceinline__ int grow_at(const Pools &P, int t, int d, bool in) {
     return d == 0 ? ec : (vcap == 0 ? 1 : min(2 * vcap, ec));
 }
 
+// per-phase cycle probes of k_backup_h (diagnostic builds only, -DBACKUP_PROBE=1; never the
+// product): per wave, s_memtime deltas summed over the waves of every launch
+#ifndef BACKUP_PROBE
+#define BACKUP_PROBE 0
+#endif
+#if BACKUP_PROBE
+__device__ unsigned long long g_bk_probe[16];
+#define BPROBE(k)                                                  \
+    {                                                              \
+        const uint64_t c_ = __builtin_readcyclecounter();          \
+        bacc[k] += c_ - blast;                                     \
+        blast = c_;                                                \
+    }
+#else
+#define BPROBE(k)
+#endif
+
 #ifndef WD_MAX
 #define WD_MAX 4           // withdrawals per search (k_backup)
 #endif
@@ -2109,6 +2129,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         lid = path_n[depth];
     }
     const int dmax = max(__shfl(depth, 0, 64), __shfl(depth, 32, 64));   // (uniform group loops)
+#if BACKUP_PROBE
+    uint64_t bacc[6] = {0, 0, 0, 0, 0, 0}, blast = __builtin_readcyclecounter();
+    int bexact = 0, bgroups = 0;
+#endif
     // ---- pass A (as k_backup)
     Level V;
     load_levels_at(P, t, hl, depth, lid, V, act && hl < min(depth, 32));
@@ -2131,6 +2155,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         if (g0 == 0) V.nb = nb;
         else if (grow > 0) P.path_b[pb0 + g0 + hl] = nb;
     }
+    BPROBE(0)
     int g = -1, ec = 0;
     int64_t eb = -1;
     if (kind == LEAF_NN) {
@@ -2234,7 +2259,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         if (expand && hl == 0) {
             P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
             Node nn;
-            nn.h.bchild = -1; nn.h.h2 = -1; nn.h.h3 = -1;
+            nn.h.bchild = -1; nn.h.rsv0 = -1; nn.h.rsv1 = -1;
             nn.h.set_pick(bsel, bact, 0); nn.h.ns = 0;
             nn.h.term = 0; nn.h.round = (uint8_t)h_round; nn.h.bvi = -1;
             nn.h.qs = (double)val[0];
@@ -2250,6 +2275,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         if (expand) lid = g;
     }
     if (!done && depth > 0 && kind == LEAF_NN && hl == (depth - 1 < 32 ? depth - 1 : 32)) V.child = lid;
+    BPROBE(1)
     // ---- pass B (as k_backup), levels in groups of 32 per half
     int moved = 0x7fffffff, n_wide_lo = 0, n_wide_hi = 0, n_big_lo = 0, n_big_hi = 0;
     for (int g0 = 0; g0 < dmax; g0 += 32) {
@@ -2314,6 +2340,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             }
             V.rchild = V.rchild >= 0 ? V.rchild : V.child;
         }
+        BPROBE(2)
+#if BACKUP_PROBE
+        bgroups++;
+#endif
         const bool wide = in && V.r.vcnt > BK_WIDE;
         {
             const uint64_t wm = __ballot(wide && d > 0);
@@ -2355,6 +2385,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             uc = u;
         }
         wave_lds_fence();
+        BPROBE(3)
+#if BACKUP_PROBE
+        bexact += __popcll(__ballot(open));
+#endif
         for (uint64_t ex = __ballot(open); ex; ex &= ex - 1) {
             const int j = __ffsll((unsigned long long)ex) - 1;
             int rk, ak, ck, vk;
@@ -2365,21 +2399,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                         __builtin_amdgcn_readlane(ac, j), __builtin_amdgcn_readlane(rc, j), rk, ak, ck, vk);
             if (l == j) { bsel = rk; bact = ak; bch = ck; bvi = vk; }
         }
-        // descent hints: a level whose pick stays on the path edge names the new picks of the
-        // next two path levels (lanes hl + 1, hl + 2 of this half; none across a group boundary)
+        BPROBE(4)
         const bool stay = in && bsel == V.off;
         if (stay) { bch = V.rchild; bvi = vidx; }
-        const int src1 = min(l + 1, 63), src2 = min(l + 2, 63);
-        const int nb1 = __shfl(bch, src1, 64), nb2 = __shfl(bch, src2, 64);
-        const int ns1 = __shfl((int)stay, src1, 64);
-        const int hh2 = stay && hl < 31 && d + 1 < depth ? nb1 : -1;
-        const int hh3 = hh2 >= 0 && ns1 && hl < 30 && d + 2 < depth ? nb2 : -1;
         if (in) {                                        // the level's record, written once
             int bt_;
             if (stay) bt_ = kind == LEAF_TERMINAL && bch >= 0 && bch == lid;   // (the path's child:
             else bt_ = bch >= 0 ? (int)P.nd[bch].h.term : 0;                   //  terminal only as the leaf)
             NodeHot w;                                   // (the second half: written with a new record)
-            w.bchild = bch; w.h2 = hh2; w.h3 = hh3;
+            w.bchild = bch; w.rsv0 = -1; w.rsv1 = -1;
             w.set_pick(bsel, bact, bt_); w.ns = nns;
             w.term = 0; w.round = (uint8_t)V.round; w.bvi = (int16_t)bvi;
             w.qs = nqs;
@@ -2399,6 +2427,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         if (n_wide) H->exact_wide += n_wide;
         if (n_big) H->big_moves += n_big;
     }
+#if BACKUP_PROBE
+    BPROBE(5)
+    if (l == 0) {
+        for (int k = 0; k < 6; k++) atomicAdd(&g_bk_probe[k], (unsigned long long)bacc[k]);
+        atomicAdd(&g_bk_probe[6], 1ull);
+        atomicAdd(&g_bk_probe[7], (unsigned long long)bexact);
+        atomicAdd(&g_bk_probe[8], (unsigned long long)bgroups);
+    }
+#endif
 }
 
 // ------------------------------------------------------------ arena move
@@ -2729,6 +2766,20 @@ int spl_diag_select_probe(unsigned long long *out16, int reset) {
     if (reset) {
         unsigned long long z[16] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_sel_probe), z, sizeof(z)) != hipSuccess) return SPL_EDEVICE;
+    }
+    return 0;
+}
+#endif
+
+#if BACKUP_PROBE
+// k_backup_h phase probes: [0] header + pass A [1] expansion [2] pass B loads / updates [3]
+// screen [4] exact levels [5] record writes + end (cycles summed over waves), [6] waves, [7]
+// levels evaluated exactly, [8] level groups
+int spl_diag_backup_probe(unsigned long long *out16, int reset) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_bk_probe), 16 * 8) != hipSuccess) return SPL_EDEVICE;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bk_probe), z, sizeof(z)) != hipSuccess) return SPL_EDEVICE;
     }
     return 0;
 }

@@ -28,6 +28,23 @@
 
 #include "../../include/splendor_amd.h"
 
+// per-layer cycle probes (diagnostic builds only, -DNN_PROBE=1; never the product): wave 0's
+// s_memtime at every layer boundary, summed over the workgroups (spl_diag_nn_probe)
+#ifndef NN_PROBE
+#define NN_PROBE 0
+#endif
+#if NN_PROBE
+__device__ unsigned long long g_nn_probe[16];
+#define NPROBE(k)                                                  \
+    if (threadIdx.x == 0) {                                        \
+        const uint64_t c_ = __builtin_readcyclecounter();          \
+        atomicAdd(&g_nn_probe[k], (unsigned long long)(c_ - nlast)); \
+        nlast = c_;                                                \
+    }
+#else
+#define NPROBE(k)
+#endif
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -409,6 +426,10 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     RingS rings;                                           // per-column weight parts, one layer ahead
     rings_load<C1>(W + Nt::soff(0), wc, rings);
 
+#if NN_PROBE
+    uint64_t nlast = __builtin_readcyclecounter();
+    if (threadIdx.x == 0) atomicAdd(&g_nn_probe[15], 1ull);
+#endif
     // ---- input: x[column c][leaf i][row r] = state[leaf][r][c] as int8 (token c*32+i)
     int8_t *x0 = reinterpret_cast<int8_t *>(bufA);
     for (int j = tid; j < 7 * ML * X0S / 4; j += NNT) reinterpret_cast<int32_t *>(x0)[j] = 0;
@@ -473,6 +494,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 for (int r = 0; r < 16; r++)
                     bufA[((t0 + t) * ML + acc_row(r)) * XS + coloff] = f(acc[t][r], t0 + t);
     };
+    NPROBE(0)
     // ---- dense2d_1: relu(s1[c] * (W1 x + b1) + t1[c])
     // (each layer's bias is read before its GEMM, ahead of the next layer's ring: vmcnt
     // retires loads in order)
@@ -487,6 +509,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         store_tiles(col, [&](float x, int t) { return fmaxf((x + bias) * aff[t] + aff[7 + t], 0.f); });
         lds_barrier();
     }
+    NPROBE(1)
     // ---- dense2d_1[3]: relu(W2 x + b2)
     {
         const float bias = W[Nt::boff(1) + col];
@@ -495,6 +518,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         store_tiles(col, [&](float x, int) { return fmaxf(x + bias, 0.f); });
         lds_barrier();
     }
+    NPROBE(2)
     // ---- partialgpool_1: [max, mean over 4 groups of 8 of x[0:32]] ++ relu(BN(Wp1 x[32:] + bp1))
     {
         const float bias = W[Nt::boff(2) + col];  // 0-padded to 128 columns
@@ -523,6 +547,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             store_tiles(8 + col, [&](float x, int t) { return fmaxf((x + bias) * aff[14 + t] + aff[21 + t], 0.f); });
         lds_barrier();
     }
+    NPROBE(3)
     // ---- dense2d_3: relu(W3 x + b3), written straight into the flattened per-leaf image
     // Z[leaf][704] = [max_c<5 x[c][:64]][mean_c<5 x[c][:64]][x[5][:64]][x[6][:64]][x[c][64:], c<7]
     // (FlattenAndPartialGPool(64, 5)), so dense1d_4 reads plain rows
@@ -574,6 +599,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
         lds_barrier();
     }
+    NPROBE(4)
     // ---- per-leaf layers: split activations in SB0 / SB1 / SB2 (SplitAct), 16x16x32 tiles
     f32x4 a16[4][2];
     // bias of this lane's column in tile ct of a per-leaf layer (0-padded to whole tiles), read
@@ -644,10 +670,12 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         lds_barrier();
     };
     auto ringn = [&](int layer) { return [&, layer] { ringl_load<4>(W + Nt::soff(layer), w, 8, 8, ring1); }; };
+    NPROBE(5)
     pool44(SB0, SB1, 5, ringn(6));          // partialgpool_4
     dense128(SB1, SB2, 6, ringn(7));        // dense1d_5[0] (+BN folded)
     dense128(SB2, SB1, 7, ringn(8));        // dense1d_5[3]
     pool44(SB1, SB0, 8, ringn(9));          // partialgpool_5 -> trunk output in SB0
+    NPROBE(6)
     // ---- heads: PI[0] -> SB1, V[0] -> SB2 (no activation); wave w: column tile w of both
     constexpr int CT = ntiles16(ACT);      // PI[1] column tiles
     static_assert(CT > 24 && CT <= 32, "PI[1] tiles: 3 or 4 per wave");
@@ -661,6 +689,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         store_split(1, w, SB2, 0, 128, [&](float x) { return x + bv; });
         lds_barrier();
     }
+    NPROBE(7)
     // ---- PI[1] (409 outputs, 26 column tiles: waves 0-1 take 4, the others 3) and V[1]
     // (NP outputs, wave 7, whose ring is loaded behind its last PI[1] MFMA)
     {
@@ -703,6 +732,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
         lds_barrier();
     }
+    NPROBE(8)
     // ---- masked softmax (invalid -> -1e8, as the reference's masked_fill + log_softmax);
     // the wave's leaves are processed together so their reductions overlap
     {
@@ -747,6 +777,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             }
         }
     }
+    NPROBE(9)
 }
 
 inline int check_launch() { return hipGetLastError() == hipSuccess ? 0 : SPL_EDEVICE; }
@@ -754,6 +785,20 @@ inline int check_launch() { return hipGetLastError() == hipSuccess ? 0 : SPL_EDE
 }  // namespace
 
 extern "C" {
+
+#if NN_PROBE
+// k_nn_forward probes: wave 0's cycles summed over workgroups, [0] input staging [1] dense2d_1
+// [2] dense2d_1[3] [3] partialgpool_1 [4] dense2d_3 + flatten [5] dense1d_4 [6] pgp4 .. pgp5
+// [7] heads PI[0] / V[0] [8] PI[1] + V[1] [9] softmax, [15] workgroups
+int spl_diag_nn_probe(unsigned long long *out16, int reset) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_nn_probe), 16 * 8) != hipSuccess) return SPL_EDEVICE;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_nn_probe), z, sizeof(z)) != hipSuccess) return SPL_EDEVICE;
+    }
+    return 0;
+}
+#endif
 
 int spl_nn_packed_floats(int n_players) {
     switch (n_players) {

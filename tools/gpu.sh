@@ -9,21 +9,26 @@
 #   smoke     __graft_entry__.smoke()                                  -> gpurun_out/smoke.log
 #   bench     the default bench line (headline + secondary objects)    -> gpurun_out/bench.json
 #   selfplay  the config-3 headline alone                              -> gpurun_out/selfplay.json
-#   trace     config-3 kernel trace + stats (rocprofv3)                -> gpurun_out/prof_sp/
+#   trace     config-3 kernel trace + stats (rocprofv3)                -> gpurun_out/prof_sp/ (or prof_<TREE>)
 #   split     per-iteration kernel split from the trace (needs trace)  -> gpurun_out/split.txt
+#   spikes    the slowest launches of each kernel and their iterations (needs trace) -> gpurun_out/spikes.json
 #   pmc       PMC passes over the self-play kernels (pmc_selfplay.sh)  -> gpurun_out/pmc_sp/
 #   nn        full-batch network trace + HBM counters (nn_fullbatch.sh) -> gpurun_out/nnfb/
 #   ab        interleaved A/B of the product against each V in $AB: ablib/lib<V>.so, or a whole
 #             older tree ablib/<V>/ (bench.py + package) (config-3 bench twice each) -> gpurun_out/ab.txt
-#   probe     k_select_lanes phase probes (ablib/libprobe.so, -DSELECT_PROBE=1) -> gpurun_out/probe.json
+#   probe     k_select_lanes phase probes (ablib/lib<V>.so for V in ${PROBES:-probe}, -DSELECT_PROBE=1) -> gpurun_out/<V>.json
+#   nnprobe   per-layer cycle probes of the network kernel (ablib/libnnprobe.so, -DNN_PROBE=1) -> gpurun_out/nnprobe.json
 #   bounds    the bounds-checked build (ablib/libchk.so: tools/bounds_check.sh on
 #             the host first) under capacity pressure                   -> gpurun_out/bounds_chk.json
-# ROUND (default r05) names the summaries; EXTRA adds bench arguments to selfplay/trace.
+# ROUND (default r05) names the summaries; EXTRA adds bench arguments to selfplay/trace; TREE=<V>
+# makes trace / split / spikes run the older tree ablib/<V>/ (outputs *_<V>).
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 ROUND=${ROUND:-r05}
+TR=${TREE:-sp}                                             # trace / split / spikes: TREE=<V> traces
+TB=bench.py; [ -n "${TREE:-}" ] && TB="ablib/$TREE/bench.py"  # the older tree ablib/<V>/ instead
 step() {
     echo "$(date +%T) $1 start" >> gpurun_out/progress.log
     case "$1" in
@@ -38,12 +43,15 @@ step() {
         timeout -k 10 300 python3 -u bench.py --workload selfplay --no-cpu-baseline ${EXTRA:-} \
             > gpurun_out/selfplay.json 2> gpurun_out/selfplay.err ;;
     trace)
-        timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sp -o sp -- \
-            python3 bench.py --workload selfplay --steps 2000 --window 4000 --no-cpu-baseline ${EXTRA:-} \
-            > gpurun_out/prof_sp.log 2>&1 ;;
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TR -o sp -- \
+            python3 "$TB" --workload selfplay --steps 2000 --window 4000 --no-cpu-baseline ${EXTRA:-} \
+            > gpurun_out/prof_$TR.log 2>&1 ;;
     split)
-        python3 tools/trace_split.py "$(find gpurun_out/prof_sp -name '*kernel_trace.csv' | head -n 1)" 6000 \
-            > gpurun_out/split.txt ;;
+        python3 tools/trace_split.py "$(find gpurun_out/prof_$TR -name '*kernel_trace.csv' | head -n 1)" 6000 \
+            > gpurun_out/split_$TR.txt ;;
+    spikes)
+        python3 tools/trace_spikes.py "$(find gpurun_out/prof_$TR -name '*kernel_trace.csv' | head -n 1)" 4000 8 \
+            > gpurun_out/spikes_$TR.json ;;
     pmc)
         timeout -k 10 1000 bash tools/pmc_selfplay.sh gpurun_out/pmc_sp "$ROUND" > gpurun_out/pmc_sp.log 2>&1 ;;
     nn)
@@ -62,8 +70,13 @@ step() {
             done
         done ;;
     probe)
-        SPLENDOR_AMD_LIB=$PWD/ablib/libprobe.so timeout -k 10 200 python3 -u tools/select_probe.py \
-            > gpurun_out/probe.json 2> gpurun_out/probe.err ;;
+        for v in ${PROBES:-probe}; do
+            SPLENDOR_AMD_LIB=$PWD/ablib/lib$v.so timeout -k 10 200 python3 -u tools/select_probe.py \
+                > gpurun_out/$v.json 2> gpurun_out/$v.err || { echo "$v rc=$?" >> gpurun_out/progress.log; return 1; }
+        done ;;
+    nnprobe)
+        SPLENDOR_AMD_LIB=$PWD/ablib/libnnprobe.so timeout -k 10 200 python3 -u tools/nn_probe.py \
+            > gpurun_out/nnprobe.json 2> gpurun_out/nnprobe.err ;;
     bounds)
         SPLENDOR_AMD_LIB=$PWD/ablib/libchk.so timeout -k 10 300 python3 -u tools/bounds_check.py --tag chk \
             --iters "${ITERS:-6000}" > gpurun_out/bounds_chk.json 2> gpurun_out/bounds_chk.err ;;

@@ -29,17 +29,26 @@ def main():
     a = ap.parse_args()
     from splendor import _lib
     L = _lib.lib()
-    L.spl_diag_select_probe.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    has_sel = hasattr(L, "spl_diag_select_probe")   # (a -DBACKUP_PROBE=1 build has only that one)
+    if has_sel:
+        L.spl_diag_select_probe.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     out = (ctypes.c_ulonglong * 16)()
+
+    bk = (ctypes.c_ulonglong * 16)()
 
     def reset(sp):
         torch.cuda.synchronize()
-        L.spl_diag_select_probe(out, 1)
+        if has_sel:
+            L.spl_diag_select_probe(out, 1)
+        if hasattr(L, "spl_diag_backup_probe"):
+            L.spl_diag_backup_probe.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+            L.spl_diag_backup_probe(bk, 1)
     dev = torch.device("cuda", 0)
     r = bench.run_selfplay("config3", 0, 1, dev, None, a.steps, 20, a.prefill, 0, 0x5EED,
                            stagger=min(4800, a.prefill), on_steady=reset)
     torch.cuda.synchronize()
-    L.spl_diag_select_probe(out, 0)
+    if has_sel:
+        L.spl_diag_select_probe(out, 0)
     waves = max(int(out[5]), 1)
     names = ("prologue", "descents", "staging", "expansions", "leaf_outputs")
     res = {"steps": a.steps, "ms_per_iteration": r["elapsed"] / a.steps * 1e3, "waves": waves,
@@ -49,6 +58,13 @@ def main():
            "most_levels": int(out[10]), "expansion_rounds_per_wave": out[11] / waves,
            "cycles_per_level_of_deepest_lane": out[1] / max(out[8], 1),
            "leaf_depth_max": r["tree"]["leaf_depth_max"]}
+    if hasattr(L, "spl_diag_backup_probe"):
+        L.spl_diag_backup_probe.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+        L.spl_diag_backup_probe(bk, 0)
+        bw = max(int(bk[6]), 1)
+        res["backup"] = {"waves": bw, "cycles_per_wave": {n: bk[k] / bw for k, n in enumerate(
+            ("pass_a", "expansion", "pass_b_updates", "screen", "exact_levels", "writes_end"))},
+            "exact_levels_per_wave": bk[7] / bw, "groups_per_wave": bk[8] / bw}
     print(json.dumps(res), flush=True)
 
 
