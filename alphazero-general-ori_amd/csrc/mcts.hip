@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstring>
 #include <new>
 
 #include "../../include/splendor_amd.h"
@@ -955,7 +956,9 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
 // slowest collection however many run beside it: the cap is one round of workgroups (a
 // smaller cap spreads a burst over more launches that each pay that latency — round 4
 // measured 16 per launch at 195 us per launch, ~390 us per iteration at config 3).
-constexpr int GC_WG = 256;      // one per CU
+#ifndef GC_WG
+#define GC_WG 256               // one per CU (168 VGPRs x 8 waves: a second one does not fit;
+#endif                          //  512 measured no change, r05)
 #ifndef GC_SHOULD_CAP
 #define GC_SHOULD_CAP GC_WG
 #endif
@@ -2001,7 +2004,10 @@ __device__ __forceinline__ int grow_at(const Pools &P, int t, int d, bool in) {
 #define BACKUP_PROBE 0
 #endif
 #if BACKUP_PROBE
-__device__ unsigned long long g_bk_probe[16];
+// one slot per wave of a launch (plain read-modify-writes: launches run one after another), so
+// the probes add no atomic contention of their own; spl_diag_backup_probe sums the slots
+constexpr int BK_PSLOTS = 32768;
+__device__ unsigned long long g_bk_probe[BK_PSLOTS][16];
 #define BPROBE(k)                                                  \
     {                                                              \
         const uint64_t c_ = __builtin_readcyclecounter();          \
@@ -2130,7 +2136,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     }
     const int dmax = max(__shfl(depth, 0, 64), __shfl(depth, 32, 64));   // (uniform group loops)
 #if BACKUP_PROBE
-    uint64_t bacc[6] = {0, 0, 0, 0, 0, 0}, blast = __builtin_readcyclecounter();
+    uint64_t bacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, blast = __builtin_readcyclecounter();
     int bexact = 0, bgroups = 0;
 #endif
     // ---- pass A (as k_backup)
@@ -2169,6 +2175,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     }
     g = __shfl(g, hb, 64);
     eb = shfl64(eb, hb);
+    BPROBE(6)
     if (act && (fail || (kind == LEAF_NN && eb < 0)) && C.selfplay && depth > 0 &&
         (h_gc == 0 || h_gc == 5 || (h_gc == 2 && H->wd_search < WD_MAX))) {
         if (hl == 0) {                                   // withdrawn (see k_backup)
@@ -2191,14 +2198,16 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         root_noise_lds(C, __builtin_amdgcn_readlane(t, j), ST_DIR | (uint32_t)__builtin_amdgcn_readlane(H->move_no, j),
                        Sj.pr, Sj.bits, __builtin_amdgcn_readlane(ec, j));
     }
+    if (expand && !noise) {
+        float *pr = S.pr;
+        const float sum = half_np_sum409(pr);
+        wave_lds_fence();
+        for (int a = hl; a < SPL_ACTIONS; a += 32) pr[a] = pr[a] / sum;
+        wave_lds_fence();
+    }
+    BPROBE(7)
     if (expand) {
         float *pr = S.pr;
-        if (!noise) {
-            const float sum = half_np_sum409(pr);
-            wave_lds_fence();
-            for (int a = hl; a < SPL_ACTIONS; a += 32) pr[a] = pr[a] / sum;
-            wave_lds_fence();
-        }
         int run = 0;
 #pragma unroll
         for (int k = 0; k < 7; k++) {
@@ -2217,6 +2226,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         wave_lds_fence();
         half_write_new_run(P, eb, ec, S.cp, S.ca);
     }
+    BPROBE(8)
     {                                                    // the new node's arg-max (see k_backup)
         int bsel = -1, bact = 0;
         double bu = -INFINITY;
@@ -2256,6 +2266,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         npm = half_max_f32(npm);
         if (narg) bsel = r;
         else bact = 0;
+        BPROBE(9)
         if (expand && hl == 0) {
             P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
             Node nn;
@@ -2430,10 +2441,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
 #if BACKUP_PROBE
     BPROBE(5)
     if (l == 0) {
-        for (int k = 0; k < 6; k++) atomicAdd(&g_bk_probe[k], (unsigned long long)bacc[k]);
-        atomicAdd(&g_bk_probe[6], 1ull);
-        atomicAdd(&g_bk_probe[7], (unsigned long long)bexact);
-        atomicAdd(&g_bk_probe[8], (unsigned long long)bgroups);
+        unsigned long long *g = g_bk_probe[(blockIdx.x * WAVES + w) % BK_PSLOTS];
+        for (int k = 0; k < 10; k++) g[k] += bacc[k];
+        g[12] += 1;
+        g[13] += bexact;
+        g[14] += bgroups;
     }
 #endif
 }
@@ -2772,14 +2784,19 @@ int spl_diag_select_probe(unsigned long long *out16, int reset) {
 #endif
 
 #if BACKUP_PROBE
-// k_backup_h phase probes: [0] header + pass A [1] expansion [2] pass B loads / updates [3]
-// screen [4] exact levels [5] record writes + end (cycles summed over waves), [6] waves, [7]
-// levels evaluated exactly, [8] level groups
+// k_backup_h phase probes (cycles summed over waves): [0] header + pass A [1] expansion's node
+// record / table insert [2] pass B loads / updates [3] screen [4] exact levels [5] record writes
+// + end, expansion's [6] allocations [7] noise + normalisation [8] sorted run [9] arg-max; [12]
+// waves, [13] levels evaluated exactly, [14] level groups
 int spl_diag_backup_probe(unsigned long long *out16, int reset) {
-    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_bk_probe), 16 * 8) != hipSuccess) return SPL_EDEVICE;
+    static unsigned long long h[BK_PSLOTS][16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bk_probe), sizeof(h)) != hipSuccess) return SPL_EDEVICE;
+    for (int k = 0; k < 16; k++) out16[k] = 0;
+    for (int i = 0; i < BK_PSLOTS; i++)
+        for (int k = 0; k < 16; k++) out16[k] += h[i][k];
     if (reset) {
-        unsigned long long z[16] = {0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bk_probe), z, sizeof(z)) != hipSuccess) return SPL_EDEVICE;
+        memset(h, 0, sizeof(h));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bk_probe), h, sizeof(h)) != hipSuccess) return SPL_EDEVICE;
     }
     return 0;
 }

@@ -12,8 +12,9 @@
 //   * Per-column layers (dense2d_1, its second linear, partialgpool_1, dense2d_3; round 4)
 //     on v_mfma_f32_32x32x16_bf16: the 7 board columns of the 32 leaves as 7 token tiles of
 //     32 (channel-major, so the per-column BatchNorm affine is uniform across a tile); wave w
-//     owns output columns [32(w&3), 32(w&3)+32) for half of the token tiles (w>>2); the
-//     activations (f32 LDS rows, 132-float stride) are split in registers.
+//     owns output column blocks 2(w&1), 2(w&1)+1 of token tiles 2(w>>1), 2(w>>1)+1 (wave 6, 7:
+//     tile 6 alone); the activations (f32 LDS rows, 132-float stride) are split in registers,
+//     each A fragment once for both column blocks (round 5: 2 splits per token tile, was 4).
 //   * Per-leaf layers (round 5) on v_mfma_f32_16x16x32_bf16 over 16-leaf row tiles. Their
 //     activations live in LDS ALREADY SPLIT: each producing epilogue writes its outputs as
 //     three bf16 planes (SplitAct), split once instead of once per consuming wave (8 waves
@@ -49,6 +50,7 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int NNT = 512;      // threads per workgroup (8 waves)
 constexpr int ML = 32;         // leaves per workgroup
@@ -141,33 +143,39 @@ template <int V> struct IntC {
 // accumulator.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#ifndef NN_PFS
-#define NN_PFS 2
+#ifndef NN_PFC
+#define NN_PFC 1
 #endif
-constexpr int PFS = NN_PFS;            // chunks of weight parts in flight
-struct RingS {
-    bf16x8 b[PFS][3];
+constexpr int PFC = NN_PFC;            // per-column layers: chunks in flight (two blocks each)
+struct RingS {                         // two column blocks' weight parts, PFC chunks ahead
+    bf16x8 b[PFC][2][3];
 };
 struct F8 {
     float4 lo, hi;                     // 8 consecutive k of one lane's A row
 };
 
+// the bf16 pair (upper halves of a, b) -> one dword, b low: one v_perm_b32
+__device__ __forceinline__ uint32_t hi_pair(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
 __device__ __forceinline__ void split8(const F8 &x, bf16x8 &hi, bf16x8 &mid, bf16x8 &lo) {
     const float xs[8] = {x.lo.x, x.lo.y, x.lo.z, x.lo.w, x.hi.x, x.hi.y, x.hi.z, x.hi.w};
-    uint32_t h[8], m[8], l[8];
+    float r1[8], r2[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        h[j] = __float_as_uint(xs[j]) & 0xFFFF0000u;
-        const float r1 = xs[j] - __uint_as_float(h[j]);
-        m[j] = __float_as_uint(r1) & 0xFFFF0000u;
-        l[j] = __float_as_uint(r1 - __uint_as_float(m[j]));
+    for (int j = 0; j < 8; j += 2) {                     // (pairs: v_pk_add_f32)
+        const f32x2 x2 = {xs[j], xs[j + 1]};
+        const f32x2 h2 = {__uint_as_float(__float_as_uint(xs[j]) & 0xFFFF0000u),
+                          __uint_as_float(__float_as_uint(xs[j + 1]) & 0xFFFF0000u)};
+        const f32x2 a2 = x2 - h2;
+        const f32x2 m2 = {__uint_as_float(__float_as_uint(a2[0]) & 0xFFFF0000u),
+                          __uint_as_float(__float_as_uint(a2[1]) & 0xFFFF0000u)};
+        const f32x2 b2 = a2 - m2;
+        r1[j] = a2[0]; r1[j + 1] = a2[1]; r2[j] = b2[0]; r2[j + 1] = b2[1];
     }
     u32x4 H, M, L;
 #pragma unroll
     for (int p = 0; p < 4; p++) {
-        H[p] = (h[2 * p] >> 16) | h[2 * p + 1];
-        M[p] = (m[2 * p] >> 16) | m[2 * p + 1];
-        L[p] = (l[2 * p] >> 16) | (l[2 * p + 1] & 0xFFFF0000u);
+        H[p] = hi_pair(__float_as_uint(xs[2 * p]), __float_as_uint(xs[2 * p + 1]));
+        M[p] = hi_pair(__float_as_uint(r1[2 * p]), __float_as_uint(r1[2 * p + 1]));
+        L[p] = hi_pair(__float_as_uint(r2[2 * p]), __float_as_uint(r2[2 * p + 1]));
     }
     hi = __builtin_bit_cast(bf16x8, H);
     mid = __builtin_bit_cast(bf16x8, M);
@@ -179,73 +187,79 @@ __device__ __forceinline__ bf16x8 i8_to_bf16x8(int v0, int v1) {
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         const int v = p < 2 ? v0 : v1, sh = 16 * (p & 1);
-        const uint32_t e0 = __float_as_uint((float)(int8_t)(v >> sh)) >> 16;
-        const uint32_t e1 = __float_as_uint((float)(int8_t)(v >> (sh + 8))) & 0xFFFF0000u;
-        r[p] = e0 | e1;
+        r[p] = hi_pair(__float_as_uint((float)(int8_t)(v >> sh)), __float_as_uint((float)(int8_t)(v >> (sh + 8))));
     }
     return __builtin_bit_cast(bf16x8, r);
 }
 
-// first PFS chunks of column block nt of a split layer (C chunks of 16 k) into the ring
+// first PFC chunks of column blocks nt0, nt0 + 1 of a split layer (C chunks of 16 k) into the ring
 template <int C>
-__device__ __forceinline__ void rings_load(const float *__restrict__ ws, int nt, RingS &r) {
-    const bf16x8 *w = reinterpret_cast<const bf16x8 *>(ws) + (size_t)nt * C * 3 * 64 + (threadIdx.x & 63);
+__device__ __forceinline__ void rings_load(const float *__restrict__ ws, int nt0, RingS &r) {
+    const bf16x8 *w = reinterpret_cast<const bf16x8 *>(ws) + (size_t)nt0 * C * 3 * 64 + (threadIdx.x & 63);
 #pragma unroll
-    for (int p = 0; p < PFS; p++)
+    for (int p = 0; p < PFC; p++)
 #pragma unroll
-        for (int q = 0; q < 3; q++) r.b[p][q] = w[((p < C ? p : C - 1) * 3 + q) * 64];
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int q = 0; q < 3; q++) r.b[p][b][q] = w[b * C * 3 * 64 + ((p < C ? p : C - 1) * 3 + q) * 64];
 }
 
-// gemm_tiles on split operands: token tiles t0 .. t0+T-1 x column block nt over C chunks of
-// 16 k. INT8: afetch(t, k) -> bf16x8 (exact A, three products); else afetch(t, k) -> F8
-// (A split here, six products). Lane l: A[row l % 32][k = 16 c + 8 (l / 32) + j].
+// gemm_tiles on split operands: token tiles t0 .. t0+T-1 x column blocks nt0, nt0 + 1 over C
+// chunks of 16 k (accumulator 2 t + b). INT8: afetch(t, k) -> bf16x8 (exact A, three
+// products); else afetch(t, k) -> F8, split here once for both column blocks (six products
+// each, the five smaller first, into the tile's one accumulator: 6 roundings per 16 k, still
+// fewer than the f32 MFMA's one per 2 k; the 4 tiles' second accumulators would not fit the
+// register budget next to the two blocks' weight ring). Lane l: A[row l % 32][k = 16 c + 8 (l / 32) + j].
 template <int T, int C, bool INT8, class AF, class NX>
-__device__ __forceinline__ void gemm_split(const float *__restrict__ ws, int nt, int t0, RingS &r, AF afetch,
+__device__ __forceinline__ void gemm_split(const float *__restrict__ ws, int nt0, int t0, RingS &r, AF afetch,
                                            f32x16 *acc, NX next) {
     const int lane = threadIdx.x & 63, h = lane >> 5;
-    const bf16x8 *w = reinterpret_cast<const bf16x8 *>(ws) + (size_t)nt * C * 3 * 64 + lane;
-    f32x16 acl[T];                                       // the five smaller products
+    const bf16x8 *w = reinterpret_cast<const bf16x8 *>(ws) + (size_t)nt0 * C * 3 * 64 + lane;
 #pragma unroll
-    for (int t = 0; t < T; t++) { acc[t] = zero16(); acl[t] = zero16(); }
+    for (int i = 0; i < 2 * T; i++) acc[i] = zero16();
 #pragma unroll
     for (int c = 0; c < C; c++) {
-        const bf16x8 b0 = r.b[c % PFS][0], b1 = r.b[c % PFS][1], b2 = r.b[c % PFS][2];
-        if (c + PFS < C)
+        bf16x8 bb[2][3];
 #pragma unroll
-            for (int q = 0; q < 3; q++) r.b[c % PFS][q] = w[((c + PFS) * 3 + q) * 64];
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int q = 0; q < 3; q++) bb[b][q] = r.b[c % PFC][b][q];
+        if (c + PFC < C)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int q = 0; q < 3; q++) r.b[c % PFC][b][q] = w[b * C * 3 * 64 + ((c + PFC) * 3 + q) * 64];
+        // (product-major order: the 2 T accumulators' chains interleave, no MFMA waits on the
+        // one just issued)
         if constexpr (INT8) {
             bf16x8 a[T];
 #pragma unroll
             for (int t = 0; t < T; t++) a[t] = afetch(t0 + t, 16 * c + 8 * h);
 #pragma unroll
-            for (int t = 0; t < T; t++) {
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b2, acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b1, acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b0, acc[t], 0, 0, 0);
-            }
+            for (int p = 2; p >= 0; p--)
+#pragma unroll
+                for (int t = 0; t < T; t++)
+#pragma unroll
+                    for (int b = 0; b < 2; b++)
+                        acc[2 * t + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], bb[b][p], acc[2 * t + b], 0, 0, 0);
         } else {
-            F8 x[T];
+            bf16x8 a[T][3];
 #pragma unroll
-            for (int t = 0; t < T; t++) x[t] = afetch(t0 + t, 16 * c + 8 * h);
+            for (int t = 0; t < T; t++) split8(afetch(t0 + t, 16 * c + 8 * h), a[t][0], a[t][1], a[t][2]);
+            // (A part, B part) of the six products, smallest first
+            constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
-            for (int t = 0; t < T; t++) {
-                bf16x8 a0, a1, a2;
-                split8(x[t], a0, a1, a2);
-                acl[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acl[t], 0, 0, 0);
-                acl[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acl[t], 0, 0, 0);
-                acl[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acl[t], 0, 0, 0);
-                acl[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acl[t], 0, 0, 0);
-                acl[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acl[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[t], 0, 0, 0);
-            }
+            for (int p = 0; p < 6; p++)
+#pragma unroll
+                for (int t = 0; t < T; t++)
+#pragma unroll
+                    for (int b = 0; b < 2; b++)
+                        acc[2 * t + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t][PA[p]], bb[b][PB[p]], acc[2 * t + b], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
     }
     next();
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!INT8)
-#pragma unroll
-        for (int t = 0; t < T; t++) acc[t] += acl[t];
 }
 
 
@@ -413,7 +427,9 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ uint64_t mskl[ML * 7];                      // legality masks (read at the softmax)
     // wave index in an SGPR: every per-wave choice below is a scalar branch
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, li = lane & 31;
-    const int wc = w & 3, wg = w >> 2;                     // column block, wave group
+    // per-column layers: wave w owns column blocks 2 cp, 2 cp + 1 of token tiles 2 q, 2 q + 1
+    // (q = 3: tile 6 alone), so each token tile's activations are split by 2 waves, not 4
+    const int cp = w & 1, q = w >> 1;
     const int b0 = blockIdx.x * ML;
     const int cnt = count ? __builtin_amdgcn_readfirstlane(*count) : B;
     if (b0 >= cnt) return;
@@ -421,10 +437,10 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // row of leaf i of this tile (its board, mask and outputs)
     const auto rowof = [&](int i) -> size_t { return idx ? (size_t)idx[b0 + i] : (size_t)(b0 + i); };
     const float *aff = W + Nt::AFF;                        // s1, t1, sp1, tp1
-    const int t0 = 4 * wg, ntok = wg ? 3 : 4;              // this wave's token tiles (per-column layers)
+    const int t0 = 2 * q, ntok = q == 3 ? 1 : 2;           // this wave's token tiles (per-column layers)
     constexpr int C1 = kp16(R) / 16;
     RingS rings;                                           // per-column weight parts, one layer ahead
-    rings_load<C1>(W + Nt::soff(0), wc, rings);
+    rings_load<C1>(W + Nt::soff(0), 2 * cp, rings);
 
 #if NN_PROBE
     uint64_t nlast = __builtin_readcyclecounter();
@@ -467,17 +483,16 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     lds_barrier();
 
-    f32x16 acc[4];
-    const int col = 32 * wc + acc_col();
-    // this wave's 4 (group 0) or 3 (group 1) token tiles of column block wc
+    f32x16 acc[4];                                         // token tile t, column block b: acc[2 t + b]
+    auto colb = [&](int b) { return 32 * (2 * cp + b) + acc_col(); };
     // (c_const: chunks of 16 k; i8_const: A is the int8 input)
     auto gemm_cols = [&](auto c_const, auto i8_const, const float *ws, auto afetch, auto next) {
         constexpr int C = decltype(c_const)::value;
         constexpr bool I8 = decltype(i8_const)::value != 0;
-        if (wg == 0)
-            gemm_split<4, C, I8>(ws, wc, 0, rings, afetch, acc, next);
+        if (ntok == 2)
+            gemm_split<2, C, I8>(ws, 2 * cp, t0, rings, afetch, acc, next);
         else
-            gemm_split<3, C, I8>(ws, wc, 4, rings, afetch, acc, next);
+            gemm_split<1, C, I8>(ws, 2 * cp, t0, rings, afetch, acc, next);
     };
     auto fetchA8 = [&](int col0) {
         return [&, col0](int t, int c) {
@@ -485,66 +500,72 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             return F8{ld4(p), ld4(p + 4)};
         };
     };
-    // per-column epilogue over this wave's token tiles: dst = f(acc, t, n)
-    auto store_tiles = [&](int coloff, auto f) {
+    // per-column epilogue over this wave's tiles, output columns < nmax: dst = f(acc, t, b)
+    auto store_tiles = [&](int coloff, int nmax, auto f) {
 #pragma unroll
-        for (int t = 0; t < 4; t++)
+        for (int t = 0; t < 2; t++)
             if (t < ntok)
 #pragma unroll
-                for (int r = 0; r < 16; r++)
-                    bufA[((t0 + t) * ML + acc_row(r)) * XS + coloff] = f(acc[t][r], t0 + t);
+                for (int b = 0; b < 2; b++)
+                    if (colb(b) < nmax)
+#pragma unroll
+                        for (int r = 0; r < 16; r++)
+                            bufA[((t0 + t) * ML + acc_row(r)) * XS + coloff + colb(b)] = f(acc[2 * t + b][r], t0 + t, b);
     };
+    auto biases = [&](int layer, float *bb) { bb[0] = W[Nt::boff(layer) + colb(0)]; bb[1] = W[Nt::boff(layer) + colb(1)]; };
     NPROBE(0)
     // ---- dense2d_1: relu(s1[c] * (W1 x + b1) + t1[c])
     // (each layer's bias is read before its GEMM, ahead of the next layer's ring: vmcnt
     // retires loads in order)
     {
-        const float bias = W[Nt::boff(0) + col];
+        float bias[2];
+        biases(0, bias);
         // (k past R reads zero padding or the next row's bytes: their weights are 0)
         gemm_cols(IntC<C1>(), IntC<1>(), W + Nt::soff(0), [&](int t, int c) {
             const int32_t *p = reinterpret_cast<const int32_t *>(x0 + (t * ML + li) * X0S + c);
             return i8_to_bf16x8(p[0], p[1]);
-        }, [&] { rings_load<8>(W + Nt::soff(1), wc, rings); });
+        }, [&] { rings_load<8>(W + Nt::soff(1), 2 * cp, rings); });
         lds_barrier();
-        store_tiles(col, [&](float x, int t) { return fmaxf((x + bias) * aff[t] + aff[7 + t], 0.f); });
+        store_tiles(0, 128, [&](float x, int t, int b) { return fmaxf((x + bias[b]) * aff[t] + aff[7 + t], 0.f); });
         lds_barrier();
     }
     NPROBE(1)
     // ---- dense2d_1[3]: relu(W2 x + b2)
     {
-        const float bias = W[Nt::boff(1) + col];
-        gemm_cols(IntC<8>(), IntC<0>(), W + Nt::soff(1), fetchA8(0), [&] { rings_load<6>(W + Nt::soff(2), wc, rings); });
+        float bias[2];
+        biases(1, bias);
+        gemm_cols(IntC<8>(), IntC<0>(), W + Nt::soff(1), fetchA8(0), [&] { rings_load<6>(W + Nt::soff(2), 2 * cp, rings); });
         lds_barrier();
-        store_tiles(col, [&](float x, int) { return fmaxf(x + bias, 0.f); });
+        store_tiles(0, 128, [&](float x, int, int b) { return fmaxf(x + bias[b], 0.f); });
         lds_barrier();
     }
     NPROBE(2)
     // ---- partialgpool_1: [max, mean over 4 groups of 8 of x[0:32]] ++ relu(BN(Wp1 x[32:] + bp1))
     {
-        const float bias = W[Nt::boff(2) + col];  // 0-padded to 128 columns
-        gemm_cols(IntC<6>(), IntC<0>(), W + Nt::soff(2), fetchA8(32), [&] { rings_load<8>(W + Nt::soff(3), wc, rings); });
+        float bias[2];                     // (0-padded to 128 columns)
+        biases(2, bias);
+        gemm_cols(IntC<6>(), IntC<0>(), W + Nt::soff(2), fetchA8(32), [&] { rings_load<8>(W + Nt::soff(3), 2 * cp, rings); });
         constexpr int NQ = (7 * ML * 8 + NNT - 1) / NNT;
         float pv[NQ];
 #pragma unroll
-        for (int q = 0; q < NQ; q++) {
-            const int item = tid + NNT * q, tok = item >> 3, j = item & 7, g = j & 3;
-            pv[q] = 0.f;
+        for (int u = 0; u < NQ; u++) {
+            const int item = tid + NNT * u, tok = item >> 3, j = item & 7, g = j & 3;
+            pv[u] = 0.f;
             if (item < 7 * ML * 8) {
                 const float *p = bufA + tok * XS + 8 * g;
                 float m = p[0], s = p[0];
 #pragma unroll
                 for (int k = 1; k < 8; k++) { m = fmaxf(m, p[k]); s += p[k]; }
-                pv[q] = j < 4 ? m : s / 8.f;
+                pv[u] = j < 4 ? m : s / 8.f;
             }
         }
         lds_barrier();
 #pragma unroll
-        for (int q = 0; q < NQ; q++) {
-            const int item = tid + NNT * q;
-            if (item < 7 * ML * 8) bufA[(item >> 3) * XS + (item & 7)] = pv[q];
+        for (int u = 0; u < NQ; u++) {
+            const int item = tid + NNT * u;
+            if (item < 7 * ML * 8) bufA[(item >> 3) * XS + (item & 7)] = pv[u];
         }
-        if (col < 120)
-            store_tiles(8 + col, [&](float x, int t) { return fmaxf((x + bias) * aff[14 + t] + aff[21 + t], 0.f); });
+        store_tiles(8, 120, [&](float x, int t, int b) { return fmaxf((x + bias[b]) * aff[14 + t] + aff[21 + t], 0.f); });
         lds_barrier();
     }
     NPROBE(3)
@@ -561,41 +582,62 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int rt4 = w & 1, ct4 = 2 * (w >> 1);
     RingL<2, 2> ring2;
     {
-        const float bias = W[Nt::boff(3) + col];
+        float bias[2];
+        biases(3, bias);
         gemm_cols(IntC<8>(), IntC<0>(), W + Nt::soff(3), fetchA8(0),
                   [&] { ringl_load<22>(W + Nt::soff(4), ct4, 1, 8, ring2); });
         lds_barrier();
 #pragma unroll
-        for (int t = 0; t < 4; t++)
+        for (int i = 0; i < 4; i++)
 #pragma unroll
-            for (int r = 0; r < 16; r++) acc[t][r] = fmaxf(acc[t][r] + bias, 0.f);
-        if (col >= 64) {
+            for (int r = 0; r < 16; r++) acc[i][r] = fmaxf(acc[i][r] + bias[i & 1], 0.f);
+        // channels 0-63 of board columns 0-4: max and mean in column order (((c0 + c1) + c2) + c3)
+        // + c4 over three steps (q = 0, 1, 2), partials in `part`; columns 5, 6 pass through
+        if (cp == 1) {                     // channels 64-127
 #pragma unroll
-            for (int t = 0; t < 4; t++)
+            for (int t = 0; t < 2; t++)
                 if (t < ntok)
 #pragma unroll
-                    for (int r = 0; r < 16; r++) Z[acc_row(r) * ZS + 256 + 64 * (t0 + t) + col - 64] = acc[t][r];
-        } else if (wg == 0) {              // channels 0-3: partial max / sum -> part
+                    for (int b = 0; b < 2; b++)
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                part[acc_row(r) * 128 + col] = fmaxf(fmaxf(acc[0][r], acc[1][r]), fmaxf(acc[2][r], acc[3][r]));
-                part[acc_row(r) * 128 + 64 + col] = acc[0][r] + acc[1][r] + acc[2][r] + acc[3][r];
-            }
-        } else {                           // channels 5, 6 pass through
+                        for (int r = 0; r < 16; r++)
+                            Z[acc_row(r) * ZS + 256 + 64 * (t0 + t) + colb(b) - 64] = acc[2 * t + b][r];
+        } else if (q == 0) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                Z[acc_row(r) * ZS + 128 + col] = acc[1][r];
-                Z[acc_row(r) * ZS + 192 + col] = acc[2][r];
-            }
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    part[acc_row(r) * 128 + colb(b)] = fmaxf(acc[b][r], acc[2 + b][r]);
+                    part[acc_row(r) * 128 + 64 + colb(b)] = acc[b][r] + acc[2 + b][r];
+                }
         }
         lds_barrier();
-        if (col < 64 && wg == 1) {         // channel 4 closes the pool
+        if (cp == 0 && q == 1) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int i = acc_row(r);
-                Z[i * ZS + col] = fmaxf(part[i * 128 + col], acc[0][r]);
-                Z[i * ZS + 64 + col] = (part[i * 128 + 64 + col] + acc[0][r]) / 5.f;
-            }
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    float *pm = part + acc_row(r) * 128 + colb(b);
+                    pm[0] = fmaxf(pm[0], fmaxf(acc[b][r], acc[2 + b][r]));
+                    pm[64] = (pm[64] + acc[b][r]) + acc[2 + b][r];
+                }
+        }
+        lds_barrier();
+        if (cp == 0 && q == 2) {           // column 4 closes the pool, column 5 passes through
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int i = acc_row(r), c = colb(b);
+                    Z[i * ZS + c] = fmaxf(part[i * 128 + c], acc[b][r]);
+                    Z[i * ZS + 64 + c] = (part[i * 128 + 64 + c] + acc[b][r]) / 5.f;
+                    Z[i * ZS + 128 + c] = acc[2 + b][r];
+                }
+        } else if (cp == 0 && q == 3) {    // column 6 passes through
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) Z[acc_row(r) * ZS + 192 + colb(b)] = acc[b][r];
         }
         lds_barrier();
     }

@@ -61,10 +61,11 @@ def main():
     if hasattr(L, "spl_diag_backup_probe"):
         L.spl_diag_backup_probe.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
         L.spl_diag_backup_probe(bk, 0)
-        bw = max(int(bk[6]), 1)
+        bw = max(int(bk[12]), 1)
         res["backup"] = {"waves": bw, "cycles_per_wave": {n: bk[k] / bw for k, n in enumerate(
-            ("pass_a", "expansion", "pass_b_updates", "screen", "exact_levels", "writes_end"))},
-            "exact_levels_per_wave": bk[7] / bw, "groups_per_wave": bk[8] / bw}
+            ("pass_a", "expansion_node_write", "pass_b_updates", "screen", "exact_levels", "writes_end",
+             "expansion_alloc", "expansion_normalise", "expansion_sorted_run", "expansion_argmax"))},
+            "exact_levels_per_wave": bk[13] / bw, "groups_per_wave": bk[14] / bw}
     print(json.dumps(res), flush=True)
 
 
