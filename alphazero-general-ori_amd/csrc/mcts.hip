@@ -2078,23 +2078,31 @@ __device__ __forceinline__ float half_np_sum409(const float *a) {
     const float b2 = __shfl(blockv, hb + 16, 64), b3 = __shfl(blockv, hb + 24, 64);
     return (b0 + b1) + (b2 + b3);
 }
-// write_sorted_run of a new node (no visit records yet) on a half
+// write_sorted_run of a new node (no visit records yet) on a half: edge i's rank is the number
+// of edges with a larger prior or an equal one earlier in action order. cp: 16-byte aligned,
+// -inf past ec up to a multiple of 4 (never counted: priors are >= 0), read 4 at a time.
 __device__ __forceinline__ void half_write_new_run(const Pools &P, int64_t eb, int ec, const float *cp,
                                                    const int16_t *ca) {
+    const float4 *c4 = reinterpret_cast<const float4 *>(cp);
+    const int n4 = (ec + 3) >> 2;
     for (int i = lane_id() & 31; i < ec; i += 32) {
         const float pi = cp[i];
         int r = 0;
-        for (int j = 0; j < ec; j++) {
-            const float pj = cp[j];
-            r += (pj > pi) || (pj == pi && j < i);
+        for (int q = 0; q < n4; q++) {
+            const float4 v = c4[q];
+            const int j = 4 * q;
+            r += (v.x > pi) || (v.x == pi && j < i);
+            r += (v.y > pi) || (v.y == pi && j + 1 < i);
+            r += (v.z > pi) || (v.z == pi && j + 2 < i);
+            r += (v.w > pi) || (v.w == pi && j + 3 < i);
         }
         *P.ep(eb + r) = EdgeP{pi, ca[i], (int16_t)-1};
     }
 }
-struct BkScr {                         // a half's scratch: the leaf's policy and mask, its run
-    uint64_t bits[7];
+struct __align__(16) BkScr {           // a half's scratch: the leaf's policy and mask, its run
     float pr[416];
-    float cp[SPL_ACTIONS];
+    float cp[416];                     // (float4 reads: -inf pads past ec)
+    uint64_t bits[7];
     int16_t ca[SPL_ACTIONS];
 };
 
@@ -2198,13 +2206,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         root_noise_lds(C, __builtin_amdgcn_readlane(t, j), ST_DIR | (uint32_t)__builtin_amdgcn_readlane(H->move_no, j),
                        Sj.pr, Sj.bits, __builtin_amdgcn_readlane(ec, j));
     }
-    if (expand && !noise) {
-        float *pr = S.pr;
-        const float sum = half_np_sum409(pr);
-        wave_lds_fence();
-        for (int a = hl; a < SPL_ACTIONS; a += 32) pr[a] = pr[a] / sum;
-        wave_lds_fence();
-    }
+    // the normalisation (Ps * valids / sum, MCTS.py:117-121) of the legal priors only, as
+    // the run is built (root noise normalises its own)
+    float psum = 1.f;
+    if (expand && !noise) psum = half_np_sum409(S.pr);
     BPROBE(7)
     if (expand) {
         float *pr = S.pr;
@@ -2217,12 +2222,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 const int bit = 32 * hh + hl;
                 if ((wd >> bit) & 1) {
                     const int r = run + __popcll(wd & ((1ull << bit) - 1));
-                    S.cp[r] = pr[64 * k + bit];
+                    S.cp[r] = noise ? pr[64 * k + bit] : pr[64 * k + bit] / psum;
                     S.ca[r] = (int16_t)(64 * k + bit);
                 }
             }
             run += __popcll(wd);
         }
+        if (hl < 4) S.cp[ec + hl] = -INFINITY;
         wave_lds_fence();
         half_write_new_run(P, eb, ec, S.cp, S.ca);
     }
@@ -2252,7 +2258,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         int r = 0, cam = 0x7fffffff;
         float npm = -1.f;
         if (expand) {
-            const float pb = narg ? S.pr[bact] : 0.f;
+            const float pb = narg ? S.pr[bact] / psum : 0.f;     // (narg: depth > 0, no noise)
             for (int i = hl; i < ec; i += 32) {
                 const float p = S.cp[i];
                 const int a = S.ca[i];
