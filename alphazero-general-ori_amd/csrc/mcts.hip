@@ -386,6 +386,16 @@ __device__ __forceinline__ int noise_kept_root(const Pools &P, const SearchCfg &
 }
 
 // ------------------------------------------------------------ page allocation
+// Home pages (Pools::nhome / ehome): a tree's first SPL_HOME_N node pages (x 64 nodes) and
+// SPL_HOME_E edge pages (x 16 KB) are fixed, so a tree of average size (config 3: ~24 node and
+// ~18 edge pages) lives in one contiguous stretch per pool and the 64 trees of a wave in a few
+// 2 MB translations; pages beyond come from the shared free stacks.
+#ifndef SPL_HOME_N
+#define SPL_HOME_N 32
+#endif
+#ifndef SPL_HOME_E
+#define SPL_HOME_E 24
+#endif
 // Pop a page from a free stack (one lane). Only k_select / k_backup pop, and no launch both
 // pops and pushes, so an array stack with one atomic top is exact: a pop that finds the
 // stack empty undoes its decrement.
@@ -404,7 +414,7 @@ __device__ int node_slot(const Pools &P, TreeHdr *H, int t, int id) {
     const int pi = id >> NPG_SHIFT;
     int32_t *tab = P.ntab + (size_t)t * P.nptab;
     if (pi >= H->npg) {
-        const int pg = pop_page(P.nfree, P.alloc + 0);
+        const int pg = pi < P.nhome ? t * P.nhome + pi : pop_page(P.nfree, P.alloc + 0);
         if (pg < 0) { atomicAdd(P.alloc + 2, 1); return -1; }
         tab[pi] = pg;
         P.npidx[pg] = pi;
@@ -419,7 +429,7 @@ __device__ int node_slot(const Pools &P, TreeHdr *H, int t, int id) {
 __device__ int64_t unit_alloc(const Pools &P, TreeHdr *H, int t, int n) {
     if (H->eleft < n) {
         if (H->epg >= P.eptab) return -1;
-        const int pg = pop_page(P.efree, P.alloc + 1);
+        const int pg = H->epg < P.ehome ? t * P.ehome + H->epg : pop_page(P.efree, P.alloc + 1);
         if (pg < 0) { atomicAdd(P.alloc + 3, 1); return -1; }
         P.etab[(size_t)t * P.eptab + H->epg] = pg;
         P.epidx[pg] = H->epg;
@@ -434,8 +444,13 @@ __device__ int64_t unit_alloc(const Pools &P, TreeHdr *H, int t, int n) {
     return b;
 }
 
-// push n page ids (src[0..n)) back to a free stack, wave-collective
-__device__ __forceinline__ void push_pages(int32_t *stack, int32_t *top, int cap, const int32_t *src, int n) {
+// push tree pages [from, to) of a page table (tab) back to a free stack, the home entries
+// (< home) excepted, wave-collective
+__device__ __forceinline__ void push_pages(int32_t *stack, int32_t *top, int cap, const int32_t *tab, int from, int to,
+                                           int home) {
+    from = max(from, home);
+    const int n = to - from;
+    const int32_t *src = tab + from;
     if (n <= 0) return;
     int base = 0;
     if (lane_id() == 0) base = atomicAdd(top, n);
@@ -823,8 +838,8 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     const int64_t enext = eleft > 0 ? unit_g(P, t, run) : 0;
     __syncthreads();
     if (tid < 64) {
-        push_pages(P.nfree, P.alloc + 0, P.npages, P.ntab + (size_t)t * P.nptab + npg, onpg - npg);
-        push_pages(P.efree, P.alloc + 1, P.epages, P.etab + (size_t)t * P.eptab + epg, oepg - epg);
+        push_pages(P.nfree, P.alloc + 0, P.npages, P.ntab + (size_t)t * P.nptab, npg, onpg, P.nhome);
+        push_pages(P.efree, P.alloc + 1, P.epages, P.etab + (size_t)t * P.eptab, epg, oepg, P.ehome);
     }
     if (tid == 0) {
         H->node_count = kept; H->edge_count = units;
@@ -847,8 +862,8 @@ __device__ __forceinline__ bool tree_fits(const Pools &P, const SearchCfg &C, co
 __device__ void empty_tree(const Pools &P, int t) {
     TreeHdr *H = P.hdr + t;
     const int npg = H->npg, epg = H->epg;
-    push_pages(P.nfree, P.alloc + 0, P.npages, P.ntab + (size_t)t * P.nptab, npg);
-    push_pages(P.efree, P.alloc + 1, P.epages, P.etab + (size_t)t * P.eptab, epg);
+    push_pages(P.nfree, P.alloc + 0, P.npages, P.ntab + (size_t)t * P.nptab, 0, npg, P.nhome);
+    push_pages(P.efree, P.alloc + 1, P.epages, P.etab + (size_t)t * P.eptab, 0, epg, P.ehome);
     int32_t *hs = P.hslot + (size_t)t * P.hcap;
     if (H->node_count > 0 || npg > 0)
         for (int i = lane_id(); i < P.hcap; i += 64) hs[i] = -1;
@@ -913,7 +928,9 @@ __device__ void begin_search(const Pools &P, const SearchCfg &C, int t, const in
         // it shrinks as the shared pools fill (free share f: alpha = 8 while f >= 3/4, 4 while
         // f >= 1/2, then down to 1/8; config 3: 8 instead of 4 halves the collections, 0.628 ->
         // 0.619 ms per iteration, A/B)
-        const float f = fminf((float)P.alloc[0] / (float)P.npages, (float)P.alloc[1] / (float)P.epages);
+        // (the shared pages: the stacks' capacity)
+        const float f = fminf((float)P.alloc[0] / (float)max(P.npages - P.nhome * P.ntrees, 1),
+                              (float)P.alloc[1] / (float)max(P.epages - P.ehome * P.ntrees, 1));
         const float alpha = f >= 0.75f ? GC_ALPHA_FREE : (f >= 0.5f ? 4.f : fmaxf(0.125f, 8.f * f));
         const bool should = nc > (int)((1.f + alpha) * (float)H->live_gc) + budget + NPG ||
                             used > (long long)((1.f + alpha) * (float)H->units_gc) +
@@ -2691,9 +2708,11 @@ __global__ __launch_bounds__(256) void k_hash_eval(int B, const int8_t *__restri
 __global__ void k_init_pools(Pools P, int B) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
     for (size_t i = tid; i < (size_t)B; i += nth) P.order[i] = (int32_t)i;
-    for (size_t i = tid; i < (size_t)P.npages; i += nth) P.nfree[i] = (int32_t)i;
-    for (size_t i = tid; i < (size_t)P.epages; i += nth) P.efree[i] = (int32_t)i;
-    if (tid == 0) { P.alloc[0] = P.npages; P.alloc[1] = P.epages; P.alloc[2] = 0; P.alloc[3] = 0; }
+    // free stacks: every page past the home pages, lowest on top
+    const int nsh = P.npages - P.nhome * B, esh = P.epages - P.ehome * B;
+    for (size_t i = tid; i < (size_t)nsh; i += nth) P.nfree[i] = (int32_t)(P.npages - 1 - i);
+    for (size_t i = tid; i < (size_t)esh; i += nth) P.efree[i] = (int32_t)(P.epages - 1 - i);
+    if (tid == 0) { P.alloc[0] = nsh; P.alloc[1] = esh; P.alloc[2] = 0; P.alloc[3] = 0; }
 }
 
 inline int check_launch() { return hipGetLastError() == hipSuccess ? 0 : SPL_EDEVICE; }
@@ -2845,6 +2864,10 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.nmax = L.nmax; P.emax = L.emax; P.hcap = L.hcap; P.pcap = L.pcap;
     P.nptab = L.nptab; P.eptab = L.eptab;
     P.npages = (int)L.npages; P.epages = (int)L.epages;
+    // home pages: at most a quarter of each pool, SPL_HOME_N / SPL_HOME_E per tree
+    P.ntrees = B;
+    P.nhome = min(min(SPL_HOME_N, P.nptab), (int)(L.npages / (4 * (long long)B)));
+    P.ehome = min(min(SPL_HOME_E, P.eptab), (int)(L.epages / (4 * (long long)B)));
     const size_t nn = (size_t)L.npages * NPG, ne = (size_t)L.epages * UPG;
     const int excap = L.excap;
     const size_t nx = (size_t)B * excap, no = (size_t)L.out_cap;
