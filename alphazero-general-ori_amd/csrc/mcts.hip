@@ -182,19 +182,28 @@ __device__ __forceinline__ int best_unvisited(const Pools &P, int64_t eb, int ec
 // prior (-1: none; the runs are sorted by prior, so that is the largest smaller prior). One lane.
 __device__ __forceinline__ void lane_cand(const Pools &P, int64_t eb, int ec, int from, int &cand, int &ca, float &cp,
                                           float &np) {
-    int j = from;
-    while (j < ec && P.ep(eb + j)->vi >= 0) j++;
-    cand = j; ca = 0; cp = 0.f; np = -1.f;
-    if (j >= ec) return;
-    const EdgeP c = *P.ep(eb + j);
-    ca = c.a; cp = c.p;
-    if (c.p > 0.f)
-        for (int k = j + 1; k < ec; k++) {
-            const EdgeP e = *P.ep(eb + k);
-            if (e.vi >= 0 || e.p == c.p) continue;
-            np = e.p;
-            break;
+    cand = ec; ca = 0; cp = 0.f; np = -1.f;
+    bool found = false;
+    // eight edges per round trip (their loads issued together), scanned in registers
+    for (int c0 = from; c0 < ec; c0 += 8) {
+        EdgeP e[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) e[k] = c0 + k < ec ? *P.ep(eb + c0 + k) : EdgeP{0.f, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (c0 + k >= ec) return;
+            if (!found) {
+                if (e[k].vi < 0) {
+                    found = true;
+                    cand = c0 + k; ca = e[k].a; cp = e[k].p;
+                    if (!(cp > 0.f)) return;
+                }
+            } else if (e[k].vi < 0 && e[k].p != cp) {
+                np = e[k].p;
+                return;
+            }
         }
+    }
 }
 // the same with `cand` known, wave-collective (ranks lane-parallel); uniform results
 __device__ __forceinline__ void wave_cand(const Pools &P, int64_t eb, int ec, int cand, int &ca, float &cp, float &np) {
@@ -2146,12 +2155,24 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     float val[4] = {0, 0, 0, 0};
     int lid = -1;
     BkScr &S = scr[2 * w + half];
+    // the leaf's policy and mask: loaded here, staged in LDS after pass A's loads are issued
+    // (an LDS store would wait for them first: one round trip less per tree)
+#ifndef BK_DEFER_PI
+#define BK_DEFER_PI 1
+#endif
+    float prv[13];
+    uint64_t mbits = 0;
     if (kind == LEAF_NN) {
         const float *gp = pi + (size_t)t * SPL_ACTIONS;
 #pragma unroll
-        for (int k = 0; k < 13; k++)
-            if (32 * k + hl < SPL_ACTIONS) S.pr[32 * k + hl] = gp[32 * k + hl];
-        if (hl < 7) S.bits[hl] = leaf_mask[(size_t)t * 7 + hl];
+        for (int k = 0; k < 13; k++) prv[k] = 32 * k + hl < SPL_ACTIONS ? gp[32 * k + hl] : 0.f;
+        if (hl < 7) mbits = leaf_mask[(size_t)t * 7 + hl];
+        if (!BK_DEFER_PI) {
+#pragma unroll
+            for (int k = 0; k < 13; k++)
+                if (32 * k + hl < SPL_ACTIONS) S.pr[32 * k + hl] = prv[k];
+            if (hl < 7) S.bits[hl] = mbits;
+        }
 #pragma unroll
         for (int i = 0; i < N; i++) val[i] = v[(size_t)t * N + i];
     } else if (kind == LEAF_TERMINAL) {
@@ -2190,6 +2211,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     int g = -1, ec = 0;
     int64_t eb = -1;
     if (kind == LEAF_NN) {
+        if (BK_DEFER_PI) {
+#pragma unroll
+            for (int k = 0; k < 13; k++)
+                if (32 * k + hl < SPL_ACTIONS) S.pr[32 * k + hl] = prv[k];
+            if (hl < 7) S.bits[hl] = mbits;
+        }
         wave_lds_fence();
 #pragma unroll
         for (int k = 0; k < 7; k++) ec += __popcll(S.bits[k]);
