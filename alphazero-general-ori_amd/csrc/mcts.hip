@@ -589,6 +589,23 @@ __device__ __forceinline__ int block_scan(int x, int &total, GcLds &L) {   // ex
     return off + incl - x;
 }
 
+// per-phase cycle probes of compact_tree (diagnostic builds only, -DGC_PROBE=1; never the
+// product): thread 0 of each workgroup adds its phase cycles into the workgroup's slot
+#ifndef GC_PROBE
+#define GC_PROBE 0
+#endif
+#if GC_PROBE
+constexpr int GC_WG_MAX_PROBE = 1024;
+__device__ unsigned long long g_gc_probe[GC_WG_MAX_PROBE][16];
+#define GPROBE(k)                                                                 \
+    if (threadIdx.x == 0) {                                                       \
+        const uint64_t c_ = __builtin_readcyclecounter();                         \
+        gacc[k] += c_ - glast;                                                    \
+        glast = c_;                                                               \
+    }
+#else
+#define GPROBE(k)
+#endif
 constexpr int GC_NOFIT = -2;   // compact_tree: the compacted tree would not fit the edge pages it holds
 template <int CR = 4>   // board units per thread per round trip of the node-board move (x2)
 __device__ int compact_tree(const Pools &P, int t, int root, int root_round, const GcScr &S, GcLds &L,
@@ -598,6 +615,10 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     const int nc = H->node_count;
     const int rootl = root >= 0 ? node_l(P, root) : -1;
     int32_t *remap = S.remap;
+#if GC_PROBE
+    uint64_t gacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, glast = __builtin_readcyclecounter();
+    const uint64_t gstart = glast;
+#endif
     if (linked) {
         if (tid < 64) mark_linked(P, t, rootl, remap, S.queue);
         __syncthreads();
@@ -613,6 +634,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         kept += tot;
     }
     __syncthreads();
+    GPROBE(0)
     // new unit position of every kept node's allocation (run + visit records): packed in local
     // order, an allocation that would straddle an edge page starts the next page. The sizes
     // are staged (all threads), then ONE wave walks the nodes 64 at a time with wave prefix
@@ -673,6 +695,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     }
     __syncthreads();
     const int run = L.bc[0];
+    GPROBE(1)
     // packed with page-end gaps in an order other than the allocation order (a node's run and
     // visit block together, by local index), the kept units may need more edge pages than the
     // tree holds (the compaction moves units within its own pages and takes none from the
@@ -716,6 +739,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     }
     int units;
     (void)block_scan(my_units, units, L);
+    GPROBE(2)
     // the cached arg-max's link (NodeStat) remapped like the visit records' links below
     for (int ni = tid; ni < kept; ni += GCT) {
         const int ch = S.queue[ni];
@@ -735,6 +759,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         for (int e = 0; e < c; e++) S.own[c0 + e] = ni;
     }
     __syncthreads();
+    GPROBE(3)
     // units staged by new position (a run's EdgeP units verbatim, visit records with their
     // links remapped), then written back; every thread writes back exactly the positions it
     // staged, so only the workgroup barrier between the two passes is needed. SR positions
@@ -786,6 +811,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
             if (j[r] >= 0) S.buf[k0 + GCT * r + tid] = v[r];
     }
     __syncthreads();
+    GPROBE(4)
     for (int k0 = 0; k0 < run; k0 += GCT * SR) {
         int j[SR];
         uint64_t v[SR];
@@ -829,6 +855,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
             __syncthreads();
         }
     }
+    GPROBE(5)
     // rebuild the transposition table
     int32_t *hs = P.hslot + (size_t)t * P.hcap;
     for (int i = tid; i < P.hcap; i += GCT) hs[i] = -1;
@@ -856,6 +883,17 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
         H->live_gc = kept; H->units_gc = units; H->gcs += 1;
     }
     __syncthreads();
+    GPROBE(6)
+#if GC_PROBE
+    if (tid == 0) {
+        unsigned long long *g = g_gc_probe[blockIdx.x % GC_WG_MAX_PROBE];
+        for (int k = 0; k < 7; k++) g[k] += gacc[k];
+        g[8] += 1;
+        const unsigned long long tot = glast - gstart;
+        g[9] += tot;
+        if (tot > g[10]) { g[10] = tot; g[11] = (unsigned long long)run; g[12] = (unsigned long long)kept; g[13] = (unsigned long long)nc; }
+    }
+#endif
     return nroot;
 }
 
@@ -2835,6 +2873,28 @@ int spl_diag_select_probe(unsigned long long *out16, int reset) {
 }
 #endif
 
+#if GC_PROBE
+// compact_tree phase probes (cycles summed over collections): [0] keep / remap scan [1] sizes +
+// page packing [2] node records moved [3] arg-max links + owner map [4] unit staging [5]
+// write-back + node boards [6] table rebuild + pages; [8] collections [9] total cycles [10]
+// the slowest collection's cycles, [11] its units, [12] its kept nodes, [13] its nodes before
+int spl_diag_gc_probe(unsigned long long *out16, int reset) {
+    static unsigned long long h[GC_WG_MAX_PROBE][16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_gc_probe), sizeof(h)) != hipSuccess) return SPL_EDEVICE;
+    for (int k = 0; k < 16; k++) out16[k] = 0;
+    for (int i = 0; i < GC_WG_MAX_PROBE; i++) {
+        for (int k = 0; k < 10; k++) out16[k] += h[i][k];
+        if (h[i][10] > out16[10])
+            for (int k = 10; k < 14; k++) out16[k] = h[i][k];
+    }
+    if (reset) {
+        memset(h, 0, sizeof(h));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_gc_probe), h, sizeof(h)) != hipSuccess) return SPL_EDEVICE;
+    }
+    return 0;
+}
+#endif
+
 #if BACKUP_PROBE
 // k_backup_h phase probes (cycles summed over waves): [0] header + pass A [1] expansion's node
 // record / table insert [2] pass B loads / updates [3] screen [4] exact levels [5] record writes
@@ -2894,6 +2954,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     // home pages: at most a quarter of each pool, SPL_HOME_N / SPL_HOME_E per tree
     P.ntrees = B;
     P.nhome = min(min(SPL_HOME_N, P.nptab), (int)(L.npages / (4 * (long long)B)));
+    while (P.nhome & (P.nhome - 1)) P.nhome &= P.nhome - 1;   // (a power of two: node_l masks)
     P.ehome = min(min(SPL_HOME_E, P.eptab), (int)(L.epages / (4 * (long long)B)));
     const size_t nn = (size_t)L.npages * NPG, ne = (size_t)L.epages * UPG;
     const int excap = L.excap;

@@ -181,7 +181,7 @@ struct Pools {
     int nptab, eptab;                    // page-table entries per tree (nmax / NPG, emax / UPG)
     int npages, epages;                  // pages in the pools
     int ntrees;                          // B
-    int nhome, ehome;                    // home pages per tree: tree t's page-table entries
+    int nhome, ehome;                    // home pages per tree (nhome a power of two or 0): tree t's page-table entries
                                          // i < nhome are node pages t nhome + i (edge pages
                                          // t ehome + i), never on the free stacks, so a tree's
                                          // first nodes and edges sit together and a wave's
@@ -232,14 +232,22 @@ struct Pools {
 };
 
 // tree t's local node slot i / local (virtual) unit position v -> global
+// (a home page needs no table load: tree t's page i < nhome is t nhome + i; nhome is a power
+// of two, so the reverse map of a home page is a mask)
 __device__ __forceinline__ int node_g(const Pools &P, int t, int i) {
-    return P.ntab[(size_t)t * P.nptab + (i >> NPG_SHIFT)] * NPG + (i & (NPG - 1));
+    const int pi = i >> NPG_SHIFT;
+    const int pg = pi < P.nhome ? t * P.nhome + pi : P.ntab[(size_t)t * P.nptab + pi];
+    return pg * NPG + (i & (NPG - 1));
 }
 __device__ __forceinline__ int node_l(const Pools &P, int g) {
-    return P.npidx[g >> NPG_SHIFT] * NPG + (g & (NPG - 1));
+    const int pg = g >> NPG_SHIFT;
+    const int pi = pg < P.nhome * P.ntrees ? (pg & (P.nhome - 1)) : P.npidx[pg];
+    return pi * NPG + (g & (NPG - 1));
 }
 __device__ __forceinline__ int64_t unit_g(const Pools &P, int t, int v) {
-    return (int64_t)P.etab[(size_t)t * P.eptab + (v >> UPG_SHIFT)] * UPG + (v & (UPG - 1));
+    const int pi = v >> UPG_SHIFT;
+    const int64_t pg = pi < P.ehome ? (int64_t)t * P.ehome + pi : (int64_t)P.etab[(size_t)t * P.eptab + pi];
+    return pg * UPG + (v & (UPG - 1));
 }
 
 // per-node board slot (Pools::nbrd): the LDS row format padded to 16 bytes

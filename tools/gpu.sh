@@ -17,6 +17,7 @@
 #   ab        interleaved A/B of the product against each V in $AB: ablib/lib<V>.so, or a whole
 #             older tree ablib/<V>/ (bench.py + package) (config-3 bench twice each) -> gpurun_out/ab.txt
 #   probe     k_select_lanes phase probes (ablib/lib<V>.so for V in ${PROBES:-probe}, -DSELECT_PROBE=1) -> gpurun_out/<V>.json
+#   gcprobe   compact_tree phase probes (ablib/libgcprobe.so, -DGC_PROBE=1)    -> gpurun_out/gcprobe.json
 #   nnprobe   per-layer cycle probes of the network kernel (ablib/libnnprobe.so, -DNN_PROBE=1) -> gpurun_out/nnprobe.json
 #   bounds    the bounds-checked build (ablib/libchk.so: tools/bounds_check.sh on
 #             the host first) under capacity pressure                   -> gpurun_out/bounds_chk.json
@@ -74,6 +75,9 @@ step() {
             SPLENDOR_AMD_LIB=$PWD/ablib/lib$v.so timeout -k 10 200 python3 -u tools/select_probe.py \
                 > gpurun_out/$v.json 2> gpurun_out/$v.err || { echo "$v rc=$?" >> gpurun_out/progress.log; return 1; }
         done ;;
+    gcprobe)
+        SPLENDOR_AMD_LIB=$PWD/ablib/libgcprobe.so timeout -k 10 200 python3 -u tools/gc_probe.py \
+            > gpurun_out/gcprobe.json 2> gpurun_out/gcprobe.err ;;
     nnprobe)
         SPLENDOR_AMD_LIB=$PWD/ablib/libnnprobe.so timeout -k 10 200 python3 -u tools/nn_probe.py \
             > gpurun_out/nnprobe.json 2> gpurun_out/nnprobe.err ;;
