@@ -92,13 +92,14 @@ constexpr int REC_UNITS = 3;
 // half per level, no edge scan). The root level scans when its priors were just noised or forced
 // playouts are on. Invariant (k_backup, k_select's links, k_gc's remap): bchild is the child of
 // edge `best` (-1: not linked), bterm whether that child is terminal.
-// Bytes 4-11 are reserved (-1): round 5 measured descent hints there (the cached picks of the
-// next two levels, loaded ahead of the authoritative link) and dropped them — the compiler
-// serialises the queue's conditional loads (s_waitcnt vmcnt(0) after each), 0.606 vs 0.557 ms
-// per iteration at config 3.
+// Descent hint (round 5): h2 names the cached pick's child's own cached child as the last backup
+// through the node saw it (k_backup_h; -1: none; k_gc clears it). It may be stale (a
+// transposition's other parent moved that pick), so the descent only uses it as a prefetch
+// address, checked against the authoritative link of the level above (descend_linked_asm).
 struct NodeHot {             // first half: the descent reads its first 16 bytes per level
     int32_t bchild;          // cached arg-max's child (global id, -1: not linked)
-    int32_t rsv0, rsv1;      // reserved (-1)
+    int32_t h2;              // descent hint (-1: none)
+    int32_t rsv;             // reserved (-1)
     int16_t best;            // cached arg-max: rank of the edge in the run (-1: unknown, scan)
     uint16_t babt;           // its action | (1: that child is terminal) << 15
     int32_t ns;              // Ns
@@ -116,7 +117,7 @@ struct NodeHot {             // first half: the descent reads its first 16 bytes
 };
 // the descent's view of a record (NodeHot's first 16 bytes: one dwordx4 load)
 struct __align__(16) NodeLink {
-    int32_t bchild, rsv0, rsv1;
+    int32_t bchild, h2, rsv;
     int16_t best;
     uint16_t babt;
     __device__ __forceinline__ int ba() const { return babt & 0x7FFF; }
