@@ -731,7 +731,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                 w.c.set_eb(ec > 0 ? unit_g(P, t, vs) : 0, vcnt);
                 w.c.set_vb(vcnt > 0 ? unit_g(P, t, vs + ec) : 0, vcnt);
             }
-            w.h.h2 = -1; w.h.rsv = -1;
+            w.h.h2 = -1; w.h.h3 = -1;
             P.nkey0[ng] = k0; P.nkey1[ng] = k1;
             P.nd[ng] = w;
             S.cs[ni] = vs; S.cnt[ni] = sz; S.inv[ni] = i;
@@ -1377,7 +1377,7 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
             w2.c.cand = (int16_t)cand; w2.c.ca = (int16_t)ca; w2.c.cp = cp; w2.c.np = np;
             w2.h.set_pick(pk.e, pk.a, pk.e >= 0 && pk.child >= 0 ? P.nd[pk.child].h.term : 0);   // (-1: scans)
             w2.h.bchild = pk.e >= 0 ? pk.child : -1;
-            w2.h.h2 = -1; w2.h.rsv = -1;
+            w2.h.h2 = -1; w2.h.h3 = -1;
             w2.h.bvi = pk.e >= 0 ? P.ep(r.eb + pk.e)->vi : (int16_t)-1;
             P.nd[nroot] = w2;
         }
@@ -1433,7 +1433,7 @@ __device__ __forceinline__ void term_values(const Pools &P, int g, float v[4]) {
 // the record of a new terminal node of round rd with end values v
 __device__ __forceinline__ Node term_node(const float v[4], int rd) {
     Node n{};
-    n.h.bchild = -1; n.h.h2 = -1; n.h.rsv = -1; n.h.set_pick(-1, 0, 0); n.h.ns = 0;
+    n.h.bchild = -1; n.h.h2 = -1; n.h.h3 = -1; n.h.set_pick(-1, 0, 0); n.h.ns = 0;
     n.h.term = 1; n.h.round = (uint8_t)rd; n.h.qs = 0.0;
     *reinterpret_cast<float4 *>(&n.c) = make_float4(v[0], v[1], v[2], v[3]);
     n.h.bvi = -1;
@@ -1525,22 +1525,23 @@ __device__ unsigned long long g_sel_probe[16];
 enum { LS_DESCEND = 0, LS_EXPAND = 1, LS_DONE = 2 };
 
 // The linked run of the descent (levels whose cached pick is linked to a non-terminal child)
-// with the descent hint h2 (NodeHot: the cached pick's child's own cached child, written by
-// k_backup_h): every level loads, besides nothing else, the record h2 names — the record the
-// level after next most likely needs — so along a correct chain a level's record was requested
-// one level earlier. A lane whose child is not the hinted one loads its child's record on the
-// spot (into the same registers: loads return in order). The wave then waits for the older
-// load only when every active lane's hint held (vmcnt(5): the record requested a level ago;
-// else vmcnt(3): this level's own load) — compiled code cannot express that data-dependent wait
-// (its waits follow the registers: a loop-carried prefetch was measured to cost 0.606 vs 0.557 ms),
-// so the loop is one assembly block with its own registers (v232-v255) and a unique label set.
+// with the descent hints (NodeHot h2 / h3: the cached picks two and three levels down, written
+// by k_backup_h): every level requests the record its h3 names — the record three levels down
+// most likely needs — so along a correct chain a level's record was requested two levels
+// earlier. A lane whose child is not the predicted node loads its child's record on the spot
+// (into the same registers: loads return in order). The wave waits for the older load only
+// when every active lane's prediction held (vmcnt(8) / (9): the record requested two levels
+// ago, behind 8 or 9 younger memory instructions; else vmcnt(3): this level's own load) —
+// compiled code cannot express that data-dependent wait (its waits follow the registers: a
+// compiled loop-carried prefetch measured 0.606 vs 0.557 ms), so the loop is one assembly block
+// with its own registers (v226-v255), three rotating record slots and a unique label set.
 // In: lanes in `runm` descend from (node, depth) with rec = node's link record (arrived). Out:
 // each lane at the first level that is not a plain link, rec = its record; the path entries
 // [depth_in, depth_out) written. The records and path are the C loop's (SELECT_ASM=0).
 #ifndef SELECT_ASM
 #define SELECT_ASM (!SPL_BOUNDS_CHECK)
 #endif
-#define SEL_BODY(SO, SN, K)                                                                     \
+#define SEL_BODY(SA, SC, K)                                                                     \
     "v_cmp_le_i32 vcc, 0, v240\n"                 /* a linked pick                     */      \
     "v_cmp_le_i32 %[T], 0, v243\n"                /* whose child is not terminal       */      \
     "s_and_b64 vcc, vcc, %[T]\n"                                                               \
@@ -1548,18 +1549,18 @@ enum { LS_DESCEND = 0, LS_EXPAND = 1, LS_DONE = 2 };
     "s_and_b64 vcc, vcc, %[T]\n"                                                               \
     "s_and_b64 exec, exec, vcc\n"                                                              \
     "s_cbranch_execz L_done_%=\n"                                                              \
-    "v_cmp_ne_u32 vcc, v240, v234\n"              /* the child is not the hinted node:  */      \
+    "v_cmp_ne_u32 vcc, v240, v234\n"              /* the child is not the predicted node: */    \
     "s_and_saveexec_b64 %[SV], vcc\n"             /* load its record now                */      \
     "s_mov_b64 %[INV], exec\n"                                                                 \
     "s_cbranch_execz L_nf" K "_%=\n"                                                           \
     "v_mad_u64_u32 v[238:239], %[CC], v240, 64, %[nd]\n"                                       \
-    "global_load_dwordx4 " SO ", v[238:239], off\n"                                            \
+    "global_load_dwordx4 " SA ", v[238:239], off\n"                                            \
     "L_nf" K "_%=:\n"                                                                          \
     "s_mov_b64 exec, %[SV]\n"                                                                  \
-    "v_cmp_gt_u32 vcc, %[lim], v241\n"           /* the hint, if a node id (else the   */      \
-    "v_cndmask_b32 v235, v240, v241, vcc\n"      /* child again)                        */      \
-    "v_mad_u64_u32 v[238:239], %[CC], v235, 64, %[nd]\n"                                       \
-    "global_load_dwordx4 " SN ", v[238:239], off\n"                                            \
+    "v_cmp_gt_u32 vcc, %[lim], v242\n"            /* h3, if a node id (else the child   */      \
+    "v_cndmask_b32 v226, v240, v242, vcc\n"       /* again): three levels down          */      \
+    "v_mad_u64_u32 v[238:239], %[CC], v226, 64, %[nd]\n"                                       \
+    "global_load_dwordx4 " SC ", v[238:239], off\n"                                            \
     "v_mad_u64_u32 v[238:239], %[CC], v233, 4, v[252:253]\n"   /* path_n[depth] = node */      \
     "global_store_dword v[238:239], v232, off\n"                                               \
     "v_and_b32 v236, 0xffff, v243\n"                           /* path_x: rank | a << 9 */     \
@@ -1569,21 +1570,35 @@ enum { LS_DESCEND = 0, LS_EXPAND = 1, LS_DONE = 2 };
     "global_store_dword v[238:239], v236, off\n"                                               \
     "v_add_u32 v233, 1, v233\n"                                                                \
     "v_mov_b32 v232, v240\n"                                                                   \
-    "v_mov_b32 v234, v235\n"                                                                   \
+    "v_mov_b32 v234, v235\n"                      /* predictions: next level, the one after */ \
+    "v_mov_b32 v235, v226\n"                                                                   \
     "s_cmp_eq_u64 %[INV], 0\n"                                                                 \
     "s_cbranch_scc1 L_av" K "_%=\n"                                                            \
     "s_waitcnt vmcnt(3)\n"                        /* some lane loaded its child now     */      \
+    "s_mov_b32 %[F], 1\n"                                                                      \
     "s_branch L_sel" K "_%=\n"                                                                 \
-    "L_av" K "_%=:\n"                                                                          \
-    "s_waitcnt vmcnt(5)\n"                        /* every record was requested a level ago */ \
+    "L_av" K "_%=:\n"                             /* every record requested two levels  */      \
+    "s_cmp_eq_u32 %[F], 0\n"                      /* ago: behind 8 memory instructions, */      \
+    "s_cbranch_scc1 L_a8" K "_%=\n"               /* 9 if the last level loaded a child */      \
+    "s_waitcnt vmcnt(9)\n"                                                                     \
+    "s_branch L_a0" K "_%=\n"                                                                  \
+    "L_a8" K "_%=:\n"                                                                          \
+    "s_waitcnt vmcnt(8)\n"                                                                     \
+    "L_a0" K "_%=:\n"                                                                          \
+    "s_mov_b32 %[F], 0\n"                                                                      \
     "L_sel" K "_%=:\n"
+#define SEL_TAKE(R)                                                                             \
+    "v_mov_b32 v240, v" #R "\n"                                                                \
+    "v_mov_b32 v241, v" #R "+1\n"
 __device__ __forceinline__ void descend_linked_asm(int &node, int &depth, NodeLink &rec, const Node *nd, int pcap,
                                                    int32_t *path_n, int32_t *path_x, uint64_t runm, int lim) {
-    int r0 = rec.bchild, r1 = rec.h2, r2 = rec.rsv;
+    int r0 = rec.bchild, r1 = rec.h2, r2 = rec.h3;
     int r3 = (int)((uint32_t)(uint16_t)rec.best | ((uint32_t)rec.babt << 16));
     uint64_t T, SV, INV, CC, SAVE;
+    int F;
     asm volatile(
         "s_mov_b64 %[SAVE], exec\n"
+        "s_mov_b32 %[F], 1\n"
         "v_mov_b32 v232, %[node]\n"
         "v_mov_b32 v233, %[depth]\n"
         "v_mov_b32 v240, %[r0]\n"
@@ -1591,21 +1606,18 @@ __device__ __forceinline__ void descend_linked_asm(int &node, int &depth, NodeLi
         "v_mov_b32 v242, %[r2]\n"
         "v_mov_b32 v243, %[r3]\n"
         "v_mov_b32 v234, -1\n"
+        "v_mov_b32 v235, -1\n"
         "v_mov_b64 v[252:253], %[pn]\n"
         "v_mov_b64 v[254:255], %[pxp]\n"
         "s_and_b64 exec, exec, %[runm]\n"
         "s_cbranch_execz L_done_%=\n"
         "L_top_%=:\n"
-        SEL_BODY("v[244:247]", "v[248:251]", "0")
-        "v_mov_b32 v240, v244\n"
-        "v_mov_b32 v241, v245\n"
-        "v_mov_b32 v242, v246\n"
-        "v_mov_b32 v243, v247\n"
+        SEL_BODY("v[244:247]", "v[228:231]", "0")
+        "v_mov_b32 v240, v244\n" "v_mov_b32 v241, v245\n" "v_mov_b32 v242, v246\n" "v_mov_b32 v243, v247\n"
         SEL_BODY("v[248:251]", "v[244:247]", "1")
-        "v_mov_b32 v240, v248\n"
-        "v_mov_b32 v241, v249\n"
-        "v_mov_b32 v242, v250\n"
-        "v_mov_b32 v243, v251\n"
+        "v_mov_b32 v240, v248\n" "v_mov_b32 v241, v249\n" "v_mov_b32 v242, v250\n" "v_mov_b32 v243, v251\n"
+        SEL_BODY("v[228:231]", "v[248:251]", "2")
+        "v_mov_b32 v240, v228\n" "v_mov_b32 v241, v229\n" "v_mov_b32 v242, v230\n" "v_mov_b32 v243, v231\n"
         "s_branch L_top_%=\n"
         "L_done_%=:\n"
         "s_waitcnt vmcnt(0)\n"
@@ -1617,15 +1629,16 @@ __device__ __forceinline__ void descend_linked_asm(int &node, int &depth, NodeLi
         "v_mov_b32 %[r2], v242\n"
         "v_mov_b32 %[r3], v243\n"
         : [node] "+v"(node), [depth] "+v"(depth), [r0] "+v"(r0), [r1] "+v"(r1), [r2] "+v"(r2), [r3] "+v"(r3),
-          [T] "=&s"(T), [SV] "=&s"(SV), [INV] "=&s"(INV), [CC] "=&s"(CC), [SAVE] "=&s"(SAVE)
+          [T] "=&s"(T), [SV] "=&s"(SV), [INV] "=&s"(INV), [CC] "=&s"(CC), [SAVE] "=&s"(SAVE), [F] "=&s"(F)
         : [nd] "s"(nd), [pcap] "s"(pcap), [pn] "v"(path_n), [pxp] "v"(path_x), [runm] "s"(runm), [lim] "s"(lim)
-        : "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243", "v244",
-          "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255", "vcc", "exec", "scc",
-          "memory");
-    rec.bchild = r0; rec.h2 = r1; rec.rsv = r2;
+        : "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238",
+          "v239", "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251",
+          "v252", "v253", "v254", "v255", "vcc", "scc", "memory");
+    rec.bchild = r0; rec.h2 = r1; rec.h3 = r2;
     rec.best = (int16_t)(r3 & 0xFFFF); rec.babt = (uint16_t)((uint32_t)r3 >> 16);
 }
 #undef SEL_BODY
+#undef SEL_TAKE
 
 template <int N>
 __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B, int lim,
@@ -2477,7 +2490,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         if (expand && hl == 0) {
             P.nkey0[g] = h_k0; P.nkey1[g] = h_k1;
             Node nn;
-            nn.h.bchild = -1; nn.h.h2 = -1; nn.h.rsv = -1;
+            nn.h.bchild = -1; nn.h.h2 = -1; nn.h.h3 = -1;
             nn.h.set_pick(bsel, bact, 0); nn.h.ns = 0;
             nn.h.term = 0; nn.h.round = (uint8_t)h_round; nn.h.bvi = -1;
             nn.h.qs = (double)val[0];
@@ -2620,16 +2633,18 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         BPROBE(4)
         const bool stay = in && bsel == V.off;
         if (stay) { bch = V.rchild; bvi = vidx; }
-        // the descent hint: a level whose pick stays on the path edge names the next path
-        // level's new pick (lane hl + 1 of this half; none across a group boundary)
-        const int nb1 = __shfl(bch, min(l + 1, 63), 64);
+        // the descent hints: a level whose pick stays on the path edge names the next two path
+        // levels' new picks (lanes hl + 1, hl + 2 of this half; none across a group boundary)
+        const int nb1 = __shfl(bch, min(l + 1, 63), 64), nb2 = __shfl(bch, min(l + 2, 63), 64);
+        const int ns1 = __shfl((int)stay, min(l + 1, 63), 64);
         const int hh2 = stay && hl < 31 && d + 1 < depth ? nb1 : -1;
+        const int hh3 = hh2 >= 0 && ns1 && hl < 30 && d + 2 < depth ? nb2 : -1;
         if (in) {                                        // the level's record, written once
             int bt_;
             if (stay) bt_ = kind == LEAF_TERMINAL && bch >= 0 && bch == lid;   // (the path's child:
             else bt_ = bch >= 0 ? (int)P.nd[bch].h.term : 0;                   //  terminal only as the leaf)
             NodeHot w;                                   // (the second half: written with a new record)
-            w.bchild = bch; w.h2 = hh2; w.rsv = -1;
+            w.bchild = bch; w.h2 = hh2; w.h3 = hh3;
             w.set_pick(bsel, bact, bt_); w.ns = nns;
             w.term = 0; w.round = (uint8_t)V.round; w.bvi = (int16_t)bvi;
             w.qs = nqs;

@@ -92,14 +92,13 @@ constexpr int REC_UNITS = 3;
 // half per level, no edge scan). The root level scans when its priors were just noised or forced
 // playouts are on. Invariant (k_backup, k_select's links, k_gc's remap): bchild is the child of
 // edge `best` (-1: not linked), bterm whether that child is terminal.
-// Descent hint (round 5): h2 names the cached pick's child's own cached child as the last backup
-// through the node saw it (k_backup_h; -1: none; k_gc clears it). It may be stale (a
-// transposition's other parent moved that pick), so the descent only uses it as a prefetch
-// address, checked against the authoritative link of the level above (descend_linked_asm).
+// Descent hints (round 5): h2 / h3 name the nodes two / three levels down along the cached
+// picks as the last backup through the node saw them (k_backup_h; -1: none; k_gc clears them).
+// They may be stale (a transposition's other parent moved a pick), so the descent uses them only
+// as prefetch addresses, checked against the authoritative link above (descend_linked_asm).
 struct NodeHot {             // first half: the descent reads its first 16 bytes per level
     int32_t bchild;          // cached arg-max's child (global id, -1: not linked)
-    int32_t h2;              // descent hint (-1: none)
-    int32_t rsv;             // reserved (-1)
+    int32_t h2, h3;          // descent hints (-1: none)
     int16_t best;            // cached arg-max: rank of the edge in the run (-1: unknown, scan)
     uint16_t babt;           // its action | (1: that child is terminal) << 15
     int32_t ns;              // Ns
@@ -117,7 +116,7 @@ struct NodeHot {             // first half: the descent reads its first 16 bytes
 };
 // the descent's view of a record (NodeHot's first 16 bytes: one dwordx4 load)
 struct __align__(16) NodeLink {
-    int32_t bchild, h2, rsv;
+    int32_t bchild, h2, h3;
     int16_t best;
     uint16_t babt;
     __device__ __forceinline__ int ba() const { return babt & 0x7FFF; }

@@ -27,7 +27,7 @@ def main():
     from splendor import _lib
     L = _lib.lib()
     L.spl_diag_gc_probe.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    out = (ctypes.c_ulonglong * 16)()
+    out = (ctypes.c_ulonglong * 24)()
 
     def reset(sp):
         torch.cuda.synchronize()
@@ -44,7 +44,8 @@ def main():
                       "cycles_per_collection": {nm: out[k] / n for k, nm in enumerate(names)},
                       "total_cycles_per_collection": out[9] / n,
                       "slowest": {"cycles": int(out[10]), "units": int(out[11]), "kept_nodes": int(out[12]),
-                                  "nodes_before": int(out[13])}}), flush=True)
+                                  "nodes_before": int(out[13]),
+                                  "phases": {nm: int(out[16 + k]) for k, nm in enumerate(names)}}}), flush=True)
 
 
 if __name__ == "__main__":
