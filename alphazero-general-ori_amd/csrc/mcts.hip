@@ -418,18 +418,20 @@ __device__ __forceinline__ int pop_page(int32_t *stack, int32_t *top) {
 // the pool when the slot opens one; -1 when the tree is at its maximum or the pool is empty.
 // Idempotent until node_count advances (a slot reserved by k_select is the one k_backup
 // fills). One lane.
-__device__ int node_slot(const Pools &P, TreeHdr *H, int t, int id) {
+__device__ int node_slot(const Pools &P, TreeHdr *H, int t, int id, int *npg_reg = nullptr) {
     if (id >= P.nmax) return -1;
     const int pi = id >> NPG_SHIFT;
     int32_t *tab = P.ntab + (size_t)t * P.nptab;
-    if (pi >= H->npg) {
+    if (pi >= (npg_reg ? *npg_reg : H->npg)) {
         const int pg = pi < P.nhome ? t * P.nhome + pi : pop_page(P.nfree, P.alloc + 0);
         if (pg < 0) { atomicAdd(P.alloc + 2, 1); return -1; }
         tab[pi] = pg;
         P.npidx[pg] = pi;
         H->npg = pi + 1;
+        if (npg_reg) *npg_reg = pi + 1;
+        return pg * NPG + (id & (NPG - 1));
     }
-    return tab[pi] * NPG + (id & (NPG - 1));
+    return node_g(P, t, id);
 }
 
 // n contiguous edge units for tree t (a run or a visit block: global base), from the tree's
@@ -1662,13 +1664,14 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
     const int t = live ? P.order[slot] : 0;
     TreeHdr *H = P.hdr + t;
     int8_t *s = boards + l * ST;
-    int sims = 0, root = -1, hdepth = 0, mv = 0;
+    int sims = 0, root = -1, hdepth = 0, mv = 0, hnc = 0, hnpg = 0;
     bool act = false, noise = false, forced = false;
     if (live) {
         sims = H->sims_done;
         act = sims < H->budget && !H->overflow;
         root = H->root; hdepth = H->depth; mv = H->move_no;
         noise = H->noise_pending != 0; forced = H->forced != 0;
+        hnc = H->node_count; hnpg = H->npg;          // (k_select's own writes update them)
         if (!act) { leaf_valid[t] = 0; H->leaf_kind = LEAF_NONE; }
     }
     const uint64_t *nbrd = reinterpret_cast<const uint64_t *>(P.nbrd);
@@ -1866,8 +1869,8 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                         kind = LEAF_TERMINAL;
 #pragma unroll
                         for (int i = 0; i < N; i++) val[i] = es[i];
-                        const int id = H->node_count;
-                        const int g = node_slot(P, H, t, id);
+                        const int id = hnc;
+                        const int g = node_slot(P, H, t, id, &hnpg);
                         if (g < 0) {                     // no room: back up, do not store
                             H->unexpanded += 1;
                         } else {
@@ -1876,6 +1879,7 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
                             hash_insert(P, t, k0, g);
                             if (cached) { P.nd[node].h.bchild = g; P.nd[node].h.babt = (uint16_t)(pk.a | (1 << 15)); }
                             H->node_count = id + 1;
+                            hnc = id + 1;
                         }
                         leaf_node = g;
                     }
@@ -1891,10 +1895,15 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
         for (int u = 0; u < Conv<N>::UNITS; u++) Conv<N>::store(leaf_state + (size_t)t * Lx::S, s, u);
         int g = -1;
         if (P.nbrd) {                                    // the slot k_backup will insert it at
-            g = node_slot(P, H, t, H->node_count);
+            g = node_slot(P, H, t, hnc, &hnpg);
             if (g >= 0) {
-                uint64_t *dst = reinterpret_cast<uint64_t *>(P.nbrd + (size_t)g * NodeBoard<N>::BYTES);
-                for (int r = 0; r < Lx::ROWS; r++) dst[r] = row(s, r);
+                u32x4 *dst = reinterpret_cast<u32x4 *>(P.nbrd + (size_t)g * NodeBoard<N>::BYTES);
+                static_assert(NodeBoard<N>::BYTES % 16 == 0, "node boards: 16-byte stores");
+#pragma unroll
+                for (int r = 0; r < Lx::ROWS; r += 2) {      // (two rows per 16-byte store)
+                    const uint64_t a = row(s, r), b = r + 1 < Lx::ROWS ? row(s, r + 1) : 0;
+                    dst[r >> 1] = u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+                }
             }
         }
         H->leaf_slot = g;
