@@ -447,9 +447,10 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (threadIdx.x == 0) atomicAdd(&g_nn_probe[15], 1ull);
 #endif
     // ---- input: x[column c][leaf i][row r] = state[leaf][r][c] as int8 (token c*32+i)
+    // (no zero fill: the k past R of a row read the row's padding, the next row or, after the
+    // last one, stale LDS bytes — any int8 is finite and those k have zero weights; rows of
+    // missing leaves are never stored)
     int8_t *x0 = reinterpret_cast<int8_t *>(bufA);
-    for (int j = tid; j < 7 * ML * X0S / 4; j += NNT) reinterpret_cast<int32_t *>(x0)[j] = 0;
-    lds_barrier();
     if (tid < nb * 7) mskl[tid] = mask[rowof(tid / 7) * 7 + tid % 7];
     if constexpr ((7 * R) % 4 == 0) {
         // the workgroup's boards: dword loads (a board is a whole number of dwords), all in
