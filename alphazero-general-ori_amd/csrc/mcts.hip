@@ -2069,7 +2069,7 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
 // then the strict-'>' arg-max. Otherwise (ties, near ties) and for levels with more than
 // BK_WIDE records (roots) the wave evaluates the level exactly in float64.
 #ifndef BK_BATCH
-#define BK_BATCH 2
+#define BK_BATCH 1
 #endif
 #ifndef BK_WIDE
 #define BK_WIDE 12
@@ -2330,7 +2330,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     const uint64_t h_k0 = H->leaf_k0, h_k1 = H->leaf_k1;
     const int h_sims = H->sims_done, h_noise = H->noise_pending, h_gc = H->gc_state;
     const int32_t *path_n = P.path_n + (size_t)(tv ? t : 0) * (P.pcap + 1);
-    const size_t pb0 = (size_t)(tv ? t : 0) * P.pcap;   // this tree's k_backup scratch in P.path_b
     float val[4] = {0, 0, 0, 0};
     int lid = -1;
     BkScr &S = scr[2 * w + half];
@@ -2359,32 +2358,53 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         for (int i = 0; i < N; i++) val[i] = H->leaf_v[i];
         lid = path_n[depth];
     }
-    const int dmax = max(__shfl(depth, 0, 64), __shfl(depth, 32, 64));   // (uniform group loops)
+    // The two trees' path levels packed over the wave's 64 lanes: position p < dA is tree A's
+    // (half 0) level p, dA <= p < dA + dB tree B's level p - dA, 64 positions per iteration
+    // (halves of 32 levels each took max(dA, dB) / 32 iterations: 1.64 per wave at config 3,
+    // packed 1.31). A level lane reads its tree's values from the tree's lane 0 / 32.
+    const int dA = __builtin_amdgcn_readlane(depth, 0), dB = __builtin_amdgcn_readlane(depth, 32);
+    const int tA = __builtin_amdgcn_readlane(t, 0), tB = __builtin_amdgcn_readlane(t, 32);
+    const int tot = dA + dB, iters = (tot + 63) >> 6;
+    const auto lev = [&](int k, int &sel, int &d) {      // this lane's level in iteration k
+        const int p = 64 * k + l;
+        sel = p >= dA;
+        d = sel ? p - dA : p;
+        return p < tot;
+    };
 #if BACKUP_PROBE
     uint64_t bacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, blast = __builtin_readcyclecounter();
     int bexact = 0, bgroups = 0;
 #endif
     // ---- pass A (as k_backup)
     Level V;
-    load_levels_at(P, t, hl, depth, lid, V, act && hl < min(depth, 32));
+    int sel0, d0;
+    const bool in0 = lev(0, sel0, d0);
+    {
+        const int lidA = __builtin_amdgcn_readlane(lid, 0), lidB = __builtin_amdgcn_readlane(lid, 32);
+        load_levels_at(P, sel0 ? tB : tA, d0, sel0 ? dB : dA, sel0 ? lidB : lidA, V, in0);
+    }
     bool fail = false;
-    for (int g0 = 0; g0 < dmax; g0 += 32) {
-        const int grow = g0 == 0 ? V.grow : grow_at(P, t, g0 + hl, act && g0 + hl < depth);
+    for (int k = 0; k < iters; k++) {
+        int sel, d;
+        const bool inl = lev(k, sel, d);
+        const int tk = sel ? tB : tA;
+        const int grow = k == 0 ? V.grow : grow_at(P, tk, d, inl);
         uint64_t gm = __ballot(grow > 0);
         int64_t nb = -1;
-        while (gm) {                                     // (both halves' blocks in turn)
-            const int j = __ffsll((unsigned long long)gm) - 1;
+        while (gm) {                                     // (both trees' blocks in turn, each by
+            const int j = __ffsll((unsigned long long)gm) - 1;   //  its tree's lane 0 / 32)
             gm &= gm - 1;
             const int units = REC_UNITS * __builtin_amdgcn_readlane(grow, j);
-            const bool mine = hb == (j & 32);
+            const int owner = __builtin_amdgcn_readlane(sel, j) ? 32 : 0;
+            const bool mine = hb == owner;
             int64_t b = -1;
-            if (l == (j & 32) && !fail) b = unit_alloc(P, H, t, units);
-            b = readlane64(b, j & 32);
+            if (l == owner && !fail) b = unit_alloc(P, H, t, units);
+            b = readlane64(b, owner);
             if (mine && b < 0) fail = true;
             if (l == j) nb = b;
         }
-        if (g0 == 0) V.nb = nb;
-        else if (grow > 0) P.path_b[pb0 + g0 + hl] = nb;
+        if (k == 0) V.nb = nb;
+        else if (grow > 0) P.path_b[(size_t)tk * P.pcap + d] = nb;
     }
     BPROBE(0)
     int g = -1, ec = 0;
@@ -2514,21 +2534,35 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         }
         if (expand) lid = g;
     }
-    if (!done && depth > 0 && kind == LEAF_NN && hl == (depth - 1 < 32 ? depth - 1 : 32)) V.child = lid;
+    // per-tree values of the level lanes (after the expansion and the withdrawals)
+    const int lidA = __builtin_amdgcn_readlane(lid, 0), lidB = __builtin_amdgcn_readlane(lid, 32);
+    const int kindA = __builtin_amdgcn_readlane(kind, 0), kindB = __builtin_amdgcn_readlane(kind, 32);
+    const int doneA = __builtin_amdgcn_readlane((int)done, 0), doneB = __builtin_amdgcn_readlane((int)done, 32);
+    float valA[4], valB[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        valA[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(val[i]), 0));
+        valB[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(val[i]), 32));
+    }
+    if (in0 && !(sel0 ? doneB : doneA) && (sel0 ? kindB : kindA) == LEAF_NN && d0 == (sel0 ? dB : dA) - 1)
+        V.child = sel0 ? lidB : lidA;                    // (the new leaf below its parent's level)
     BPROBE(1)
-    // ---- pass B (as k_backup), levels in groups of 32 per half
+    // ---- pass B (as k_backup), the packed levels 64 per iteration
     int moved = 0x7fffffff, n_wide_lo = 0, n_wide_hi = 0, n_big_lo = 0, n_big_hi = 0;
-    for (int g0 = 0; g0 < dmax; g0 += 32) {
-        const int d = g0 + hl;
-        const bool in = !done && d < depth;
-        if (g0 > 0) {
-            load_levels_at(P, t, d, depth, lid, V, in);
-            if (in && V.grow > 0) V.nb = P.path_b[pb0 + d];
+    for (int k = 0; k < iters; k++) {
+        int sel, d;
+        const bool inl = lev(k, sel, d);
+        const int tk = sel ? tB : tA, depk = sel ? dB : dA, kk = sel ? kindB : kindA, lk = sel ? lidB : lidA;
+        const bool in = !(sel ? doneB : doneA) && inl;
+        const uint64_t selm = __ballot(sel);             // (tree B's lanes)
+        if (k > 0) {
+            load_levels_at(P, tk, d, depk, lk, V, in);
+            if (in && V.grow > 0) V.nb = P.path_b[(size_t)tk * P.pcap + d];
         }
         const bool reloc = in && V.e.vi < 0 && V.grow > 0 && V.nb >= 0 && V.r.vcnt > 0;
-        {                                                // (per-half counts, in SGPRs)
+        {                                                // (per-tree counts, in SGPRs)
             const uint64_t bm = __ballot(reloc && V.grow >= 128);
-            n_big_lo += __popcll(bm & 0xFFFFFFFFull); n_big_hi += __popcll(bm >> 32);
+            n_big_lo += __popcll(bm & ~selm); n_big_hi += __popcll(bm & selm);
         }
         for (uint64_t gm = __ballot(reloc); gm; gm &= gm - 1) {
             const int j = __ffsll((unsigned long long)gm) - 1;
@@ -2540,10 +2574,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         int n1 = 0, vidx = -1, nns = 0;
         double q1 = 0.0, nqs = 0.0;
         if (in) {
-            const int rot = (depth - d) % N, vi = (N - rot) % N;
-            float vr = val[0];
+            const int rot = (depk - d) % N, vi = (N - rot) % N;
+            float vr = sel ? valB[0] : valA[0];
 #pragma unroll
-            for (int i = 1; i < N; i++) vr = vi == i ? val[i] : vr;
+            for (int i = 1; i < N; i++) vr = vi == i ? (sel ? valB[i] : valA[i]) : vr;
             const double v0 = (double)vr;
             nqs = ((double)(V.ns + 1) * V.qs + v0) / (double)(V.ns + 2);
             nns = V.ns + 1;
@@ -2587,7 +2621,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         const bool wide = in && V.r.vcnt > BK_WIDE;
         {
             const uint64_t wm = __ballot(wide && d > 0);
-            n_wide_lo += __popcll(wm & 0xFFFFFFFFull); n_wide_hi += __popcll(wm >> 32);
+            n_wide_lo += __popcll(wm & ~selm); n_wide_hi += __popcll(wm & selm);
         }
         Screen Sc = screen_init(nns, nqs, C.cpuct, C.fpu);
         bool has_c = false;
@@ -2643,14 +2677,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         const bool stay = in && bsel == V.off;
         if (stay) { bch = V.rchild; bvi = vidx; }
         // the descent hints: a level whose pick stays on the path edge names the next two path
-        // levels' new picks (lanes hl + 1, hl + 2 of this half; none across a group boundary)
+        // levels' new picks (lanes l + 1, l + 2: the same tree while d + 1 / d + 2 < its depth;
+        // none across an iteration boundary)
         const int nb1 = __shfl(bch, min(l + 1, 63), 64), nb2 = __shfl(bch, min(l + 2, 63), 64);
         const int ns1 = __shfl((int)stay, min(l + 1, 63), 64);
-        const int hh2 = stay && hl < 31 && d + 1 < depth ? nb1 : -1;
-        const int hh3 = hh2 >= 0 && ns1 && hl < 30 && d + 2 < depth ? nb2 : -1;
+        const int hh2 = stay && l < 63 && d + 1 < depk ? nb1 : -1;
+        const int hh3 = hh2 >= 0 && ns1 && l < 62 && d + 2 < depk ? nb2 : -1;
         if (in) {                                        // the level's record, written once
             int bt_;
-            if (stay) bt_ = kind == LEAF_TERMINAL && bch >= 0 && bch == lid;   // (the path's child:
+            if (stay) bt_ = kk == LEAF_TERMINAL && bch >= 0 && bch == lk;     // (the path's child:
             else bt_ = bch >= 0 ? (int)P.nd[bch].h.term : 0;                   //  terminal only as the leaf)
             NodeHot w;                                   // (the second half: written with a new record)
             w.bchild = bch; w.h2 = hh2; w.h3 = hh3;
@@ -2659,7 +2694,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             w.qs = nqs;
             P.nd[V.node].h = w;
         }
-        moved = min(moved, half_min_i32(in && bsel != V.off ? d : 0x7fffffff));
+        {                                                // first level per tree whose pick moved
+            const uint64_t mv = __ballot(in && bsel != V.off);
+            const uint64_t mA = mv & ~selm, mB = mv & selm;
+            const int mvA = mA ? 64 * k + __ffsll((unsigned long long)mA) - 1 : 0x7fffffff;
+            const int mvB = mB ? 64 * k + __ffsll((unsigned long long)mB) - 1 - dA : 0x7fffffff;
+            moved = min(moved, half ? mvB : mvA);
+        }
     }
     const int n_wide = hb ? n_wide_hi : n_wide_lo, n_big = hb ? n_big_hi : n_big_lo;
     if (!done && hl == 0) {
@@ -2675,12 +2716,16 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     }
 #if BACKUP_PROBE
     BPROBE(5)
+    // (the level-group iterations the two trees' levels would take packed into 64 lanes)
+    const int pdv = act ? depth : 0;
+    const int pdA = __builtin_amdgcn_readlane(pdv, 0), pdB = __builtin_amdgcn_readlane(pdv, 32);
     if (l == 0) {
         unsigned long long *g = g_bk_probe[(blockIdx.x * WAVES + w) % BK_PSLOTS];
         for (int k = 0; k < 10; k++) g[k] += bacc[k];
         g[12] += 1;
         g[13] += bexact;
         g[14] += bgroups;
+        g[15] += (unsigned long long)((pdA + pdB + 63) / 64);
     }
 #endif
 }

@@ -65,7 +65,8 @@ def main():
         res["backup"] = {"waves": bw, "cycles_per_wave": {n: bk[k] / bw for k, n in enumerate(
             ("pass_a", "expansion_node_write", "pass_b_updates", "screen", "exact_levels", "writes_end",
              "expansion_alloc", "expansion_normalise", "expansion_sorted_run", "expansion_argmax"))},
-            "exact_levels_per_wave": bk[13] / bw, "groups_per_wave": bk[14] / bw}
+            "exact_levels_per_wave": bk[13] / bw, "groups_per_wave": bk[14] / bw,
+            "packed_groups_per_wave": bk[15] / bw}
     print(json.dumps(res), flush=True)
 
 
