@@ -436,22 +436,29 @@ __device__ int node_slot(const Pools &P, TreeHdr *H, int t, int id, int *npg_reg
 
 // n contiguous edge units for tree t (a run or a visit block: global base), from the tree's
 // current edge page or a fresh one (allocations never straddle pages); -1 when the tree's
-// edge pages are at their maximum or the pool is empty. One lane.
-__device__ int64_t unit_alloc(const Pools &P, TreeHdr *H, int t, int n) {
-    if (H->eleft < n) {
-        if (H->epg >= P.eptab) return -1;
-        const int pg = H->epg < P.ehome ? t * P.ehome + H->epg : pop_page(P.efree, P.alloc + 1);
+// edge pages are at their maximum or the pool is empty. The tree's allocator fields are held
+// in registers (k_backup_h loads them with the header's first loads, so an allocation costs
+// no dependent header load) and written through on every change. One lane per tree.
+struct AllocState {
+    int64_t enext;
+    int eleft, epg, edge_count;
+};
+__device__ __forceinline__ AllocState alloc_state(const TreeHdr *H) { return AllocState{H->enext, H->eleft, H->epg, H->edge_count}; }
+__device__ int64_t unit_alloc_s(const Pools &P, TreeHdr *H, int t, int n, AllocState &a) {
+    if (a.eleft < n) {
+        if (a.epg >= P.eptab) return -1;
+        const int pg = a.epg < P.ehome ? t * P.ehome + a.epg : pop_page(P.efree, P.alloc + 1);
         if (pg < 0) { atomicAdd(P.alloc + 3, 1); return -1; }
-        P.etab[(size_t)t * P.eptab + H->epg] = pg;
-        P.epidx[pg] = H->epg;
-        H->epg += 1;
-        H->enext = (int64_t)pg * UPG;
-        H->eleft = UPG;
+        P.etab[(size_t)t * P.eptab + a.epg] = pg;
+        P.epidx[pg] = a.epg;
+        a.epg += 1;
+        H->epg = a.epg;
+        a.enext = (int64_t)pg * UPG;
+        a.eleft = UPG;
     }
-    const int64_t b = H->enext;
-    H->enext = b + n;
-    H->eleft -= n;
-    H->edge_count += n;
+    const int64_t b = a.enext;
+    a.enext = b + n; a.eleft -= n; a.edge_count += n;
+    H->enext = a.enext; H->eleft = a.eleft; H->edge_count = a.edge_count;
     return b;
 }
 
@@ -2329,6 +2336,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
     const int h_slot = H->leaf_slot, h_hslot = H->leaf_hslot, h_round = H->leaf_round;
     const uint64_t h_k0 = H->leaf_k0, h_k1 = H->leaf_k1;
     const int h_sims = H->sims_done, h_noise = H->noise_pending, h_gc = H->gc_state;
+    AllocState al = alloc_state(H);                      // (used by the tree's lane 0 / 32)
+    int h_nc = H->node_count, h_npg = H->npg;
     const int32_t *path_n = P.path_n + (size_t)(tv ? t : 0) * (P.pcap + 1);
     float val[4] = {0, 0, 0, 0};
     int lid = -1;
@@ -2398,7 +2407,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             const int owner = __builtin_amdgcn_readlane(sel, j) ? 32 : 0;
             const bool mine = hb == owner;
             int64_t b = -1;
-            if (l == owner && !fail) b = unit_alloc(P, H, t, units);
+            if (l == owner && !fail) b = unit_alloc_s(P, H, t, units, al);
             b = readlane64(b, owner);
             if (mine && b < 0) fail = true;
             if (l == j) nb = b;
@@ -2420,8 +2429,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
 #pragma unroll
         for (int k = 0; k < 7; k++) ec += __popcll(S.bits[k]);
         if (!fail && hl == 0) {
-            g = h_slot >= 0 ? h_slot : node_slot(P, H, t, H->node_count);
-            if (g >= 0) eb = unit_alloc(P, H, t, ec);
+            g = h_slot >= 0 ? h_slot : node_slot(P, H, t, h_nc, &h_npg);
+            if (g >= 0) eb = unit_alloc_s(P, H, t, ec, al);
         }
     }
     g = __shfl(g, hb, 64);
@@ -2530,7 +2539,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             if (h_hslot >= 0) P.hslot[(size_t)t * P.hcap + h_hslot] = g;
             else hash_insert(P, t, h_k0, g);
             if (depth == 0) H->root = g;
-            H->node_count += 1;
+            H->node_count = h_nc + 1;
         }
         if (expand) lid = g;
     }
