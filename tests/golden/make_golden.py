@@ -40,8 +40,9 @@ Chance injection (the reference is unseeded):
       device / oracle (tests/golden/detrand.py), so whole episodes (Coach.executeEpisode)
       and arena games (Arena.playGames) replay with the build's random streams.
 
-Usage:  python tests/golden/make_golden.py [nnet3,train]   (writes tests/golden/*.npz; with
-        a list, only those round-3 groups)
+Usage:  python tests/golden/make_golden.py [nnet3,train,bigmcts]   (writes tests/golden/*.npz;
+        with a list, only those groups: nnet3 / train (round 3), bigmcts (round 6: 2p at 1,600
+        and 4p at 400 simulations, hash and peaked networks, tree reuse))
 """
 import os
 import sys
@@ -493,6 +494,146 @@ def mcts_fixtures(game_mod, mcts_mod, numba_logic, n_players, seed, cases):
     return res
 
 
+class PeakedNNet(FakeNNet):
+    """The peaked hash network (oracle `or_fake_predict` mode 1, device `HashEvaluator(mode=1)`)
+    restated: w_a = 1 + (splitmix64(h + a) >> 40) over the legal actions, pi[a] = (w_a / max w)^256
+    by eight squarings in float64, stored float32 (one or a few actions dominate, many are exactly
+    0); v[i] = +-(1 - (splitmix64(h ^ (0xA5A5 + i)) >> 40) * 2^-30), + for player 0. It grows
+    trees as deep as the benchmark's random-init SplendorNNet (leaf depths in the tens)."""
+
+    def predict(self, board, valid_actions):
+        valids = np.asarray(valid_actions, dtype=bool)
+        h = fnv1a64(np.ascontiguousarray(board).view(np.uint8).tobytes())
+        w = {int(a): float(1 + (splitmix64((h + int(a)) & M64) >> 40)) for a in np.flatnonzero(valids)}
+        wmax = max(w.values())
+        pi = np.zeros(len(valids), dtype=np.float32)
+        for a, wa in w.items():
+            x = wa / wmax
+            for _ in range(8):
+                x = x * x
+            pi[a] = np.float32(x)
+        v = np.array([np.float32((1.0 if i == 0 else -1.0) *
+                                 (1.0 - (splitmix64(h ^ (0xA5A5 + i)) >> 40) * 2.0 ** -30))
+                      for i in range(self.n)], dtype=np.float32)
+        return pi, v
+
+
+def _track_leaf_depths(m):
+    """Wraps MCTS.search (the recursion resolves self.search through the instance) to record,
+    per simulation, the number of edges from the root to the node it ends at (a new leaf or a
+    terminal node): the oracle's or_depth_stats / the device's depth_sum definition."""
+    depths, st = [], {"d": 0, "max": 0}
+    orig = m.search
+
+    def search(*a, **k):
+        st["d"] += 1
+        st["max"] = max(st["max"], st["d"])
+        try:
+            return orig(*a, **k)
+        finally:
+            st["d"] -= 1
+            if st["d"] == 0:
+                depths.append(st["max"] - 1)
+                st["max"] = 0
+    m.search = search
+    return depths
+
+
+def big_mcts_fixtures(game_mod, mcts_mod, numba_logic, n, seed, sims, n_roots, n_peaked, seq_moves):
+    """Round 6: the reference's MCTS (MCTS.py:45-97, 99-177, 199-219) at the large budgets of
+    BASELINE configs 4 (2p, numMCTSSims 1,600) and 5 (4p, 400), genbu.pt's cpuct 2.5 / fpu 0.3:
+    n_roots single searches under the hash network (mode 0) from positions spread over random
+    games, n_peaked more under the peaked network (mode 1: deep trees), and one multi-move game
+    with tree reuse (the first arg-max of the counts is played, chance injected). Dirichlet off,
+    forced playouts off, every search full (force_full_search, as mcts_fixtures)."""
+    Game = game_mod.SplendorGame
+    Board = numba_logic.Board
+    game_rng = np.random.default_rng(seed)
+    pool = []
+    STREAM.set_source(np.random.default_rng([seed, 7]))
+    b = Board(n)
+    state, player = b.get_state().copy(), 0
+    scratch = Board(n)
+    while len(pool) < 120:
+        scratch.copy_state(state, True)
+        if player != 0:
+            scratch.swap_players(player)
+        pool.append(scratch.get_state().copy())
+        scratch.copy_state(state, True)
+        v = np.flatnonzero(scratch.valid_moves(player))
+        STREAM.set_source(np.random.default_rng([seed, 8, len(pool)]))
+        scratch.copy_state(state, True)
+        player = scratch.make_move(int(v[game_rng.integers(len(v))]), player, False)
+        state = scratch.get_state().copy()
+        scratch.copy_state(state, True)
+        if scratch.check_end_game().any():
+            STREAM.set_source(np.random.default_rng([seed, 9, len(pool)]))
+            b = Board(n)
+            state, player = b.get_state().copy(), 0
+    args = {"numMCTSSims": sims, "cpuct": 2.5, "fpu": 0.3, "prob_fullMCTS": 1.0, "ratio_fullMCTS": 5,
+            "forced_playouts": False, "no_mem_optim": False, "dirichletAlpha": 0.0,
+            "temperature": [1.25, 0.8]}
+    out = {k: [] for k in ("root", "mode", "counts", "qsa", "probs", "q", "ns", "nodes", "depth")}
+    step = len(pool) // (n_roots + n_peaked)
+    roots = pool[::step][:n_roots + n_peaked]
+    for i, root in enumerate(roots):
+        mode = 0 if i < n_roots else 1
+        g = Game(n)
+        net = FakeNNet(n) if mode == 0 else PeakedNNet(n)
+        m = mcts_mod.MCTS(g, net, _DotDict(args), dirichlet_noise=False)
+        depths = _track_leaf_depths(m)
+        probs, q, _ = m.getActionProb(root.copy(), temp=1, force_full_search=True)
+        node = m.nodes_data[g.stringRepresentation(root)]
+        out["root"].append(root.copy())
+        out["mode"].append(mode)
+        out["nodes"].append(len(m.nodes_data))
+        out["depth"].append([sum(depths), max(depths), len(depths)])
+        out["counts"].append(np.asarray(node[5], dtype=np.int64))
+        out["qsa"].append(np.asarray(node[4], dtype=np.float64))
+        out["probs"].append(np.asarray(probs, dtype=np.float64))
+        out["q"].append(np.asarray(q, dtype=np.float64))
+        out["ns"].append(int(node[3]))
+        print(f"  {n}p {sims} sims root {i} mode {mode}: {int((out['counts'][-1] > 0).sum())} visited edges, "
+              f"max N {int(out['counts'][-1].max())}, {len(m.nodes_data)} nodes, leaf depth mean "
+              f"{sum(depths) / len(depths):.1f} max {max(depths)}", flush=True)
+    seq = {k: [] for k in ("root", "counts", "probs", "q", "action", "uoff", "ulen")}
+    seq_uni = []
+    g = Game(n)
+    m = mcts_mod.MCTS(g, FakeNNet(n), _DotDict(args), dirichlet_noise=False)
+    STREAM.set_source(np.random.default_rng([seed, 11]))
+    board = g.getInitBoard().copy()
+    init_uniforms, init_state = np.array(STREAM.used, dtype=np.float64), board.copy()
+    cur = 0
+    for move in range(seq_moves):
+        canon = g.getCanonicalForm(board, cur).copy()
+        probs, q, _ = m.getActionProb(canon, temp=1, force_full_search=True)
+        counts = np.asarray(m.nodes_data[g.stringRepresentation(canon)][5], dtype=np.int64)
+        a = int(np.argmax(counts))
+        seq["root"].append(canon)
+        seq["counts"].append(counts)
+        seq["probs"].append(np.asarray(probs, dtype=np.float64))
+        seq["q"].append(np.asarray(q, dtype=np.float64))
+        seq["action"].append(a)
+        STREAM.set_source(np.random.default_rng([seed, 12, move]))
+        board, cur = g.getNextState(board, cur, a)
+        board = board.copy()
+        seq["uoff"].append(len(seq_uni))
+        seq["ulen"].append(len(STREAM.used))
+        seq_uni.extend(STREAM.used)
+        if g.getGameEnded(board, cur).any():
+            break
+    res = {k: np.array(v) for k, v in out.items()}
+    for k, v in seq.items():
+        res["seq_" + k] = np.array(v)
+    res["seq_uniforms"] = np.array(seq_uni, dtype=np.float64)
+    res["seq_init_uniforms"] = init_uniforms
+    res["seq_init_state"] = init_state
+    res["sims"] = np.array(sims)
+    res["cpuct"] = np.array(2.5)
+    res["fpu"] = np.array(0.3)
+    return res
+
+
 class _DotDict(dict):
     def __getattr__(self, k):
         return self[k]
@@ -925,6 +1066,12 @@ def main(only=None):
                 tag = f"{n}p" + ("_dropout" if dropout else "")
                 np.savez_compressed(os.path.join(OUT, f"train_{tag}.npz"), **tf)
                 print(f"train {tag}: {len(tf['sample_ids'])} steps, first losses {tf['losses'][0].round(4).tolist()}")
+        if "bigmcts" in only:                # round 6: configs 4 / 5 budgets
+            for n, sims, seed in ((2, 1600, 6002), (4, 400, 6004)):
+                bf = big_mcts_fixtures(game_mod, mcts_mod, numba_logic, n, seed, sims, n_roots=6, n_peaked=4,
+                                       seq_moves=12)
+                np.savez_compressed(os.path.join(OUT, f"bigmcts_{n}p.npz"), **bf)
+                print(f"bigmcts {n}p: {len(bf['root'])} searches at {sims}, seq moves {len(bf['seq_root'])}")
         return
     # tables: checked by the oracle tests against its own restatement
     np.savez_compressed(

@@ -63,6 +63,45 @@ def test_multi_move_tree_reuse_matches_reference(engines, n):
         np.testing.assert_array_equal(q.cpu().numpy()[0], d["seq_q"][k])
 
 
+@pytest.mark.parametrize("n", (2, 4))
+def test_large_budget_searches_match_reference(engines, n):
+    """Round 6: the device's root statistics against the reference's MCTS executed at configs
+    4 / 5's budgets (2p 1,600, 4p 400 simulations; `bigmcts_*.npz`), under the hash network and
+    under the peaked one (deep trees: leaf depths to ~100), with every simulation's leaf depth
+    (sum and maximum per tree) as the reference's recursion reached it."""
+    from splendor.mcts import HashEvaluator
+    d = load(f"bigmcts_{n}p.npz")
+    for mode in (0, 1):
+        idx = np.flatnonzero(d["mode"] == mode)
+        m = mcts_for(engines[n], len(idx), int(d["sims"]), float(d["cpuct"]), float(d["fpu"]), False,
+                     evaluator=HashEvaluator(engines[n], mode=mode))
+        probs, q, _, counts = m.get_action_prob(torch.from_numpy(d["root"][idx]).cuda(), force_full_search=True,
+                                                keep_tree=False)
+        _, qsa, _, _ = m.root_stats()
+        msg = f"{n}p mode {mode}"
+        np.testing.assert_array_equal(counts.cpu().numpy(), d["counts"][idx], err_msg=msg)
+        np.testing.assert_array_equal(qsa.cpu().numpy(), d["qsa"][idx], err_msg=msg)
+        np.testing.assert_array_equal(probs.cpu().numpy(), d["probs"][idx], err_msg=msg)
+        np.testing.assert_array_equal(q.cpu().numpy(), d["q"][idx], err_msg=msg)
+        h = m.headers()
+        np.testing.assert_array_equal(h["depth_sum"], d["depth"][idx, 0], err_msg=msg)
+        np.testing.assert_array_equal(h["depth_max"], d["depth"][idx, 1], err_msg=msg)
+        assert h["prunes"].sum() == h["resets"].sum() == h["unexpanded"].sum() == 0
+
+
+@pytest.mark.parametrize("n", (2, 4))
+def test_large_budget_tree_reuse_matches_reference(engines, n):
+    """The reference's 12-move game at the large budget with its tree kept between moves."""
+    d = load(f"bigmcts_{n}p.npz")
+    m = mcts_for(engines[n], 1, int(d["sims"]), float(d["cpuct"]), float(d["fpu"]), False)
+    for k in range(len(d["seq_root"])):
+        root = torch.from_numpy(d["seq_root"][k][None]).cuda()
+        probs, q, _, counts = m.get_action_prob(root, force_full_search=True, keep_tree=True)
+        np.testing.assert_array_equal(counts.cpu().numpy()[0], d["seq_counts"][k], err_msg=f"{n}p move {k}")
+        np.testing.assert_array_equal(probs.cpu().numpy()[0], d["seq_probs"][k])
+        np.testing.assert_array_equal(q.cpu().numpy()[0], d["seq_q"][k])
+
+
 @pytest.mark.parametrize("n,sims", [(2, 100), (3, 40), (4, 64)])
 def test_batch_searches_match_oracle(engines, n, sims):
     d = load(f"env_{n}p.npz")

@@ -135,6 +135,57 @@ def test_mcts_multi_move_tree_reuse(n):
         st, player, _ = O.make_move(n, st, a, player, False, uni[off:off + ln])
 
 
+@pytest.mark.parametrize("n", (2, 4))
+def test_mcts_large_budget_searches(n):
+    """Round 6: the reference's MCTS executed at BASELINE configs 4 / 5's budgets (2p 1,600, 4p
+    400 simulations; genbu.pt's cpuct 2.5 / fpu 0.3) from 10 roots spread over random games,
+    6 under the hash network (mode 0) and 4 under the peaked one (mode 1: deep trees). Beyond
+    the root statistics, the table size and every simulation's leaf depth (sum, max, count)."""
+    d = load(f"bigmcts_{n}p.npz")
+    sims = int(d["sims"])
+    try:
+        for i in range(len(d["root"])):
+            O.set_fake_mode(int(d["mode"][i]))
+            O.depth_stats(reset=True)
+            m = O.Mcts(n, sims, float(d["cpuct"]), float(d["fpu"]), False)
+            counts, qsa, probs, q, nodes = m.search(d["root"][i])
+            msg = f"root {i} (mode {int(d['mode'][i])})"
+            np.testing.assert_array_equal(counts, d["counts"][i], err_msg=msg)
+            np.testing.assert_array_equal(qsa, d["qsa"][i], err_msg=msg)
+            np.testing.assert_array_equal(probs, d["probs"][i], err_msg=msg)
+            np.testing.assert_array_equal(q, d["q"][i], err_msg=msg)
+            assert nodes == d["nodes"][i], msg
+            assert O.depth_stats(reset=True) == tuple(int(x) for x in d["depth"][i]), msg
+    finally:
+        O.set_fake_mode(0)
+    # the set reaches the deep regime the large-budget self-play tests run in
+    deep = d["depth"][d["mode"] == 1]
+    assert (deep[:, 1] >= 20).any()
+
+
+@pytest.mark.parametrize("n", (2, 4))
+def test_mcts_large_budget_tree_reuse(n):
+    """A 12-move game at the large budget with the tree kept between moves (MCTS.py:79-85
+    cleaning included), chance injected, arg-max play."""
+    d = load(f"bigmcts_{n}p.npz")
+    m = O.Mcts(n, int(d["sims"]), float(d["cpuct"]), float(d["fpu"]), False)
+    st, used = O.init(n, d["seq_init_uniforms"])
+    np.testing.assert_array_equal(st, d["seq_init_state"])
+    uni = d["seq_uniforms"]
+    player = 0
+    for k in range(len(d["seq_root"])):
+        canon = O.swap_players(n, st, player) if player else st
+        np.testing.assert_array_equal(canon, d["seq_root"][k])
+        counts, qsa, probs, q, _ = m.search(canon)
+        np.testing.assert_array_equal(counts, d["seq_counts"][k], err_msg=f"move {k}")
+        np.testing.assert_array_equal(probs, d["seq_probs"][k])
+        np.testing.assert_array_equal(q, d["seq_q"][k])
+        a = int(np.argmax(counts))
+        assert a == d["seq_action"][k]
+        off, ln = int(d["seq_uoff"][k]), int(d["seq_ulen"][k])
+        st, player, _ = O.make_move(n, st, a, player, False, uni[off:off + ln])
+
+
 def test_philox_known_answer():
     # Random123 Philox4x32-10 known-answer vector (ctr=0,key=0)
     import ctypes as C

@@ -14,6 +14,8 @@
 #   spikes    the slowest launches of each kernel and their iterations (needs trace) -> gpurun_out/spikes.json
 #   pmc       PMC passes over the self-play kernels (pmc_selfplay.sh)  -> gpurun_out/pmc_sp/
 #   nn        full-batch network trace + HBM counters (nn_fullbatch.sh) -> gpurun_out/nnfb/
+#   accuracy  the fused network vs float64 on 4,096 positions at 2p and 4p (nn_accuracy.py)
+#             -> gpurun_out/nn_accuracy.jsonl
 #   ab        interleaved A/B of the product against each V in $AB: ablib/lib<V>.so, or a whole
 #             older tree ablib/<V>/ (bench.py + package) (config-3 bench twice each) -> gpurun_out/ab.txt
 #   probe     k_select_lanes phase probes (ablib/lib<V>.so for V in ${PROBES:-probe}, -DSELECT_PROBE=1) -> gpurun_out/<V>.json
@@ -27,7 +29,7 @@ set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 TR=${TREE:-sp}                                             # trace / split / spikes: TREE=<V> traces
 TB=bench.py; [ -n "${TREE:-}" ] && TB="ablib/$TREE/bench.py"  # the older tree ablib/<V>/ instead
 step() {
@@ -57,6 +59,12 @@ step() {
         timeout -k 10 1000 bash tools/pmc_selfplay.sh gpurun_out/pmc_sp "$ROUND" > gpurun_out/pmc_sp.log 2>&1 ;;
     nn)
         timeout -k 10 400 bash tools/nn_fullbatch.sh "$ROUND" > gpurun_out/nnfb.log 2>&1 ;;
+    accuracy)
+        rm -f gpurun_out/nn_accuracy.jsonl
+        for np_ in 2 4; do
+            timeout -k 10 240 python3 -u tools/nn_accuracy.py 4096 $np_ >> gpurun_out/nn_accuracy.jsonl \
+                2> gpurun_out/nn_accuracy.err || return 1
+        done ;;
     ab)
         rm -f gpurun_out/ab.txt
         for rep in 1 2; do
