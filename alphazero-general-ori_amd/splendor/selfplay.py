@@ -13,6 +13,7 @@ Coach.py:91-98, drained as device tensors (`drain()`), optionally gathered acros
 """
 import ctypes as C
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -150,6 +151,23 @@ class SelfPlay(BatchedMCTS):
                 "exact_wide": int(h["exact_wide"].astype("int64").sum()),
                 "big_moves": int(h["big_moves"].astype("int64").sum()),
                 **self.capacity_events(h), "examples_dropped": self.dropped_examples()}
+
+    # per-tree cumulative 32-bit header counters (depth_sum wraps after ~40 M simulations of a
+    # long-lived tree at depth ~50); window deltas are taken per tree modulo 2^32, then summed
+    COUNTERS = {"games_done": "games_done", "moves": "moves", "withdrawals": "withdrawals",
+                "collections": "gcs", "depth_sum": "depth_sum", "sims_backed": "sims_backed",
+                "exact_wide": "exact_wide", "big_moves": "big_moves", "prunes": "prunes", "resets": "resets",
+                "unexpanded": "unexpanded"}
+
+    def counter_snapshot(self):
+        h = self.headers()
+        return {k: h[f].astype(np.uint32) for k, f in self.COUNTERS.items()}
+
+    @staticmethod
+    def counter_delta(before, after):
+        """Window totals of counter_snapshot()s: wrap-safe as long as no single tree's counter
+        advances by 2^32 or more inside the window."""
+        return {k: int((after[k] - before[k]).astype(np.int64).sum()) for k in before}
 
 
 def pack_examples(examples):

@@ -248,7 +248,11 @@ CONFIGS = {  # BASELINE.json configs: (players, games per GPU, numMCTSSims)
 # (~ one game length), and the statistics window after the timed steps
 PHASES = {
     "config3": dict(prefill=6000, stagger=4800, window=10000),
-    "config4": dict(prefill=45000, stagger=40000, window=4000),
+    # config 4: a game is ~76 K iterations (0.25 x 1,600 + 0.75 x 320 simulations per move, ~119
+    # plies), so the stagger spans one game (restarts every 4,800 iterations) and the prefill
+    # ends with the games' ages spread over 12 K .. 84 K iterations (45 K / 40 K had
+    # left the window with 39 finished games, i.e. no end-game phases)
+    "config4": dict(prefill=84000, stagger=80000, window=4000),
     "config5": dict(prefill=40000, stagger=32000, window=6000),
 }
 
@@ -343,7 +347,7 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
         elapsed = float(t.item())
     iter_ms_events = ev0.elapsed_time(ev1) / steps
     # extended window: capacity events, games, examples drained + gathered
-    st0 = sp.stats()
+    c0 = sp.counter_snapshot()
     pool0 = sp.pool_state()
     ex_local = 0
     tw = time.perf_counter()
@@ -384,9 +388,7 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     e1.record()
     torch.cuda.synchronize(dev)
     nn_us = e0.elapsed_time(e1) / nk * 1e3
-    keys = ("games_done", "moves", "prunes", "resets", "unexpanded", "withdrawals", "collections", "depth_sum",
-            "sims_backed", "exact_wide", "big_moves")
-    delta = {k: st[k] - st0[k] for k in keys}
+    delta = sp.counter_delta(c0, sp.counter_snapshot())     # per tree, modulo 2^32, then summed
     # leaf depth over every simulation backed up in the window (a snapshot of the trees'
     # current path depths swings with the 20-iteration search cycle)
     depth_mean = delta["depth_sum"] / delta["sims_backed"] if delta["sims_backed"] else st["leaf_depth_now"]
@@ -395,6 +397,10 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     delta["rollouts_per_s"] = world * B * window / window_s
     delta["node_page_misses"] = pool["node_page_misses"] - pool0["node_page_misses"]
     delta["edge_page_misses"] = pool["edge_page_misses"] - pool0["edge_page_misses"]
+    # steady-state check: at a steady population every game finishes within the window at the
+    # rate B / (game length), i.e. the window's moves per finished game ~ plies per game (~119 at
+    # 2 players); a population still in its first games shows thousands
+    delta["moves_per_game_finished"] = delta["moves"] / max(1, delta["games_done"])
     delta["events_per_1000_moves"] = {k: 1000.0 * delta[k] / max(1, delta["moves"])
                                       for k in ("prunes", "resets", "unexpanded")}
     delta["examples_drained"] = ex_local

@@ -77,11 +77,21 @@ def test_config4_multi_rank_dry_run(workload):
     c4 = out["selfplay"] if workload == "config4" else out["config4_shard"]
     assert out["n_gpus"] == 2 and c4["n_gpus"] == 2 and c4["global_games"] == 65536
     assert c4["window"]["examples_gathered"] == 3 + 4          # rank 0: 3 examples, rank 1: 4
-    assert (c4["window"]["prefill"], c4["window"]["stagger"], c4["window"]["window"]) == (45000, 40000, 4000)
+    assert (c4["window"]["prefill"], c4["window"]["stagger"], c4["window"]["window"]) == (84000, 80000, 4000)
     if workload == "all":
         assert out["selfplay"]["global_games"] == 65536 and out["selfplay"]["numMCTSSims"] == 100
 
 
 def test_phase_defaults_per_workload(bench):
     assert bench.PHASES["config3"] == dict(prefill=6000, stagger=4800, window=10000)
-    assert bench.PHASES["config4"]["prefill"] == 45000 and bench.PHASES["config5"]["prefill"] == 40000
+    assert bench.PHASES["config4"]["prefill"] == 84000 and bench.PHASES["config5"]["prefill"] == 40000
+
+
+def test_window_counters_are_wrap_safe():
+    """the per-tree 32-bit header counters (depth_sum wraps after ~40 M simulations
+    of a long-lived tree) are differenced per tree modulo 2^32 before summing."""
+    import numpy as np
+    from splendor.selfplay import SelfPlay
+    before = {"depth_sum": np.array([2**32 - 10, 5, 2**31 - 1], np.uint32)}
+    after = {"depth_sum": np.array([20, 9, 2**31 + 99], np.uint32)}
+    assert SelfPlay.counter_delta(before, after) == {"depth_sum": 30 + 4 + 100}

@@ -203,7 +203,7 @@ def test_search_arena_spends_whole_budget_under_pressure():
 
 @pytest.mark.parametrize("n,B,sims,prefill,window,stagger", [(2, 32768, 100, 3000, 3000, 0),
                                                              (4, 16384, 400, 30000, 8000, 0),
-                                                             (2, 32768, 1600, 45000, 4000, 40000)])
+                                                             (2, 32768, 1600, "bench", 4000, "bench")])
 def test_steady_state_search_is_reference_exact(n, B, sims, prefill, window, stagger):
     """Configs 3, 5 and 4's per-GPU shard at full size with SplendorNNet leaves on the default
     shared pools, run to their steady state (config 3: games finish from ~2,400 iterations
@@ -218,6 +218,8 @@ def test_steady_state_search_is_reference_exact(n, B, sims, prefill, window, sta
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
+    if prefill == "bench":                      # config 4: bench.py's own phases (~ one game)
+        prefill, stagger = bench.PHASES["config4"]["prefill"], bench.PHASES["config4"]["stagger"]
     e = SplendorEngine(n)
     ev = LeafEvaluator(e, random_net(n, seed=0), B, use_graph=False)
     _, sp = selfplay(n, B, sims, evaluator=ev)

@@ -263,6 +263,14 @@ def _grad_worker(rank, world, port, q):
         ps[1].grad = torch.full((3,), 4.0)                    # on rank 0 only
     _allreduce_grads(ps)                                      # ps[2]: on no rank
     out = [None if p.grad is None else p.grad.tolist() for p in ps]
+    # weighted (uneven per-rank batches): each rank scaled by its share, summed;
+    # the flags still travel unscaled, so the no-rank parameter stays None
+    qs = [torch.nn.Parameter(torch.zeros(3)) for _ in range(3)]
+    qs[0].grad = torch.full((3,), 2.0 + rank)
+    if rank == 0:
+        qs[1].grad = torch.full((3,), 4.0)
+    _allreduce_grads(qs, weight=(0.25, 0.75)[rank])
+    out += [None if p.grad is None else p.grad.tolist() for p in qs]
     q.put(out)
     dist.barrier()
     dist.destroy_process_group()
@@ -283,6 +291,7 @@ def test_allreduce_grads_keeps_absent_gradients_none():
         assert p.exitcode == 0
     for out in outs:
         assert out[0] == [2.5] * 3 and out[1] == [2.0] * 3 and out[2] is None
+        assert out[3] == [0.25 * 2.0 + 0.75 * 3.0] * 3 and out[4] == [0.25 * 4.0] * 3 and out[5] is None
 
 
 def test_content_checksum_is_chunk_independent(monkeypatch):
