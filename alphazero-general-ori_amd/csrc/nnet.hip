@@ -54,7 +54,6 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int NNT = 512;      // threads per workgroup (8 waves)
 constexpr int ML = 32;         // leaves per workgroup
-constexpr int XS = 132;        // per-column activation row stride (floats)
 constexpr int LS = 420;        // logits row stride (floats)
 constexpr int ZS = 712;        // flattened trunk row stride (704 features; 8 mod 64 dwords)
 constexpr int ACT = 409;
@@ -66,12 +65,23 @@ struct SplitAct {
     uint16_t p[3][ML][SS];
 };
 constexpr int SAB = (int)sizeof(SplitAct);                 // 27,648 bytes
-// bufA (bytes) holds the per-column activations (7 x ML x XS floats), then the flattened trunk
-// Z, then — once dense1d_4 has read Z — split buffers SB1 [0, SAB), SB2 [SAB, 2 SAB) and the
-// logits from 2 SAB on; SB0 has its own array (dense2d_3's pool partials before dense1d_4)
-constexpr int BUFA = 7 * ML * XS * 4;
-static_assert(ML * ZS * 4 <= BUFA && 2 * SAB + ML * LS * 4 <= BUFA, "bufA overlays");
-static_assert(2 * 64 * ML * 4 <= SAB, "dense2d_3 pool partials fit SB0");
+// Per-column stage (round 6): wave w < 7 owns board column w of the ML leaves (one 32-token
+// tile) and keeps its 128-channel activation in registers through all four per-column layers;
+// the layers' split weights stream through LDS, once per workgroup, in stages of at most
+// RSTAGE 16-k chunks (RSLOT bytes each: 4 column blocks x 3 parts x 64 lanes x 16 B, lane-linear
+// MFMA fragments), double-buffered and filled by wave 7 with LDS-DMA loads.
+constexpr int RSLOT = 4 * 3 * 1024;
+constexpr int RSTAGE = 4;
+constexpr int RING = 2 * RSTAGE * RSLOT;                   // 98,304 bytes
+constexpr int PS = 64;                                     // pool staging row (floats, 16-B units swizzled)
+// bufA (bytes): the int8 input staging and the weight ring (per-column stage), then the
+// flattened trunk Z [ML][ZS] with the pool staging P [5][ML][PS] of columns 0-4's channels 0-63
+// behind it, then — once dense1d_4 has read Z — split buffers SB1 [0, SAB), SB2 [SAB, 2 SAB)
+// and the logits from 2 SAB on; SB0 has its own array (the per-column biases before dense1d_4)
+constexpr int ZBYTES = ML * ZS * 4;
+constexpr int BUFA = ZBYTES + 5 * ML * PS * 4;             // 132,096 bytes
+static_assert(2 * SAB + ML * LS * 4 <= BUFA, "bufA overlays");
+static_assert(4 * 128 * 4 <= SAB, "per-column biases fit SB0");
 
 __host__ __device__ constexpr int kpad(int K) { return (K + 7) / 8 * 8; }
 __host__ __device__ constexpr int ntiles(int N) { return (N + 31) / 32; }
@@ -116,14 +126,31 @@ struct Net {
     }
     static constexpr int TOTAL = soff(NL);
     static constexpr int X0S = (kpad(R) / 4) % 2 ? kpad(R) : kpad(R) + 4;   // int8 input stride (odd dwords)
+    // per-column stage: 16-k chunks per layer, each layer split into one or two LDS stages
+    static constexpr int CL[4] = {kp16(R) / 16, 8, 6, 8};
+    static constexpr int XR = (7 * ML * X0S + 15) / 16 * 16;  // weight ring offset in bufA (bytes)
+    static constexpr int first(int l) { return CL[l] > RSTAGE ? (CL[l] + 1) / 2 : CL[l]; }
+    static constexpr int nstages(int l) { return CL[l] > RSTAGE ? 2 : 1; }
+    static constexpr int NSTG = nstages(0) + nstages(1) + nstages(2) + nstages(3);
+    // stage s: (layer, first chunk, chunks)
+    static constexpr int stg_layer(int s) {
+        for (int l = 0; l < 4; l++) {
+            if (s < nstages(l)) return l;
+            s -= nstages(l);
+        }
+        return -1;
+    }
+    static constexpr int stg_index(int s) {
+        for (int l = 0; l < 4; l++) {
+            if (s < nstages(l)) return s;
+            s -= nstages(l);
+        }
+        return -1;
+    }
+    static constexpr int stg_c0(int s) { return stg_index(s) ? first(stg_layer(s)) : 0; }
+    static constexpr int stg_nc(int s) { return stg_index(s) ? CL[stg_layer(s)] - first(stg_layer(s)) : first(stg_layer(s)); }
 };
-
-__device__ __forceinline__ f32x16 zero16() {
-    f32x16 z;
-#pragma unroll
-    for (int i = 0; i < 16; i++) z[i] = 0.f;
-    return z;
-}
+static_assert(Net<4>::XR + RING <= BUFA, "input staging + weight ring fit bufA");
 
 template <int V> struct IntC {
     static constexpr int value = V;
@@ -143,13 +170,6 @@ template <int V> struct IntC {
 // accumulator.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#ifndef NN_PFC
-#define NN_PFC 1
-#endif
-constexpr int PFC = NN_PFC;            // per-column layers: chunks in flight (two blocks each)
-struct RingS {                         // two column blocks' weight parts, PFC chunks ahead
-    bf16x8 b[PFC][2][3];
-};
 struct F8 {
     float4 lo, hi;                     // 8 consecutive k of one lane's A row
 };
@@ -191,77 +211,6 @@ __device__ __forceinline__ bf16x8 i8_to_bf16x8(int v0, int v1) {
     }
     return __builtin_bit_cast(bf16x8, r);
 }
-
-// first PFC chunks of column blocks nt0, nt0 + 1 of a split layer (C chunks of 16 k) into the ring
-template <int C>
-__device__ __forceinline__ void rings_load(const float *__restrict__ ws, int nt0, RingS &r) {
-    const bf16x8 *w = reinterpret_cast<const bf16x8 *>(ws) + (size_t)nt0 * C * 3 * 64 + (threadIdx.x & 63);
-#pragma unroll
-    for (int p = 0; p < PFC; p++)
-#pragma unroll
-        for (int b = 0; b < 2; b++)
-#pragma unroll
-            for (int q = 0; q < 3; q++) r.b[p][b][q] = w[b * C * 3 * 64 + ((p < C ? p : C - 1) * 3 + q) * 64];
-}
-
-// gemm_tiles on split operands: token tiles t0 .. t0+T-1 x column blocks nt0, nt0 + 1 over C
-// chunks of 16 k (accumulator 2 t + b). INT8: afetch(t, k) -> bf16x8 (exact A, three
-// products); else afetch(t, k) -> F8, split here once for both column blocks (six products
-// each, the five smaller first, into the tile's one accumulator: 6 roundings per 16 k, still
-// fewer than the f32 MFMA's one per 2 k; the 4 tiles' second accumulators would not fit the
-// register budget next to the two blocks' weight ring). Lane l: A[row l % 32][k = 16 c + 8 (l / 32) + j].
-template <int T, int C, bool INT8, class AF, class NX>
-__device__ __forceinline__ void gemm_split(const float *__restrict__ ws, int nt0, int t0, RingS &r, AF afetch,
-                                           f32x16 *acc, NX next) {
-    const int lane = threadIdx.x & 63, h = lane >> 5;
-    const bf16x8 *w = reinterpret_cast<const bf16x8 *>(ws) + (size_t)nt0 * C * 3 * 64 + lane;
-#pragma unroll
-    for (int i = 0; i < 2 * T; i++) acc[i] = zero16();
-#pragma unroll
-    for (int c = 0; c < C; c++) {
-        bf16x8 bb[2][3];
-#pragma unroll
-        for (int b = 0; b < 2; b++)
-#pragma unroll
-            for (int q = 0; q < 3; q++) bb[b][q] = r.b[c % PFC][b][q];
-        if (c + PFC < C)
-#pragma unroll
-            for (int b = 0; b < 2; b++)
-#pragma unroll
-                for (int q = 0; q < 3; q++) r.b[c % PFC][b][q] = w[b * C * 3 * 64 + ((c + PFC) * 3 + q) * 64];
-        // (product-major order: the 2 T accumulators' chains interleave, no MFMA waits on the
-        // one just issued)
-        if constexpr (INT8) {
-            bf16x8 a[T];
-#pragma unroll
-            for (int t = 0; t < T; t++) a[t] = afetch(t0 + t, 16 * c + 8 * h);
-#pragma unroll
-            for (int p = 2; p >= 0; p--)
-#pragma unroll
-                for (int t = 0; t < T; t++)
-#pragma unroll
-                    for (int b = 0; b < 2; b++)
-                        acc[2 * t + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], bb[b][p], acc[2 * t + b], 0, 0, 0);
-        } else {
-            bf16x8 a[T][3];
-#pragma unroll
-            for (int t = 0; t < T; t++) split8(afetch(t0 + t, 16 * c + 8 * h), a[t][0], a[t][1], a[t][2]);
-            // (A part, B part) of the six products, smallest first
-            constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-            for (int p = 0; p < 6; p++)
-#pragma unroll
-                for (int t = 0; t < T; t++)
-#pragma unroll
-                    for (int b = 0; b < 2; b++)
-                        acc[2 * t + b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t][PA[p]], bb[b][PB[p]], acc[2 * t + b], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    next();
-    __builtin_amdgcn_sched_barrier(0);
-}
-
 
 // workgroup barrier for LDS traffic only: waits for this wave's LDS operations, not for its
 // global loads, so weight fragments prefetched for the next layer stay in flight across it
@@ -377,9 +326,6 @@ struct NoNext {
 __device__ __forceinline__ int acc16_row(int r) { return ((threadIdx.x & 63) >> 4) * 4 + r; }
 __device__ __forceinline__ int acc16_col() { return threadIdx.x & 15; }
 
-// accumulator element r of this lane: (row, col) of the 32x32 tile (C/D map of gfx950)
-__device__ __forceinline__ int acc_row(int r) { return (r & 3) + 8 * (r >> 2) + 4 * ((threadIdx.x & 63) >> 5); }
-__device__ __forceinline__ int acc_col() { return threadIdx.x & 31; }
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
@@ -408,6 +354,15 @@ __device__ __forceinline__ float wave_sum_f32(float v) {
     return (rows_f32(v, 0) + rows_f32(v, 1)) + (rows_f32(v, 2) + rows_f32(v, 3));
 }
 
+// LDS-DMA of one 1 KB MFMA fragment: 16 bytes per lane from src (this lane's address) to the
+// wave-uniform LDS base dst (+ 16 x lane); counted by vmcnt, no VGPR destination
+__device__ __forceinline__ void glds16(const char *src, char *dst) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
+}
+__device__ __forceinline__ f32x4 relu4(f32x4 v) {
+    return f32x4{fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
+}
+
 template <int NP>
 // one workgroup per CU (LDS) = 2 waves per SIMD: the register budget is 256, and without
 // saying so the scheduler sinks the prefetched weight loads next to their MFMAs
@@ -421,15 +376,16 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                                                     const int32_t *__restrict__ idx,
                                                     const int32_t *__restrict__ count) {
     using Nt = Net<NP>;
-    constexpr int R = Nt::R, X0S = Nt::X0S;
-    __shared__ __align__(16) float bufA[BUFA / 4];         // per-column activations, Z, SB1, SB2, logits
-    __shared__ __align__(16) SplitAct sb0;                 // per-leaf split activations
-    __shared__ uint64_t mskl[ML * 7];                      // legality masks (read at the softmax)
+    constexpr int R = Nt::R, X0S = Nt::X0S, NSTG = Nt::NSTG;
+    // all LDS in one array (a second __shared__ object beside LDS-DMA targets can make the
+    // compiler drain vmcnt before LDS reads): bufA, SB0, the legality masks
+    __shared__ __align__(16) char lds[BUFA + SAB + ML * 7 * 8];
+    float *bufA = reinterpret_cast<float *>(lds);
+    SplitAct *SB0 = reinterpret_cast<SplitAct *>(lds + BUFA);
+    uint64_t *mskl = reinterpret_cast<uint64_t *>(lds + BUFA + SAB);
     // wave index in an SGPR: every per-wave choice below is a scalar branch
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, li = lane & 31;
-    // per-column layers: wave w owns column blocks 2 cp, 2 cp + 1 of token tiles 2 q, 2 q + 1
-    // (q = 3: tile 6 alone), so each token tile's activations are split by 2 waves, not 4
-    const int cp = w & 1, q = w >> 1;
+    const int h = lane >> 5;
     const int b0 = blockIdx.x * ML;
     const int cnt = count ? __builtin_amdgcn_readfirstlane(*count) : B;
     if (b0 >= cnt) return;
@@ -437,10 +393,29 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // row of leaf i of this tile (its board, mask and outputs)
     const auto rowof = [&](int i) -> size_t { return idx ? (size_t)idx[b0 + i] : (size_t)(b0 + i); };
     const float *aff = W + Nt::AFF;                        // s1, t1, sp1, tp1
-    const int t0 = 2 * q, ntok = q == 3 ? 1 : 2;           // this wave's token tiles (per-column layers)
-    constexpr int C1 = kp16(R) / 16;
-    RingS rings;                                           // per-column weight parts, one layer ahead
-    rings_load<C1>(W + Nt::soff(0), 2 * cp, rings);
+    char *ring = lds + Nt::XR;                             // per-column weight stages (2 buffers)
+    float *biasL = reinterpret_cast<float *>(SB0);         // [4][128] per-column biases (until dense1d_4)
+    // wave 7 (it owns no board column) fills the weight stages: stage S's split weight chunks
+    // into buffer S & 1, one 1 KB fragment (column block b, part p, chunk c) per instruction
+    auto load_stage = [&](auto s_const) {
+        constexpr int S = decltype(s_const)::value;
+        if constexpr (S < NSTG) {
+            constexpr int L = Nt::stg_layer(S), C0 = Nt::stg_c0(S), NC = Nt::stg_nc(S), C = Nt::CL[L];
+            const char *src = reinterpret_cast<const char *>(W + Nt::soff(L)) + lane * 16;
+            char *dst = ring + (S & 1) * RSTAGE * RSLOT;
+#pragma unroll
+            for (int j = 0; j < NC; j++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+#pragma unroll
+                    for (int p = 0; p < 3; p++)
+                        glds16(src + ((b * C + C0 + j) * 3 + p) * 1024, dst + ((j * 4 + b) * 3 + p) * 1024);
+        }
+    };
+    if (w == 7) {
+        load_stage(IntC<0>());
+        load_stage(IntC<1>());
+    }
 
 #if NN_PROBE
     uint64_t nlast = __builtin_readcyclecounter();
@@ -448,10 +423,16 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #endif
     // ---- input: x[column c][leaf i][row r] = state[leaf][r][c] as int8 (token c*32+i)
     // (no zero fill: the k past R of a row read the row's padding, the next row or, after the
-    // last one, stale LDS bytes — any int8 is finite and those k have zero weights; rows of
-    // missing leaves are never stored)
-    int8_t *x0 = reinterpret_cast<int8_t *>(bufA);
+    // last one, the bytes behind it — any int8 is finite and those k have zero weights; rows
+    // of missing leaves are never stored)
+    int8_t *x0 = reinterpret_cast<int8_t *>(lds);
     if (tid < nb * 7) mskl[tid] = mask[rowof(tid / 7) * 7 + tid % 7];
+    {
+        // per-column biases; partialgpool_1's outputs land on channels 8..127 (its 8 pooled
+        // channels come first), so its bias is shifted by 8
+        const int l = tid >> 7, c = tid & 127;
+        biasL[tid] = l == 2 ? (c >= 8 ? W[Nt::boff(2) + c - 8] : 0.f) : W[Nt::boff(l) + c];
+    }
     if constexpr ((7 * R) % 4 == 0) {
         // the workgroup's boards: dword loads (a board is a whole number of dwords), all in
         // flight at once, then each byte scattered to its (column, leaf, row) slot
@@ -482,166 +463,174 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             for (int c = 0; c < 7; c++) x0[(c * ML + i) * X0S + r] = src[c];
         }
     }
+    if (w == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stages 0 and 1 landed
     lds_barrier();
-
-    f32x16 acc[4];                                         // token tile t, column block b: acc[2 t + b]
-    auto colb = [&](int b) { return 32 * (2 * cp + b) + acc_col(); };
-    // (c_const: chunks of 16 k; i8_const: A is the int8 input)
-    auto gemm_cols = [&](auto c_const, auto i8_const, const float *ws, auto afetch, auto next) {
-        constexpr int C = decltype(c_const)::value;
-        constexpr bool I8 = decltype(i8_const)::value != 0;
-        if (ntok == 2)
-            gemm_split<2, C, I8>(ws, 2 * cp, t0, rings, afetch, acc, next);
-        else
-            gemm_split<1, C, I8>(ws, 2 * cp, t0, rings, afetch, acc, next);
-    };
-    auto fetchA8 = [&](int col0) {
-        return [&, col0](int t, int c) {
-            const float *p = bufA + (t * ML + li) * XS + col0 + c;
-            return F8{ld4(p), ld4(p + 4)};
-        };
-    };
-    // per-column epilogue over this wave's tiles, output columns < nmax: dst = f(acc, t, b)
-    auto store_tiles = [&](int coloff, int nmax, auto f) {
-#pragma unroll
-        for (int t = 0; t < 2; t++)
-            if (t < ntok)
-#pragma unroll
-                for (int b = 0; b < 2; b++)
-                    if (colb(b) < nmax)
-#pragma unroll
-                        for (int r = 0; r < 16; r++)
-                            bufA[((t0 + t) * ML + acc_row(r)) * XS + coloff + colb(b)] = f(acc[2 * t + b][r], t0 + t, b);
-    };
-    auto biases = [&](int layer, float *bb) { bb[0] = W[Nt::boff(layer) + colb(0)]; bb[1] = W[Nt::boff(layer) + colb(1)]; };
     NPROBE(0)
+
+    // ---- per-column layers (round 6), wave w < 7 = board column w of the ML leaves, in
+    // registers: out^T[channel][leaf] = W[channel][k] x^T[k][leaf] on v_mfma_f32_32x32x16_bf16
+    // with the weights as the A operand (rows = output channels, 4 blocks of 32) and the
+    // activations as B (columns = this tile's 32 leaves). An accumulator's lane l holds leaf
+    // l % 32 at channels (r & 3) + 8 (r >> 2) + 4 (l >> 5) of its block, so the next layer's
+    // B fragment of a 16-channel chunk (lane l: channels 8 (l >> 5) .. + 7) is two 4-register
+    // groups of one block with their 32-lane halves exchanged (4 v_permlane32_swap), then split
+    // into three bf16 parts once for all 4 output blocks. Six part products per chunk, hi x hi
+    // into the block's accumulator X (started at the bias), the five smaller ones into a second
+    // accumulator Xs (round 4's two-accumulator precision, now for every per-column layer).
+    f32x16 X[4], Y[4], Ys[4];
+    RingL<2, 2> ring2;                                     // dense1d_4's first weight chunks
+    const int rt4 = w & 1, ct4 = 2 * (w >> 1);             // dense1d_4: row tile, first column tile
+    auto stage = [&](auto s_const) {
+        constexpr int S = decltype(s_const)::value;
+        constexpr int L = Nt::stg_layer(S), C0 = Nt::stg_c0(S), NC = Nt::stg_nc(S);
+        if (w < 7) {
+            if constexpr (C0 == 0) {                       // a layer's first stage: bias, zero
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        const f32x4 bb = *reinterpret_cast<const f32x4 *>(biasL + 128 * L + 32 * b + 8 * g + 4 * h);
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            Y[b][4 * g + i] = bb[i];
+                            Ys[b][4 * g + i] = 0.f;
+                        }
+                    }
+            }
+            const char *buf = ring + (S & 1) * RSTAGE * RSLOT + lane * 16;
+#pragma unroll
+            for (int j = 0; j < NC; j++) {
+                bf16x8 bh, bm, bl;
+                if constexpr (L == 0) {                    // int8 boards: exact in one bf16 part
+                    const int32_t *px = reinterpret_cast<const int32_t *>(x0 + (w * ML + li) * X0S + 16 * (C0 + j) + 8 * h);
+                    bh = i8_to_bf16x8(px[0], px[1]);
+                } else {                                   // (partialgpool_1 reads channels 32..127)
+                    const int kk = C0 + j + (L == 2 ? 2 : 0), blk = kk >> 1, sh = kk & 1;
+                    float v[8];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(X[blk][8 * sh + i]),
+                                                                         __float_as_uint(X[blk][8 * sh + 4 + i]), false, false);
+                        v[i] = __uint_as_float(r2[0]);
+                        v[4 + i] = __uint_as_float(r2[1]);
+                    }
+                    split8(F8{float4{v[0], v[1], v[2], v[3]}, float4{v[4], v[5], v[6], v[7]}}, bh, bm, bl);
+                }
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const char *f = buf + (j * 4 + b) * 3 * 1024;
+                    const bf16x8 wh = *reinterpret_cast<const bf16x8 *>(f);
+                    const bf16x8 wm = *reinterpret_cast<const bf16x8 *>(f + 1024);
+                    const bf16x8 wl = *reinterpret_cast<const bf16x8 *>(f + 2048);
+                    if constexpr (L == 0) {
+                        Ys[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, bh, Ys[b], 0, 0, 0);
+                        Ys[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, bh, Ys[b], 0, 0, 0);
+                    } else {
+                        Ys[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, bh, Ys[b], 0, 0, 0);
+                        Ys[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, bm, Ys[b], 0, 0, 0);
+                        Ys[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, bl, Ys[b], 0, 0, 0);
+                        Ys[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, bh, Ys[b], 0, 0, 0);
+                        Ys[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, bm, Ys[b], 0, 0, 0);
+                    }
+                    Y[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, bh, Y[b], 0, 0, 0);
+                }
+            }
+        }
+        if constexpr (S == NSTG - 1) {
+            // dense1d_4's first weight chunks into registers behind the last MFMA (wave 7 has no
+            // LDS-DMA in flight any more)
+            ringl_load<22>(W + Nt::soff(4), ct4, 1, 8, ring2);
+        } else if (w == 7) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stage S + 1 landed
+        }
+        lds_barrier();                                     // buffer S & 1 read by every wave
+        if (w == 7) load_stage(IntC<S + 2>());
+    };
+    auto layer = [&](auto l_const) {
+        constexpr int L = decltype(l_const)::value;
+        constexpr int S0 = L == 0 ? 0 : (L == 1 ? Nt::nstages(0) : (L == 2 ? Nt::nstages(0) + Nt::nstages(1)
+                                                                         : Nt::NSTG - Nt::nstages(3)));
+        stage(IntC<S0>());
+        if constexpr (Nt::nstages(L) == 2) stage(IntC<S0 + 1>());
+    };
     // ---- dense2d_1: relu(s1[c] * (W1 x + b1) + t1[c])
-    // (each layer's bias is read before its GEMM, ahead of the next layer's ring: vmcnt
-    // retires loads in order)
-    {
-        float bias[2];
-        biases(0, bias);
-        // (k past R reads zero padding or the next row's bytes: their weights are 0)
-        gemm_cols(IntC<C1>(), IntC<1>(), W + Nt::soff(0), [&](int t, int c) {
-            const int32_t *p = reinterpret_cast<const int32_t *>(x0 + (t * ML + li) * X0S + c);
-            return i8_to_bf16x8(p[0], p[1]);
-        }, [&] { rings_load<8>(W + Nt::soff(1), 2 * cp, rings); });
-        lds_barrier();
-        store_tiles(0, 128, [&](float x, int t, int b) { return fmaxf((x + bias[b]) * aff[t] + aff[7 + t], 0.f); });
-        lds_barrier();
+    layer(IntC<0>());
+    if (w < 7) {
+        const float sc = aff[w], tc = aff[7 + w];
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) X[b][r] = fmaxf((Y[b][r] + Ys[b][r]) * sc + tc, 0.f);
     }
     NPROBE(1)
     // ---- dense2d_1[3]: relu(W2 x + b2)
-    {
-        float bias[2];
-        biases(1, bias);
-        gemm_cols(IntC<8>(), IntC<0>(), W + Nt::soff(1), fetchA8(0), [&] { rings_load<6>(W + Nt::soff(2), 2 * cp, rings); });
-        lds_barrier();
-        store_tiles(0, 128, [&](float x, int, int b) { return fmaxf(x + bias[b], 0.f); });
-        lds_barrier();
+    layer(IntC<1>());
+    if (w < 7) {
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) X[b][r] = fmaxf(Y[b][r] + Ys[b][r], 0.f);
     }
     NPROBE(2)
     // ---- partialgpool_1: [max, mean over 4 groups of 8 of x[0:32]] ++ relu(BN(Wp1 x[32:] + bp1))
-    {
-        float bias[2];                     // (0-padded to 128 columns)
-        biases(2, bias);
-        gemm_cols(IntC<6>(), IntC<0>(), W + Nt::soff(2), fetchA8(32), [&] { rings_load<8>(W + Nt::soff(3), 2 * cp, rings); });
-        constexpr int NQ = (7 * ML * 8 + NNT - 1) / NNT;
-        float pv[NQ];
+    // (the GEMM's outputs on channels 8..127: its weight rows are shifted by 8 on the host)
+    layer(IntC<2>());
+    if (w < 7) {
+        // group g = channels 8g .. 8g+7 of block 0 = registers 4g .. 4g+3 of both lane halves
+        float pm[4], ps[4];
 #pragma unroll
-        for (int u = 0; u < NQ; u++) {
-            const int item = tid + NNT * u, tok = item >> 3, j = item & 7, g = j & 3;
-            pv[u] = 0.f;
-            if (item < 7 * ML * 8) {
-                const float *p = bufA + tok * XS + 8 * g;
-                float m = p[0], s = p[0];
-#pragma unroll
-                for (int k = 1; k < 8; k++) { m = fmaxf(m, p[k]); s += p[k]; }
-                pv[u] = j < 4 ? m : s / 8.f;
-            }
+        for (int g = 0; g < 4; g++) {
+            const float a0 = X[0][4 * g], a1 = X[0][4 * g + 1], a2 = X[0][4 * g + 2], a3 = X[0][4 * g + 3];
+            const float m = fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)), sm = ((a0 + a1) + a2) + a3;
+            const auto rm = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+            const auto rs = __builtin_amdgcn_permlane32_swap(__float_as_uint(sm), __float_as_uint(sm), false, false);
+            const float om = __uint_as_float(h ? rm[0] : rm[1]), os = __uint_as_float(h ? rs[0] : rs[1]);
+            pm[g] = fmaxf(m, om);
+            ps[g] = h ? os + sm : sm + os;                 // (lower half first in both halves)
         }
-        lds_barrier();
+        const float sc = aff[14 + w], tc = aff[21 + w];
 #pragma unroll
-        for (int u = 0; u < NQ; u++) {
-            const int item = tid + NNT * u;
-            if (item < 7 * ML * 8) bufA[(item >> 3) * XS + (item & 7)] = pv[u];
-        }
-        store_tiles(8, 120, [&](float x, int t, int b) { return fmaxf((x + bias[b]) * aff[14 + t] + aff[21 + t], 0.f); });
-        lds_barrier();
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) X[b][r] = fmaxf((Y[b][r] + Ys[b][r]) * sc + tc, 0.f);
+#pragma unroll
+        for (int g = 0; g < 4; g++) X[0][g] = h ? ps[g] / 8.f : pm[g];   // channels 0-3 max, 4-7 mean
     }
     NPROBE(3)
-    // ---- dense2d_3: relu(W3 x + b3), written straight into the flattened per-leaf image
+    // ---- dense2d_3: relu(W3 x + b3), then the flattened per-leaf image
     // Z[leaf][704] = [max_c<5 x[c][:64]][mean_c<5 x[c][:64]][x[5][:64]][x[6][:64]][x[c][64:], c<7]
     // (FlattenAndPartialGPool(64, 5)), so dense1d_4 reads plain rows
+    layer(IntC<3>());
     float *Z = bufA;
-    SplitAct *SB0 = &sb0;
+    float *P = bufA + ML * ZS;                             // [5][ML][PS]: columns 0-4, channels 0-63
     SplitAct *SB1 = reinterpret_cast<SplitAct *>(bufA);
     SplitAct *SB2 = reinterpret_cast<SplitAct *>(reinterpret_cast<char *>(bufA) + SAB);
     float *logits = reinterpret_cast<float *>(reinterpret_cast<char *>(bufA) + 2 * SAB);
-    float *part = reinterpret_cast<float *>(&sb0);         // (channels 0-3: pool partials)
-    // dense1d_4: wave w takes row tile w & 1 and column tiles 2 (w >> 1), 2 (w >> 1) + 1
-    const int rt4 = w & 1, ct4 = 2 * (w >> 1);
-    RingL<2, 2> ring2;
-    {
-        float bias[2];
-        biases(3, bias);
-        gemm_cols(IntC<8>(), IntC<0>(), W + Nt::soff(3), fetchA8(0),
-                  [&] { ringl_load<22>(W + Nt::soff(4), ct4, 1, 8, ring2); });
-        lds_barrier();
+    if (w < 7) {                                           // (the ring is dead: every wave passed
+#pragma unroll                                             //  the last stage's barrier)
+        for (int b = 0; b < 4; b++)
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[i][r] = fmaxf(acc[i][r] + bias[i & 1], 0.f);
-        // channels 0-63 of board columns 0-4: max and mean in column order (((c0 + c1) + c2) + c3)
-        // + c4 over three steps (q = 0, 1, 2), partials in `part`; columns 5, 6 pass through
-        if (cp == 1) {                     // channels 64-127
-#pragma unroll
-            for (int t = 0; t < 2; t++)
-                if (t < ntok)
-#pragma unroll
-                    for (int b = 0; b < 2; b++)
-#pragma unroll
-                        for (int r = 0; r < 16; r++)
-                            Z[acc_row(r) * ZS + 256 + 64 * (t0 + t) + colb(b) - 64] = acc[2 * t + b][r];
-        } else if (q == 0) {
-#pragma unroll
-            for (int b = 0; b < 2; b++)
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    part[acc_row(r) * 128 + colb(b)] = fmaxf(acc[b][r], acc[2 + b][r]);
-                    part[acc_row(r) * 128 + 64 + colb(b)] = acc[b][r] + acc[2 + b][r];
-                }
-        }
-        lds_barrier();
-        if (cp == 0 && q == 1) {
-#pragma unroll
-            for (int b = 0; b < 2; b++)
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    float *pm = part + acc_row(r) * 128 + colb(b);
-                    pm[0] = fmaxf(pm[0], fmaxf(acc[b][r], acc[2 + b][r]));
-                    pm[64] = (pm[64] + acc[b][r]) + acc[2 + b][r];
-                }
-        }
-        lds_barrier();
-        if (cp == 0 && q == 2) {           // column 4 closes the pool, column 5 passes through
-#pragma unroll
-            for (int b = 0; b < 2; b++)
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int i = acc_row(r), c = colb(b);
-                    Z[i * ZS + c] = fmaxf(part[i * 128 + c], acc[b][r]);
-                    Z[i * ZS + 64 + c] = (part[i * 128 + 64 + c] + acc[b][r]) / 5.f;
-                    Z[i * ZS + 128 + c] = acc[2 + b][r];
-                }
-        } else if (cp == 0 && q == 3) {    // column 6 passes through
-#pragma unroll
-            for (int b = 0; b < 2; b++)
-#pragma unroll
-                for (int r = 0; r < 16; r++) Z[acc_row(r) * ZS + 192 + colb(b)] = acc[b][r];
-        }
-        lds_barrier();
+            for (int g = 0; g < 4; g++) {
+                const f32x4 v = relu4(f32x4{Y[b][4 * g], Y[b][4 * g + 1], Y[b][4 * g + 2], Y[b][4 * g + 3]} +
+                                      f32x4{Ys[b][4 * g], Ys[b][4 * g + 1], Ys[b][4 * g + 2], Ys[b][4 * g + 3]});
+                const int ch = 32 * b + 8 * g + 4 * h;     // 4 consecutive channels of leaf li
+                if (b >= 2)
+                    *reinterpret_cast<f32x4 *>(Z + li * ZS + 256 + 64 * w + ch - 64) = v;
+                else if (w < 5)                            // 16-B units swizzled by leaf (banks)
+                    *reinterpret_cast<f32x4 *>(P + (w * ML + li) * PS + 4 * ((ch >> 2) ^ (li & 15))) = v;
+                else
+                    *reinterpret_cast<f32x4 *>(Z + li * ZS + (w == 5 ? 128 : 192) + ch) = v;
+            }
     }
+    lds_barrier();
+    for (int t = tid; t < ML * 64; t += NNT) {             // channels 0-63 of columns 0-4: max, mean
+        const int i = t >> 6, c = t & 63, o = i * PS + 4 * ((c >> 2) ^ (i & 15)) + (c & 3);
+        const float p0 = P[o], p1 = P[ML * PS + o], p2 = P[2 * ML * PS + o], p3 = P[3 * ML * PS + o],
+                    p4 = P[4 * ML * PS + o];
+        Z[i * ZS + c] = fmaxf(fmaxf(fmaxf(p0, p1), fmaxf(p2, p3)), p4);
+        Z[i * ZS + 64 + c] = ((((p0 + p1) + p2) + p3) + p4) / 5.f;
+    }
+    lds_barrier();
     NPROBE(4)
     // ---- per-leaf layers: split activations in SB0 / SB1 / SB2 (SplitAct), 16x16x32 tiles
     f32x4 a16[4][2];

@@ -200,14 +200,16 @@ def _bf16_parts(w):
     return [(x >> 16) & 0xFFFF for x in (hi, mid, r2)]
 
 
-def _split_layer(w):
-    """The bf16 x 3 copy of a per-column layer (NN_SPLIT kernels): [4][Kp16/16][3][64][8]
-    bf16, element (nt, c, p, l, j) = part p of W[32 nt + l % 32][16 c + 8 (l / 32) + j], as
-    float32 storage (two bf16 per float, little-endian)."""
+def _split_layer(w, row0=0):
+    """The bf16 x 3 copy of a per-column layer: [4][Kp16/16][3][64][8] bf16, element
+    (nt, c, p, l, j) = part p of W[32 nt + l % 32 - row0][16 c + 8 (l / 32) + j] (0 outside), as
+    float32 storage (two bf16 per float, little-endian). The kernel multiplies these fragments as
+    the A operand of v_mfma_f32_32x32x16_bf16 (rows = output channels); row0 = 8 puts
+    partialgpool_1's outputs on channels 8..127, behind its 8 pooled channels."""
     N, K = w.shape
     k16 = (K + 15) // 16 * 16
     wp = torch.zeros((128, k16), dtype=torch.float32, device=w.device)
-    wp[:N, :K] = w
+    wp[row0:row0 + N, :K] = w
     parts = torch.stack(_bf16_parts(wp))                           # [3][128][k16]
     # [p][nt][col][c][g][j] -> [nt][c][p][g][col][j]; lane = 32 g + col
     t = parts.view(3, 4, 32, k16 // 16, 2, 8).permute(1, 3, 0, 4, 2, 5).reshape(-1, 2)
@@ -238,8 +240,8 @@ def pack_weights(folded, n_players):
     S = Kp/2; layers 4-12 (16x16x4, Kp % 16 == 0): [NT][Kp/16][64][4], element (nt, q, l, j)
     = W[16 nt + (l & 15)][16 q + 4 (l >> 4) + j] — then the 0-padded bias; then the
     per-column BN affines; then (16-byte aligned) the bf16 x 3 copies the kernel multiplies:
-    layers 0-3 in 32x32x16 fragments (_split_layer), layers 4-12 in 16x16x32 fragments
-    (_split_leaf_layer)."""
+    layers 0-3 in 32x32x16 fragments (_split_layer; partialgpool_1's rows shifted by 8), layers
+    4-12 in 16x16x32 fragments (_split_leaf_layer)."""
     f = folded
     layers = [(f.w1, f.b1), (f.w2, f.b2), (f.wp1, f.bp1), (f.w3, f.b3), (f.w4, f.b4), (f.wp4, f.bp4),
               (f.w5a, f.b5a), (f.w5b, f.b5b), (f.wp5, f.bp5), (f.wpi1, f.bpi1), (f.wpi2, f.bpi2),
@@ -268,7 +270,7 @@ def pack_weights(folded, n_players):
         parts += [f.s1.reshape(7), f.t1.reshape(7), f.sp1.reshape(7), f.tp1.reshape(7)]
         pad = -sum(p.numel() for p in parts) % 4                    # 16-byte aligned split copies
         parts.append(torch.zeros(pad, dtype=torch.float32, device=f.w1.device))
-        parts += [_split_layer(w) for w, _ in layers[:4]]
+        parts += [_split_layer(w, row0=8 if li == 2 else 0) for li, (w, _) in enumerate(layers[:4])]
         parts += [_split_leaf_layer(w) for w, _ in layers[4:]]
         out = torch.cat([p.float() for p in parts]).contiguous()
     want = _lib.lib().spl_nn_packed_floats(n_players)
