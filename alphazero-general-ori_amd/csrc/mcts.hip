@@ -795,7 +795,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                 } else {
                     const int rr = rel - ec;
                     src[r] = S.ovb[j[r]] + rr;
-                    link[r] = rr % REC_UNITS == 1;       // {n, child}: the link remapped
+                    link[r] = rr % REC_UNITS == REC_LINK_UNIT;   // {child, rank | action}: the link remapped
                 }
             }
         }
@@ -805,7 +805,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
 #pragma unroll
         for (int r = 0; r < SR; r++) {
             if (!link[r]) continue;
-            const int ch = (int)(v[r] >> 32);
+            const int ch = (int)(uint32_t)v[r];
             int nch = -1;
             if (ch >= 0) {
                 BCHK(IN_TREE(P, t, ch, nc), 57, ((long long)j[r] << 32) | (uint32_t)ch, t, (void)0);
@@ -814,7 +814,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
                 BCHK(nl < 0 || P.nd[nch].h.round == P.nd[node_g(P, t, j[r])].h.round + 1, 41,
                      ((long long)j[r] << 32) | (uint32_t)nl, t, (void)0);
             }
-            v[r] = (v[r] & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)nch << 32);
+            v[r] = (v[r] & 0xFFFFFFFF00000000ull) | (uint64_t)(uint32_t)nch;
         }
 #pragma unroll
         for (int r = 0; r < SR; r++)
@@ -2075,8 +2075,8 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
 // of every other item; that is below L exactly when one edge can hold the maximum, which is
 // then the strict-'>' arg-max. Otherwise (ties, near ties) and for levels with more than
 // BK_WIDE records (roots) the wave evaluates the level exactly in float64.
-#ifndef BK_BATCH
-#define BK_BATCH 1
+#ifndef BK_PF
+#define BK_PF 4            // visit-record heads requested together by the screen
 #endif
 #ifndef BK_WIDE
 #define BK_WIDE 12
@@ -2115,6 +2115,22 @@ __device__ __forceinline__ void screen_item(Screen &S, bool vis, float p, int n,
     } else {
         S.H2 = fmaxf(S.H2, hi);
     }
+}
+
+// screen_item for a visited edge in branch-free form (the backup's record loop: no branch may
+// separate a record's load from its use, or the compiler waits vmcnt(0) at every use and the
+// prefetch is lost); a visited leader is kept by its record index only
+__device__ __forceinline__ void screen_visited(Screen &S, bool valid, float p, int n, double q, int vi) {
+    const float rc = __builtin_amdgcn_rcpf(1.f + (float)n);
+    const float qf = (float)q;
+    const float uf = qf + S.cf * p * S.sqv * rc;
+    const float er = 2.1e-6f * (fabsf(uf) + fabsf(qf)) + 1e-30f;
+    const float lo = uf - er, hi = uf + er;
+    const bool lead = valid && lo > S.L1;
+    S.H2 = valid ? fmaxf(S.H2, lead ? S.H1 : hi) : S.H2;
+    S.L1 = lead ? lo : S.L1;
+    S.H1 = lead ? hi : S.H1;
+    S.vi = lead ? vi : S.vi;
 }
 
 // exact arg-max of one level (wave-uniform arguments): its visit records lane-parallel, the
@@ -2606,7 +2622,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                     V.r.vcap = (int16_t)V.grow;
                 }
                 vidx = V.r.vcnt;
-                *P.vr(V.r.vb + REC_UNITS * vidx) = VisitRec{q1, n1, V.child, V.e.p, (int16_t)V.off, (int16_t)V.act};
+                *P.vr(V.r.vb + REC_UNITS * vidx) = VisitRec{q1, n1, V.e.p, V.child, (int16_t)V.off, (int16_t)V.act};
                 P.ep(V.r.eb + V.off)->vi = (int16_t)vidx;
                 V.r.vcnt = (int16_t)(vidx + 1);
                 // (a record elsewhere leaves np an upper bound: the screen stays exact)
@@ -2642,21 +2658,34 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             screen_item(Sc, false, V.cp, 0, 0.0, rc, V.ca, -1);
             if (V.np >= 0.f) screen_item(Sc, false, V.np, 0, 0.0, 0, 0, -1);   // (never leads: np < cp)
         }
+        // the level's visit records (round 6): only their 16-byte heads {Qsa, Nsa, P}, BK_PF
+        // requested ahead (round 5 waited one round trip per record); a visited leader is kept
+        // by index, its link / rank / action read afterwards (only when it is not the path edge,
+        // whose values the lane holds)
         const int myv = in && !wide ? V.r.vcnt : 0;
         const int maxv = wave_max_i32(myv);
-        for (int base = 0; base < maxv; base += BK_BATCH) {
-            VisitRec rb[BK_BATCH];
+        {
+            const int64_t vb0 = myv ? V.r.vb : 0;
+            const auto head = [&](int i) { return *P.vh(vb0 + REC_UNITS * (i < myv ? i : 0)); };
+            VisitHead hd[BK_PF];
 #pragma unroll
-            for (int k = 0; k < BK_BATCH; k++)
-                if (base + k < myv) rb[k] = *P.vr(V.r.vb + REC_UNITS * (base + k));
+            for (int k = 0; k < BK_PF; k++) hd[k] = head(k);
+            for (int base = 0; base < maxv; base += BK_PF) {
 #pragma unroll
-            for (int k = 0; k < BK_BATCH; k++) {
-                const int i = base + k;
-                if (i < myv) {
-                    const VisitRec &R = rb[k];
+                for (int k = 0; k < BK_PF; k++) {
+                    const int i = base + k;
                     const bool mine = i == vidx;
-                    screen_item(Sc, true, R.p, mine ? n1 : R.n, mine ? q1 : R.q, R.off, R.a, mine ? V.rchild : R.child, i);
+                    screen_visited(Sc, i < myv, hd[k].p, mine ? n1 : hd[k].n, mine ? q1 : hd[k].q, i);
+                    hd[k] = head(base + BK_PF + k);       // (unconditional: see screen_visited)
                 }
+            }
+        }
+        if (Sc.vi >= 0) {                                // a visited leader: its link, rank, action
+            if (Sc.vi == vidx) {
+                Sc.off = V.off; Sc.a = V.act; Sc.child = V.rchild;
+            } else {
+                const VisitTail tl = *P.vt(V.r.vb + REC_UNITS * Sc.vi);
+                Sc.off = tl.off; Sc.a = tl.a; Sc.child = tl.child;
             }
         }
         bool open = in && (wide || !(Sc.H2 < Sc.L1));

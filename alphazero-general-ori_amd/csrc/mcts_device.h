@@ -71,16 +71,30 @@ struct EdgeP {
     int16_t vi;    // its VisitRec in the node's block, -1: none (Nsa = 0, Qsa = -42)
 };
 static_assert(sizeof(EdgeP) == 8, "EdgeP layout");
+// (round 6: the fields the backup's float32 screen reads — Qsa, Nsa, the prior — are the first
+// 16 bytes, one dwordx4 per record; the link, rank and action, which only the level's new pick
+// needs, are the third unit)
 struct VisitRec {
     double q;      // Qsa
     int32_t n;     // Nsa
-    int32_t child; // link: child node (global id), -1: not linked
     float p;       // the edge's prior (copy of its EdgeP)
+    int32_t child; // link: child node (global id), -1: not linked
     int16_t off;   // its rank in the run
     int16_t a;     // its action
 };
 static_assert(sizeof(VisitRec) == 24, "VisitRec layout");
 constexpr int REC_UNITS = 3;
+constexpr int REC_LINK_UNIT = 2;   // the unit holding the link (low 32 bits), rank and action
+struct VisitHead {                 // the first 16 bytes of a VisitRec
+    double q;
+    int32_t n;
+    float p;
+};
+struct VisitTail {                 // its third unit
+    int32_t child;
+    int16_t off;
+    int16_t a;
+};
 
 // A node is one 64-byte record (round 5; round 4 kept a 32-byte NodeStat, a 24-byte NodeRun, a
 // round and a terminal flag in four arrays: three to four lines per path level for k_backup).
@@ -229,6 +243,10 @@ struct Pools {
 
     __device__ __forceinline__ EdgeP *ep(int64_t u) const { return reinterpret_cast<EdgeP *>(eu + u); }
     __device__ __forceinline__ VisitRec *vr(int64_t u) const { return reinterpret_cast<VisitRec *>(eu + u); }
+    __device__ __forceinline__ const VisitHead *vh(int64_t u) const { return reinterpret_cast<const VisitHead *>(eu + u); }
+    __device__ __forceinline__ const VisitTail *vt(int64_t u) const {
+        return reinterpret_cast<const VisitTail *>(eu + u + REC_LINK_UNIT);
+    }
 };
 
 // tree t's local node slot i / local (virtual) unit position v -> global

@@ -121,7 +121,7 @@ struct Net {
     static constexpr int SBASE = (AFF + 28 + 3) / 4 * 4;
     static constexpr int soff(int l) {
         int o = SBASE;
-        for (int j = 0; j < l; j++) o += j < 4 ? sfloats(Ks[j]) : lfloats(Ns[j], Ks[j]);
+        for (int j = 0; j < l; j++) o += j < 5 ? sfloats(Ks[j]) : lfloats(Ns[j], Ks[j]);
         return o;
     }
     static constexpr int TOTAL = soff(NL);
@@ -426,44 +426,53 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // last one, the bytes behind it — any int8 is finite and those k have zero weights; rows
     // of missing leaves are never stored)
     int8_t *x0 = reinterpret_cast<int8_t *>(lds);
-    if (tid < nb * 7) mskl[tid] = mask[rowof(tid / 7) * 7 + tid % 7];
-    {
+    // (waves 0-6 stage the input, so wave 7's vmcnt counts its LDS-DMA only)
+    constexpr int NS7 = NNT - 64;
+    if (w < 7) {
+        if (tid < nb * 7) mskl[tid] = mask[rowof(tid / 7) * 7 + tid % 7];
         // per-column biases; partialgpool_1's outputs land on channels 8..127 (its 8 pooled
         // channels come first), so its bias is shifted by 8
-        const int l = tid >> 7, c = tid & 127;
-        biasL[tid] = l == 2 ? (c >= 8 ? W[Nt::boff(2) + c - 8] : 0.f) : W[Nt::boff(l) + c];
-    }
-    if constexpr ((7 * R) % 4 == 0) {
-        // the workgroup's boards: dword loads (a board is a whole number of dwords), all in
-        // flight at once, then each byte scattered to its (column, leaf, row) slot
-        constexpr int BW = R * 7 / 4;                      // dwords per board
-        constexpr int PER = (ML * BW + NNT - 1) / NNT;
-        int32_t d[PER];
-#pragma unroll
-        for (int k = 0; k < PER; k++) {
-            const int j = tid + k * NNT, i = j / BW;
-            d[k] = j < nb * BW ? reinterpret_cast<const int32_t *>(state + rowof(i) * R * 7)[j - i * BW] : 0;
+        for (int t = tid; t < 4 * 128; t += NS7) {
+            const int l = t >> 7, c = t & 127;
+            biasL[t] = l == 2 ? (c >= 8 ? W[Nt::boff(2) + c - 8] : 0.f) : W[Nt::boff(l) + c];
         }
+        if constexpr ((7 * R) % 4 == 0) {
+            // the workgroup's boards: dword loads (a board is a whole number of dwords), all in
+            // flight at once, then each byte scattered to its (column, leaf, row) slot
+            constexpr int BW = R * 7 / 4;                  // dwords per board
+            constexpr int PER = (ML * BW + NS7 - 1) / NS7;
+            int32_t d[PER];
 #pragma unroll
-        for (int k = 0; k < PER; k++) {
-            const int j = tid + k * NNT;
-            if (j < nb * R * 7 / 4) {
+            for (int k = 0; k < PER; k++) {
+                const int j = tid + k * NS7, i = j / BW;
+                d[k] = j < nb * BW ? reinterpret_cast<const int32_t *>(state + rowof(i) * R * 7)[j - i * BW] : 0;
+            }
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int o = 4 * j + q, i = o / (R * 7), rem = o - i * (R * 7), r = rem / 7, c = rem - 7 * r;
-                    x0[(c * ML + i) * X0S + r] = (int8_t)(d[k] >> (8 * q));
+            for (int k = 0; k < PER; k++) {
+                const int j = tid + k * NS7;
+                if (j < nb * R * 7 / 4) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int o = 4 * j + q, i = o / (R * 7), rem = o - i * (R * 7), r = rem / 7, c = rem - 7 * r;
+                        x0[(c * ML + i) * X0S + r] = (int8_t)(d[k] >> (8 * q));
+                    }
                 }
+            }
+        } else {
+            for (int j = tid; j < nb * R; j += NS7) {      // one board row (7 bytes) per thread
+                const int i = j / R, r = j - i * R;
+                const int8_t *src = state + (rowof(i) * R + r) * 7;
+#pragma unroll
+                for (int c = 0; c < 7; c++) x0[(c * ML + i) * X0S + r] = src[c];
             }
         }
     } else {
-        for (int j = tid; j < nb * R; j += NNT) {          // one board row (7 bytes) per thread
-            const int i = j / R, r = j - i * R;
-            const int8_t *src = state + (rowof(i) * R + r) * 7;
-#pragma unroll
-            for (int c = 0; c < 7; c++) x0[(c * ML + i) * X0S + r] = src[c];
-        }
+        // stage 0 landed (stage 1's 12 x nc fragments may stay in flight): vmcnt(N) encoded as
+        // vmcnt[3:0] | vmcnt[5:4] << 14, expcnt and lgkmcnt at their maxima (no wait)
+        constexpr int N1 = 12 * Nt::stg_nc(1);
+        static_assert(N1 < 64, "vmcnt range");
+        __builtin_amdgcn_s_waitcnt((N1 & 15) | ((N1 >> 4) << 14) | (7 << 4) | (15 << 8));
     }
-    if (w == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stages 0 and 1 landed
     lds_barrier();
     NPROBE(0)
 
@@ -478,8 +487,14 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // into the block's accumulator X (started at the bias), the five smaller ones into a second
     // accumulator Xs (round 4's two-accumulator precision, now for every per-column layer).
     f32x16 X[4], Y[4], Ys[4];
-    RingL<2, 2> ring2;                                     // dense1d_4's first weight chunks
-    const int rt4 = w & 1, ct4 = 2 * (w >> 1);             // dense1d_4: row tile, first column tile
+    // dense1d_4 (see there): wave w computes output blocks 2 (w & 1), + 1 over K quarter w >> 1;
+    // its weight fragments (A operand, 32x32x16 order) PF4 chunks ahead in registers
+    constexpr int C4 = 11, PF4 = 2;
+    const int bp4 = w & 1, kq4 = w >> 1;
+    const bf16x8 *w4 = reinterpret_cast<const bf16x8 *>(W + Nt::soff(4)) + (size_t)(2 * bp4 * 4 * C4 + kq4 * C4) * 3 * 64 + lane;
+    constexpr int W4B = 4 * C4 * 3 * 64;                   // the next block's fragments (bf16x8)
+    bf16x8 r4[PF4][2][3];
+    RingL<1, 2> ring1;                                     // per-leaf layers' weight ring
     auto stage = [&](auto s_const) {
         constexpr int S = decltype(s_const)::value;
         constexpr int L = Nt::stg_layer(S), C0 = Nt::stg_c0(S), NC = Nt::stg_nc(S);
@@ -539,7 +554,12 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if constexpr (S == NSTG - 1) {
             // dense1d_4's first weight chunks into registers behind the last MFMA (wave 7 has no
             // LDS-DMA in flight any more)
-            ringl_load<22>(W + Nt::soff(4), ct4, 1, 8, ring2);
+#pragma unroll
+            for (int c = 0; c < PF4; c++)
+#pragma unroll
+                for (int b = 0; b < 2; b++)
+#pragma unroll
+                    for (int q = 0; q < 3; q++) r4[c][b][q] = w4[b * W4B + (c * 3 + q) * 64];
         } else if (w == 7) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stage S + 1 landed
         }
@@ -656,29 +676,108 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 for (int r = 0; r < 4; r++) put_split(dst, 16 * t + acc16_row(r), dst_off + c, f(a16[j][t][r]));
         }
     };
-    RingL<1, 2> ring1;
-    // ---- dense1d_4 over the 704 flattened features Z (f32, split here: this wave's row tile)
+    // ---- dense1d_4 (round 6) over the 704 flattened features: out^T[128][leaf] = W4 Z^T on
+    // v_mfma_f32_32x32x16_bf16 with the weights as the A operand, K split in four quarters: wave
+    // w computes output blocks 2 (w & 1), + 1 over chunks 11 (w >> 1) .. + 10, its B fragment (8
+    // features of leaf l % 32) read from Z and split here once for both blocks. Every weight
+    // fragment is loaded once per workgroup (round 5's row-tile mapping loaded each twice).
+    // Two accumulators as in the per-column layers; waves 2-7 hand their partial sums to waves
+    // 0-1 through LDS (RED, over the dead Z), which add them in K order, the bias and the relu,
+    // and write the split planes of SB0.
     {
-        const float b4a = bias16(4, ct4), b4b = bias16(4, ct4 + 1);
-        gemm_leaf<2, 1, 22>(W + Nt::soff(4), ct4, 1, ring2, [&](int, int c, bf16x8 &a0, bf16x8 &a1, bf16x8 &a2) {
-            const float *p = Z + (16 * rt4 + (lane & 15)) * ZS + 32 * c + 8 * (lane >> 4);
-            split8(F8{ld4(p), ld4(p + 4)}, a0, a1, a2);
-        }, a16, [&] { ringl_load<4>(W + Nt::soff(5), w, 8, 8, ring1); });
-        lds_barrier();                     // (Z read by every wave: SB1 / SB2 may overwrite it)
-        // the split buffers' padding columns [128, 144) to zero (SB1 / SB2 overlay Z, SB0 held
-        // dense2d_3's pool partials)
-        for (int i = tid; i < 3 * 3 * ML * 8; i += NNT) {
+        f32x16 D[2], Ds[2];
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+            const float *b4 = W + Nt::boff(4) + 32 * (2 * bp4 + b) + 4 * h;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const float4 bb = ld4(b4 + 8 * g);
+                D[b][4 * g] = kq4 ? 0.f : bb.x;
+                D[b][4 * g + 1] = kq4 ? 0.f : bb.y;
+                D[b][4 * g + 2] = kq4 ? 0.f : bb.z;
+                D[b][4 * g + 3] = kq4 ? 0.f : bb.w;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; r++) Ds[b][r] = 0.f;
+        }
+#pragma unroll
+        for (int c = 0; c < C4; c++) {
+            bf16x8 wv[2][3];
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int q = 0; q < 3; q++) {
+                    wv[b][q] = r4[c % PF4][b][q];
+                    if (c + PF4 < C4) r4[c % PF4][b][q] = w4[b * W4B + ((c + PF4) * 3 + q) * 64];
+                }
+            const float *zp = Z + li * ZS + 16 * (kq4 * C4 + c) + 8 * h;
+            bf16x8 bh, bm, bl;
+            split8(F8{ld4(zp), ld4(zp + 4)}, bh, bm, bl);
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+                Ds[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wv[b][2], bh, Ds[b], 0, 0, 0);
+                Ds[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wv[b][1], bm, Ds[b], 0, 0, 0);
+                Ds[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wv[b][0], bl, Ds[b], 0, 0, 0);
+                Ds[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wv[b][1], bh, Ds[b], 0, 0, 0);
+                Ds[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wv[b][0], bm, Ds[b], 0, 0, 0);
+                D[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wv[b][0], bh, D[b], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        ringl_load<4>(W + Nt::soff(5), w, 8, 8, ring1);   // partialgpool_4's first chunks
+        __builtin_amdgcn_sched_barrier(0);
+        lds_barrier();                                     // (every wave has read Z: RED overlays it)
+        float *RED = Z;                                    // [3][2][2][ML][32]: quarters 1-3, block pair, block
+        if (kq4) {
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+                    *reinterpret_cast<f32x4 *>(RED + ((((kq4 - 1) * 2 + bp4) * 2 + b) * ML + li) * 32 + 8 * g + 4 * h) =
+                        f32x4{D[b][4 * g], D[b][4 * g + 1], D[b][4 * g + 2], D[b][4 * g + 3]} +
+                        f32x4{Ds[b][4 * g], Ds[b][4 * g + 1], Ds[b][4 * g + 2], Ds[b][4 * g + 3]};
+        }
+        // SB0's padding columns [128, 144) to zero (it held the per-column biases)
+        for (int i = tid; i < 3 * ML * 8; i += NNT)
+            reinterpret_cast<uint32_t *>(&SB0->p[i / (ML * 8)][(i >> 3) % ML][128])[i & 7] = 0u;
+        lds_barrier();
+        if (!kq4) {
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    f32x4 o = f32x4{D[b][4 * g], D[b][4 * g + 1], D[b][4 * g + 2], D[b][4 * g + 3]} +
+                              f32x4{Ds[b][4 * g], Ds[b][4 * g + 1], Ds[b][4 * g + 2], Ds[b][4 * g + 3]};
+#pragma unroll
+                    for (int qq = 0; qq < 3; qq++)         // K quarters 1, 2, 3 in order
+                        o += *reinterpret_cast<const f32x4 *>(RED + (((qq * 2 + bp4) * 2 + b) * ML + li) * 32 + 8 * g + 4 * h);
+                    const int ch = 32 * (2 * bp4 + b) + 8 * g + 4 * h;
+                    uint32_t hi[2], mi[2], lo[2];          // 4 consecutive channels per plane
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const float x = fmaxf(o[i], 0.f);
+                        const uint32_t hh = __float_as_uint(x) & 0xFFFF0000u;
+                        const float r1 = x - __uint_as_float(hh);
+                        const uint32_t mm = __float_as_uint(r1) & 0xFFFF0000u;
+                        const uint32_t ll = __float_as_uint(r1 - __uint_as_float(mm)) & 0xFFFF0000u;
+                        const int sh = 16 * (i & 1);
+                        if (!(i & 1)) hi[i >> 1] = mi[i >> 1] = lo[i >> 1] = 0u;
+                        hi[i >> 1] |= (hh >> 16) << sh;
+                        mi[i >> 1] |= (mm >> 16) << sh;
+                        lo[i >> 1] |= (ll >> 16) << sh;
+                    }
+                    *reinterpret_cast<uint2 *>(&SB0->p[0][li][ch]) = uint2{hi[0], hi[1]};
+                    *reinterpret_cast<uint2 *>(&SB0->p[1][li][ch]) = uint2{mi[0], mi[1]};
+                    *reinterpret_cast<uint2 *>(&SB0->p[2][li][ch]) = uint2{lo[0], lo[1]};
+                }
+        }
+        lds_barrier();
+        // SB1 / SB2's padding columns to zero (they overlay RED; partialgpool_5 reads SB1's)
+        for (int i = tid; i < 2 * 3 * ML * 8; i += NNT) {
             const int b = i / (3 * ML * 8), rem = i - b * 3 * ML * 8, pl = rem / (ML * 8), rr = (rem >> 3) % ML;
-            SplitAct *d = b == 0 ? SB0 : (b == 1 ? SB1 : SB2);
+            SplitAct *d = b == 0 ? SB1 : SB2;
             reinterpret_cast<uint32_t *>(&d->p[pl][rr][128])[i & 7] = 0u;
         }
-        const int c = acc16_col();
-#pragma unroll
-        for (int j = 0; j < 2; j++)
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-                put_split(SB0, 16 * rt4 + acc16_row(r), 16 * (ct4 + j) + c, fmaxf(a16[j][0][r] + (j ? b4b : b4a), 0.f));
-        lds_barrier();
     }
     // partial pool over 4 groups of 4 of x[0:16] ++ relu(Wp x[16:] + bp) (BN folded): src -> dst
     auto pool44 = [&](const SplitAct *src, SplitAct *dst, int layer, auto next) {

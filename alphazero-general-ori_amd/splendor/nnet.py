@@ -240,8 +240,8 @@ def pack_weights(folded, n_players):
     S = Kp/2; layers 4-12 (16x16x4, Kp % 16 == 0): [NT][Kp/16][64][4], element (nt, q, l, j)
     = W[16 nt + (l & 15)][16 q + 4 (l >> 4) + j] — then the 0-padded bias; then the
     per-column BN affines; then (16-byte aligned) the bf16 x 3 copies the kernel multiplies:
-    layers 0-3 in 32x32x16 fragments (_split_layer; partialgpool_1's rows shifted by 8), layers
-    4-12 in 16x16x32 fragments (_split_leaf_layer)."""
+    layers 0-4 in 32x32x16 fragments (_split_layer; partialgpool_1's rows shifted by 8), layers
+    5-12 in 16x16x32 fragments (_split_leaf_layer)."""
     f = folded
     layers = [(f.w1, f.b1), (f.w2, f.b2), (f.wp1, f.bp1), (f.w3, f.b3), (f.w4, f.b4), (f.wp4, f.bp4),
               (f.w5a, f.b5a), (f.w5b, f.b5b), (f.wp5, f.bp5), (f.wpi1, f.bpi1), (f.wpi2, f.bpi2),
@@ -270,8 +270,8 @@ def pack_weights(folded, n_players):
         parts += [f.s1.reshape(7), f.t1.reshape(7), f.sp1.reshape(7), f.tp1.reshape(7)]
         pad = -sum(p.numel() for p in parts) % 4                    # 16-byte aligned split copies
         parts.append(torch.zeros(pad, dtype=torch.float32, device=f.w1.device))
-        parts += [_split_layer(w, row0=8 if li == 2 else 0) for li, (w, _) in enumerate(layers[:4])]
-        parts += [_split_leaf_layer(w) for w, _ in layers[4:]]
+        parts += [_split_layer(w, row0=8 if li == 2 else 0) for li, (w, _) in enumerate(layers[:5])]
+        parts += [_split_leaf_layer(w) for w, _ in layers[5:]]
         out = torch.cat([p.float() for p in parts]).contiguous()
     want = _lib.lib().spl_nn_packed_floats(n_players)
     if out.numel() != want:

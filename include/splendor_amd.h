@@ -302,11 +302,12 @@ int spl_hash_eval_mode(const spl_ctx *ctx, int B, const int8_t *state, const uin
  *     bias    [T NT] (0-padded)
  * then the per-board-column BatchNorm affines of dense2d_1 and partialgpool_1:
  * s1[7], t1[7], sp1[7], tp1[7] (y = x * s + t); then, from the next 16-byte boundary, the
- * first 4 layers again as exact three-part bf16 splits (w = hi + mid + lo by truncation) for
- * the bf16-MFMA form of those layers: per layer [4][Kp16/16][3][64][8] bf16 (Kp16 = K rounded
+ * 13 layers again as exact three-part bf16 splits (w = hi + mid + lo by truncation) for the
+ * bf16-MFMA form of those layers: the first 5 (the per-column layers and dense1d_4, whose
+ * weights are the A operand of v_mfma_f32_32x32x16_bf16) per layer [4][Kp16/16][3][64][8] bf16 (Kp16 = K rounded
  * up to 16), element (nt, c, p, l, j) = part p of W[32 nt + l % 32 - o][16 c + 8 (l / 32) + j]
  * (o = 8 for partialgpool_1, whose outputs follow its 8 pooled channels, else 0; 0 outside),
- * two bf16 per float slot; then the other 9 layers the same way for 16x16x32: per layer
+ * two bf16 per float slot; then the other 8 layers the same way for 16x16x32: per layer
  * [NT16][Kp32/32][3][64][8] bf16 (NT16 = ceil(N / 16), Kp32 = K rounded up to 32), element
  * (nt, c, p, l, j) = part p of W[16 nt + l % 16][32 c + 8 (l / 16) + j]. The f32 copies of the
  * 13 layers stay in the layout (the biases are read from them). Returns the float count or
