@@ -317,23 +317,44 @@ __device__ int write_sorted_run(const Pools &P, int64_t eb, int64_t vb, int ec, 
 // normalised like numpy's dirichlet (sequential sum, times its reciprocal).
 // pr: LDS, the priors by action (0 for illegal actions; 416 floats), replaced by the noised
 // ones; bits: the legal actions (LDS), ec of them. Wave-collective.
-__device__ void root_noise_lds(const SearchCfg &C, int t, uint32_t stream, float *pr, const uint64_t *bits, int ec) {
+// gbuf (optional, LDS, gcap doubles, not overlapping pr / bits): when ec <= gcap the legal
+// actions' powered priors and then their gammas are kept there, in legal order, instead of
+// being evaluated twice (round 6: k_commit noises the kept root of every tree in the commit
+// iteration at once; the same values, so the same bits)
+__device__ void root_noise_lds(const SearchCfg &C, int t, uint32_t stream, float *pr, const uint64_t *bits, int ec,
+                               double *gbuf = nullptr, int gcap = 0) {
     const int l = lane_id();
     const uint32_t gb = C.board_base + (uint32_t)t;
+    if (ec > gcap) gbuf = nullptr;
     if (C.dir_temp != 1.0) {
         const double e = 1.0 / C.dir_temp;
-        const double s = wave_np_sum409_f64(pr, [e](float x) { return det_pow((double)x, e); });
-        wave_lds_fence();
-        for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = (float)(det_pow((double)pr[a], e) / s);
+        if (gbuf) {
+            for (int k = l; k < ec; k += 64) gbuf[k] = det_pow((double)pr[action_at(bits, k)], e);
+            wave_lds_fence();
+            // (an illegal action's prior is 0 and det_pow(0) = 0: the pairwise sum of the same
+            // 409 values)
+            const double s = wave_np_sum409_f64_at([&](int p) {
+                return (bits[p >> 6] >> (p & 63)) & 1 ? gbuf[order_of(bits, p)] : 0.0;
+            });
+            for (int k = l; k < ec; k += 64) {
+                const int a = action_at(bits, k);
+                pr[a] = (float)(gbuf[k] / s);
+            }
+        } else {
+            const double s = wave_np_sum409_f64(pr, [e](float x) { return det_pow((double)x, e); });
+            wave_lds_fence();
+            for (int a = l; a < SPL_ACTIONS; a += 64) pr[a] = (float)(det_pow((double)pr[a], e) / s);
+        }
         wave_lds_fence();
     }
-    // Dirichlet: gammas lane-parallel, their sum sequential in action order; the gammas
-    // are drawn again for the mix (deterministic) instead of being kept in registers
+    // Dirichlet: gammas lane-parallel, their sum sequential in action order; without gbuf the
+    // gammas are drawn again for the mix (deterministic) instead of being kept in registers
     double acc = 0.0;
 #pragma unroll 1
     for (int j = 0; j < (ec + 63) / 64; j++) {
         const int i = 64 * j + l;
         const double g = i < ec ? det_gamma(C.dir_alpha, C.seed, gb, stream, (uint32_t)i * 4096u) : 0.0;
+        if (gbuf && i < ec) gbuf[i] = g;
         const int m = min(64, ec - 64 * j);
         const int lo = __double2loint(g), hi = __double2hiint(g);
         for (int k = 0; k < m; k++)
@@ -346,8 +367,8 @@ __device__ void root_noise_lds(const SearchCfg &C, int t, uint32_t stream, float
         const int i = 64 * j + l;
         if (i < ec) {
             const int a = action_at(bits, i);
-            const double d = ok ? det_gamma(C.dir_alpha, C.seed, gb, stream, (uint32_t)i * 4096u) * inv
-                                : 1.0 / (double)ec;
+            const double g = gbuf ? gbuf[i] : (ok ? det_gamma(C.dir_alpha, C.seed, gb, stream, (uint32_t)i * 4096u) : 0.0);
+            const double d = ok ? g * inv : 1.0 / (double)ec;
             pr[a] = (float)(0.75 * (double)pr[a] + 0.25 * d);
         }
     }
@@ -370,8 +391,10 @@ struct RunScr {
 // root noise on an expanded root (MCTS.py:150-154, the stored priors): its run re-noised,
 // re-sorted, its visit records' priors and ranks updated; returns the new candidate rank.
 // LDS scratch: bits[7], pr[416], cp / ca / cvi [409]. Wave-collective.
+// gbuf / gcap: root_noise_lds's scratch; callers pass cp (written only after it)
 __device__ int noise_kept_root(const Pools &P, const SearchCfg &C, int t, const NodeRun &r, uint32_t stream,
-                               uint64_t *bits, float *pr, float *cp, int16_t *ca, int16_t *cvi) {
+                               uint64_t *bits, float *pr, float *cp, int16_t *ca, int16_t *cvi, double *gbuf = nullptr,
+                               int gcap = 0) {
     const int l = lane_id();
     run_bits(P, r, bits);
     for (int a = l; a < 416; a += 64) pr[a] = 0.f;
@@ -384,7 +407,8 @@ __device__ int noise_kept_root(const Pools &P, const SearchCfg &C, int t, const 
         cvi[k] = e.vi;
     }
     wave_lds_fence();
-    root_noise_lds(C, t, stream, pr, bits, r.ec);
+    root_noise_lds(C, t, stream, pr, bits, r.ec, gbuf, gcap);
+    wave_lds_fence();                                    // (gbuf may overlay cp)
     for (int k = l; k < r.ec; k += 64) cp[k] = pr[ca[k]];
     wave_lds_fence();
     return write_sorted_run(P, r.eb, r.vb, r.ec, cp, ca, cvi);
@@ -1205,7 +1229,8 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     __shared__ double pterm[WAVES][SPL_ACTIONS];         // random_pick's per-edge terms
     __shared__ int16_t pact[WAVES][SPL_ACTIONS];         // the root's edges in action order:
     __shared__ int32_t pcnt[WAVES][SPL_ACTIONS];         // action, visit count, prior
-    __shared__ float pprior[WAVES][SPL_ACTIONS];
+    __shared__ __align__(16) float pprior[WAVES][SPL_ACTIONS + 3];   // (rows 16-byte aligned: they
+                                                                     //  double as root noise's scratch)
     __shared__ uint64_t pbits[WAVES][7];
     const int w = threadIdx.x >> 6, t = blockIdx.x * WAVES + w;
     if (t >= B) return;
@@ -1275,24 +1300,42 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
     // (the per-edge terms lane-parallel into LDS, the order-dependent sums on lane 0)
     int action = 408;
     const double T = C.temp_threshold > 0 ? (step < C.temp_threshold ? 2.0 : 0.2) : 1.0;
+    // (round 6: the same operations in the same order, but every division off the sequential
+    // chain: p[i] = pt[i] / sum lane-parallel, cdf = cumsum(p) on lane 0 (its last entry is
+    // the normaliser), the first i with cdf[i] / cdf[-1] > u found lane-parallel)
     for (int i = l; i < ec; i += 64) pterm[w][i] = temp_pow((double)POLICY_COUNT(i) / (double)tot, T);
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
+    double sum = 0.0;
     if (l == 0) {
         const double *pt = pterm[w];
-        double sum = 0.0;
         for (int i = 0; i < ec; i++) sum += pt[i];
-        double last = 0.0;
-        for (int i = 0; i < ec; i++) last += pt[i] / sum;
-        const double u = philox_u01(C.seed, gb, ST_PICK | (uint32_t)cm, 0);
+    }
+    sum = readlane_f64(sum, 0);
+    for (int i = l; i < ec; i += 64) pterm[w][i] = pterm[w][i] / sum;
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    if (l == 0) {
+        double *pt = pterm[w];
         double cdf = 0.0;
-        action = pact[w][ec - 1];
         for (int i = 0; i < ec; i++) {
-            cdf += pt[i] / sum;
-            if (cdf / last > u) { action = pact[w][i]; break; }
+            cdf += pt[i];
+            pt[i] = cdf;
         }
     }
-    action = __shfl(action, 0, 64);
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    {
+        const double last = pterm[w][ec - 1];
+        const double u = philox_u01(C.seed, gb, ST_PICK | (uint32_t)cm, 0);
+        int first = ec - 1;
+        for (int base = 0; base < ec; base += 64) {
+            const int i = base + l;
+            const uint64_t m = __ballot(i < ec && pterm[w][i] / last > u);
+            if (m) { first = base + __ffsll((unsigned long long)m) - 1; break; }
+        }
+        action = pact[w][first];
+    }
 #undef POLICY_COUNT
     // getNextState with chance (Coach.py:86), getGameEnded (:88)
     wave_load_board<N>(b, P.board + (size_t)t * Lx::S);
@@ -1372,7 +1415,8 @@ __global__ __launch_bounds__(THREADS) void k_commit(Pools P, SearchCfg C, int B,
         r.ec = uniform(r.ec);
         const int cand = noise_kept_root(P, C, t, r, ST_DIR | (uint32_t)uniform(H->move_no), pbits[w],
                                          reinterpret_cast<float *>(pterm[w]), pprior[w], pact[w],
-                                         reinterpret_cast<int16_t *>(pcnt[w]));
+                                         reinterpret_cast<int16_t *>(pcnt[w]),
+                                         reinterpret_cast<double *>(pprior[w]), (int)(sizeof(pprior[w]) / 8));
         wave_lds_fence();                                        // (the re-sorted run, read below)
         int ca;
         float cp, np;
@@ -1548,8 +1592,22 @@ enum { LS_DESCEND = 0, LS_EXPAND = 1, LS_DONE = 2 };
 // each lane at the first level that is not a plain link, rec = its record; the path entries
 // [depth_in, depth_out) written. The records and path are the C loop's (SELECT_ASM=0).
 #ifndef SELECT_ASM
-#define SELECT_ASM (!SPL_BOUNDS_CHECK)
+#define SELECT_ASM 1       // (bounds-checked builds too: their check follows the block)
 #endif
+// The block's waits count memory instructions per level: an optional child-record load (SA),
+// the h3 record load (SC) and SEL_STORES path stores, in that order. A lane's child loaded on
+// the spot is SEL_W_OWN instructions back; a record requested two levels ago (that level's SC)
+// is behind its SEL_STORES stores and the two later levels' SC + stores: SEL_W_HINT, plus one
+// when the previous level loaded a child. Change the body and these together.
+#define SEL_STORES 2
+#define SEL_W_OWN 3
+#define SEL_W_HINT 8
+#define SEL_W_HINT1 9
+static_assert(SEL_W_OWN == 1 + SEL_STORES, "own child load: behind SC + the stores");
+static_assert(SEL_W_HINT == SEL_STORES + 2 * (1 + SEL_STORES) && SEL_W_HINT1 == SEL_W_HINT + 1,
+              "hinted record: two levels back");
+#define SEL_STR2(x) #x
+#define SEL_STR(x) SEL_STR2(x)
 #define SEL_BODY(SA, SC, K)                                                                     \
     "v_cmp_le_i32 vcc, 0, v240\n"                 /* a linked pick                     */      \
     "v_cmp_le_i32 %[T], 0, v243\n"                /* whose child is not terminal       */      \
@@ -1583,16 +1641,16 @@ enum { LS_DESCEND = 0, LS_EXPAND = 1, LS_DONE = 2 };
     "v_mov_b32 v235, v226\n"                                                                   \
     "s_cmp_eq_u64 %[INV], 0\n"                                                                 \
     "s_cbranch_scc1 L_av" K "_%=\n"                                                            \
-    "s_waitcnt vmcnt(3)\n"                        /* some lane loaded its child now     */      \
+    "s_waitcnt vmcnt(" SEL_STR(SEL_W_OWN) ")\n"    /* some lane loaded its child now     */      \
     "s_mov_b32 %[F], 1\n"                                                                      \
     "s_branch L_sel" K "_%=\n"                                                                 \
     "L_av" K "_%=:\n"                             /* every record requested two levels  */      \
     "s_cmp_eq_u32 %[F], 0\n"                      /* ago: behind 8 memory instructions, */      \
     "s_cbranch_scc1 L_a8" K "_%=\n"               /* 9 if the last level loaded a child */      \
-    "s_waitcnt vmcnt(9)\n"                                                                     \
+    "s_waitcnt vmcnt(" SEL_STR(SEL_W_HINT1) ")\n"                                              \
     "s_branch L_a0" K "_%=\n"                                                                  \
     "L_a8" K "_%=:\n"                                                                          \
-    "s_waitcnt vmcnt(8)\n"                                                                     \
+    "s_waitcnt vmcnt(" SEL_STR(SEL_W_HINT) ")\n"                                               \
     "L_a0" K "_%=:\n"                                                                          \
     "s_mov_b32 %[F], 0\n"                                                                      \
     "L_sel" K "_%=:\n"
@@ -1769,12 +1827,21 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
         bool run = state == LS_DESCEND && !have_pk && nbrd;
 #if SELECT_ASM
         {
-#if SELECT_PROBE
+#if SELECT_PROBE || SPL_BOUNDS_CHECK
             const int d0 = depth;
 #endif
             descend_linked_asm(node, depth, rec, P.nd, P.pcap, path_n, path_x, __ballot(run), P.npages * NPG);
 #if SELECT_PROBE
             plev += depth - d0;
+#endif
+#if SPL_BOUNDS_CHECK
+            // the assembly descent's new path entries [d0, depth): every level's child in the
+            // tree and one round deeper (the C loop's sites 52 / 30)
+            for (int d = d0; d < depth; d++) {
+                const int pn = path_n[d], c = d + 1 < depth ? path_n[d + 1] : node;
+                BCHK(IN_TREE(P, t, c, H->node_count), 52, c, t, (void)0);
+                BCHK(P.nd[c].h.round == P.nd[pn].h.round + 1, 30, ((long long)pn << 32) | (uint32_t)c, t, (void)0);
+            }
 #endif
             run = false;
         }

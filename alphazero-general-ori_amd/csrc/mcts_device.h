@@ -417,6 +417,27 @@ __device__ __forceinline__ float np_sum409(const float *a) {
 
 // pairwise(409) of a double-valued function of a 409-float array (NumPy's float64 pairwise
 // order, the block tree of np_sum409); 32 lanes, lane = 8*block + j, uniform result.
+// (the element at position p is g(p))
+template <class G>
+__device__ __forceinline__ double wave_np_sum409_f64_at(G g) {
+    const int l = lane_id();
+    const int blk = (l >> 3) & 3, j = l & 7;
+    const int off = blk == 0 ? 0 : (blk == 1 ? 96 : (blk == 2 ? 200 : 304));
+    const int len = blk == 0 ? 96 : (blk == 3 ? 105 : 104);
+    double r = g(off + j);
+    for (int i = 8; i < len - (len % 8); i += 8) r += g(off + i + j);
+    const double r1 = __shfl_xor(r, 1, 64);
+    const double p01 = (j & 1) ? r1 + r : r + r1;
+    const double p23 = __shfl_xor(p01, 2, 64);
+    const double q = (j & 2) ? p23 + p01 : p01 + p23;
+    const double q2 = __shfl_xor(q, 4, 64);
+    const double res = (j & 4) ? q2 + q : q + q2;
+    double blockv = __shfl(res, 8 * blk, 64);
+    if (blk == 3) blockv = blockv + g(off + 104);
+    const double b0 = __shfl(blockv, 0, 64), b1 = __shfl(blockv, 8, 64);
+    const double b2 = __shfl(blockv, 16, 64), b3 = __shfl(blockv, 24, 64);
+    return (b0 + b1) + (b2 + b3);
+}
 template <class F>
 __device__ __forceinline__ double wave_np_sum409_f64(const float *a, F f) {
     const int l = lane_id();

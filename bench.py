@@ -268,7 +268,7 @@ def stagger_marks(stagger, groups, sims, ratio):
 
 
 def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, seed, node_boards=-1,
-                 stagger=0, groups=16, mem_gib=0.0, on_steady=None):
+                 stagger=0, groups=16, mem_gib=0.0, on_steady=None, net_path=None):
     """Self-play at one BASELINE config: B games per GPU (shard board_base = rank * B), one
     MCTS simulation per game per iteration, leaves evaluated by the fused SplendorNNet kernel
     (fp32, random init), moves committed on device. `prefill` untimed iterations bring the
@@ -299,6 +299,10 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     eng = SplendorEngine(n, device=dev)
     sargs = dict(GENBU_ARGS, numMCTSSims=sims)
     net = random_net(n, seed=rank, device=dev)
+    if net_path:                               # trained weights (tools/train_prior.py): a plain
+        data = torch.load(net_path, map_location=dev, weights_only=True)      # state_dict only
+        net.load_state_dict(data["state_dict"] if "state_dict" in data else data)
+        net.eval()
     if dist:
         broadcast_network(net)                 # every rank searches with rank 0's network
     ev = LeafEvaluator(eng, net, B, use_graph=False)
@@ -372,6 +376,13 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     st = sp.stats()
     pool = sp.pool_state()
     ts = sp.tree_sizes()
+    # the share of simulations whose leaf needs the network (the rest end on a terminal
+    # state): the compacted NN-leaf count of 200 single iterations
+    nn_leaves = 0
+    for _ in range(200):
+        sp.run(1, use_graph=True)
+        nn_leaves += int(sp.leaf_count.item())
+    nn_leaf_frac = nn_leaves / (200 * B)
     nsym = min(int(ex["board"].shape[0]), 200000)
     t_s = time.perf_counter()
     sym = expand_symmetries(eng, {k: v[:nsym] for k, v in ex.items()}) if nsym else None
@@ -425,7 +436,7 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     res = {"elapsed": elapsed, "iter_ms_events": iter_ms_events, "window": delta, "tree": tree,
            "prefill": prefill, "prefill_s": prefill_s, "stagger": {"iterations": stagger, "groups": groups},
            "symmetry": {"examples": nsym, "variants": int(sym["board"].shape[0]) if sym else 0, "s": sym_s},
-           "nn_kernel_us": nn_us}
+           "nn_kernel_us": nn_us, "nn_leaf_fraction": nn_leaf_frac}
     del sp, ev, net
     return res
 
@@ -445,6 +456,7 @@ def selfplay_record(cfg, r, world, steps, warmup):
             # every search ran on the reference's table (no prune / reset / unexpanded leaf in the
             # window; withdrawals repeat a simulation exactly): False marks a non-conforming record
             "reference_table": not any(r["window"].get(k, 0) for k in ("prunes", "resets", "unexpanded")),
+            "nn_leaf_fraction": r["nn_leaf_fraction"],
             "network_kernel": _network_kernel(n, B, r["nn_kernel_us"])}
 
 
@@ -720,6 +732,8 @@ def main():
                     "(default: on unless the pools do not fit)")
     ap.add_argument("--mem-gib", type=float, default=0.0, help="selfplay: arena budget in GiB (default: "
                     "BatchedMCTS.MEM_FRACTION of the free HBM)")
+    ap.add_argument("--net", default=None, help="selfplay headline: a trained network (state_dict checkpoint, "
+                    "tools/train_prior.py) instead of the random-init one")
     ap.add_argument("--dry-run", action="store_true", help="multi-rank plumbing only (gloo, no GPU): "
                     "prints the line with value null")
     args = ap.parse_args()
@@ -767,7 +781,7 @@ def main():
     n, B, sims = CONFIGS[head]
     ph = {k: (getattr(args, k) if getattr(args, k) is not None else v) for k, v in PHASES[head].items()}
     r = run_selfplay(head, rank, world, dev, dist, args.steps, args.warmup, ph["prefill"], ph["window"], args.seed,
-                     args.node_boards, stagger=ph["stagger"], mem_gib=args.mem_gib)
+                     args.node_boards, stagger=ph["stagger"], mem_gib=args.mem_gib, net_path=args.net)
     rec = selfplay_record(head, r, world, args.steps, args.warmup)
     torch.cuda.empty_cache()
     extra = {}
@@ -800,8 +814,9 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": rec["ms_per_iteration"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp32 (network) / int8 (boards) / f64 (tree statistics)",
-            "data": "synthetic (Philox-seeded deals), random-init SplendorNNet (genbu.pt is refused by the "
-                    "weights-only loader)",
+            "data": ("synthetic (Philox-seeded deals), random-init SplendorNNet (genbu.pt is refused by the "
+                     "weights-only loader)") if not args.net else
+                    f"synthetic (Philox-seeded deals), SplendorNNet trained by tools/train_prior.py ({args.net})",
             "config": {"workload": rec["workload"], "players": n, "games_per_gpu": B, "global_games": world * B,
                        "numMCTSSims": sims, "prefill_iterations": ph["prefill"],
                        "phase_stagger_iterations": ph["stagger"],
