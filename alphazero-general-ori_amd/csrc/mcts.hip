@@ -249,6 +249,12 @@ __device__ __forceinline__ void wave_lds_fence() {
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
 }
+// the same for LDS traffic only: waits for this wave's LDS operations, not for its global stores
+// (a __threadfence_block is s_waitcnt vmcnt(0): every outstanding store's acknowledgement)
+__device__ __forceinline__ void wave_lds_only_fence() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
 // index of action a among the legal actions `bits` (the reference's array order)
 __device__ __forceinline__ int order_of(const uint64_t *bits, int a) {
     const int w = a >> 6;
@@ -2508,7 +2514,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 if (32 * k + hl < SPL_ACTIONS) S.pr[32 * k + hl] = prv[k];
             if (hl < 7) S.bits[hl] = mbits;
         }
-        wave_lds_fence();
+        wave_lds_only_fence();
 #pragma unroll
         for (int k = 0; k < 7; k++) ec += __popcll(S.bits[k]);
         if (!fail && hl == 0) {
@@ -2564,7 +2570,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             run += __popcll(wd);
         }
         if (hl < 4) S.cp[ec + hl] = -INFINITY;
-        wave_lds_fence();
+        wave_lds_only_fence();
         half_write_new_run(P, eb, ec, S.cp, S.ca);
     }
     BPROBE(8)
@@ -2662,7 +2668,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             const int nu = REC_UNITS * __builtin_amdgcn_readlane((int)V.r.vcnt, j);
             for (int k = l; k < nu; k += 64) P.eu[nb + k] = P.eu[ob + k];
         }
-        wave_lds_fence();
+        // (no fence, round 6: the screen below reads the block as it was before this level's
+        // update — a moved block's old copy stays until the tree's next collection — so only
+        // the exact evaluation, which reads other lanes' records, waits for these stores)
+        const int64_t ovb = V.r.vb;
+        const int ovc = V.r.vcnt;
         int n1 = 0, vidx = -1, nns = 0;
         double q1 = 0.0, nqs = 0.0;
         if (in) {
@@ -2729,11 +2739,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
         // requested ahead (round 5 waited one round trip per record); a visited leader is kept
         // by index, its link / rank / action read afterwards (only when it is not the path edge,
         // whose values the lane holds)
+        // (the block before the update, ovb: records [0, ovc); a new record, index ovc, is the
+        // level's own — its values are the lane's)
         const int myv = in && !wide ? V.r.vcnt : 0;
         const int maxv = wave_max_i32(myv);
         {
-            const int64_t vb0 = myv ? V.r.vb : 0;
-            const auto head = [&](int i) { return *P.vh(vb0 + REC_UNITS * (i < myv ? i : 0)); };
+            const int64_t vb0 = myv && ovc ? ovb : 0;
+            const auto head = [&](int i) { return *P.vh(vb0 + REC_UNITS * (i < myv && i < ovc ? i : 0)); };
             VisitHead hd[BK_PF];
 #pragma unroll
             for (int k = 0; k < BK_PF; k++) hd[k] = head(k);
@@ -2742,7 +2754,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                 for (int k = 0; k < BK_PF; k++) {
                     const int i = base + k;
                     const bool mine = i == vidx;
-                    screen_visited(Sc, i < myv, hd[k].p, mine ? n1 : hd[k].n, mine ? q1 : hd[k].q, i);
+                    screen_visited(Sc, i < myv, mine && i >= ovc ? V.e.p : hd[k].p, mine ? n1 : hd[k].n,
+                                   mine ? q1 : hd[k].q, i);
                     hd[k] = head(base + BK_PF + k);       // (unconditional: see screen_visited)
                 }
             }
@@ -2751,7 +2764,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
             if (Sc.vi == vidx) {
                 Sc.off = V.off; Sc.a = V.act; Sc.child = V.rchild;
             } else {
-                const VisitTail tl = *P.vt(V.r.vb + REC_UNITS * Sc.vi);
+                const VisitTail tl = *P.vt(ovb + REC_UNITS * Sc.vi);
                 Sc.off = tl.off; Sc.a = tl.a; Sc.child = tl.child;
             }
         }
@@ -2763,7 +2776,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(BACKUP_
                                 u, ac);
             uc = u;
         }
-        wave_lds_fence();
+        if (__ballot(open)) wave_lds_fence();             // (exact_level reads every lane's records)
         BPROBE(3)
 #if BACKUP_PROBE
         bexact += __popcll(__ballot(open));

@@ -14,6 +14,8 @@
 #   spikes    the slowest launches of each kernel and their iterations (needs trace) -> gpurun_out/spikes.json
 #   pmc       PMC passes over the self-play kernels (pmc_selfplay.sh)  -> gpurun_out/pmc_sp/
 #   nn        full-batch network trace + HBM counters (nn_fullbatch.sh) -> gpurun_out/nnfb/
+#   trainprior  tools/train_prior.py: a few Coach.learn iterations -> gpurun_out/trained_2p.pt,
+#             then the config-3 headline on those weights -> gpurun_out/selfplay_trained.json
 #   accuracy  the fused network vs float64 on 4,096 positions at 2p and 4p (nn_accuracy.py)
 #             -> gpurun_out/nn_accuracy.jsonl
 #   ab        interleaved A/B of the product against each V in $AB: ablib/lib<V>.so, or a whole
@@ -59,6 +61,11 @@ step() {
         timeout -k 10 1000 bash tools/pmc_selfplay.sh gpurun_out/pmc_sp "$ROUND" > gpurun_out/pmc_sp.log 2>&1 ;;
     nn)
         timeout -k 10 400 bash tools/nn_fullbatch.sh "$ROUND" > gpurun_out/nnfb.log 2>&1 ;;
+    trainprior)
+        timeout -k 10 900 python3 -u tools/train_prior.py gpurun_out/trained_2p.pt "${ITERS:-4}" "${GAMES:-4096}" \
+            > gpurun_out/train_prior.jsonl 2> gpurun_out/train_prior.err &&
+        timeout -k 10 300 python3 -u bench.py --workload selfplay --no-cpu-baseline --net gpurun_out/trained_2p.pt \
+            > gpurun_out/selfplay_trained.json 2> gpurun_out/selfplay_trained.err ;;
     accuracy)
         rm -f gpurun_out/nn_accuracy.jsonl
         for np_ in 2 4; do

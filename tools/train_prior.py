@@ -25,7 +25,8 @@ from splendor.coach import Coach  # noqa: E402
 out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/trained_2p.pt"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 games = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
-folder = os.path.join(os.path.dirname(os.path.abspath(out)), "train_prior_ckpt")
+# (Coach.learn's checkpoints and example history stay out of gpurun_out: only OUT is kept)
+folder = os.path.join(os.environ.get("TMPDIR", "/tmp"), "train_prior_ckpt")
 g = SplendorGame(2)
 torch.manual_seed(0)
 nn = NNetWrapper(g, dict(epochs=2, batch_size=512, learn_rate=1e-3, dropout=0.3), seed=0)
