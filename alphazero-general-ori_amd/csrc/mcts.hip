@@ -647,6 +647,12 @@ __device__ unsigned long long g_gc_probe_max[GC_WG_MAX_PROBE][8];   // the slowe
 #define GPROBE(k)
 #endif
 constexpr int GC_NOFIT = -2;   // compact_tree: the compacted tree would not fit the edge pages it holds
+#ifndef GC_SR
+#define GC_SR 8            // edge units per thread per batch of the unit staging / write-back
+#endif
+#ifndef GC_CR
+#define GC_CR 4            // node-board units per thread per round trip of the board move (x2)
+#endif
 template <int CR = 4>   // board units per thread per round trip of the node-board move (x2)
 __device__ int compact_tree(const Pools &P, int t, int root, int root_round, const GcScr &S, GcLds &L,
                             int bunits, bool linked = false) {
@@ -805,7 +811,7 @@ __device__ int compact_tree(const Pools &P, int t, int root, int root_round, con
     // staged, so only the workgroup barrier between the two passes is needed. SR positions
     // per thread per batch with each stage's loads issued together (owner -> its old bases ->
     // the unit -> the link's remap: four dependent round trips per batch, not per unit)
-    constexpr int SR = 8;
+    constexpr int SR = GC_SR;
     for (int k0 = 0; k0 < run; k0 += GCT * SR) {
         int j[SR];
 #pragma unroll
@@ -1099,13 +1105,13 @@ __global__ __launch_bounds__(GCT) void k_gc(Pools P, SearchCfg C) {
             // above the root round
             const int rr = st == 1 && root >= 0 ? P.nd[root].h.round : H->root_round;
             const int r0 = root;
-            root = compact_tree<4>(P, t, r0, rr, S, L, NodeBoard<N>::UNITS);
+            root = compact_tree<GC_CR>(P, t, r0, rr, S, L, NodeBoard<N>::UNITS);
             // capacity pressure (search start: the search would not fit; any: the compacted
             // layout would not fit the page table): prune to the linked nodes, else empty
             bool prune = root == GC_NOFIT;
             if (!prune && st != 1) prune = !tree_fits(P, C, H) && root >= 0;
             if (prune) {
-                root = compact_tree<4>(P, t, root == GC_NOFIT ? r0 : root, rr, S, L, NodeBoard<N>::UNITS, true);
+                root = compact_tree<GC_CR>(P, t, root == GC_NOFIT ? r0 : root, rr, S, L, NodeBoard<N>::UNITS, true);
                 if (tid == 0) H->prunes += 1;
             }
             __syncthreads();
