@@ -3395,6 +3395,8 @@ int spl_mcts_select_compact(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask
 
 int spl_mcts_backup_kind(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v, int kinds,
                          void *hs) {
+    const bool defer_gc = (kinds & SPL_BACKUP_DEFER_GC) != 0;
+    kinds &= ~SPL_BACKUP_DEFER_GC;
     if (!m || kinds < 1 || kinds > 3 || ((kinds & SPL_LEAF_NN) && (!leaf_mask || !pi || !v))) return SPL_EINVAL;
     const dim3 grid = wave_grid((m->B + 1) / 2);
     if (kinds == 3) {
@@ -3407,8 +3409,9 @@ int spl_mcts_backup_kind(spl_mcts *m, const uint64_t *leaf_mask, const float *pi
         SPL_DISPATCH(m->n, hipLaunchKernelGGL((k_backup_h<N, 2>), grid, dim3(THREADS), 0, (hipStream_t)hs, m->P,
                                               m->cfg, m->B, leaf_mask, pi, v));
     }
-    // trees whose simulation was withdrawn (NN leaves only)
-    if (m->cfg.selfplay && (kinds & SPL_LEAF_NN)) launch_gc(m, (hipStream_t)hs);
+    // trees whose simulation was withdrawn (NN leaves only; deferred: the caller's commit
+    // collects them before the next select)
+    if (m->cfg.selfplay && (kinds & SPL_LEAF_NN) && !defer_gc) launch_gc(m, (hipStream_t)hs);
     return check_launch();
 }
 

@@ -229,12 +229,15 @@ class BatchedMCTS:
     # terminal leaves backed up on a side stream during the network (SPLENDOR_OVERLAP=1: on; measured slower: the backup waves delay the network workgroups)
     OVERLAP_TERMINAL = os.environ.get("SPLENDOR_OVERLAP", "0") != "0"
 
-    def simulate(self):
+    def simulate(self, defer_gc=False):
         """One simulation on every tree with budget left: select -> evaluate -> backup. An
         evaluator that can take a compacted leaf list (`indexed`, the fused network) runs on
         the trees whose leaf needs the network only; the trees whose leaf is terminal are
-        backed up meanwhile on a side stream (trees are independent; spl_mcts_backup_kind)."""
+        backed up meanwhile on a side stream (trees are independent; spl_mcts_backup_kind).
+        defer_gc (self-play): the caller commits before the next select, and that commit's
+        collection takes the withdrawn simulations' trees (SPL_BACKUP_DEFER_GC)."""
         s = self.e._s()
+        dg = _lib.BACKUP_DEFER_GC if defer_gc else 0
         if getattr(self.evaluator, "indexed", False):
             _lib.check(self.L.spl_mcts_select_compact(self.h, _ptr(self.leaf_state), _ptr(self.leaf_mask),
                                                       _ptr(self.leaf_valid), _ptr(self.leaf_index),
@@ -250,7 +253,7 @@ class BatchedMCTS:
                 pi, v = self.evaluator(self.leaf_state, self.leaf_mask, self.leaf_valid, index=self.leaf_index,
                                        count=self.leaf_count)
                 cur.wait_stream(side)
-                _lib.check(self.L.spl_mcts_backup_kind(self.h, _ptr(self.leaf_mask), _ptr(pi), _ptr(v), 1, s),
+                _lib.check(self.L.spl_mcts_backup_kind(self.h, _ptr(self.leaf_mask), _ptr(pi), _ptr(v), 1 | dg, s),
                            "spl_mcts_backup_kind")
                 return
             pi, v = self.evaluator(self.leaf_state, self.leaf_mask, self.leaf_valid, index=self.leaf_index,
@@ -259,8 +262,8 @@ class BatchedMCTS:
             _lib.check(self.L.spl_mcts_select(self.h, _ptr(self.leaf_state), _ptr(self.leaf_mask),
                                               _ptr(self.leaf_valid), s), "spl_mcts_select")
             pi, v = self.evaluator(self.leaf_state, self.leaf_mask, self.leaf_valid)
-        _lib.check(self.L.spl_mcts_backup(self.h, _ptr(self.leaf_mask), _ptr(pi), _ptr(v), s),
-                   "spl_mcts_backup")
+        _lib.check(self.L.spl_mcts_backup_kind(self.h, _ptr(self.leaf_mask), _ptr(pi), _ptr(v), 3 | dg, s),
+                   "spl_mcts_backup_kind")
 
     def headers(self):
         _lib.check(self.L.spl_mcts_headers(self.h, _ptr(self._hdr), self.e._s()), "spl_mcts_headers")

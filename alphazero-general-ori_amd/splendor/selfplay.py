@@ -12,6 +12,7 @@ Coach.py:91-98, drained as device tensors (`drain()`), optionally gathered acros
 (`gather_examples`, RCCL all-gather) and expanded with `symmetries`.
 """
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -81,8 +82,12 @@ class SelfPlay(BatchedMCTS):
         _lib.check(self.L.spl_mcts_restart_games(self.h, _ptr(mask), self.e._s()), "spl_mcts_restart_games")
         self._keep = mask                        # alive until the stream has used it
 
+    # the backup leaves the withdrawn simulations' trees to the commit's collection
+    # (SPL_BACKUP_DEFER_GC; SPLENDOR_DEFER_GC=0: collect after the backup as well)
+    DEFER_GC = os.environ.get("SPLENDOR_DEFER_GC", "1") != "0"
+
     def _iteration(self):
-        self.simulate()
+        self.simulate(defer_gc=self.DEFER_GC)
         _lib.check(self.L.spl_mcts_commit(self.h, self.e._s()), "spl_mcts_commit")
 
     def step(self, use_graph=False):

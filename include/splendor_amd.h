@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 9
+#define SPL_ABI_VERSION 10
 #define SPL_ACTIONS 409
 #define SPL_MASK_WORDS 7
 #define SPL_EINVAL (-1)
@@ -211,6 +211,12 @@ int spl_mcts_backup(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, con
  * while the network evaluates the NN leaves (their backup needs no pi / v: NULL allowed). */
 #define SPL_LEAF_NN 1
 #define SPL_LEAF_TERMINAL 2
+/* kinds | SPL_BACKUP_DEFER_GC (self-play handles, ABI 10): no collection launch for the trees
+ * whose simulation was withdrawn (a leaf that did not fit); the caller runs spl_mcts_commit
+ * before the next select, and the collection it launches takes them. The self-play driver
+ * backs up this way: one k_gc launch per iteration instead of two (~5 us, empty at steady
+ * state). Without it, or without a commit before the next select, collect as before. */
+#define SPL_BACKUP_DEFER_GC 4
 int spl_mcts_backup_kind(spl_mcts *m, const uint64_t *leaf_mask, const float *pi, const float *v, int kinds,
                          void *hip_stream);
 /* counts B x 409 i64 (root visit counts Nsa), qsa B x 409 f64 (-42 = unvisited), probs
