@@ -65,6 +65,11 @@ namespace {
 #endif                     // at different depths, and a 1-wave workgroup frees its slot at once
 constexpr int WAVES = TREE_WG;
 constexpr int THREADS = 64 * WAVES;
+// k_leaf_mask's filing regions (see DEEP_FIRST): FILE_RWG workgroups of 64 trees each
+#ifndef FILE_RWG
+#define FILE_RWG 8
+#endif
+__host__ __device__ constexpr int file_regions(int B) { return ((B + 63) / 64 + FILE_RWG - 1) / FILE_RWG; }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const int l = lane_id();
@@ -1722,8 +1727,7 @@ __device__ __forceinline__ void descend_linked_asm(int &node, int &depth, NodeLi
 template <int N>
 __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B, int lim,
                                                      int8_t *__restrict__ leaf_state,
-                                                     uint8_t *__restrict__ leaf_valid,
-                                                     int32_t *__restrict__ leaf_count) {
+                                                     uint8_t *__restrict__ leaf_valid) {
     using Lx = Lay<N>;
     constexpr int ST = (Lx::ROWS % 2 ? Lx::ROWS : Lx::ROWS + 1) * 8;   // odd row count per board:
     __shared__ __align__(16) int8_t boards[64 * ST];                    // lanes on distinct banks
@@ -1735,8 +1739,8 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
     int plev = 0, pexp = 0;                              // levels descended, expansion rounds
 #endif
     const int slot = blockIdx.x * 64 + l;
-    if (blockIdx.x == 0 && l < 2) P.counters[6 + l] = 0;     // k_leaf_mask's filing counters
-    if (blockIdx.x == 0 && l == 2 && leaf_count) *leaf_count = 0;
+    if (l < 2 && blockIdx.x < file_regions(B)) P.fcnt[2 * blockIdx.x + l] = 0;   // k_leaf_mask's
+                                                                                 // filing counters
     const bool live = slot < B;
     const int t = live ? P.order[slot] : 0;
     TreeHdr *H = P.hdr + t;
@@ -2037,13 +2041,32 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
 // the wave-per-board mask of the descent kernel (its lanes are idle for it anyway).
 // A select's launch time is set by its deepest descents (one dependent round trip per level,
 // up to ~115 levels at steady state), so the next select dispatches the trees whose leaf was
-// at least DEEP_FIRST deep first: k_leaf_mask files every tree into P.order (one atomic per
-// 64 trees and bucket; counters [6] [7] are cleared by k_select).
+// at least DEEP_FIRST deep first: k_leaf_mask files every tree into P.order, region by region
+// (FILE_RWG workgroups = 64 FILE_RWG consecutive trees and slots: the region's deep trees from
+// its first slot up, the others from its last slot down; one atomic per workgroup on each of
+// the region's two counters, P.fcnt, cleared by k_select). One pair of counters for the whole
+// batch had 512 workgroups' returning atomics queue at one address: 10 of this kernel's 20 us
+// at config 3 (LM_PROBE).
 #ifndef DEEP_FIRST
 #define DEEP_FIRST 48
 #endif
-// leaf_index / leaf_count (optional): the NN leaves listed compactly (any order) for the
-// indexed network kernel, one atomic per 64 leaves (the count is cleared by k_select)
+// leaf_index / leaf_count (optional): the NN leaves for the indexed network kernel, segment by
+// segment without atomics: segment j = this kernel's workgroup j (trees 64 j .. 64 j + 63) lists
+// its leaves at leaf_index[64 j ..] and their number at leaf_count[j] (nn_list_rows)
+// per-workgroup timestamps of the last k_leaf_mask launch (diagnostic builds only,
+// -DLM_PROBE=1; never the product): s_memrealtime (100 MHz) at entry, after each of the three
+// barriers and at exit
+#ifndef LM_PROBE
+#define LM_PROBE 0
+#endif
+#if LM_PROBE
+constexpr int LM_PSLOTS = 4096;
+__device__ unsigned long long g_lm_probe[LM_PSLOTS][8];
+#define LMPROBE(k) \
+    if (threadIdx.x == 0 && blockIdx.x < LM_PSLOTS) g_lm_probe[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();
+#else
+#define LMPROBE(k)
+#endif
 template <int N>
 __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, const int8_t *__restrict__ leaf_state,
                                                    const uint8_t *__restrict__ leaf_valid,
@@ -2059,34 +2082,70 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
     __shared__ uint32_t pcond[RB];
     __shared__ uint8_t pbad[4][RB];
     __shared__ uint64_t msk[RB][7];
+    LMPROBE(0)
     const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
     if (w == 3) {                                        // launch order of the next select
         const bool in = l < nb;
         const bool deep = in && P.hdr[b0 + l].depth >= DEEP_FIRST;
         const uint64_t bd = __ballot(deep), bs = __ballot(in && !deep);
+        const int r = blockIdx.x / FILE_RWG, lo = 64 * FILE_RWG * r, hi = min(lo + 64 * FILE_RWG, B);
         int kd = 0, ks = 0;
+#if LM_PROBE
+        if (l == 0 && blockIdx.x < LM_PSLOTS) g_lm_probe[blockIdx.x][6] = __builtin_amdgcn_s_memrealtime();
+#endif
         if (l == 0) {
-            if (bd) kd = atomicAdd(&P.counters[6], __popcll(bd));
-            if (bs) ks = atomicAdd(&P.counters[7], __popcll(bs));
+            if (bd) kd = atomicAdd(&P.fcnt[2 * r], __popcll(bd));
+            if (bs) ks = atomicAdd(&P.fcnt[2 * r + 1], __popcll(bs));
         }
         kd = __shfl(kd, 0, 64); ks = __shfl(ks, 0, 64);
-        if (deep) P.order[kd + __popcll(bd & lanemask_lt())] = b0 + l;
-        else if (in) P.order[B - 1 - (ks + __popcll(bs & lanemask_lt()))] = b0 + l;
-    } else if (w == 2 && leaf_index) {                   // the NN leaves, compacted
+#if LM_PROBE
+        if (l == 0 && blockIdx.x < LM_PSLOTS) g_lm_probe[blockIdx.x][7] = __builtin_amdgcn_s_memrealtime() + (uint64_t)(kd & 0);
+#endif
+        if (deep) P.order[lo + kd + __popcll(bd & lanemask_lt())] = b0 + l;
+        else if (in) P.order[hi - 1 - (ks + __popcll(bs & lanemask_lt()))] = b0 + l;
+    } else if (w == 2 && leaf_index) {                   // the segment's NN leaves
         const bool v = l < nb && leaf_valid[b0 + l];
         const uint64_t bv = __ballot(v);
-        int k = 0;
-        if (l == 0 && bv) k = atomicAdd(leaf_count, __popcll(bv));
-        k = __shfl(k, 0, 64);
-        if (v) leaf_index[k + __popcll(bv & lanemask_lt())] = b0 + l;
+        if (v) leaf_index[b0 + __popcll(bv & lanemask_lt())] = b0 + l;
+        if (l == 0) leaf_count[blockIdx.x] = __popcll(bv);
     }
-    for (int i = tid; i < nb * Cv::UNITS; i += 256) {
-        const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
-        Cv::load(lds + b * ST, leaf_state + (size_t)(b0 + b) * Lx::S, u);
+    // the boards and the mask factors: every load issued before the first LDS store (a loop of
+    // load -> store pairs waits one round trip per iteration — 17 of this kernel's 19 us at
+    // config 3, LM_PROBE; now one)
+    constexpr int FW = (7 * 116 + 255) / 256;            // factor words per thread
+    uint64_t fw[FW];
+#pragma unroll
+    for (int k = 0; k < FW; k++) {
+        const int i = tid + 256 * k;
+        fw[k] = i < 7 * 116 ? (&K_MASK_FACTORS[0][0])[i] : 0;
     }
-    for (int i = tid; i < 7 * 116; i += 256) mfac[i] = (&K_MASK_FACTORS[0][0])[i];
+    if constexpr (Cv::QUAD) {
+        constexpr int BU = (RB * Cv::UNITS + 255) / 256;  // board units (4 rows) per thread
+        uint32_t d[BU][7];
+#pragma unroll
+        for (int k = 0; k < BU; k++) {
+            const int i = min(tid + 256 * k, nb * Cv::UNITS - 1), b = i / Cv::UNITS, u = i - b * Cv::UNITS;
+            const uint32_t *g = reinterpret_cast<const uint32_t *>(leaf_state + (size_t)(b0 + b) * Lx::S) + 7 * u;
+#pragma unroll
+            for (int q = 0; q < 7; q++) d[k][q] = g[q];
+        }
+#pragma unroll
+        for (int k = 0; k < BU; k++) {
+            const int i = tid + 256 * k, b = i / Cv::UNITS, u = i - b * Cv::UNITS;
+            if (i < nb * Cv::UNITS) quad_rows_put(d[k], reinterpret_cast<uint64_t *>(lds + b * ST) + 4 * u);
+        }
+    } else {
+        for (int i = tid; i < nb * Cv::UNITS; i += 256) {
+            const int b = i / Cv::UNITS, u = i - b * Cv::UNITS;
+            Cv::load(lds + b * ST, leaf_state + (size_t)(b0 + b) * Lx::S, u);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < FW; k++)
+        if (tid + 256 * k < 7 * 116) mfac[tid + 256 * k] = fw[k];
     lds_sync();
+    LMPROBE(1)
     if (l < nb) {                                        // predicates: part w of every leaf
         uint64_t f0, f1;
         uint32_t cc;
@@ -2104,6 +2163,7 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
         pbad[w][l] = bad;
     }
     lds_sync();
+    LMPROBE(2)
     if (l < nb) {                                        // mask words w and w+4
         const bool bad = pbad[0][l] | pbad[1][l] | pbad[2][l] | pbad[3][l];
         if (bad) {
@@ -2130,6 +2190,7 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
         }
     }
     lds_sync();
+    LMPROBE(3)
     {                                                    // pass bit, lane l < 16 of wave w
         const int b = 16 * w + l;
         if (l < 16 && b < nb) {
@@ -2140,8 +2201,10 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
         }
     }
     lds_sync();
+    LMPROBE(4)
     for (int i = tid; i < nb * 7; i += 256)
         if (leaf_valid[b0 + i / 7]) leaf_mask[(size_t)b0 * 7 + i] = (&msk[0][0])[i];
+    LMPROBE(5)
 }
 
 // k_backup_h: expansion of the NN leaf, the path backup (MCTS.py:169-176) and every path node's
@@ -3156,7 +3219,7 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
     acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
     acc(16 * no); acc(64); acc((size_t)L.nbb * nn); acc(4 * (size_t)B); acc(4 * (size_t)B); acc(8 * no);
-    acc(4 * (size_t)B);
+    acc(4 * (size_t)B); acc(8 * (size_t)file_regions(B));
     L.bytes = bytes;
     return L;
 }
@@ -3213,6 +3276,13 @@ int spl_diag_gc_probe(unsigned long long *out24, int reset) {
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_gc_probe_max), hm, sizeof(hm)) != hipSuccess) return SPL_EDEVICE;
     }
     return 0;
+}
+#endif
+
+#if LM_PROBE
+// the last k_leaf_mask launch's per-workgroup timestamps (LM_PSLOTS x 8)
+int spl_diag_lm_probe(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lm_probe), sizeof(g_lm_probe)) == hipSuccess ? 0 : SPL_EDEVICE;
 }
 #endif
 
@@ -3315,6 +3385,7 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.gcq2 = carve<int32_t>(p, (size_t)B);
     P.flq = carve<int2>(p, no);
     P.order = carve<int32_t>(p, (size_t)B);
+    P.fcnt = carve<int32_t>(p, 2 * (size_t)file_regions(B));
     // zero the small state (headers, counters); the pools need no initialisation (a slot
     // is written before it is read); free stacks hold every page, tables are empty
     bool ok = hipMemset(P.hdr, 0, sizeof(TreeHdr) * B) == hipSuccess &&
@@ -3374,7 +3445,7 @@ static int launch_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, u
                          int32_t *leaf_index, int32_t *leaf_count, void *hs) {
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_select_lanes<N>, dim3((unsigned)((m->B + 63) / 64)), dim3(64), 0,
                                           (hipStream_t)hs, m->P, m->cfg, m->B, m->token_limit,
-                                          leaf_state, leaf_valid, leaf_count));
+                                          leaf_state, leaf_valid));
     SPL_DISPATCH(m->n, hipLaunchKernelGGL(k_leaf_mask<N>, dim3((unsigned)((m->B + 63) / 64)), dim3(256), 0,
                                           (hipStream_t)hs, m->P, m->B, m->token_limit, leaf_state, leaf_valid,
                                           leaf_mask, leaf_index, leaf_count));

@@ -363,12 +363,75 @@ __device__ __forceinline__ f32x4 relu4(f32x4 v) {
     return f32x4{fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
 }
 
+// The search's NN leaves as k_leaf_mask lists them (ABI 11): segment j (trees 64 j .. 64 j + 63)
+// has count[j] leaves at idx[64 j ..]; the list is their concatenation in segment order.
+// Wave-collective: returns the list's length; with rowt / offv (ML ints each, the wave's own),
+// rowt[i] (i < ML) = the idx position of list entry b0 + i. A lane holds 8 consecutive
+// segments' counts (two 16-byte loads) and one DPP scan gives every segment's first entry; each
+// segment that reaches into the tile marks the slot where it starts (slot, and 64 j - start
+// in offv), and a prefix maximum over the slots gives every slot its segment.
+__device__ __forceinline__ int nn_list_rows(const int32_t *__restrict__ count, int nseg, int b0, int *rowt, int *offv) {
+    const int lane = threadIdx.x & 63;
+    if (rowt && lane < ML) rowt[lane] = -1;
+    int base = 0;
+    for (int c0 = 0; c0 < nseg; c0 += 512) {
+        const int j0 = c0 + 8 * lane;
+        int v[8];
+        if (j0 + 8 <= nseg) {
+            const int4 a = *reinterpret_cast<const int4 *>(count + j0), b = *reinterpret_cast<const int4 *>(count + j0 + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; q++) v[q] = j0 + q < nseg ? count[j0 + q] : 0;
+        }
+        int own = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) own += v[q];
+        // inclusive scan of the lanes' sums on DPP: row_shr 1 / 2 / 4 / 8 inside each 16-lane
+        // row (lanes without a source add 0), then row_bcast 15 (rows 1, 3) and 31 (rows 2, 3)
+        int inc = own;
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xf, 0xf, true);
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xf, 0xf, true);
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xf, 0xf, true);
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xf, 0xf, true);
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x142, 0xa, 0xf, false);
+        inc += __builtin_amdgcn_update_dpp(0, inc, 0x143, 0xc, 0xf, false);
+        if (rowt) {
+            int ex = base + inc - own;                   // first list entry of segment j0
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                if (v[q] > 0 && ex + v[q] > b0 && ex < b0 + ML) {
+                    const int sl = max(ex - b0, 0);
+                    rowt[sl] = sl;
+                    offv[sl] = 64 * (j0 + q) - ex;
+                }
+                ex += v[q];
+            }
+        }
+        base += __builtin_amdgcn_readlane(inc, 63);
+    }
+    if (rowt) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        int f = lane < ML ? rowt[lane] : -1;             // prefix maximum over slots 0 .. 31
+        f = max(f, __builtin_amdgcn_update_dpp(-1, f, 0x111, 0xf, 0xf, false));
+        f = max(f, __builtin_amdgcn_update_dpp(-1, f, 0x112, 0xf, 0xf, false));
+        f = max(f, __builtin_amdgcn_update_dpp(-1, f, 0x114, 0xf, 0xf, false));
+        f = max(f, __builtin_amdgcn_update_dpp(-1, f, 0x118, 0xf, 0xf, false));
+        f = max(f, __builtin_amdgcn_update_dpp(-1, f, 0x142, 0xa, 0xf, false));
+        const int pos = f >= 0 ? b0 + lane + offv[f] : 0;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < ML) rowt[lane] = pos;
+    }
+    return base;
+}
+
 template <int NP>
 // one workgroup per CU (LDS) = 2 waves per SIMD: the register budget is 256, and without
 // saying so the scheduler sinks the prefetched weight loads next to their MFMAs
-// idx (optional): the kernel evaluates rows idx[0 .. *count) — board / mask / output row
-// idx[k] — instead of 0 .. B (the search's NN leaves, compacted by k_leaf_mask); tiles past
-// *count exit at once.
+// idx / count (optional): the kernel evaluates the search's NN leaves as k_leaf_mask lists
+// them (nn_list_rows: B trees in segments of 64) — board / mask / output row idx[...] —
+// instead of rows 0 .. B; tiles past the list's end exit at once.
 __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_nn_forward(int B, const int8_t *__restrict__ state,
                                                     const uint64_t *__restrict__ mask,
                                                     const float *__restrict__ W, float *__restrict__ pi_out,
@@ -379,7 +442,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     constexpr int R = Nt::R, X0S = Nt::X0S, NSTG = Nt::NSTG;
     // all LDS in one array (a second __shared__ object beside LDS-DMA targets can make the
     // compiler drain vmcnt before LDS reads): bufA, SB0, the legality masks
-    __shared__ __align__(16) char lds[BUFA + SAB + ML * 7 * 8];
+    __shared__ __align__(16) char lds[BUFA + SAB + ML * 7 * 8 + 15 * ML * 4];
     float *bufA = reinterpret_cast<float *>(lds);
     SplitAct *SB0 = reinterpret_cast<SplitAct *>(lds + BUFA);
     uint64_t *mskl = reinterpret_cast<uint64_t *>(lds + BUFA + SAB);
@@ -387,11 +450,6 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, li = lane & 31;
     const int h = lane >> 5;
     const int b0 = blockIdx.x * ML;
-    const int cnt = count ? __builtin_amdgcn_readfirstlane(*count) : B;
-    if (b0 >= cnt) return;
-    const int nb = min(ML, cnt - b0);
-    // row of leaf i of this tile (its board, mask and outputs)
-    const auto rowof = [&](int i) -> size_t { return idx ? (size_t)idx[b0 + i] : (size_t)(b0 + i); };
     const float *aff = W + Nt::AFF;                        // s1, t1, sp1, tp1
     char *ring = lds + Nt::XR;                             // per-column weight stages (2 buffers)
     float *biasL = reinterpret_cast<float *>(SB0);         // [4][128] per-column biases (until dense1d_4)
@@ -412,10 +470,31 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                         glds16(src + ((b * C + C0 + j) * 3 + p) * 1024, dst + ((j * 4 + b) * 3 + p) * 1024);
         }
     };
-    if (w == 7) {
-        load_stage(IntC<0>());
+    if (w == 7) {                                        // (first: the weights do not depend on
+        load_stage(IntC<0>());                           //  the tile's leaves)
         load_stage(IntC<1>());
     }
+    // the tile's idx positions (nn_list_rows): a copy per input wave, each mapped by its own
+    // wave (no barrier before the input loads; wave 7, which stages no input, needs only the
+    // list's length); wave 0 also resolves the rows themselves into rowv for the epilogues
+    int *rowt = reinterpret_cast<int *>(lds + BUFA + SAB + ML * 7 * 8);
+    int *rowt_w = rowt + (w < 7 ? w : 0) * ML, *rowv = rowt + 7 * ML, *offv_w = rowt + (8 + (w < 7 ? w : 0)) * ML;
+    int cnt = B;
+    if (count) {
+        cnt = __builtin_amdgcn_readfirstlane(
+            nn_list_rows(count, (B + 63) >> 6, b0, w < 7 ? rowt_w : nullptr, offv_w));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // (the wave's own LDS writes,
+        __builtin_amdgcn_wave_barrier();                        //  read back by its lanes)
+    }
+    if (b0 >= cnt) {                                     // (past the list: wave 7's stages land
+        if (w == 7) __builtin_amdgcn_s_waitcnt(0);       //  before the workgroup's LDS is freed)
+        return;
+    }
+    const int nb = min(ML, cnt - b0);
+    // row of leaf i of this tile (its board, mask and outputs): rowin while the wave stages the
+    // input, rowof in the epilogues
+    const auto rowin = [&](int i) -> size_t { return count ? (size_t)idx[rowt_w[i]] : (size_t)(b0 + i); };
+    const auto rowof = [&](int i) -> size_t { return count ? (size_t)rowv[i] : (size_t)(b0 + i); };
 
 #if NN_PROBE
     uint64_t nlast = __builtin_readcyclecounter();
@@ -429,7 +508,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // (waves 0-6 stage the input, so wave 7's vmcnt counts its LDS-DMA only)
     constexpr int NS7 = NNT - 64;
     if (w < 7) {
-        if (tid < nb * 7) mskl[tid] = mask[rowof(tid / 7) * 7 + tid % 7];
+        if (tid < nb * 7) mskl[tid] = mask[rowin(tid / 7) * 7 + tid % 7];
         // per-column biases; partialgpool_1's outputs land on channels 8..127 (its 8 pooled
         // channels come first), so its bias is shifted by 8
         for (int t = tid; t < 4 * 128; t += NS7) {
@@ -445,7 +524,7 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
             for (int k = 0; k < PER; k++) {
                 const int j = tid + k * NS7, i = j / BW;
-                d[k] = j < nb * BW ? reinterpret_cast<const int32_t *>(state + rowof(i) * R * 7)[j - i * BW] : 0;
+                d[k] = j < nb * BW ? reinterpret_cast<const int32_t *>(state + rowin(i) * R * 7)[j - i * BW] : 0;
             }
 #pragma unroll
             for (int k = 0; k < PER; k++) {
@@ -461,11 +540,12 @@ __global__ __launch_bounds__(NNT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         } else {
             for (int j = tid; j < nb * R; j += NS7) {      // one board row (7 bytes) per thread
                 const int i = j / R, r = j - i * R;
-                const int8_t *src = state + (rowof(i) * R + r) * 7;
+                const int8_t *src = state + (rowin(i) * R + r) * 7;
 #pragma unroll
                 for (int c = 0; c < 7; c++) x0[(c * ML + i) * X0S + r] = src[c];
             }
         }
+        if (count && w == 0 && lane < nb) rowv[lane] = (int)rowin(lane);   // (after the input loads)
     } else {
         // stage 0 landed (stage 1's 12 x nc fragments may stay in flight): vmcnt(N) encoded as
         // vmcnt[3:0] | vmcnt[5:4] << 14, expcnt and lgkmcnt at their maxima (no wait)
@@ -966,7 +1046,7 @@ int spl_nn_forward(int n_players, int B, const int8_t *leaf_state, const uint64_
 int spl_nn_forward_indexed(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
                            const int32_t *leaf_index, const int32_t *leaf_count, const float *packed_weights,
                            float *pi, float *v, void *hs) {
-    if (!leaf_index || !leaf_count) return SPL_EINVAL;
+    if (!leaf_index || !leaf_count || reinterpret_cast<uintptr_t>(leaf_count) % 16) return SPL_EINVAL;
     return launch_nn(n_players, B, leaf_state, leaf_mask, packed_weights, pi, v, leaf_index, leaf_count, hs);
 }
 

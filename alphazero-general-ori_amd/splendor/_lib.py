@@ -10,7 +10,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("SPLENDOR_AMD_LIB") or os.path.join(PKG_ROOT, "libsplendor_amd.so")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 EINVAL, EDEVICE = -1, -2
 BACKUP_DEFER_GC = 4                 # spl_mcts_backup_kind: SPL_BACKUP_DEFER_GC
 

@@ -105,7 +105,7 @@ class BatchedMCTS:
         self.leaf_mask = torch.zeros((B, MASK_WORDS), dtype=torch.int64, device=dev)
         self.leaf_valid = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.leaf_index = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.leaf_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.leaf_count = torch.zeros((B + 63) // 64, dtype=torch.int32, device=dev)   # per 64-tree segment
         self.evaluator = evaluator or HashEvaluator(engine)
         self._hdr = torch.empty((B, HDR_DTYPE.itemsize // 4), dtype=torch.int32, device=dev)
 

@@ -289,8 +289,9 @@ class FusedNet:
         self.w = pack_weights(FoldedNet(net).to(self.device).eval(), n_players)
 
     def __call__(self, leaf_state, leaf_mask, pi=None, v=None, index=None, count=None):
-        """index / count (device int32 [B] / [1], spl_mcts_select_compact): evaluate only rows
-        index[:count] (other rows of pi / v are left as they are)."""
+        """index / count (device int32, spl_mcts_select_compact's segmented list: B entries and
+        ceil(B / 64) segment counts): evaluate only the listed rows (other rows of pi / v are
+        left as they are)."""
         B = leaf_state.shape[0]
         pi = pi if pi is not None else torch.empty((B, ACTIONS), dtype=torch.float32, device=self.device)
         v = v if v is not None else torch.empty((B, self.n), dtype=torch.float32, device=self.device)

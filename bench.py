@@ -381,7 +381,7 @@ def run_selfplay(cfg, rank, world, dev, dist, steps, warmup, prefill, window, se
     nn_leaves = 0
     for _ in range(200):
         sp.run(1, use_graph=True)
-        nn_leaves += int(sp.leaf_count.item())
+        nn_leaves += int(sp.leaf_count.sum().item())
     nn_leaf_frac = nn_leaves / (200 * B)
     nsym = min(int(ex["board"].shape[0]), 200000)
     t_s = time.perf_counter()

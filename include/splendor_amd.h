@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 10
+#define SPL_ABI_VERSION 11
 #define SPL_ACTIONS 409
 #define SPL_MASK_WORDS 7
 #define SPL_EINVAL (-1)
@@ -195,11 +195,14 @@ int spl_mcts_pick_best(spl_mcts *m, const uint8_t *active, uint32_t board_base, 
 /* leaf_state: B x S int8, leaf_mask: B x 7 u64, leaf_valid: B u8 (1 = needs the network) */
 int spl_mcts_select(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
                     void *hip_stream);
-/* select + the trees whose leaf needs the network listed compactly: leaf_index (B i32,
- * device) holds their tree ids in [0, *leaf_count) in no particular order, leaf_count (device
- * i32) their number; pair with spl_nn_forward_indexed so the network runs on those leaves
- * only (terminal leaves and idle trees need no evaluation: ~half of all trees per iteration
- * at BASELINE config 3's steady state). */
+/* select + the trees whose leaf needs the network listed segment by segment (ABI 11):
+ * segment j = trees 64 j .. 64 j + 63; leaf_count (device, ceil(B / 64) i32, 16-byte aligned)
+ * holds each segment's number of such trees and leaf_index (device, B i32) their ids at
+ * leaf_index[64 j .. 64 j + leaf_count[j]) in no particular order; the list is the segments'
+ * entries in segment order. Pair with spl_nn_forward_indexed so the network runs on those
+ * leaves only (terminal leaves and idle trees need no evaluation: ~30 % of all trees per
+ * iteration at BASELINE config 3's steady state). (ABI 10 kept one compact list and one count:
+ * every 64-tree workgroup then took its place with a returning atomic on one counter.) */
 int spl_mcts_select_compact(spl_mcts *m, int8_t *leaf_state, uint64_t *leaf_mask, uint8_t *leaf_valid,
                             int32_t *leaf_index, int32_t *leaf_count, void *hip_stream);
 /* pi: B x 409 f32 (policy over all actions, as predict returns), v: B x n f32 */
@@ -321,9 +324,10 @@ int spl_hash_eval_mode(const spl_ctx *ctx, int B, const int8_t *state, const uin
 int spl_nn_packed_floats(int n_players);
 int spl_nn_forward(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
                    const float *packed_weights, float *pi, float *v, void *hip_stream);
-/* the same network on the rows leaf_index[0 .. *leaf_count) only (device i32 list and count,
- * as spl_mcts_select_compact writes them): boards, masks and outputs of row r = leaf_index[k]
- * (B bounds the list); other rows of pi / v are left untouched. */
+/* the same network on the rows listed by leaf_index / leaf_count only, in the segmented form
+ * spl_mcts_select_compact writes (B = the number of trees: ceil(B / 64) segment counts,
+ * leaf_count 16-byte aligned): boards, masks and outputs of row r = every listed leaf_index
+ * entry; other rows of pi / v are left untouched. */
 int spl_nn_forward_indexed(int n_players, int B, const int8_t *leaf_state, const uint64_t *leaf_mask,
                            const int32_t *leaf_index, const int32_t *leaf_count, const float *packed_weights,
                            float *pi, float *v, void *hip_stream);

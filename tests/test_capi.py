@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(LIB)
     missing = [n for n in declared() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.spl_abi_version() == 10
+    assert lib.spl_abi_version() == 11
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libsplendor_amd.so not built")

@@ -168,9 +168,10 @@ def test_fused_kernel_many_tiles(n):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", (2, 3, 4))
 def test_fused_kernel_indexed_rows(n):
-    """spl_nn_forward_indexed on a scattered subset of rows (the search's compacted NN leaves)
-    writes exactly those rows, bit-identical to the full-batch kernel, and leaves every other
-    row untouched."""
+    """spl_nn_forward_indexed on a scattered subset of rows (the search's NN leaves, listed per
+    64-row segment as k_leaf_mask writes them: counts per segment, entries in any order inside
+    their segment, an empty segment and a ragged last one) writes exactly those rows,
+    bit-identical to the full-batch kernel, and leaves every other row untouched."""
     from splendor.nnet import FusedNet, random_net
     with np.load(os.path.join(GOLD, f"env_{n}p.npz")) as z:
         st, mk = z["state"], z["mask_player"]
@@ -181,10 +182,18 @@ def test_fused_kernel_indexed_rows(n):
     mask = torch.from_numpy(_pack_mask(mk[idx].astype(bool))).cuda()
     fused = FusedNet(random_net(n, seed=5), n, "cuda")
     pi_full, v_full = fused(boards, mask)
-    rows = np.sort(rng.choice(B, 301, replace=False)).astype(np.int32)[::-1].copy()    # any order
-    index = torch.zeros(B, dtype=torch.int32, device="cuda")
-    index[:len(rows)] = torch.from_numpy(rows).cuda()
-    count = torch.tensor([len(rows)], dtype=torch.int32, device="cuda")
+    rows = np.sort(rng.choice(B, 301, replace=False)).astype(np.int32)
+    rows = rows[(rows // 64) != 3]                                            # segment 3: empty
+    nseg = (B + 63) // 64
+    index_np = np.full(B, -1, dtype=np.int32)
+    count_np = np.zeros(nseg, dtype=np.int32)
+    for j in range(nseg):
+        r = rows[(rows // 64) == j][::-1]                                     # any order
+        index_np[64 * j:64 * j + len(r)] = r
+        count_np[j] = len(r)
+    assert count_np[3] == 0 and count_np[-1] > 0 and B % 64
+    index = torch.from_numpy(index_np).cuda()
+    count = torch.from_numpy(count_np).cuda()
     pi = torch.full((B, 409), -7.0, device="cuda")
     v = torch.full((B, n), -7.0, device="cuda")
     fused(boards, mask, pi, v, index=index, count=count)

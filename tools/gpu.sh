@@ -23,6 +23,8 @@
 #   probe     k_select_lanes phase probes (ablib/lib<V>.so for V in ${PROBES:-probe}, -DSELECT_PROBE=1) -> gpurun_out/<V>.json
 #   gcprobe   compact_tree phase probes (ablib/libgcprobe.so, -DGC_PROBE=1)    -> gpurun_out/gcprobe.json
 #   nnprobe   per-layer cycle probes of the network kernel (ablib/libnnprobe.so, -DNN_PROBE=1) -> gpurun_out/nnprobe.json
+#   lmprobe   per-workgroup timeline of k_leaf_mask (ablib/liblmprobe.so, -DLM_PROBE=1) -> gpurun_out/lmprobe.json
+#   nnidx     the network on the search's NN-leaf list alone (tools/nn_indexed_time.py)  -> gpurun_out/nnidx.jsonl
 #   bounds    the bounds-checked build (ablib/libchk.so: tools/bounds_check.sh on
 #             the host first) under capacity pressure                   -> gpurun_out/bounds_chk.json
 # ROUND (default r05) names the summaries; EXTRA adds bench arguments to selfplay/trace; TREE=<V>
@@ -93,6 +95,11 @@ step() {
     gcprobe)
         SPLENDOR_AMD_LIB=$PWD/ablib/libgcprobe.so timeout -k 10 200 python3 -u tools/gc_probe.py \
             > gpurun_out/gcprobe.json 2> gpurun_out/gcprobe.err ;;
+    lmprobe)
+        SPLENDOR_AMD_LIB=$PWD/ablib/liblmprobe.so timeout -k 10 300 python3 -u tools/lm_probe.py \
+            > gpurun_out/lmprobe.json 2> gpurun_out/lmprobe.err ;;
+    nnidx)
+        timeout -k 10 120 python3 -u tools/nn_indexed_time.py >> gpurun_out/nnidx.jsonl 2>> gpurun_out/nnidx.err ;;
     nnprobe)
         SPLENDOR_AMD_LIB=$PWD/ablib/libnnprobe.so timeout -k 10 200 python3 -u tools/nn_probe.py \
             > gpurun_out/nnprobe.json 2> gpurun_out/nnprobe.err ;;
