@@ -65,11 +65,6 @@ namespace {
 #endif                     // at different depths, and a 1-wave workgroup frees its slot at once
 constexpr int WAVES = TREE_WG;
 constexpr int THREADS = 64 * WAVES;
-// k_leaf_mask's filing regions (see DEEP_FIRST): FILE_RWG workgroups of 64 trees each
-#ifndef FILE_RWG
-#define FILE_RWG 8
-#endif
-__host__ __device__ constexpr int file_regions(int B) { return ((B + 63) / 64 + FILE_RWG - 1) / FILE_RWG; }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const int l = lane_id();
@@ -1739,10 +1734,8 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
     int plev = 0, pexp = 0;                              // levels descended, expansion rounds
 #endif
     const int slot = blockIdx.x * 64 + l;
-    if (l < 2 && blockIdx.x < file_regions(B)) P.fcnt[2 * blockIdx.x + l] = 0;   // k_leaf_mask's
-                                                                                 // filing counters
     const bool live = slot < B;
-    const int t = live ? P.order[slot] : 0;
+    const int t = live ? slot : 0;
     TreeHdr *H = P.hdr + t;
     int8_t *s = boards + l * ST;
     int sims = 0, root = -1, hdepth = 0, mv = 0, hnc = 0, hnpg = 0;
@@ -2039,17 +2032,11 @@ __global__ __launch_bounds__(64) void k_select_lanes(Pools P, SearchCfg C, int B
 // (splendor_device.h lane_predicates_part / lane_mask_word_fast, exact path for boards
 // outside the fast domain), then the pass bit iff nothing else is legal (:263). Replaces
 // the wave-per-board mask of the descent kernel (its lanes are idle for it anyway).
-// A select's launch time is set by its deepest descents (one dependent round trip per level,
-// up to ~115 levels at steady state), so the next select dispatches the trees whose leaf was
-// at least DEEP_FIRST deep first: k_leaf_mask files every tree into P.order, region by region
-// (FILE_RWG workgroups = 64 FILE_RWG consecutive trees and slots: the region's deep trees from
-// its first slot up, the others from its last slot down; one atomic per workgroup on each of
-// the region's two counters, P.fcnt, cleared by k_select). One pair of counters for the whole
-// batch had 512 workgroups' returning atomics queue at one address: 10 of this kernel's 20 us
-// at config 3 (LM_PROBE).
-#ifndef DEEP_FIRST
-#define DEEP_FIRST 48
-#endif
+// (Until late round 6 this kernel also filed the trees whose leaf was deep into the first
+// launch slots of the next select, behind one returning atomic per workgroup on a shared
+// counter — 10 of its 20 us at config 3, LM_PROBE. A select's 64-lane waves are all resident
+// at once, so its launch lasts as long as its deepest descent whatever the grouping: the
+// select now takes tree = slot, A/B 0.4471 / 0.4462 vs 0.4486 / 0.4485 ms.)
 // leaf_index / leaf_count (optional): the NN leaves for the indexed network kernel, segment by
 // segment without atomics: segment j = this kernel's workgroup j (trees 64 j .. 64 j + 63) lists
 // its leaves at leaf_index[64 j ..] and their number at leaf_count[j] (nn_list_rows)
@@ -2085,26 +2072,7 @@ __global__ __launch_bounds__(256) void k_leaf_mask(Pools P, int B, int lim, cons
     LMPROBE(0)
     const int b0 = blockIdx.x * RB, nb = min(RB, B - b0);
     const int tid = threadIdx.x, w = tid >> 6, l = lane_id();
-    if (w == 3) {                                        // launch order of the next select
-        const bool in = l < nb;
-        const bool deep = in && P.hdr[b0 + l].depth >= DEEP_FIRST;
-        const uint64_t bd = __ballot(deep), bs = __ballot(in && !deep);
-        const int r = blockIdx.x / FILE_RWG, lo = 64 * FILE_RWG * r, hi = min(lo + 64 * FILE_RWG, B);
-        int kd = 0, ks = 0;
-#if LM_PROBE
-        if (l == 0 && blockIdx.x < LM_PSLOTS) g_lm_probe[blockIdx.x][6] = __builtin_amdgcn_s_memrealtime();
-#endif
-        if (l == 0) {
-            if (bd) kd = atomicAdd(&P.fcnt[2 * r], __popcll(bd));
-            if (bs) ks = atomicAdd(&P.fcnt[2 * r + 1], __popcll(bs));
-        }
-        kd = __shfl(kd, 0, 64); ks = __shfl(ks, 0, 64);
-#if LM_PROBE
-        if (l == 0 && blockIdx.x < LM_PSLOTS) g_lm_probe[blockIdx.x][7] = __builtin_amdgcn_s_memrealtime() + (uint64_t)(kd & 0);
-#endif
-        if (deep) P.order[lo + kd + __popcll(bd & lanemask_lt())] = b0 + l;
-        else if (in) P.order[hi - 1 - (ks + __popcll(bs & lanemask_lt()))] = b0 + l;
-    } else if (w == 2 && leaf_index) {                   // the segment's NN leaves
+    if (w == 2 && leaf_index) {                          // the segment's NN leaves
         const bool v = l < nb && leaf_valid[b0 + l];
         const uint64_t bv = __ballot(v);
         if (v) leaf_index[b0 + __popcll(bv & lanemask_lt())] = b0 + l;
@@ -3151,7 +3119,6 @@ __global__ __launch_bounds__(256) void k_hash_eval(int B, const int8_t *__restri
 // free stacks = every page, allocation counters
 __global__ void k_init_pools(Pools P, int B) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = tid; i < (size_t)B; i += nth) P.order[i] = (int32_t)i;
     // free stacks: every page past the home pages, lowest on top
     const int nsh = P.npages - P.nhome * B, esh = P.epages - P.ehome * B;
     for (size_t i = tid; i < (size_t)nsh; i += nth) P.nfree[i] = (int32_t)(P.npages - 1 - i);
@@ -3219,7 +3186,6 @@ static Plan plan_pools(int n, int B, const spl_mcts_config *cfg) {
     acc((size_t)B * L.S); acc(nx * L.S); acc(4 * nx * SPL_ACTIONS); acc(16 * nx); acc(56 * nx); acc(4 * nx);
     acc(no * L.S); acc(4 * no * SPL_ACTIONS); acc(16 * no); acc(16 * no); acc(56 * no); acc(16 * no);
     acc(16 * no); acc(64); acc((size_t)L.nbb * nn); acc(4 * (size_t)B); acc(4 * (size_t)B); acc(8 * no);
-    acc(4 * (size_t)B); acc(8 * (size_t)file_regions(B));
     L.bytes = bytes;
     return L;
 }
@@ -3384,8 +3350,6 @@ int spl_mcts_create(const spl_ctx *ctx, int B, const spl_mcts_config *cfg, spl_m
     P.gcq = carve<int32_t>(p, (size_t)B);
     P.gcq2 = carve<int32_t>(p, (size_t)B);
     P.flq = carve<int2>(p, no);
-    P.order = carve<int32_t>(p, (size_t)B);
-    P.fcnt = carve<int32_t>(p, 2 * (size_t)file_regions(B));
     // zero the small state (headers, counters); the pools need no initialisation (a slot
     // is written before it is read); free stacks hold every page, tables are empty
     bool ok = hipMemset(P.hdr, 0, sizeof(TreeHdr) * B) == hipSuccess &&

@@ -233,14 +233,12 @@ struct Pools {
     int32_t *out_scdiff, *out_meta;      // out_cap x 4, out_cap x 4 (board id, game, index, player)
     int32_t *counters;                   // [0] queued examples [1] dropped [2] GC queue
                                          // [5] example-row queue [4] k_gc workgroups done
-                                         // [6] [7] unused (round 6: P.fcnt)
+                                         // [6] [7] unused
                                          // [8] should-collections taken by this k_gc launch
                                          // [9] deferred entries (gcq2)
     int32_t *gcq;                        // B: trees whose garbage collection k_gc runs
     int32_t *gcq2;                       // B: entries deferred to the next k_gc launch
     int2 *flq;                           // out_cap: (staging row, queue slot) rows k_gc copies
-    int32_t *order;                      // B: the trees in k_select's launch order (deep first)
-    int32_t *fcnt;                       // 2 per filing region: deep / other trees filed there
 
     __device__ __forceinline__ EdgeP *ep(int64_t u) const { return reinterpret_cast<EdgeP *>(eu + u); }
     __device__ __forceinline__ VisitRec *vr(int64_t u) const { return reinterpret_cast<VisitRec *>(eu + u); }

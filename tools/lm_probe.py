@@ -46,9 +46,7 @@ def main():
                       "launch_span_us": float((t[:, 5].max() - t0) * us),
                       "entry_offset_us": pct(t[:, 0] - t0), "exit_offset_us": pct(t[:, 5] - t0),
                       "lifetime_us": pct(t[:, 5] - t[:, 0]),
-                      "phases_us": {nm: pct(t[:, k + 1] - t[:, k]) for k, nm in enumerate(names)},
-                      "filing_atomics_us": pct(t[:, 7] - t[:, 6]),
-                      "filing_atomics_issue_offset_us": pct(t[:, 6] - t0)}), flush=True)
+                      "phases_us": {nm: pct(t[:, k + 1] - t[:, k]) for k, nm in enumerate(names)}}), flush=True)
 
 
 if __name__ == "__main__":
