@@ -166,6 +166,45 @@ def test_fused_kernel_many_tiles(n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", (2, 4))
+def test_fused_kernel_indexed_rows_many_segments(n):
+    """The segmented NN-leaf list past 512 segments (B = 40,000 trees: nn_list_rows' second block
+    of segments) with segment counts of 0, 1, 2, 5, 63 and 64 mixed, so 32-leaf tiles span up to
+    32 segments: exactly the listed rows, bit-identical to the full-batch kernel."""
+    from splendor.nnet import FusedNet, random_net
+    with np.load(os.path.join(GOLD, f"env_{n}p.npz")) as z:
+        st, mk = z["state"], z["mask_player"]
+    rng = np.random.default_rng(20 + n)
+    B = 40000
+    pick = rng.integers(0, len(st), B)
+    boards = torch.from_numpy(st[pick].copy()).cuda()
+    mask = torch.from_numpy(_pack_mask(mk[pick].astype(bool))).cuda()
+    fused = FusedNet(random_net(n, seed=6), n, "cuda")
+    pi_full, v_full = fused(boards, mask)
+    nseg = (B + 63) // 64
+    index_np = np.zeros(B, dtype=np.int32)
+    count_np = np.zeros(nseg, dtype=np.int32)
+    rows = []
+    for j in range(nseg):
+        size = min(64, B - 64 * j)
+        c = min(size, int(rng.choice([0, 1, 1, 2, 5, 63, 64])))
+        r = rng.choice(size, c, replace=False).astype(np.int32) + 64 * j
+        index_np[64 * j:64 * j + c] = r
+        count_np[j] = c
+        rows.append(r)
+    rows = np.concatenate(rows)
+    assert nseg > 512 and (count_np == 1).sum() > 32
+    pi = torch.full((B, 409), -7.0, device="cuda")
+    v = torch.full((B, n), -7.0, device="cuda")
+    fused(boards, mask, pi, v, index=torch.from_numpy(index_np).cuda(), count=torch.from_numpy(count_np).cuda())
+    sel = torch.from_numpy(rows.astype(np.int64)).cuda()
+    assert torch.equal(pi[sel], pi_full[sel]) and torch.equal(v[sel], v_full[sel])
+    other = torch.ones(B, dtype=torch.bool, device="cuda")
+    other[sel] = False
+    assert bool((pi[other] == -7.0).all()) and bool((v[other] == -7.0).all())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", (2, 3, 4))
 def test_fused_kernel_indexed_rows(n):
     """spl_nn_forward_indexed on a scattered subset of rows (the search's NN leaves, listed per
